@@ -1,0 +1,175 @@
+#!/usr/bin/env python3
+"""Headline benchmark: on-device LLM generation throughput and energy per token.
+
+Metric (BASELINE.json): "Joules/generated-token (on-device vs remote) +
+tokens/sec, per model/length".  This bench measures the on-device arm of the
+flagship config — llama3.1:8b, 1000-word requests (⌈4/3·1000⌉ = 1334 forced
+tokens), bf16, random-init weights, synthetic prompts built
+from the reference's own topics list — on N GPUs of one node, one process per
+GPU (weak scaling: every rank runs the same per-GPU trial batch).
+
+A *step* is one batch of ``--batch`` concurrent trials on every GPU: prefill of
+the prompts, then the full generation of 1334 tokens per trial with Ollama's
+default sampling (temperature 0.8, top-k 40, top-p 0.9, repeat penalty 1.1),
+EOS disabled so every trial produces the requested length.  ``value`` is the
+whole-job generated tokens/s; the JSON also reports measured GPU energy per
+generated token from the amd-smi counters (``J_per_token``; idle-subtracted
+variant too).  Baseline: the reference's llama3.1:8b on-device 1000-word cell,
+est. 19.2 tok/s and 0.574 J/token on a MacBook Pro M2.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--model M] [--words W] [--batch B]
+       (multi-GPU: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...)
+"""
+from __future__ import annotations
+
+import argparse
+import csv
+import json
+import math
+import os
+import sys
+import time
+from pathlib import Path
+
+BASELINE = {  # BASELINE.md §2, on_device rows: (est. tok/s, est. J/token) per requested length
+    ("llama3.1:8b", 100): (7.9, 0.483), ("llama3.1:8b", 500): (14.9, 0.726), ("llama3.1:8b", 1000): (19.2, 0.574),
+    ("qwen2:1.5b", 100): (12.8, 0.180), ("qwen2:1.5b", 500): (43.5, 0.081), ("qwen2:1.5b", 1000): (76.5, 0.056),
+    ("gemma:2b", 100): (12.1, 0.212), ("gemma:2b", 500): (34.3, 0.132), ("gemma:2b", 1000): (67.2, 0.077),
+    ("phi3:3.8b", 100): (8.8, 0.401), ("phi3:3.8b", 500): (15.6, 0.619), ("phi3:3.8b", 1000): (25.3, 0.398),
+    ("qwen2:7b", 100): (6.2, 1.105), ("qwen2:7b", 500): (15.2, 0.703), ("qwen2:7b", 1000): (25.1, 0.436),
+    ("gemma:7b", 100): (8.0, 0.496), ("gemma:7b", 500): (17.4, 0.651), ("gemma:7b", 1000): (32.7, 0.329),
+    ("mistral:7b", 100): (7.1, 0.653), ("mistral:7b", 500): (15.9, 0.648), ("mistral:7b", 1000): (28.3, 0.366),
+}
+
+
+def topics():
+    p = Path(__file__).resolve().parent / "experiments" / "topics.csv"
+    try:
+        with open(p, newline="") as fh:
+            return [r["Topic"] for r in csv.DictReader(fh)]
+    except OSError:
+        return ["United States", "India", "Elizabeth II", "World War II"]
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--model", default="llama3.1:8b")
+    ap.add_argument("--words", type=int, default=1000)
+    ap.add_argument("--batch", type=int, default=64, help="concurrent trials per GPU (trial batching)")
+    ap.add_argument("--context", type=int, default=1536)
+    ap.add_argument("--steps-per-graph", type=int, default=16)
+    ap.add_argument("--no-energy", action="store_true")
+    ns = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    from cain_amd.engine import DecodeEngine
+    from cain_amd.models.tokenizer import tokens_for_words
+
+    n_tok = tokens_for_words(ns.words)
+    eng = DecodeEngine(ns.model, device=dev, max_batch=ns.batch, max_context=ns.context, seed=1234 + rank,
+                       steps_per_graph=ns.steps_per_graph)
+    tps = topics()
+    opts = {"eos_id": -1}  # forced length: random weights never emit a meaningful EOS
+
+    def prompts(step):
+        return [f"In {ns.words} words, please give me information about {tps[(step * ns.batch + i + rank * 7) % len(tps)]}"
+                for i in range(ns.batch)]
+
+    def one_step(step):
+        res = eng.generate(prompts(step), n_tok, [dict(opts, seed=step * 100003 + i + 1) for i in range(ns.batch)])
+        return sum(r.eval_count for r in res)
+
+    for w in range(ns.warmup):
+        one_step(-1 - w)
+
+    meter = None
+    if not ns.no_energy:
+        try:
+            from cain_amd.energy import EnergyMeter
+            meter = EnergyMeter(devices=[local], period_ms=100.0, keep_samples=False)
+            meter.measure_idle(1.0)
+        except Exception as exc:  # energy is auxiliary to the throughput metric
+            print(f"[bench] energy meter unavailable: {exc}", file=sys.stderr)
+            meter = None
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+
+    barrier()
+    if meter:
+        meter.start()
+    t0 = time.perf_counter()
+    toks = 0
+    for s in range(ns.steps):
+        toks += one_step(s)
+    barrier()
+    dt = time.perf_counter() - t0
+    reading = meter.stop() if meter else None
+
+    vals = torch.tensor([dt, float(toks), reading.gpu_energy_j if reading else float("nan"),
+                         reading.idle_subtracted_j if reading else float("nan")], dtype=torch.float64, device=dev)
+    if world > 1:
+        allv = [torch.zeros_like(vals) for _ in range(world)]
+        dist.all_gather(allv, vals)
+        allv = torch.stack(allv).cpu()
+    else:
+        allv = vals[None].cpu()
+    t_max = float(allv[:, 0].max())
+    tokens = float(allv[:, 1].sum())
+    energy = float(allv[:, 2].sum())
+    energy_idle_sub = float(allv[:, 3].sum())
+    value = tokens / t_max
+    base_tps, base_jpt = BASELINE.get((ns.model, ns.words), (None, None))
+    if rank == 0:
+        out = {
+            "metric": "tokens/sec (on-device generation; also J/generated-token)",
+            "value": round(value, 2),
+            "unit": "tokens/s",
+            "n_gpus": world,
+            "steps": ns.steps,
+            "warmup": ns.warmup,
+            "ms_per_step": round(1000 * t_max / ns.steps, 2),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": round(value / base_tps, 2) if base_tps else None,
+            "dtype": "bf16",
+            "data": "synthetic (reference topics.csv prompts, random-init weights)",
+            "config": {"model": ns.model, "global_batch": ns.batch * world, "seq_len": n_tok,
+                       "parallelism": f"dp{world}", "words": ns.words, "trials_per_gpu": ns.batch,
+                       "sampling": "ollama defaults (T=0.8, top_k=40, top_p=0.9, repeat_penalty=1.1), eos disabled"},
+            "tokens_generated": int(tokens),
+            "J_per_token": round(energy / tokens, 5) if not math.isnan(energy) else None,
+            "J_per_token_idle_subtracted": (round(energy_idle_sub / tokens, 5)
+                                            if not math.isnan(energy_idle_sub) else None),
+            "avg_gpu_power_W": round(energy / t_max / world, 1) if not math.isnan(energy) else None,
+            "baseline": {"tok_per_s": base_tps, "J_per_token": base_jpt, "hardware": "MacBook Pro M2 (est.)"},
+            "vs_baseline_J_per_token": (round(base_jpt / (energy / tokens), 2)
+                                        if base_jpt and not math.isnan(energy) and energy > 0 else None),
+        }
+        print(json.dumps(out), flush=True)
+    if meter:
+        meter.close()
+    eng.close()
+    if world > 1:
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

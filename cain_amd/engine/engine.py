@@ -1,0 +1,436 @@
+"""Autoregressive decode engine (the on-device arm's LLM; replaces Ollama/llama.cpp).
+
+Reference: the reference never runs a model itself — it POSTs to an external
+Ollama server (experiment/RunnerConfig.py:122-131).  SURVEY §2.3 row 1 and
+§3.4 specify what replaces it: tokenize, prefill, autoregressive decode with a
+KV cache and Ollama's sampling, returning Ollama's statistics
+(``prompt_eval_count``, ``eval_count``, ``*_duration`` in ns).
+
+Backends
+--------
+``hip``    the MI355X path: packed bf16 weights resident in HBM, the hand-written
+           gfx950 kernels of ``cain_amd.ops`` sequenced by the native runtime
+           (``csrc/runtime.hip``) and replayed from hipGraphs — ``steps_per_graph``
+           decode steps per graph launch, the sampler advancing tok/pos on the
+           device, one host sync per generation.
+``torch``  torch-eager oracle (``models/reference.py``): CPU tests / debugging.
+
+Batching: up to ``max_batch`` (≤ 64) sequences decode together ("trial
+batching") — each row has its own cache slot, position, budget
+and sampling options; rows that finish early idle until the batch ends.
+Prefill: every prompt token but the last goes through the same forward as
+≤64-row chunks (rows carry their own slot/position, so the decode attention
+kernel doubles as causal prefill attention); the last prompt token is the
+first decode step's input, so no separate prefill LM-head path exists.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+import time
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence, Union
+
+import numpy as np
+import torch
+
+from ..models.config import ModelConfig, get_config, rope_inv_freq
+from ..models.tokenizer import SyntheticTokenizer, get_tokenizer
+from ..models.weights import ModelWeights, pack_for_engine, random_weights
+
+#: Ollama's default sampling options (SURVEY §2.4 "Sampling" row)
+OLLAMA_DEFAULTS = dict(temperature=0.8, top_k=40, top_p=0.9, repeat_penalty=1.1, repeat_last_n=64, seed=None)
+
+MAX_ROWS = 64
+
+
+@dataclass
+class GenResult:
+    model: str
+    prompt_tokens: List[int]
+    tokens: List[int]
+    text: str
+    done_reason: str
+    load_duration_ns: int = 0
+    prompt_eval_duration_ns: int = 0
+    eval_duration_ns: int = 0
+    total_duration_ns: int = 0
+
+    @property
+    def prompt_eval_count(self) -> int:
+        return len(self.prompt_tokens)
+
+    @property
+    def eval_count(self) -> int:
+        return len(self.tokens)
+
+    def ollama_json(self, created_at: Optional[str] = None) -> Dict:
+        import datetime
+
+        return {
+            "model": self.model,
+            "created_at": created_at or datetime.datetime.utcnow().isoformat() + "Z",
+            "response": self.text,
+            "done": True,
+            "done_reason": self.done_reason,
+            "context": [],
+            "total_duration": self.total_duration_ns,
+            "load_duration": self.load_duration_ns,
+            "prompt_eval_count": self.prompt_eval_count,
+            "prompt_eval_duration": self.prompt_eval_duration_ns,
+            "eval_count": self.eval_count,
+            "eval_duration": self.eval_duration_ns,
+        }
+
+
+def _row_options(opts: Optional[Dict], cfg: ModelConfig, index: int, base_seed: int) -> Dict:
+    o = dict(OLLAMA_DEFAULTS)
+    if opts:
+        o.update({k: v for k, v in opts.items() if v is not None and k in OLLAMA_DEFAULTS})
+    seed = o.get("seed")
+    if seed is None:
+        seed = (base_seed * 1000003 + index * 7919 + time.monotonic_ns()) & 0xFFFFFFFFFFFF
+    return dict(temperature=float(o["temperature"]), top_p=float(o["top_p"]),
+                repeat_penalty=float(o["repeat_penalty"]), top_k=int(o["top_k"]),
+                repeat_last_n=int(o["repeat_last_n"]),
+                eos_id=int(opts.get("eos_id", cfg.eos_id)) if opts and "eos_id" in opts else int(cfg.eos_id),
+                seed=int(seed) & 0xFFFFFFFFFFFFFFFF)
+
+
+# ============================================================== ctypes structs
+class _CainLayer(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_void_p) for n in ("attn_norm", "wqkv", "bqkv", "wo", "mlp_norm", "wgu", "wdown")]
+
+
+class _CainPlanDesc(ctypes.Structure):
+    _fields_ = ([(n, ctypes.c_int) for n in ("n_layers", "d", "H", "Hkv", "hd", "ffn", "V", "act_kind", "T_max",
+                                            "Mpad", "nsplit", "waves")]
+                + [(n, ctypes.c_float) for n in ("eps", "embed_scale", "attn_scale")]
+                + [(n, ctypes.c_void_p) for n in ("embed", "final_norm", "lm_head", "layers", "kcache", "vtcache")]
+                + [("kv_layer_elems", ctypes.c_longlong)]
+                + [(n, ctypes.c_void_p) for n in ("cos_t", "sin_t", "x", "h", "qkv", "q", "attn", "act", "logits",
+                                                 "part_o", "part_ml")])
+
+
+class _CainRows(ctypes.Structure):
+    _fields_ = ([(n, ctypes.c_void_p) for n in ("tok", "pos", "slot", "n_gen", "max_new", "done", "hist", "gen")]
+                + [("ldg", ctypes.c_int), ("sample_params", ctypes.c_void_p)])
+
+
+def _ptr(t: Optional[torch.Tensor]) -> Optional[int]:
+    return None if t is None else t.data_ptr()
+
+
+def attention_splits(M: int, Hkv: int, T_max: int) -> int:
+    return int(max(1, min(T_max // 32, math.ceil(2048 / (M * Hkv)))))
+
+
+class DecodeEngine:
+    def __init__(self, model: Union[str, ModelConfig], device: Union[str, torch.device] = "cuda",
+                 max_batch: int = 16, max_context: int = 2048, seed: int = 0, backend: Optional[str] = None,
+                 steps_per_graph: int = 8, weights: Optional[ModelWeights] = None, tokenizer=None,
+                 keep_natural: bool = False):
+        self.cfg = get_config(model) if isinstance(model, str) else model
+        self.device = torch.device(device)
+        if backend is None:
+            backend = "hip" if self.device.type == "cuda" else "torch"
+        self.backend = backend
+        self.max_batch = int(min(max_batch, MAX_ROWS))
+        self.T_max = int(math.ceil(min(max_context, self.cfg.max_context) / 32) * 32)
+        self.seed = seed
+        self.steps_per_graph = max(1, int(steps_per_graph))
+        self.tokenizer = tokenizer or get_tokenizer(self.cfg)
+        self.keep_natural = keep_natural
+        t0 = time.perf_counter_ns()
+        if weights is None:
+            weights = random_weights(self.cfg, device=self.device, seed=seed)
+        self.weights = weights
+        if backend == "hip":
+            self._init_hip()
+        elif backend == "torch":
+            from ..models.reference import ReferenceModel
+            self.ref = ReferenceModel(weights)
+        else:
+            raise ValueError(f"unknown backend {backend!r}")
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+        self.load_duration_ns = time.perf_counter_ns() - t0
+        self._first_call = True
+
+    # ---------------------------------------------------------------- hip setup
+    def _init_hip(self) -> None:
+        from .. import ops
+
+        self.lib = ops.load()
+        cfg, dev = self.cfg, self.device
+        if self.device.type != "cuda":
+            raise ValueError("hip backend needs a GPU device")
+        packed = pack_for_engine(self.weights, free_natural=not self.keep_natural)
+        torch.cuda.synchronize(dev)
+        S, T, L = self.max_batch, self.T_max, cfg.n_layers
+        bf = torch.bfloat16
+        kv_layer = S * cfg.n_kv_heads * T * cfg.head_dim
+        # zero-init: positions past a row's length must hold finite values (masked P = 0 multiplies them)
+        self.kcache = torch.zeros(L * kv_layer, device=dev, dtype=bf)
+        self.vtcache = torch.zeros(L * kv_layer, device=dev, dtype=bf)
+        inv = rope_inv_freq(cfg)
+        ang = np.arange(T, dtype=np.float64)[:, None] * inv[None, :]
+        self.cos_t = torch.tensor(np.cos(ang), dtype=torch.float32, device=dev).contiguous()
+        self.sin_t = torch.tensor(np.sin(ang), dtype=torch.float32, device=dev).contiguous()
+        R = MAX_ROWS
+        z = lambda *s, dt=bf: torch.zeros(*s, device=dev, dtype=dt)  # noqa: E731
+        self.buf = dict(x=z(R, cfg.d_model), h=z(R, cfg.d_model), qkv=z(R, cfg.qkv_dim), q=z(R, cfg.q_dim),
+                        attn=z(R, cfg.q_dim), act=z(R, cfg.ffn), logits=z(R, cfg.vocab, dt=torch.float32))
+        max_ms = max(m * attention_splits(m, cfg.n_kv_heads, T) for m in range(1, R + 1))
+        self.part_o = z(max_ms * cfg.n_heads * cfg.head_dim, dt=torch.float32)
+        self.part_ml = z(max_ms * cfg.n_heads * 2, dt=torch.float32)
+        i32 = torch.int32
+        self.rows = dict(tok=z(R, dt=i32), pos=z(R, dt=i32), slot=torch.full((R,), -1, device=dev, dtype=i32),
+                         n_gen=z(R, dt=i32), max_new=z(R, dt=i32), done=z(R, dt=i32), hist=z(R * 64, dt=i32))
+        self.gen = z(R, self.T_max, dt=i32)
+        self.prefill_rows = dict(tok=z(R, dt=i32), pos=z(R, dt=i32), slot=torch.full((R,), -1, device=dev, dtype=i32))
+        from .. import ops as _ops
+        self.sample_params = _ops.sample_params_tensor(
+            [dict(temperature=0.0, top_p=1.0, repeat_penalty=1.0, top_k=1, repeat_last_n=0, eos_id=-1, seed=0)] * R,
+            dev)
+        self._layers = (_CainLayer * L)()
+        for i, lp in enumerate(packed["layers"]):
+            self._layers[i] = _CainLayer(_ptr(lp["attn_norm"]), _ptr(lp["wqkv"]), _ptr(lp["bqkv"]), _ptr(lp["wo"]),
+                                         _ptr(lp["mlp_norm"]), _ptr(lp["wgu"]), _ptr(lp["wdown"]))
+        self._packed = packed
+        d = _CainPlanDesc()
+        d.n_layers, d.d, d.H, d.Hkv, d.hd = L, cfg.d_model, cfg.n_heads, cfg.n_kv_heads, cfg.head_dim
+        d.ffn, d.V, d.act_kind, d.T_max, d.Mpad = cfg.ffn, cfg.vocab, 1 if cfg.act == "gelu_tanh" else 0, T, R
+        d.nsplit, d.waves = 1, 0
+        d.eps = cfg.norm_eps
+        d.embed_scale = float(torch.tensor(math.sqrt(cfg.d_model), dtype=bf).float()) if cfg.embed_scale else 1.0
+        d.attn_scale = 1.0 / math.sqrt(cfg.head_dim)
+        d.embed, d.final_norm, d.lm_head = _ptr(self.weights.embed), _ptr(packed["final_norm"]), _ptr(packed["lm_head"])
+        d.layers = ctypes.cast(self._layers, ctypes.c_void_p).value
+        d.kcache, d.vtcache, d.kv_layer_elems = _ptr(self.kcache), _ptr(self.vtcache), kv_layer
+        d.cos_t, d.sin_t = _ptr(self.cos_t), _ptr(self.sin_t)
+        for k in ("x", "h", "qkv", "q", "attn", "act", "logits"):
+            setattr(d, k, _ptr(self.buf[k]))
+        d.part_o, d.part_ml = _ptr(self.part_o), _ptr(self.part_ml)
+        self._desc = d
+        self._plans: Dict[int, int] = {}
+        self._graphs: Dict[tuple, int] = {}
+        self.stream = torch.cuda.Stream(device=dev)
+
+    def _plan(self, M: int) -> int:
+        """One native plan per attention split count (nsplit depends on the row count)."""
+        ns = attention_splits(M, self.cfg.n_kv_heads, self.T_max)
+        if ns not in self._plans:
+            self._desc.nsplit = ns
+            self._plans[ns] = self.lib.cain_plan_create(ctypes.byref(self._desc))
+        return self._plans[ns]
+
+    def _rows_struct(self, rows: Dict[str, torch.Tensor], with_sampling: bool) -> _CainRows:
+        r = _CainRows()
+        r.tok, r.pos, r.slot = _ptr(rows["tok"]), _ptr(rows["pos"]), _ptr(rows["slot"])
+        if with_sampling:
+            r.n_gen, r.max_new, r.done = _ptr(rows["n_gen"]), _ptr(rows["max_new"]), _ptr(rows["done"])
+            r.hist, r.gen, r.ldg = _ptr(rows["hist"]), _ptr(self.gen), self.gen.stride(0)
+            r.sample_params = _ptr(self.sample_params)
+        return r
+
+    def _forward(self, M: int, rows, want_logits: bool, want_sample: bool) -> None:
+        rs = self._rows_struct(rows, want_sample)
+        rc = self.lib.cain_plan_forward(ctypes.c_void_p(self._plan(M)), M, ctypes.byref(rs), int(want_logits),
+                                        int(want_sample), ctypes.c_void_p(self.stream.cuda_stream))
+        if rc != 0:
+            raise RuntimeError(f"cain_plan_forward failed rc={rc}")
+
+    def _graph(self, M: int, steps: int) -> int:
+        key = (M, steps)
+        g = self._graphs.get(key)
+        if g is None:
+            rs = self._rows_struct(self.rows, True)
+            err = ctypes.c_int(0)
+            g = self.lib.cain_plan_capture(ctypes.c_void_p(self._plan(M)), M, ctypes.byref(rs), steps,
+                                           ctypes.c_void_p(self.stream.cuda_stream), ctypes.byref(err))
+            if not g:
+                raise RuntimeError(f"hipGraph capture failed (err={err.value})")
+            self._graphs[key] = g
+        return g
+
+    def close(self) -> None:
+        lib = getattr(self, "lib", None)
+        if lib is None:
+            return
+        for g in self._graphs.values():
+            lib.cain_graph_destroy(ctypes.c_void_p(g))
+        for p in self._plans.values():
+            lib.cain_plan_destroy(ctypes.c_void_p(p))
+        self._graphs, self._plans = {}, {}
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---------------------------------------------------------------- generation
+    def encode(self, prompt: Union[str, Sequence[int]]) -> List[int]:
+        if isinstance(prompt, str):
+            return self.tokenizer.encode(prompt)
+        return [int(t) for t in prompt]
+
+    def generate(self, prompts: Sequence[Union[str, Sequence[int]]], num_predict: Union[int, Sequence[int]] = 128,
+                 options: Union[None, Dict, Sequence[Optional[Dict]]] = None, use_graph: bool = True
+                 ) -> List[GenResult]:
+        prompts = list(prompts)
+        B = len(prompts)
+        if B == 0:
+            return []
+        if B > self.max_batch:
+            out = []
+            for i in range(0, B, self.max_batch):
+                sl = slice(i, i + self.max_batch)
+                nps = num_predict[sl] if not isinstance(num_predict, int) else num_predict
+                ops_ = options[sl] if isinstance(options, (list, tuple)) else options
+                out += self.generate(prompts[sl], nps, ops_, use_graph)
+            return out
+        ids = [self.encode(p) or [self.cfg.bos_id] for p in prompts]
+        nps = [int(num_predict)] * B if isinstance(num_predict, int) else [int(x) for x in num_predict]
+        opts = list(options) if isinstance(options, (list, tuple)) else [options] * B
+        row_opts = [_row_options(o, self.cfg, i, self.seed) for i, o in enumerate(opts)]
+        for i in range(B):
+            budget = self.T_max - len(ids[i])
+            if budget < 1:
+                raise ValueError(f"prompt of {len(ids[i])} tokens exceeds the context ({self.T_max})")
+            nps[i] = max(1, min(nps[i], budget))
+        t0 = time.perf_counter_ns()
+        if self.backend == "torch":
+            gen, t_pref, t_dec = self._generate_torch(ids, nps, row_opts)
+        else:
+            gen, t_pref, t_dec = self._generate_hip(ids, nps, row_opts, use_graph)
+        total = time.perf_counter_ns() - t0
+        load = self.load_duration_ns if self._first_call else 0
+        self._first_call = False
+        steps = max(nps)
+        out = []
+        for i in range(B):
+            toks = gen[i]
+            eos = row_opts[i]["eos_id"]
+            reason = "stop" if (eos >= 0 and toks and toks[-1] == eos) else "length"
+            out.append(GenResult(self.cfg.name, ids[i], toks, self.tokenizer.decode(toks), reason,
+                                 load_duration_ns=load, prompt_eval_duration_ns=t_pref,
+                                 eval_duration_ns=int(t_dec * len(toks) / max(1, steps)),
+                                 total_duration_ns=total + load))
+        return out
+
+    def _generate_hip(self, ids, nps, row_opts, use_graph):
+        from .. import ops
+
+        dev = self.device
+        B = len(ids)
+        with torch.cuda.stream(self.stream):
+            # ---- prefill: all prompt tokens except the last, in <=64-row chunks
+            t0 = time.perf_counter_ns()
+            self._prefill(ids)
+            # ---- decode rows
+            r = self.rows
+            r["tok"][:B].copy_(torch.tensor([p[-1] for p in ids], dtype=torch.int32))
+            r["pos"][:B].copy_(torch.tensor([len(p) - 1 for p in ids], dtype=torch.int32))
+            r["slot"][:B].copy_(torch.arange(B, dtype=torch.int32))
+            r["n_gen"][:B].zero_()
+            r["done"][:B].zero_()
+            r["max_new"][:B].copy_(torch.tensor(nps, dtype=torch.int32))
+            self.sample_params[: 32 * B].copy_(ops.sample_params_tensor(row_opts, "cpu").to(dev))
+            self.stream.synchronize()
+            t1 = time.perf_counter_ns()
+            steps = max(nps)
+            if use_graph:
+                k = self.steps_per_graph
+                g = self._graph(B, k)
+                for _ in range(steps // k):
+                    rc = self.lib.cain_graph_launch(ctypes.c_void_p(g), ctypes.c_void_p(self.stream.cuda_stream))
+                    if rc != 0:
+                        raise RuntimeError(f"hipGraphLaunch failed rc={rc}")
+                rem = steps % k
+                if rem:
+                    g1 = self._graph(B, 1)
+                    for _ in range(rem):
+                        self.lib.cain_graph_launch(ctypes.c_void_p(g1), ctypes.c_void_p(self.stream.cuda_stream))
+            else:
+                for _ in range(steps):
+                    self._forward(B, r, want_logits=True, want_sample=True)
+            n_gen = r["n_gen"][:B].cpu().tolist()
+            gen = self.gen[:B].cpu()
+            t2 = time.perf_counter_ns()
+        return [gen[i, : n_gen[i]].tolist() for i in range(B)], t1 - t0, t2 - t1
+
+    @torch.no_grad()
+    def last_logits(self, prompts: Sequence[Union[str, Sequence[int]]]) -> torch.Tensor:
+        """fp32 logits [B, V] of the next token after each prompt (numerics tests / debugging)."""
+        ids = [self.encode(p) for p in prompts]
+        B = len(ids)
+        if self.backend == "torch":
+            return torch.stack([self.ref.forward(torch.tensor([p], device=self.device))[0, -1] for p in ids])
+        assert B <= self.max_batch
+        with torch.cuda.stream(self.stream):
+            self._prefill(ids)
+            r = self.rows
+            r["tok"][:B].copy_(torch.tensor([p[-1] for p in ids], dtype=torch.int32))
+            r["pos"][:B].copy_(torch.tensor([len(p) - 1 for p in ids], dtype=torch.int32))
+            r["slot"][:B].copy_(torch.arange(B, dtype=torch.int32))
+            self._forward(B, r, want_logits=True, want_sample=False)
+            out = self.buf["logits"][:B].clone()
+            self.stream.synchronize()
+        return out
+
+    def _prefill(self, ids) -> None:
+        flat_tok, flat_pos, flat_slot = [], [], []
+        for b, p in enumerate(ids):
+            for j, t in enumerate(p[:-1]):
+                flat_tok.append(t)
+                flat_pos.append(j)
+                flat_slot.append(b)
+        pr = self.prefill_rows
+        for c in range(0, len(flat_tok), MAX_ROWS):
+            n = min(MAX_ROWS, len(flat_tok) - c)
+            pr["tok"][:n].copy_(torch.tensor(flat_tok[c:c + n], dtype=torch.int32))
+            pr["pos"][:n].copy_(torch.tensor(flat_pos[c:c + n], dtype=torch.int32))
+            pr["slot"][:n].copy_(torch.tensor(flat_slot[c:c + n], dtype=torch.int32))
+            self._forward(n, pr, want_logits=False, want_sample=False)
+
+    def _generate_torch(self, ids, nps, row_opts):
+        """Oracle backend: full recompute per step, greedy or sampled on the host."""
+        t0 = time.perf_counter_ns()
+        gens = []
+        for i, p in enumerate(ids):
+            o = row_opts[i]
+            rng = np.random.default_rng(o["seed"])
+            toks = list(p)
+            out = []
+            for _ in range(nps[i]):
+                logits = self.ref.forward(torch.tensor([toks], device=self.device))[0, -1].float().cpu()
+                nxt = sample_host(logits, out, o, rng)
+                out.append(nxt)
+                toks.append(nxt)
+                if o["eos_id"] >= 0 and nxt == o["eos_id"]:
+                    break
+            gens.append(out)
+        t1 = time.perf_counter_ns()
+        return gens, 0, t1 - t0
+
+
+def sample_host(logits: torch.Tensor, history: List[int], o: Dict, rng) -> int:
+    """Host mirror of csrc/sample.hip (same pipeline; RNG differs)."""
+    lg = logits.clone()
+    if o["repeat_penalty"] != 1.0 and o["repeat_last_n"] > 0:
+        for t in set(history[-min(o["repeat_last_n"], 64):]):
+            v = lg[t]
+            lg[t] = v / o["repeat_penalty"] if v > 0 else v * o["repeat_penalty"]
+    if o["temperature"] <= 0:
+        return int(torch.argmax(lg))
+    k = o["top_k"] if 0 < o["top_k"] <= 1024 else 1024
+    vals, idx = torch.topk(lg / o["temperature"], min(k, lg.numel()))
+    p = torch.softmax(vals.double(), 0)
+    if 0 < o["top_p"] < 1:
+        c = torch.cumsum(p, 0)
+        cut = int(torch.searchsorted(c, torch.tensor(o["top_p"], dtype=c.dtype))) + 1
+        p = p[:cut] / p[:cut].sum()
+        idx = idx[:cut]
+    return int(idx[int(rng.choice(len(p), p=p.numpy()))])

@@ -1,0 +1,89 @@
+"""Deterministic synthetic tokenizer.
+
+There is no network for real tokenizers, and weights are random, so text is
+only a carrier: what the study measures is tokens and energy.  This tokenizer
+is reversible for its own output and stable across processes:
+
+* ``encode``: whitespace/punctuation pre-split, each piece hashed (blake2b)
+  into the non-special id range; long words split into 4-character pieces
+  (≈1.3 tokens/word on English prose, close to BPE's ≈4/3 — SURVEY §6.4);
+* ``decode``: each id maps to a pronounceable synthetic piece; ids with
+  ``id % 4 != 0`` start a new word, so ≈3/4 of generated tokens are words,
+  matching the tokens-per-word ratio used to size ``num_predict``.
+
+When a real ``tokenizer.json`` is available locally, ``HFTokenizer`` wraps the
+``tokenizers`` library instead (no download is attempted).
+"""
+from __future__ import annotations
+
+import hashlib
+import math
+import re
+from typing import List, Optional
+
+_SYL_C = "bdfghklmnprstvz"
+_SYL_V = "aeiou"
+_SPLIT = re.compile(r"\w+|[^\w\s]")
+
+#: tokens per requested word used to size generations
+TOKENS_PER_WORD = 4.0 / 3.0
+
+
+def tokens_for_words(words: int) -> int:
+    return int(math.ceil(TOKENS_PER_WORD * int(words)))
+
+
+class SyntheticTokenizer:
+    n_special = 16
+
+    def __init__(self, vocab: int, bos_id: int = 1, eos_id: int = 2):
+        self.vocab = vocab
+        self.bos_id = bos_id
+        self.eos_id = eos_id
+
+    def _piece_id(self, piece: str) -> int:
+        h = int.from_bytes(hashlib.blake2b(piece.encode("utf-8"), digest_size=8).digest(), "little")
+        return self.n_special + h % (self.vocab - self.n_special)
+
+    def encode(self, text: str, add_bos: bool = True) -> List[int]:
+        ids = [self.bos_id] if add_bos else []
+        for w in _SPLIT.findall(text):
+            for i in range(0, len(w), 4):
+                ids.append(self._piece_id(w[i:i + 4].lower()))
+        return ids
+
+    def piece(self, tid: int) -> str:
+        if tid < self.n_special:
+            return ""
+        x = tid * 2654435761 & 0xFFFFFFFF
+        n = 1 + (x >> 7) % 3
+        s = "".join(_SYL_C[(x >> (3 * i)) % len(_SYL_C)] + _SYL_V[(x >> (11 + 2 * i)) % len(_SYL_V)]
+                    for i in range(n))
+        return (" " + s) if tid % 4 else s
+
+    def decode(self, ids: List[int]) -> str:
+        return "".join(self.piece(int(t)) for t in ids).lstrip()
+
+    @staticmethod
+    def count_words(text: str) -> int:
+        return len(text.split())
+
+
+class HFTokenizer:  # pragma: no cover - needs a local tokenizer.json
+    def __init__(self, path: str):
+        from tokenizers import Tokenizer
+
+        self.tok = Tokenizer.from_file(path)
+        self.vocab = self.tok.get_vocab_size()
+
+    def encode(self, text: str, add_bos: bool = True) -> List[int]:
+        return self.tok.encode(text).ids
+
+    def decode(self, ids: List[int]) -> str:
+        return self.tok.decode(list(ids))
+
+
+def get_tokenizer(cfg, path: Optional[str] = None):
+    if path:
+        return HFTokenizer(path)
+    return SyntheticTokenizer(cfg.vocab, cfg.bos_id, cfg.eos_id)

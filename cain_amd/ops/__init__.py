@@ -1,0 +1,189 @@
+"""Python bindings of the hand-written gfx950 kernels (``libcain_kernels.so``).
+
+Every op takes torch tensors living on the GPU and launches on the current
+torch stream.  There is no silent eager fallback: if the native library is
+missing or fails to load, the ops raise ``NativeOpsUnavailable`` (the engine's
+torch-eager path is a separate, explicitly selected backend used on CPU).
+
+Kernel inventory:
+
+=====================  ==========================  =============================
+op                     source                      replaces (Ollama/llama.cpp)
+=====================  ==========================  =============================
+``skinny_gemm``        csrc/gemm.hip               QKV / O / gate-up / down / LM head GEMV
+``rmsnorm``            csrc/norm.hip               RMSNorm
+``embed``              csrc/norm.hip               embedding gather (+Gemma scale)
+``rope_kv``            csrc/rope_kv.hip            RoPE + KV-cache append
+``attention``          csrc/attention.hip          decode / prefill attention (split-K)
+``sample``             csrc/sample.hip             repeat-penalty/temperature/top-k/top-p
+``Plan``               csrc/runtime.hip            per-step schedule + hipGraph replay
+=====================  ==========================  =============================
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+from pathlib import Path
+from typing import Optional
+
+import torch
+
+HERE = Path(__file__).resolve().parent
+LIB_PATH = HERE / "libcain_kernels.so"
+
+EPI_BF16, EPI_RESID, EPI_F32, EPI_SILU, EPI_GELU = 0, 1, 2, 3, 4
+
+
+class NativeOpsUnavailable(RuntimeError):
+    pass
+
+
+_lib: Optional[ctypes.CDLL] = None
+_lock = threading.Lock()
+
+vp = ctypes.c_void_p
+ci = ctypes.c_int
+cf = ctypes.c_float
+
+
+def load() -> ctypes.CDLL:
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not LIB_PATH.exists():
+            if os.environ.get("CAIN_AUTOBUILD", "1") != "0":
+                from .. import build
+                build.build_kernels()
+            if not LIB_PATH.exists():
+                raise NativeOpsUnavailable(f"{LIB_PATH} missing: run `python -m cain_amd.build`")
+        try:
+            lib = ctypes.CDLL(str(LIB_PATH))
+        except OSError as exc:
+            raise NativeOpsUnavailable(f"cannot load {LIB_PATH}: {exc}") from exc
+        lib.cain_skinny_gemm.argtypes = [vp, vp, ci, ci, ci, ci, vp, ci, vp, vp, ci, ci, ci, vp]
+        lib.cain_rmsnorm.argtypes = [vp, ci, vp, vp, ci, ci, ci, cf, vp]
+        lib.cain_embed.argtypes = [vp, vp, vp, ci, ci, ci, cf, vp]
+        lib.cain_rope_kv.argtypes = [vp, ci, vp, vp, vp, vp, vp, vp, vp, ci, ci, ci, ci, ci, vp]
+        lib.cain_attention.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, ci, ci, ci, ci, ci, ci, ci, cf, vp]
+        lib.cain_sample.argtypes = [vp, ci, ci, vp, vp, vp, ci, vp, vp, vp, vp, vp, ci, ci, vp, vp]
+        lib.cain_plan_create.restype = vp
+        lib.cain_plan_create.argtypes = [vp]
+        lib.cain_plan_destroy.argtypes = [vp]
+        lib.cain_plan_forward.argtypes = [vp, ci, vp, ci, ci, vp]
+        lib.cain_plan_capture.restype = vp
+        lib.cain_plan_capture.argtypes = [vp, ci, vp, ci, vp, ctypes.POINTER(ci)]
+        lib.cain_graph_launch.argtypes = [vp, vp]
+        lib.cain_graph_destroy.argtypes = [vp]
+        _lib = lib
+        return lib
+
+
+def available() -> bool:
+    try:
+        load()
+        return True
+    except NativeOpsUnavailable:
+        return False
+
+
+def _p(t: Optional[torch.Tensor]):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def _stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _check(rc: int, what: str) -> None:
+    if rc != 0:
+        raise RuntimeError(f"{what} failed (rc={rc})")
+
+
+def _gpu(*ts):
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise ValueError("cain_amd.ops kernels need GPU tensors")
+
+
+# ---------------------------------------------------------------- ops
+def skinny_gemm(wp: torch.Tensor, x: torch.Tensor, n: int, epi: int = EPI_BF16, bias=None, resid=None,
+                out: Optional[torch.Tensor] = None, waves: int = 0) -> torch.Tensor:
+    """y[M, n] = epi(x[M, K] @ W^T) with W packed by ``pack_mfma_a`` (gate/up interleaved for act epis)."""
+    lib = load()
+    _gpu(wp, x)
+    M, K = x.shape
+    assert x.dtype == torch.bfloat16 and x.stride(1) == 1
+    assert wp.shape[1] * 32 == K and wp.shape[0] * 16 == n, (tuple(wp.shape), K, n)
+    n_out = n // 2 if epi in (EPI_SILU, EPI_GELU) else n
+    if out is None:
+        out = torch.empty(M, n_out, device=x.device, dtype=torch.float32 if epi == EPI_F32 else torch.bfloat16)
+    if resid is not None:
+        assert resid.shape == (M, n_out)
+    rc = lib.cain_skinny_gemm(_p(wp), _p(x), x.stride(0), K, n, M, _p(out), out.stride(0), _p(bias), _p(resid),
+                              0 if resid is None else resid.stride(0), epi, waves, _stream())
+    _check(rc, "skinny_gemm")
+    return out
+
+
+def rmsnorm(x: torch.Tensor, g: torch.Tensor, eps: float, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    lib = load()
+    _gpu(x, g)
+    M, d = x.shape
+    out = torch.empty_like(x) if out is None else out
+    _check(lib.cain_rmsnorm(_p(x), x.stride(0), _p(g), _p(out), out.stride(0), M, d, eps, _stream()), "rmsnorm")
+    return out
+
+
+def embed(tok: torch.Tensor, table: torch.Tensor, scale: float = 1.0, out=None) -> torch.Tensor:
+    lib = load()
+    M = tok.shape[0]
+    d = table.shape[1]
+    out = torch.empty(M, d, device=table.device, dtype=table.dtype) if out is None else out
+    _check(lib.cain_embed(_p(tok), _p(table), _p(out), out.stride(0), M, d, scale, _stream()), "embed")
+    return out
+
+
+def rope_kv(qkv, slot, pos, cos_t, sin_t, q_out, kc, vtc, H, Hkv, hd) -> None:
+    lib = load()
+    M = qkv.shape[0]
+    T_max = kc.shape[-2]
+    _check(lib.cain_rope_kv(_p(qkv), qkv.stride(0), _p(slot), _p(pos), _p(cos_t), _p(sin_t), _p(q_out), _p(kc),
+                            _p(vtc), M, H, Hkv, hd, T_max, _stream()), "rope_kv")
+
+
+def attention(q, kc, vtc, slot, pos, H, Hkv, hd, nsplit, scale, out=None, part_o=None, part_ml=None):
+    lib = load()
+    M = q.shape[0]
+    T_max = kc.shape[-2]
+    if part_o is None:
+        part_o = torch.empty(M * H * nsplit * hd, device=q.device, dtype=torch.float32)
+        part_ml = torch.empty(M * H * nsplit * 2, device=q.device, dtype=torch.float32)
+    out = torch.empty(M, H * hd, device=q.device, dtype=torch.bfloat16) if out is None else out
+    _check(lib.cain_attention(_p(q), _p(kc), _p(vtc), _p(slot), _p(pos), _p(part_o), _p(part_ml), _p(out),
+                              out.stride(0), M, H, Hkv, hd, T_max, nsplit, scale, _stream()), "attention")
+    return out
+
+
+SAMPLE_DTYPE = [("temperature", "f4"), ("top_p", "f4"), ("repeat_penalty", "f4"), ("top_k", "i4"),
+                ("repeat_last_n", "i4"), ("eos_id", "i4"), ("seed", "u8")]
+
+
+def sample_params_tensor(rows, device) -> torch.Tensor:
+    """Pack per-row sampling options (list of dicts) into the kernel's 32-byte struct array."""
+    import numpy as np
+
+    arr = np.zeros(len(rows), dtype=np.dtype(SAMPLE_DTYPE, align=True))
+    for i, r in enumerate(rows):
+        for k, _ in SAMPLE_DTYPE:
+            arr[i][k] = r[k]
+    assert arr.dtype.itemsize == 32
+    return torch.from_numpy(arr.view(np.uint8).copy()).to(device)
+
+
+def sample(logits, tok, pos, gen, n_gen, max_new, done, hist, slot, params, T_max) -> None:
+    lib = load()
+    M, V = logits.shape[0], logits.shape[1]
+    _check(lib.cain_sample(_p(logits), logits.stride(0), V, _p(tok), _p(pos), _p(gen), gen.stride(0), _p(n_gen),
+                           _p(max_new), _p(done), _p(hist), _p(slot), T_max, M, _p(params), _stream()), "sample")

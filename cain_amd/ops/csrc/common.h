@@ -1,0 +1,39 @@
+// Shared device helpers for the cain_amd gfx950 kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef uint16_t u16x8 __attribute__((ext_vector_type(8)));
+typedef uint16_t u16x4 __attribute__((ext_vector_type(4)));
+
+#define CAIN_API extern "C" __attribute__((visibility("default")))
+
+__device__ __forceinline__ float bf2f(__bf16 v) { return static_cast<float>(v); }
+__device__ __forceinline__ __bf16 f2bf(float v) { return static_cast<__bf16>(v); }  // v_cvt_pk_bf16_f32 (RNE, NaN-safe)
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+__device__ __forceinline__ float silu_f(float g) { return g / (1.0f + __expf(-g)); }
+__device__ __forceinline__ float gelu_tanh_f(float g) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  float u = k0 * (g + k1 * g * g * g);
+  // tanh(u) = 1 - 2/(exp(2u)+1)
+  float t = 1.0f - 2.0f / (__expf(2.0f * u) + 1.0f);
+  return 0.5f * g * (1.0f + t);
+}
+
+static inline int cdiv(int a, int b) { return (a + b - 1) / b; }

@@ -1,0 +1,197 @@
+// Native decode runtime: the per-step kernel schedule of one model and its
+// hipGraph capture/replay.
+//
+// The Python engine owns every buffer (torch allocations on the GPU) and hands
+// the raw pointers over once in a PlanDesc.  `cain_plan_forward` enqueues one
+// forward over M rows (decode: one row per live sequence; prefill: one row per
+// prompt token, each with its own cache slot and position):
+//
+//   embed -> L x [rmsnorm -> QKV GEMM(+bias) -> RoPE+KV append -> attention(+combine)
+//                 -> O GEMM(+residual) -> rmsnorm -> gate/up GEMM(+act*mul)
+//                 -> down GEMM(+residual)] -> rmsnorm -> LM-head GEMM -> sample
+//
+// = 9 launches per layer.  `cain_plan_capture` records `steps` consecutive
+// decode steps into ONE hipGraph; since the sampler advances tok/pos/n_gen on
+// the device, a whole generation is a handful of graph launches with no host
+// round trip per token (graph-replay floor instead of ~290 host launches per
+// token: MI355X_MICROARCH.md rows 'boundary', 'graph-replay-floor').
+#include <vector>
+
+#include "common.h"
+
+CAIN_API int cain_skinny_gemm(const void* Wp, const void* X, int ldx, int K, int N, int M, void* Y, int ldy,
+                              const float* bias, const void* resid, int ldr, int epi, int waves, hipStream_t st);
+CAIN_API int cain_rmsnorm(const void* x, int ldx, const void* g, void* y, int ldy, int M, int d, float eps,
+                          hipStream_t st);
+CAIN_API int cain_embed(const int* tok, const void* E, void* out, int ldo, int M, int d, float scale, hipStream_t st);
+CAIN_API int cain_rope_kv(const void* qkv, int ldqkv, const int* slot, const int* pos, const float* cos_t,
+                          const float* sin_t, void* q_out, void* kc, void* vtc, int M, int H, int Hkv, int hd,
+                          int T_max, hipStream_t st);
+CAIN_API int cain_attention(const void* q, const void* kc, const void* vtc, const int* slot, const int* pos,
+                            float* part_o, float* part_ml, void* out, int ldo, int M, int H, int Hkv, int hd,
+                            int T_max, int nsplit, float scale, hipStream_t st);
+CAIN_API int cain_sample(float* logits, int ldl, int V, int* tok, int* pos, int* gen, int ldg, int* n_gen,
+                         const int* max_new, int* done, int* hist, const int* slot, int T_max, int M,
+                         const void* params, hipStream_t st);
+
+extern "C" {
+
+struct CainLayer {
+  const void* attn_norm;
+  const void* wqkv;
+  const float* bqkv;
+  const void* wo;
+  const void* mlp_norm;
+  const void* wgu;
+  const void* wdown;
+};
+
+struct CainPlanDesc {
+  int n_layers, d, H, Hkv, hd, ffn, V, act_kind, T_max, Mpad, nsplit, waves;
+  float eps, embed_scale, attn_scale;
+  const void* embed;
+  const void* final_norm;
+  const void* lm_head;
+  const CainLayer* layers;
+  void* kcache;  // [L][S][Hkv][T_max][hd]
+  void* vtcache; // [L][S][Hkv][hd][T_max]
+  long long kv_layer_elems;
+  const float* cos_t;
+  const float* sin_t;
+  void* x;
+  void* h;
+  void* qkv;
+  void* q;
+  void* attn;
+  void* act;
+  float* logits;
+  float* part_o;
+  float* part_ml;
+};
+
+struct CainRows {
+  int* tok;
+  int* pos;
+  int* slot;
+  // sampling state (decode rows only; may be null for prefill)
+  int* n_gen;
+  const int* max_new;
+  int* done;
+  int* hist;
+  int* gen;
+  int ldg;
+  const void* sample_params;
+};
+
+}  // extern "C"
+
+namespace {
+
+struct Plan {
+  CainPlanDesc d;
+  std::vector<CainLayer> layers;
+};
+
+#define CK(x)                     \
+  do {                            \
+    int _e = (x);                 \
+    if (_e != 0) return _e;       \
+  } while (0)
+
+int forward(const Plan& p, int M, const CainRows& r, int want_logits, int want_sample, hipStream_t st) {
+  const CainPlanDesc& d = p.d;
+  const int qkv_dim = (d.H + 2 * d.Hkv) * d.hd;
+  const int q_dim = d.H * d.hd;
+  const int epi_act = d.act_kind == 1 ? 4 : 3;
+  CK(cain_embed(r.tok, d.embed, d.x, d.d, M, d.d, d.embed_scale, st));
+  for (int l = 0; l < d.n_layers; ++l) {
+    const CainLayer& L = p.layers[l];
+    __bf16* kc = reinterpret_cast<__bf16*>(d.kcache) + (size_t)l * d.kv_layer_elems;
+    __bf16* vc = reinterpret_cast<__bf16*>(d.vtcache) + (size_t)l * d.kv_layer_elems;
+    CK(cain_rmsnorm(d.x, d.d, L.attn_norm, d.h, d.d, M, d.d, d.eps, st));
+    CK(cain_skinny_gemm(L.wqkv, d.h, d.d, d.d, qkv_dim, M, d.qkv, qkv_dim, L.bqkv, nullptr, 0, 0, d.waves, st));
+    CK(cain_rope_kv(d.qkv, qkv_dim, r.slot, r.pos, d.cos_t, d.sin_t, d.q, kc, vc, M, d.H, d.Hkv, d.hd, d.T_max, st));
+    CK(cain_attention(d.q, kc, vc, r.slot, r.pos, d.part_o, d.part_ml, d.attn, q_dim, M, d.H, d.Hkv, d.hd, d.T_max,
+                      d.nsplit, d.attn_scale, st));
+    CK(cain_skinny_gemm(L.wo, d.attn, q_dim, q_dim, d.d, M, d.x, d.d, nullptr, d.x, d.d, 1, d.waves, st));
+    CK(cain_rmsnorm(d.x, d.d, L.mlp_norm, d.h, d.d, M, d.d, d.eps, st));
+    CK(cain_skinny_gemm(L.wgu, d.h, d.d, d.d, 2 * d.ffn, M, d.act, d.ffn, nullptr, nullptr, 0, epi_act, d.waves, st));
+    CK(cain_skinny_gemm(L.wdown, d.act, d.ffn, d.ffn, d.d, M, d.x, d.d, nullptr, d.x, d.d, 1, d.waves, st));
+  }
+  if (want_logits) {
+    CK(cain_rmsnorm(d.x, d.d, d.final_norm, d.h, d.d, M, d.d, d.eps, st));
+    CK(cain_skinny_gemm(d.lm_head, d.h, d.d, d.d, d.V, M, d.logits, d.V, nullptr, nullptr, 0, 2, d.waves, st));
+  }
+  if (want_sample) {
+    CK(cain_sample(d.logits, d.V, d.V, r.tok, r.pos, r.gen, r.ldg, r.n_gen, r.max_new, r.done, r.hist, r.slot,
+                   d.T_max, M, r.sample_params, st));
+  }
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+CAIN_API void* cain_plan_create(const CainPlanDesc* desc) {
+  auto* p = new Plan();
+  p->d = *desc;
+  p->layers.assign(desc->layers, desc->layers + desc->n_layers);
+  p->d.layers = p->layers.data();
+  return p;
+}
+
+CAIN_API void cain_plan_destroy(void* plan) { delete static_cast<Plan*>(plan); }
+
+CAIN_API int cain_plan_forward(void* plan, int M, const CainRows* rows, int want_logits, int want_sample,
+                               hipStream_t st) {
+  auto* p = static_cast<Plan*>(plan);
+  if (M < 1 || M > 64 || M > p->d.Mpad) return -1;
+  return forward(*p, M, *rows, want_logits, want_sample, st);
+}
+
+// Record `steps` decode steps over M rows into a graph; returns the executable graph (or null).
+CAIN_API void* cain_plan_capture(void* plan, int M, const CainRows* rows, int steps, hipStream_t st, int* err) {
+  auto* p = static_cast<Plan*>(plan);
+  *err = 0;
+  if (M < 1 || M > 64 || M > p->d.Mpad || steps < 1) {
+    *err = -1;
+    return nullptr;
+  }
+  hipGraph_t g = nullptr;
+  hipError_t e = hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal);
+  if (e != hipSuccess) {
+    *err = int(e);
+    return nullptr;
+  }
+  int fe = 0;
+  for (int s = 0; s < steps && fe == 0; ++s) fe = forward(*p, M, *rows, 1, 1, st);
+  e = hipStreamEndCapture(st, &g);
+  if (fe != 0 || e != hipSuccess) {
+    *err = fe ? fe : int(e);
+    if (g) (void)hipGraphDestroy(g);
+    return nullptr;
+  }
+  hipGraphExec_t ex = nullptr;
+  e = hipGraphInstantiate(&ex, g, nullptr, nullptr, 0);
+  (void)hipGraphDestroy(g);
+  if (e != hipSuccess) {
+    *err = int(e);
+    return nullptr;
+  }
+  return ex;
+}
+
+CAIN_API int cain_graph_launch(void* exec, hipStream_t st) {
+  return int(hipGraphLaunch(static_cast<hipGraphExec_t>(exec), st));
+}
+
+CAIN_API void cain_graph_destroy(void* exec) {
+  if (exec) (void)hipGraphExecDestroy(static_cast<hipGraphExec_t>(exec));
+}
+
+CAIN_API int cain_rows_size() { return int(sizeof(CainRows)); }
+CAIN_API int cain_plan_desc_size() { return int(sizeof(CainPlanDesc)); }
+CAIN_API int cain_layer_size() { return int(sizeof(CainLayer)); }
+
+}  // extern "C"

@@ -1,0 +1,207 @@
+"""Numerics of every HIP kernel against a plain PyTorch fp32 reference.
+
+Shapes cover the study's variants: head_dim 96/128/256, GQA groups 1/4/6/7/8,
+M = 1..64 rows, gate/up SiLU and GeLU-tanh epilogues, QKV bias, residual add.
+"""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+if not torch.cuda.is_available():  # pragma: no cover
+    pytest.skip("needs a GPU", allow_module_level=True)
+
+from cain_amd import ops  # noqa: E402
+from cain_amd.models.weights import interleave_tiles, pack_mfma_a  # noqa: E402
+
+DEV = torch.device("cuda")
+
+
+def rel_err(a, b):
+    a, b = a.float(), b.float()
+    return float((a - b).norm() / (b.norm() + 1e-12))
+
+
+@pytest.mark.parametrize("M", [1, 5, 16, 17, 33, 64])
+@pytest.mark.parametrize("N,K", [(512, 256), (6144, 4096), (1024, 14336)])
+def test_skinny_gemm_plain_bias(M, N, K):
+    torch.manual_seed(0)
+    W = (torch.randn(N, K, device=DEV) * 0.02).bfloat16()
+    x = torch.randn(M, K, device=DEV).bfloat16()
+    bias = torch.randn(N, device=DEV)
+    y = ops.skinny_gemm(pack_mfma_a(W), x, N, ops.EPI_BF16, bias=bias)
+    ref = x.float() @ W.float().t() + bias
+    assert rel_err(y, ref) < 1e-2
+
+
+@pytest.mark.parametrize("M", [1, 8, 32])
+def test_skinny_gemm_resid_inplace(M):
+    torch.manual_seed(1)
+    N, K = 2048, 4096
+    W = (torch.randn(N, K, device=DEV) * 0.02).bfloat16()
+    x = torch.randn(M, K, device=DEV).bfloat16()
+    r = torch.randn(M, N, device=DEV).bfloat16()
+    ref = x.float() @ W.float().t() + r.float()
+    ops.skinny_gemm(pack_mfma_a(W), x, N, ops.EPI_RESID, resid=r, out=r)
+    assert rel_err(r, ref) < 1e-2
+
+
+def test_skinny_gemm_f32_logits():
+    torch.manual_seed(2)
+    N, K, M = 32064, 3072, 3
+    W = (torch.randn(N, K, device=DEV) * 0.02).bfloat16()
+    x = torch.randn(M, K, device=DEV).bfloat16()
+    y = ops.skinny_gemm(pack_mfma_a(W), x, N, ops.EPI_F32)
+    assert y.dtype == torch.float32
+    assert rel_err(y, x.float() @ W.float().t()) < 1e-3
+
+
+@pytest.mark.parametrize("act", ["silu", "gelu"])
+@pytest.mark.parametrize("M", [1, 16, 40])
+def test_skinny_gemm_gateup(act, M):
+    torch.manual_seed(3)
+    F, K = 1536, 1024
+    Wg = (torch.randn(F, K, device=DEV) * 0.03).bfloat16()
+    Wu = (torch.randn(F, K, device=DEV) * 0.03).bfloat16()
+    x = torch.randn(M, K, device=DEV).bfloat16()
+    epi = ops.EPI_SILU if act == "silu" else ops.EPI_GELU
+    y = ops.skinny_gemm(pack_mfma_a(interleave_tiles(Wg, Wu)), x, 2 * F, epi)
+    g = x.float() @ Wg.float().t()
+    u = x.float() @ Wu.float().t()
+    a = torch.nn.functional.silu(g) if act == "silu" else torch.nn.functional.gelu(g, approximate="tanh")
+    assert y.shape == (M, F)
+    assert rel_err(y, a * u) < 1.5e-2
+
+
+@pytest.mark.parametrize("d", [1536, 2048, 3584, 4096])
+def test_rmsnorm(d):
+    x = torch.randn(7, d, device=DEV).bfloat16()
+    g = (1 + 0.1 * torch.randn(d, device=DEV)).bfloat16()
+    y = ops.rmsnorm(x, g, 1e-6)
+    xf = x.float()
+    ref = xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + 1e-6) * g.float()
+    assert rel_err(y, ref) < 1e-2
+
+
+def test_embed_scale():
+    E = torch.randn(1000, 2048, device=DEV).bfloat16()
+    tok = torch.tensor([3, 999, 0, 3], device=DEV, dtype=torch.int32)
+    y = ops.embed(tok, E, 45.25)
+    assert rel_err(y, E[tok.long()].float() * 45.25) < 1e-2
+
+
+def _attn_ref(q, K, V, L, G):
+    # q [H, hd], K/V [L, hd] per kv head list
+    H, hd = q.shape
+    out = torch.empty(H, hd, device=q.device)
+    for h in range(H):
+        kh = h // G
+        s = (q[h].float() @ K[kh][:L].float().t()) / math.sqrt(hd)
+        p = s.softmax(-1)
+        out[h] = p @ V[kh][:L].float()
+    return out
+
+
+@pytest.mark.parametrize("H,Hkv,hd", [(32, 8, 128), (12, 2, 128), (8, 1, 256), (32, 32, 96), (28, 4, 128),
+                                      (16, 16, 256)])
+@pytest.mark.parametrize("lengths", [[1], [37, 130, 1, 600], [2048]])
+def test_rope_kv_and_attention(H, Hkv, hd, lengths):
+    torch.manual_seed(4)
+    T_max, S = 2048, len(lengths)
+    M = len(lengths)
+    qkv_dim = (H + 2 * Hkv) * hd
+    kc = torch.zeros(S, Hkv, T_max, hd, device=DEV).bfloat16()
+    vt = torch.zeros(S, Hkv, hd, T_max, device=DEV).bfloat16()
+    # fill cache history directly
+    Kf = torch.randn(S, Hkv, T_max, hd, device=DEV).bfloat16()
+    Vf = torch.randn(S, Hkv, T_max, hd, device=DEV).bfloat16()
+    for s, L in enumerate(lengths):
+        kc[s, :, : L - 1] = Kf[s, :, : L - 1]
+        vt[s, :, :, : L - 1] = Vf[s, :, : L - 1].transpose(-1, -2)
+    qkv = torch.randn(M, qkv_dim, device=DEV).bfloat16()
+    slot = torch.arange(M, device=DEV, dtype=torch.int32)
+    pos = torch.tensor([L - 1 for L in lengths], device=DEV, dtype=torch.int32)
+    inv = 1.0 / (10000 ** (torch.arange(0, hd, 2, dtype=torch.float64) / hd))
+    ang = torch.arange(T_max, dtype=torch.float64)[:, None] * inv[None]
+    cos_t, sin_t = ang.cos().float().to(DEV), ang.sin().float().to(DEV)
+    q = torch.empty(M, H * hd, device=DEV).bfloat16()
+    ops.rope_kv(qkv, slot, pos, cos_t, sin_t, q, kc, vt, H, Hkv, hd)
+    # reference rope
+    half = hd // 2
+    for m, L in enumerate(lengths):
+        p = L - 1
+        c, s_ = cos_t[p], sin_t[p]
+        row = qkv[m].float()
+        qh = row[: H * hd].view(H, hd)
+        kh = row[H * hd:(H + Hkv) * hd].view(Hkv, hd)
+        vh = row[(H + Hkv) * hd:].view(Hkv, hd)
+        rot = lambda x: torch.cat([x[:, :half] * c - x[:, half:] * s_, x[:, half:] * c + x[:, :half] * s_], -1)  # noqa
+        assert rel_err(q[m].view(H, hd), rot(qh)) < 1e-2
+        assert rel_err(kc[m, :, p], rot(kh)) < 1e-2
+        assert rel_err(vt[m, :, :, p], vh) < 1e-2
+    for nsplit in (1, 7, 64):
+        out = ops.attention(q, kc, vt, slot, pos, H, Hkv, hd, nsplit, 1.0 / math.sqrt(hd))
+        for m, L in enumerate(lengths):
+            K = kc[m].float()
+            V = vt[m].float().transpose(-1, -2)
+            ref = _attn_ref(q[m].view(H, hd), K, V, L, H // Hkv)
+            assert rel_err(out[m].view(H, hd), ref) < 2e-2, (nsplit, m, L)
+
+
+def test_sample_greedy_and_topk():
+    torch.manual_seed(5)
+    M, V = 4, 151936
+    logits = torch.randn(M, V, device=DEV)
+    logits[0, 1234] = 50.0
+    logits[1, 77] = 50.0
+    tok = torch.zeros(M, device=DEV, dtype=torch.int32)
+    pos = torch.full((M,), 10, device=DEV, dtype=torch.int32)
+    gen = torch.zeros(M, 16, device=DEV, dtype=torch.int32)
+    n_gen = torch.zeros(M, device=DEV, dtype=torch.int32)
+    max_new = torch.full((M,), 8, device=DEV, dtype=torch.int32)
+    done = torch.zeros(M, device=DEV, dtype=torch.int32)
+    hist = torch.zeros(M * 64, device=DEV, dtype=torch.int32)
+    slot = torch.arange(M, device=DEV, dtype=torch.int32)
+    rows = [dict(temperature=0.0, top_p=1.0, repeat_penalty=1.0, top_k=40, repeat_last_n=64, eos_id=-1, seed=1),
+            dict(temperature=0.8, top_p=0.9, repeat_penalty=1.1, top_k=40, repeat_last_n=64, eos_id=-1, seed=2),
+            dict(temperature=1.0, top_p=1.0, repeat_penalty=1.0, top_k=1, repeat_last_n=0, eos_id=-1, seed=3),
+            dict(temperature=1.0, top_p=0.5, repeat_penalty=1.0, top_k=5, repeat_last_n=0, eos_id=-1, seed=4)]
+    params = ops.sample_params_tensor(rows, DEV)
+    ref_arg = logits.argmax(-1).cpu()
+    top5 = set(logits[3].topk(5).indices.cpu().tolist())
+    ops.sample(logits.clone(), tok, pos, gen, n_gen, max_new, done, hist, slot, params, 2048)
+    t = tok.cpu().tolist()
+    assert t[0] == 1234
+    assert t[1] == 77           # dominant logit survives temperature + top-p
+    assert t[2] == int(ref_arg[2])  # top_k = 1 is greedy
+    assert t[3] in top5
+    assert n_gen.cpu().tolist() == [1, 1, 1, 1]
+    assert pos.cpu().tolist() == [11, 11, 11, 11]
+    assert gen[:, 0].cpu().tolist() == t
+
+
+def test_sample_distribution_matches_topk_softmax():
+    """Sampling frequencies over many seeds follow softmax over the top-k (top_p off)."""
+    torch.manual_seed(6)
+    V, M = 5000, 64
+    base = torch.randn(V) * 0.1
+    base[:4] = torch.tensor([3.0, 2.5, 2.0, 1.0])
+    logits = base.to(DEV).repeat(M, 1)
+    counts = torch.zeros(4)
+    for rep in range(16):
+        tok = torch.zeros(M, device=DEV, dtype=torch.int32)
+        z = lambda: torch.zeros(M, device=DEV, dtype=torch.int32)  # noqa: E731
+        rows = [dict(temperature=1.0, top_p=1.0, repeat_penalty=1.0, top_k=3, repeat_last_n=0, eos_id=-1,
+                     seed=rep * 1000 + i) for i in range(M)]
+        ops.sample(logits.clone(), tok, z(), torch.zeros(M, 4, device=DEV, dtype=torch.int32), z(),
+                   torch.full((M,), 4, device=DEV, dtype=torch.int32), z(), torch.zeros(M * 64, device=DEV,
+                   dtype=torch.int32), torch.arange(M, device=DEV, dtype=torch.int32),
+                   ops.sample_params_tensor(rows, DEV), 2048)
+        for t in tok.cpu().tolist():
+            assert t < 3
+            counts[t] += 1
+    p = torch.softmax(torch.tensor([3.0, 2.5, 2.0]), 0)
+    freq = counts[:3] / counts.sum()
+    assert torch.allclose(freq, p, atol=0.06), (freq, p)
