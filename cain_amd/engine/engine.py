@@ -108,8 +108,8 @@ class _CainPlanDesc(ctypes.Structure):
                 + [(n, ctypes.c_float) for n in ("eps", "embed_scale", "attn_scale")]
                 + [(n, ctypes.c_void_p) for n in ("embed", "final_norm", "lm_head", "layers", "kcache", "vtcache")]
                 + [("kv_layer_elems", ctypes.c_longlong)]
-                + [(n, ctypes.c_void_p) for n in ("cos_t", "sin_t", "x", "h", "qkv", "q", "attn", "act", "logits",
-                                                 "part_o", "part_ml")])
+                + [(n, ctypes.c_void_p) for n in ("cos_t", "sin_t", "x", "q", "attn", "act", "logits",
+                                                 "part_o", "part_ml", "counters", "ss_a", "ss_b")])
 
 
 class _CainRows(ctypes.Structure):
@@ -122,7 +122,8 @@ def _ptr(t: Optional[torch.Tensor]) -> Optional[int]:
 
 
 def attention_splits(M: int, Hkv: int, T_max: int) -> int:
-    return int(max(1, min(T_max // 32, math.ceil(2048 / (M * Hkv)))))
+    """Position splits per (row, kv head): ~256 workgroups in flight, >= 4 blocks of 32 per split."""
+    return int(max(1, min(64, max(1, T_max // 128), math.ceil(256 / (M * Hkv)))))
 
 
 class DecodeEngine:
@@ -179,11 +180,14 @@ class DecodeEngine:
         self.sin_t = torch.tensor(np.sin(ang), dtype=torch.float32, device=dev).contiguous()
         R = MAX_ROWS
         z = lambda *s, dt=bf: torch.zeros(*s, device=dev, dtype=dt)  # noqa: E731
-        self.buf = dict(x=z(R, cfg.d_model), h=z(R, cfg.d_model), qkv=z(R, cfg.qkv_dim), q=z(R, cfg.q_dim),
-                        attn=z(R, cfg.q_dim), act=z(R, cfg.ffn), logits=z(R, cfg.vocab, dt=torch.float32))
+        self.buf = dict(x=z(R, cfg.d_model), q=z(R, cfg.q_dim), attn=z(R, cfg.q_dim), act=z(R, cfg.ffn),
+                        logits=z(R, cfg.vocab, dt=torch.float32), ss_a=z(R, dt=torch.float32),
+                        ss_b=z(R, dt=torch.float32), counters=z(R * cfg.n_kv_heads, dt=torch.int32))
         max_ms = max(m * attention_splits(m, cfg.n_kv_heads, T) for m in range(1, R + 1))
         self.part_o = z(max_ms * cfg.n_heads * cfg.head_dim, dt=torch.float32)
-        self.part_ml = z(max_ms * cfg.n_heads * 2, dt=torch.float32)
+        self.part_ml = z(max(ops.attention_ml_floats(m, cfg.n_heads, cfg.n_kv_heads,
+                                                     attention_splits(m, cfg.n_kv_heads, T))
+                             for m in range(1, R + 1)), dt=torch.float32)
         i32 = torch.int32
         self.rows = dict(tok=z(R, dt=i32), pos=z(R, dt=i32), slot=torch.full((R,), -1, device=dev, dtype=i32),
                          n_gen=z(R, dt=i32), max_new=z(R, dt=i32), done=z(R, dt=i32), hist=z(R * 64, dt=i32))
@@ -209,7 +213,7 @@ class DecodeEngine:
         d.layers = ctypes.cast(self._layers, ctypes.c_void_p).value
         d.kcache, d.vtcache, d.kv_layer_elems = _ptr(self.kcache), _ptr(self.vtcache), kv_layer
         d.cos_t, d.sin_t = _ptr(self.cos_t), _ptr(self.sin_t)
-        for k in ("x", "h", "qkv", "q", "attn", "act", "logits"):
+        for k in ("x", "q", "attn", "act", "logits", "ss_a", "ss_b", "counters"):
             setattr(d, k, _ptr(self.buf[k]))
         d.part_o, d.part_ml = _ptr(self.part_o), _ptr(self.part_ml)
         self._desc = d

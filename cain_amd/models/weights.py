@@ -13,9 +13,11 @@ Two layouts:
   reduction slice ``32s..32s+31`` is element ``(t, s, l)``.  One wave
   load instruction therefore reads 1 KiB of contiguous HBM (8 full lines),
   which is what a weight-streaming GEMV wants (cdna_hip_programming.md §5
-  'GEMV / M ≤ 16' row).  Gate/up are interleaved by 16-row tiles so one
-  workgroup owns matching gate and up rows and applies the activation in its
-  epilogue.  Gemma's ``(1 + w)`` norm gain is folded into the stored gain.
+  'GEMV / M ≤ 16' row).  Gate/up are interleaved by 8-row blocks so every
+  16-row tile holds 8 gate rows and the 8 matching up rows and the GEMM applies
+  the activation in its epilogue.  Gemma's ``(1 + w)`` norm gain is folded into the stored gain.  Q/K rows
+  are permuted per head (``rope_pair_order``) so every 16-row tile holds 8
+  complete RoPE pairs and the QKV GEMM can rotate in its epilogue.
 """
 from __future__ import annotations
 
@@ -43,6 +45,25 @@ def unpack_mfma_a(p: torch.Tensor) -> torch.Tensor:
     nt, ns = p.shape[0], p.shape[1]
     t = p.reshape(nt, ns, 4, 16, 8).permute(0, 3, 1, 2, 4)  # [t, r, s, g, j]
     return t.contiguous().reshape(nt * 16, ns * 32)
+
+
+def rope_pair_order(hd: int) -> torch.Tensor:
+    """Row order inside one q/k head for the fused QKV-RoPE epilogue: 16-row tile i holds
+    rotation pairs j = 8i..8i+7 as rows [j..j+8) followed by [j+hd/2 .. j+hd/2+8)."""
+    half = hd // 2
+    idx = []
+    for i in range(hd // 16):
+        idx += list(range(8 * i, 8 * i + 8)) + list(range(half + 8 * i, half + 8 * i + 8))
+    return torch.tensor(idx, dtype=torch.long)
+
+
+def qkv_row_permutation(cfg: ModelConfig) -> torch.Tensor:
+    """Permutation of the fused QKV rows (q heads, k heads permuted per head; v unchanged)."""
+    hd = cfg.head_dim
+    per_head = rope_pair_order(hd)
+    parts = [h * hd + per_head for h in range(cfg.n_heads + cfg.n_kv_heads)]
+    parts.append(torch.arange((cfg.n_heads + cfg.n_kv_heads) * hd, cfg.qkv_dim))
+    return torch.cat(parts)
 
 
 def interleave_tiles(a: torch.Tensor, b: torch.Tensor, tile: int = 16) -> torch.Tensor:
@@ -115,15 +136,16 @@ def effective_gain(cfg: ModelConfig, w: torch.Tensor) -> torch.Tensor:
 def pack_for_engine(mw: ModelWeights, free_natural: bool = False) -> Dict[str, object]:
     """Build the decode engine's packed tensors (see module doc)."""
     cfg = mw.cfg
+    perm = qkv_row_permutation(cfg).to(mw.device)
     layers = []
     for lw in mw.layers:
         layers.append({
             "attn_norm": effective_gain(cfg, lw.attn_norm).contiguous(),
-            "wqkv": pack_mfma_a(lw.wqkv),
-            "bqkv": None if lw.bqkv is None else lw.bqkv.float().contiguous(),
+            "wqkv": pack_mfma_a(lw.wqkv[perm]),
+            "bqkv": None if lw.bqkv is None else lw.bqkv.float()[perm].contiguous(),
             "wo": pack_mfma_a(lw.wo),
             "mlp_norm": effective_gain(cfg, lw.mlp_norm).contiguous(),
-            "wgu": pack_mfma_a(interleave_tiles(lw.w_gate, lw.w_up)),
+            "wgu": pack_mfma_a(interleave_tiles(lw.w_gate, lw.w_up, tile=8)),
             "wdown": pack_mfma_a(lw.w_down),
         })
         if free_natural:

@@ -10,11 +10,12 @@ Kernel inventory:
 =====================  ==========================  =============================
 op                     source                      replaces (Ollama/llama.cpp)
 =====================  ==========================  =============================
-``skinny_gemm``        csrc/gemm.hip               QKV / O / gate-up / down / LM head GEMV
-``rmsnorm``            csrc/norm.hip               RMSNorm
-``embed``              csrc/norm.hip               embedding gather (+Gemma scale)
-``rope_kv``            csrc/rope_kv.hip            RoPE + KV-cache append
-``attention``          csrc/attention.hip          decode / prefill attention (split-K)
+``skinny_gemm``        csrc/gemm.hip               O / gate-up(+act) / down / LM head GEMV,
+                                                   fused RMSNorm prologue, residual(+sum-sq) epilogue
+``qkv_rope``           csrc/gemm.hip               QKV GEMV + bias + RoPE + KV-cache append
+``rmsnorm``            csrc/norm.hip               RMSNorm (standalone; the engine fuses it)
+``embed``              csrc/norm.hip               embedding gather (+Gemma scale, +sum-sq)
+``attention``          csrc/attention.hip          decode / prefill attention (split-K, in-kernel combine)
 ``sample``             csrc/sample.hip             repeat-penalty/temperature/top-k/top-p
 ``Plan``               csrc/runtime.hip            per-step schedule + hipGraph replay
 =====================  ==========================  =============================
@@ -32,7 +33,7 @@ import torch
 HERE = Path(__file__).resolve().parent
 LIB_PATH = HERE / "libcain_kernels.so"
 
-EPI_BF16, EPI_RESID, EPI_F32, EPI_SILU, EPI_GELU = 0, 1, 2, 3, 4
+EPI_BF16, EPI_RESID, EPI_F32, EPI_SILU, EPI_GELU, EPI_QKV_ROPE = 0, 1, 2, 3, 4, 5
 
 
 class NativeOpsUnavailable(RuntimeError):
@@ -62,11 +63,11 @@ def load() -> ctypes.CDLL:
             lib = ctypes.CDLL(str(LIB_PATH))
         except OSError as exc:
             raise NativeOpsUnavailable(f"cannot load {LIB_PATH}: {exc}") from exc
-        lib.cain_skinny_gemm.argtypes = [vp, vp, ci, ci, ci, ci, vp, ci, vp, vp, ci, ci, ci, vp]
+        lib.cain_skinny_gemm_ex.argtypes = ([vp, vp, ci, ci, ci, ci, vp, ci, vp, vp, vp, cf, vp, vp, vp, vp, vp, vp,
+                                             vp, vp] + [ci] * 6 + [vp])
         lib.cain_rmsnorm.argtypes = [vp, ci, vp, vp, ci, ci, ci, cf, vp]
-        lib.cain_embed.argtypes = [vp, vp, vp, ci, ci, ci, cf, vp]
-        lib.cain_rope_kv.argtypes = [vp, ci, vp, vp, vp, vp, vp, vp, vp, ci, ci, ci, ci, ci, vp]
-        lib.cain_attention.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, ci, ci, ci, ci, ci, ci, ci, cf, vp]
+        lib.cain_embed.argtypes = [vp, vp, vp, ci, ci, ci, cf, vp, vp]
+        lib.cain_attention.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp, ci, ci, ci, ci, ci, ci, ci, cf, vp, vp]
         lib.cain_sample.argtypes = [vp, ci, ci, vp, vp, vp, ci, vp, vp, vp, vp, vp, ci, ci, vp, vp]
         lib.cain_plan_create.restype = vp
         lib.cain_plan_create.argtypes = [vp]
@@ -108,23 +109,41 @@ def _gpu(*ts):
 
 
 # ---------------------------------------------------------------- ops
-def skinny_gemm(wp: torch.Tensor, x: torch.Tensor, n: int, epi: int = EPI_BF16, bias=None, resid=None,
-                out: Optional[torch.Tensor] = None, waves: int = 0) -> torch.Tensor:
-    """y[M, n] = epi(x[M, K] @ W^T) with W packed by ``pack_mfma_a`` (gate/up interleaved for act epis)."""
+def skinny_gemm(wp: torch.Tensor, x: torch.Tensor, n: int, epi: int = EPI_BF16, bias=None,
+                out: Optional[torch.Tensor] = None, waves: int = 0, ss_in=None, gain=None, eps: float = 1e-6,
+                ss_out=None, ss_zero=None) -> torch.Tensor:
+    """y[M, n] = epi(B(x)[M, K] @ W^T) with W packed by ``pack_mfma_a`` (gate/up interleaved for act epis).
+
+    ``ss_in``/``gain``: fused RMSNorm prologue (B = x * rsqrt(ss_in/K + eps) * gain).
+    ``EPI_RESID``: ``out`` is the residual stream, updated in place; ``ss_out`` accumulates sum(y^2).
+    """
     lib = load()
     _gpu(wp, x)
     M, K = x.shape
     assert x.dtype == torch.bfloat16 and x.stride(1) == 1
     assert wp.shape[1] * 32 == K and wp.shape[0] * 16 == n, (tuple(wp.shape), K, n)
     n_out = n // 2 if epi in (EPI_SILU, EPI_GELU) else n
+    if epi == EPI_RESID:
+        assert out is not None and out.shape == (M, n_out), "EPI_RESID updates `out` (the residual) in place"
     if out is None:
         out = torch.empty(M, n_out, device=x.device, dtype=torch.float32 if epi == EPI_F32 else torch.bfloat16)
-    if resid is not None:
-        assert resid.shape == (M, n_out)
-    rc = lib.cain_skinny_gemm(_p(wp), _p(x), x.stride(0), K, n, M, _p(out), out.stride(0), _p(bias), _p(resid),
-                              0 if resid is None else resid.stride(0), epi, waves, _stream())
+    rc = lib.cain_skinny_gemm_ex(_p(wp), _p(x), x.stride(0), K, n, M, _p(out), out.stride(0), _p(bias), _p(ss_in),
+                                 _p(gain), eps, _p(ss_out), _p(ss_zero), None, None, None, None, None, None,
+                                 0, 0, 0, 0, epi, waves, _stream())
     _check(rc, "skinny_gemm")
     return out
+
+
+def qkv_rope(wp, x, n, q_out, kc, vtc, slot, pos, cos_t, sin_t, H, Hkv, hd, bias=None, ss_in=None, gain=None,
+             eps: float = 1e-6, waves: int = 0) -> None:
+    """Fused QKV projection (+RMSNorm prologue, +bias) -> RoPE -> Q buffer / K cache / V^T cache."""
+    lib = load()
+    M, K = x.shape
+    T_max = kc.shape[-2]
+    rc = lib.cain_skinny_gemm_ex(_p(wp), _p(x), x.stride(0), K, n, M, _p(q_out), q_out.stride(0), _p(bias),
+                                 _p(ss_in), _p(gain), eps, None, None, _p(slot), _p(pos), _p(cos_t), _p(sin_t),
+                                 _p(kc), _p(vtc), H, Hkv, hd, T_max, EPI_QKV_ROPE, waves, _stream())
+    _check(rc, "qkv_rope")
 
 
 def rmsnorm(x: torch.Tensor, g: torch.Tensor, eps: float, out: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -136,33 +155,35 @@ def rmsnorm(x: torch.Tensor, g: torch.Tensor, eps: float, out: Optional[torch.Te
     return out
 
 
-def embed(tok: torch.Tensor, table: torch.Tensor, scale: float = 1.0, out=None) -> torch.Tensor:
+def embed(tok: torch.Tensor, table: torch.Tensor, scale: float = 1.0, out=None, ss_out=None) -> torch.Tensor:
     lib = load()
     M = tok.shape[0]
     d = table.shape[1]
     out = torch.empty(M, d, device=table.device, dtype=table.dtype) if out is None else out
-    _check(lib.cain_embed(_p(tok), _p(table), _p(out), out.stride(0), M, d, scale, _stream()), "embed")
+    _check(lib.cain_embed(_p(tok), _p(table), _p(out), out.stride(0), M, d, scale, _p(ss_out), _stream()), "embed")
     return out
 
 
-def rope_kv(qkv, slot, pos, cos_t, sin_t, q_out, kc, vtc, H, Hkv, hd) -> None:
-    lib = load()
-    M = qkv.shape[0]
-    T_max = kc.shape[-2]
-    _check(lib.cain_rope_kv(_p(qkv), qkv.stride(0), _p(slot), _p(pos), _p(cos_t), _p(sin_t), _p(q_out), _p(kc),
-                            _p(vtc), M, H, Hkv, hd, T_max, _stream()), "rope_kv")
+def attention_ml_floats(M: int, H: int, Hkv: int, nsplit: int) -> int:
+    """Size of the (max, sum) partial workspace: one 128-B-aligned region per (row, kv head)."""
+    G = H // Hkv
+    return M * Hkv * ((G * nsplit * 2 + 31) // 32) * 32
 
 
-def attention(q, kc, vtc, slot, pos, H, Hkv, hd, nsplit, scale, out=None, part_o=None, part_ml=None):
+def attention(q, kc, vtc, slot, pos, H, Hkv, hd, nsplit, scale, out=None, part_o=None, part_ml=None,
+              counters=None, ss_zero=None):
     lib = load()
     M = q.shape[0]
     T_max = kc.shape[-2]
     if part_o is None:
         part_o = torch.empty(M * H * nsplit * hd, device=q.device, dtype=torch.float32)
-        part_ml = torch.empty(M * H * nsplit * 2, device=q.device, dtype=torch.float32)
+        part_ml = torch.empty(attention_ml_floats(M, H, Hkv, nsplit), device=q.device, dtype=torch.float32)
+    if counters is None:
+        counters = torch.zeros(M * Hkv, device=q.device, dtype=torch.int32)
     out = torch.empty(M, H * hd, device=q.device, dtype=torch.bfloat16) if out is None else out
-    _check(lib.cain_attention(_p(q), _p(kc), _p(vtc), _p(slot), _p(pos), _p(part_o), _p(part_ml), _p(out),
-                              out.stride(0), M, H, Hkv, hd, T_max, nsplit, scale, _stream()), "attention")
+    _check(lib.cain_attention(_p(q), _p(kc), _p(vtc), _p(slot), _p(pos), _p(part_o), _p(part_ml), _p(counters),
+                              _p(out), out.stride(0), M, H, Hkv, hd, T_max, nsplit, scale, _p(ss_zero), _stream()),
+           "attention")
     return out
 
 

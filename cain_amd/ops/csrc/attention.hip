@@ -1,9 +1,9 @@
 // Decode / short-prefill attention over the KV cache, split over positions
 // (flash-decoding) with both products on MFMA (SURVEY §2.4 row "Decode attention").
 //
-// One wave handles (row m, kv head kh, split sp).  The G = H/Hkv query heads of
-// the group are the 16 MFMA columns (G <= 16 covers MHA, GQA 4/6/7/8 and MQA).
-// Per 32-position block:
+// Workgroup = 4 waves = (row m, kv head kh, split sp).  The G = H/Hkv query
+// heads of the group are the 16 MFMA columns (G <= 16 covers MHA, GQA 4/6/7/8
+// and MQA).  The split's 32-position blocks are dealt to the 4 waves.  Per block:
 //   S^T[t][g] = K[t][:] . Q[g][:]     2 tiles of v_mfma_f32_16x16x32_bf16 x hd/32
 //       A = K rows (lane: row t = l&15, 16 B of K[t][32i+8(l>>4)..]) straight from HBM,
 //       B = Q^T (lane: col g) held in registers for the whole wave;
@@ -14,27 +14,37 @@
 //       permuted k order (cdna_hip_programming.md §3 'An accumulator tile as the
 //       next MFMA's operand');
 //       A = V^T rows in that same k order: two 8-byte loads from the transposed
-//       V cache (rope_kv.hip) — so nothing is staged through LDS.
-// Each split writes an unnormalised partial (O, m, l); attn_combine merges the
-// splits (and normalises).  Split geometry is fixed at launch (hipGraph
-// friendly) while the length comes from device memory each step.
+//       V cache (written by the QKV GEMM epilogue) — nothing is staged through LDS.
+// The 4 waves merge their (m, l, O) in LDS.  With one split the workgroup
+// normalises and stores bf16 directly; otherwise each workgroup publishes an
+// unnormalised partial with write-through (sc1) stores and the LAST arriving
+// workgroup of (m, kh) merges all splits with sc1 loads (per-wave vmcnt drain ->
+// barrier -> relaxed agent ticket; no release/acquire fences, counter reset by the
+// reducer: cdna_hip_programming.md §5 'In-launch split-K reduction'), so there
+// is no separate combine launch.
+// The launch also zeroes the RMSNorm sum-of-squares buffer the QKV GEMM just
+// consumed (ss_zero), keeping the fused-norm protocol launch-ordered.
 #include "common.h"
 
 constexpr float LOG2E = 1.4426950408889634f;
+constexpr int AW = 4;  // waves per workgroup
 
 template <int HD>
-__global__ __launch_bounds__(64) void attn_decode_kernel(
+__global__ __launch_bounds__(AW * 64) void attn_decode_kernel(
     const __bf16* __restrict__ q, const __bf16* __restrict__ kc, const __bf16* __restrict__ vtc,
     const int* __restrict__ slot, const int* __restrict__ pos, float* __restrict__ part_o,
-    float* __restrict__ part_ml, int H, int Hkv, int T_max, int nsplit, float scale) {
+    float* __restrict__ part_ml, unsigned* __restrict__ counters, __bf16* __restrict__ out, int ldo, int M, int H,
+    int Hkv, int T_max, int nsplit, float scale, float* __restrict__ ss_zero) {
   constexpr int NKS = HD / 32;  // MFMAs per S tile
   constexpr int NDT = HD / 16;  // O^T d-tiles
-  const int lane = threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
   const int mk = blockIdx.x;
   const int m = mk / Hkv, kh = mk - (mk / Hkv) * Hkv;
   const int sp = blockIdx.y;
   const int G = H / Hkv;
   const int g = lane & 15, hq = lane >> 4;
+  if (ss_zero && mk == 0 && sp == 0 && threadIdx.x < M) ss_zero[threadIdx.x] = 0.f;
   const int s = slot[m];
   const int L = (s >= 0) ? pos[m] + 1 : 0;
   const int nblk = (L + 31) >> 5;
@@ -42,14 +52,12 @@ __global__ __launch_bounds__(64) void attn_decode_kernel(
   const int b0 = sp * bps;
   const int b1 = min(nblk, b0 + bps);
 
-  // partial outputs: part_o[((m*H + h)*nsplit + sp)*HD + d], part_ml[((m*H + h)*nsplit + sp)*2 + {0,1}]
   float m_run = -INFINITY, l_run = 0.f;
   f32x4 o[NDT];
 #pragma unroll
   for (int i = 0; i < NDT; ++i) o[i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  if (b0 < b1) {
-    // Q^T fragments (B operand): lane (g, hq) holds q[g][32i + 8hq .. +8]
+  if (b0 + wave < b1) {
     bf16x8 qf[NKS];
     const bool gvalid = g < G;
     const __bf16* qrow = q + ((size_t)m * H + kh * G + (gvalid ? g : 0)) * HD + hq * 8;
@@ -65,11 +73,10 @@ __global__ __launch_bounds__(64) void attn_decode_kernel(
     const float sl2 = scale * LOG2E;
     const __bf16* kbase = kc + ((size_t)s * Hkv + kh) * T_max * HD;
     const __bf16* vbase = vtc + ((size_t)s * Hkv + kh) * HD * T_max;
-    for (int blk = b0; blk < b1; ++blk) {
+    for (int blk = b0 + wave; blk < b1; blk += AW) {
       const int t0 = blk * 32;
-      // ---- S^T tiles
       f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = {0.f, 0.f, 0.f, 0.f};
-      const __bf16* k0 = kbase + (size_t)(t0 + g) * HD + hq * 8;  // A: row t = l&15
+      const __bf16* k0 = kbase + (size_t)(t0 + g) * HD + hq * 8;
       const __bf16* k1 = k0 + 16 * HD;
       bf16x8 ka[NKS], kb[NKS];
 #pragma unroll
@@ -77,7 +84,6 @@ __global__ __launch_bounds__(64) void attn_decode_kernel(
         ka[i] = *reinterpret_cast<const bf16x8*>(k0 + i * 32);
         kb[i] = *reinterpret_cast<const bf16x8*>(k1 + i * 32);
       }
-      // V^T fragments for this block (issued early, consumed after softmax)
       u16x4 va[NDT], vb[NDT];
 #pragma unroll
       for (int dt = 0; dt < NDT; ++dt) {
@@ -90,7 +96,6 @@ __global__ __launch_bounds__(64) void attn_decode_kernel(
         s0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ka[i], qf[i], s0, 0, 0, 0);
         s1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kb[i], qf[i], s1, 0, 0, 0);
       }
-      // ---- mask + online softmax (column g; this lane holds t = t0+4hq+r and t0+16+4hq+r)
       float bmax = -INFINITY;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -114,7 +119,6 @@ __global__ __launch_bounds__(64) void attn_decode_kernel(
         pf[4 + r] = f2bf(pb);
       }
       l_run = l_run * alpha + psum;
-      // ---- O^T += V^T . P^T
 #pragma unroll
       for (int dt = 0; dt < NDT; ++dt) {
         o[dt] *= alpha;
@@ -124,78 +128,127 @@ __global__ __launch_bounds__(64) void attn_decode_kernel(
           vv[j] = va[dt][j];
           vv[4 + j] = vb[dt][j];
         }
-        bf16x8 vf = __builtin_bit_cast(bf16x8, vv);
-        o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf, o[dt], 0, 0, 0);
+        o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, vv), pf, o[dt], 0, 0, 0);
       }
     }
   }
-  // l: sum the 4 lane-partials of column g
   l_run += __shfl_xor(l_run, 16, 64);
   l_run += __shfl_xor(l_run, 32, 64);
-  if (g < G) {
-    const int h = kh * G + g;
-    const size_t base = ((size_t)m * H + h) * nsplit + sp;
-    float* po = part_o + base * HD;
-#pragma unroll
-    for (int dt = 0; dt < NDT; ++dt) {
-      // lane (g, hq) holds d = dt*16 + 4hq + r
-      *reinterpret_cast<f32x4*>(po + dt * 16 + hq * 4) = o[dt];
-    }
-    if (hq == 0) {
-      part_ml[base * 2 + 0] = m_run;
-      part_ml[base * 2 + 1] = l_run;
-    }
-  }
-}
 
-// out[m][h*HD + d] = sum_s O_s * 2^(m_s - M) / sum_s l_s * 2^(m_s - M)
-template <int HD>
-__global__ __launch_bounds__(HD) void attn_combine_kernel(const float* __restrict__ part_o,
-                                                          const float* __restrict__ part_ml, __bf16* __restrict__ out,
-                                                          int ldo, int H, int nsplit, const int* __restrict__ slot) {
-  const int mh = blockIdx.x;
-  const int m = mh / H, h = mh - (mh / H) * H;
-  const int d = threadIdx.x;
-  __bf16* dst = out + (size_t)m * ldo + h * HD + d;
-  if (slot[m] < 0) {
-    *dst = f2bf(0.f);
-    return;
+  // ---- merge the 4 waves in LDS: ml[w][g] = (m, l); ob[w][d][g]
+  __shared__ float s_m[AW][16], s_l[AW][16];
+  __shared__ float s_o[AW][HD][16];
+  __shared__ unsigned s_ticket;
+  if (hq == 0) {
+    s_m[wave][g] = m_run;
+    s_l[wave][g] = l_run;
   }
-  const size_t base = (size_t)mh * nsplit;
-  float M = -INFINITY;
-  for (int sp = 0; sp < nsplit; ++sp) M = fmaxf(M, part_ml[(base + sp) * 2]);
-  float num = 0.f, den = 0.f;
-  for (int sp = 0; sp < nsplit; ++sp) {
-    float ms = part_ml[(base + sp) * 2];
-    if (ms == -INFINITY) continue;
-    float w = exp2f(ms - M);
-    den += w * part_ml[(base + sp) * 2 + 1];
-    num += w * part_o[(base + sp) * HD + d];
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) s_o[wave][dt * 16 + hq * 4 + r][g] = o[dt][r];
+  __syncthreads();
+
+  // each thread finalises (g, d) pairs of this workgroup
+  const int nout = G * HD;
+  const size_t pbase = (size_t)(m * H + kh * G) * nsplit;  // partial (head kh*G+gg, split j) = pbase + gg*nsplit + j
+  // part_ml regions of different (m, kh) never share a 128-B line (ML_STRIDE), so a
+  // reducer's L2 never holds another group's line that is still being written
+  const int mls = ((G * nsplit * 2 + 31) / 32) * 32;
+  float* pml = part_ml + (size_t)mk * mls;
+  for (int e = threadIdx.x; e < nout; e += AW * 64) {
+    const int gg = e / HD, d = e - (e / HD) * HD;
+    float Mx = -INFINITY;
+#pragma unroll
+    for (int w = 0; w < AW; ++w) Mx = fmaxf(Mx, s_m[w][gg]);
+    float lsum = 0.f, osum = 0.f;
+#pragma unroll
+    for (int w = 0; w < AW; ++w) {
+      const float mw = s_m[w][gg];
+      if (mw == -INFINITY) continue;
+      const float f = exp2f(mw - Mx);
+      lsum += f * s_l[w][gg];
+      osum += f * s_o[w][d][gg];
+    }
+    if (nsplit == 1) {
+      out[(size_t)m * ldo + (kh * G + gg) * HD + d] = f2bf(lsum > 0.f ? osum / lsum : 0.f);
+    } else {
+      // publish write-through (sc1) so the reducer needs no release/acquire fences
+      // (MI355X_MICROARCH.md 'Valid forms', first table row; cdna_hip_programming.md Guideline 16)
+      const size_t pi = pbase + (size_t)gg * nsplit + sp;
+      __hip_atomic_store(part_o + pi * HD + d, osum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (d == 0) {
+        const int li = gg * nsplit + sp;
+        __hip_atomic_store(pml + li * 2 + 0, Mx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(pml + li * 2 + 1, lsum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
   }
-  *dst = f2bf(den > 0.f ? num / den : 0.f);
+  if (nsplit == 1) return;
+
+  // ---- every storing wave drains, one lane takes a ticket; the last arriver reduces
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0)
+    s_ticket = __hip_atomic_fetch_add(counters + mk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  if (s_ticket != unsigned(nsplit - 1)) return;
+  // split weights into LDS once (sc1 loads: never served from this CU's stale L1)
+  __shared__ float s_w[16 * 64];   // [gg][j] merge weight 2^(m_j - M) / den
+  const int nw = G * nsplit;      // <= 16 * 64
+  for (int e = threadIdx.x; e < nw; e += AW * 64) {
+    const int gg = e / nsplit, j = e - (e / nsplit) * nsplit;
+    s_w[gg * 64 + j] = __hip_atomic_load(pml + e * 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_o[1][j][gg] = __hip_atomic_load(pml + e * 2 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  if (threadIdx.x < G) {
+    const int gg = threadIdx.x;
+    float Mx = -INFINITY;
+    for (int j = 0; j < nsplit; ++j) Mx = fmaxf(Mx, s_w[gg * 64 + j]);
+    float den = 0.f;
+    for (int j = 0; j < nsplit; ++j) {
+      const float mj = s_w[gg * 64 + j];
+      const float f = (mj == -INFINITY) ? 0.f : exp2f(mj - Mx);
+      s_w[gg * 64 + j] = f;
+      den += f * s_o[1][j][gg];
+    }
+    s_l[0][gg] = den > 0.f ? 1.f / den : 0.f;
+  }
+  if (threadIdx.x == 0) counters[mk] = 0u;  // ready for the next launch (launch-ordered)
+  __syncthreads();
+  for (int e = threadIdx.x; e < nout; e += AW * 64) {
+    const int gg = e / HD, d = e - (e / HD) * HD;
+    const float* po = part_o + (pbase + (size_t)gg * nsplit) * HD + d;
+    float num = 0.f;
+#pragma unroll 8
+    for (int j = 0; j < nsplit; ++j)
+      num += s_w[gg * 64 + j] * __hip_atomic_load(po + (size_t)j * HD, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    out[(size_t)m * ldo + (kh * G + gg) * HD + d] = f2bf(num * s_l[0][gg]);
+  }
 }
 
 template <int HD>
 static hipError_t launch_attn(const void* q, const void* kc, const void* vtc, const int* slot, const int* pos,
-                              float* part_o, float* part_ml, void* out, int ldo, int M, int H, int Hkv, int T_max,
-                              int nsplit, float scale, hipStream_t st) {
-  hipLaunchKernelGGL(attn_decode_kernel<HD>, dim3(M * Hkv, nsplit), dim3(64), 0, st, (const __bf16*)q,
-                     (const __bf16*)kc, (const __bf16*)vtc, slot, pos, part_o, part_ml, H, Hkv, T_max, nsplit, scale);
-  hipLaunchKernelGGL(attn_combine_kernel<HD>, dim3(M * H), dim3(HD), 0, st, part_o, part_ml, (__bf16*)out, ldo, H,
-                     nsplit, slot);
+                              float* part_o, float* part_ml, unsigned* counters, void* out, int ldo, int M, int H,
+                              int Hkv, int T_max, int nsplit, float scale, float* ss_zero, hipStream_t st) {
+  hipLaunchKernelGGL(attn_decode_kernel<HD>, dim3(M * Hkv, nsplit), dim3(AW * 64), 0, st, (const __bf16*)q,
+                     (const __bf16*)kc, (const __bf16*)vtc, slot, pos, part_o, part_ml, counters, (__bf16*)out, ldo, M,
+                     H, Hkv, T_max, nsplit, scale, ss_zero);
   return hipGetLastError();
 }
 
-// Workspace: part_o  M*H*nsplit*hd floats, part_ml M*H*nsplit*2 floats.
+// Workspace: part_o M*H*nsplit*hd floats, part_ml M*Hkv*align32(G*nsplit*2) floats, counters M*Hkv uints
+// (zeroed once; the reducer resets them).
 CAIN_API int cain_attention(const void* q, const void* kc, const void* vtc, const int* slot, const int* pos,
-                            float* part_o, float* part_ml, void* out, int ldo, int M, int H, int Hkv, int hd,
-                            int T_max, int nsplit, float scale, hipStream_t st) {
-  if (H % Hkv || H / Hkv > 16 || T_max % 32 || nsplit < 1) return -1;
+                            float* part_o, float* part_ml, unsigned* counters, void* out, int ldo, int M, int H,
+                            int Hkv, int hd, int T_max, int nsplit, float scale, float* ss_zero, hipStream_t st) {
+  if (H % Hkv || H / Hkv > 16 || T_max % 32 || nsplit < 1 || nsplit > 64 || M > 256) return -1;
   switch (hd) {
-    case 64: return int(launch_attn<64>(q, kc, vtc, slot, pos, part_o, part_ml, out, ldo, M, H, Hkv, T_max, nsplit, scale, st));
-    case 96: return int(launch_attn<96>(q, kc, vtc, slot, pos, part_o, part_ml, out, ldo, M, H, Hkv, T_max, nsplit, scale, st));
-    case 128: return int(launch_attn<128>(q, kc, vtc, slot, pos, part_o, part_ml, out, ldo, M, H, Hkv, T_max, nsplit, scale, st));
-    case 256: return int(launch_attn<256>(q, kc, vtc, slot, pos, part_o, part_ml, out, ldo, M, H, Hkv, T_max, nsplit, scale, st));
+    case 64: return int(launch_attn<64>(q, kc, vtc, slot, pos, part_o, part_ml, counters, out, ldo, M, H, Hkv, T_max, nsplit, scale, ss_zero, st));
+    case 96: return int(launch_attn<96>(q, kc, vtc, slot, pos, part_o, part_ml, counters, out, ldo, M, H, Hkv, T_max, nsplit, scale, ss_zero, st));
+    case 128: return int(launch_attn<128>(q, kc, vtc, slot, pos, part_o, part_ml, counters, out, ldo, M, H, Hkv, T_max, nsplit, scale, ss_zero, st));
+    case 256: return int(launch_attn<256>(q, kc, vtc, slot, pos, part_o, part_ml, counters, out, ldo, M, H, Hkv, T_max, nsplit, scale, ss_zero, st));
     default: return -1;
   }
 }

@@ -1,42 +1,125 @@
-// Weight-streaming skinny GEMM for decode / short prefill on gfx950 MFMA.
+// Weight-streaming skinny GEMM for decode / short prefill on gfx950 MFMA,
+// with the neighbouring elementwise ops fused into its prologue and epilogue.
 //
-//   Y[m][n] = epilogue( sum_k X[m][k] * W[n][k] )      m < M <= 16*NB,  n < N
+//   Y[m][n] = epilogue( sum_k B(X)[m][k] * W[n][k] )      m < M <= 16*NB,  n < N
 //
 // W is stored MFMA-fragment-major (cain_amd/models/weights.py pack_mfma_a):
 // Wp[(t*KS + s)*64 + lane] is the 16-byte A fragment of lane `lane` of
 // v_mfma_f32_16x16x32_bf16 for rows 16t..16t+15 and k-slice 32s..32s+31, so every
 // wave load instruction streams 1 KiB of contiguous HBM with a non-temporal hint
 // (each weight byte is read once per decode step).  The B operand is the
-// activation X[m][k] (row-major, 16 B per lane straight from L2: lane = (col m,
-// k-group g) reads X[m][32s+8g .. +8]), so neither operand goes through LDS
-// (cdna_hip_programming.md §5, 'GEMV / M <= 16' row: load straight to VGPRs,
-// deep unroll, late vmcnt).
+// activation row m (16 B per lane straight from L2: lane = (col m, k-group g)
+// reads X[m][32s+8g .. +8]); neither operand goes through LDS
+// (cdna_hip_programming.md §5, 'GEMV / M <= 16' row).
+//
+// Prologue (NORM): RMSNorm is applied to the B fragment on the fly,
+//   B = bf16( X[m][k] * rsqrt(ss[m]/K + eps) * gain[k] ),
+// where ss[m] (sum of squares of row m) was accumulated by the PREVIOUS GEMM's
+// epilogue — so no separate normalisation kernel (or its launch gap) exists.
 //
 // Parallelism: a workgroup owns NT 16-row tiles; its WAVES waves split the
-// K-slices, keep U slices of weight loads in flight each, and reduce their
-// 16x16 accumulators through LDS once at the end (no cross-workgroup split-K,
-// so no inter-workgroup hand-off).  The host picks WAVES so the grid carries
-// >= ~2k waves (256 CUs x 8).
+// K-slices and run a register double-buffered loop (the next U slices' loads
+// are in flight while the current U compute), then reduce their 16x16
+// accumulators through LDS once at the end (no cross-workgroup split-K).
+// Epilogue inputs (residual, bias, RoPE tables) are loaded before the loop.
 //
-// Epilogues (fused, SURVEY §2.4 rows QKV/O/gate-up/down/LM-head):
-//   EPI_BF16   y = bf16(acc + bias)            (QKV projection, Qwen2 bias)
-//   EPI_RESID  y = bf16(acc + resid)           (o_proj / down_proj + residual, in-place OK)
-//   EPI_F32    y = acc (fp32)                  (LM-head logits)
-//   EPI_SILU / EPI_GELU: tile pairs (gate, up) -> y = bf16(act(gate) * up)
+// Epilogues (SURVEY §2.4 rows QKV / RoPE / KV-append / O / gate-up / down / LM head):
+//   EPI_BF16      y = bf16(acc + bias)
+//   EPI_RESID_SS  y = bf16(acc + resid) (in place on the residual stream) and
+//                 ss_out[m] += sum_n y^2 (for the next layer's fused RMSNorm);
+//                 block 0 zeroes ss_zero[0..M) (the buffer the previous GEMM
+//                 consumed), keeping the double-buffered ss protocol launch-ordered
+//   EPI_F32       y = acc (fp32 LM-head logits)
+//   EPI_SILU/GELU gate/up rows interleaved by 8 inside each 16-row tile
+//                 -> y = bf16(act(gate) * up)
+//   EPI_QKV_ROPE  fused QKV epilogue: + bias, RoPE (rows pre-permuted so each
+//                 16-row tile holds 8 rotation pairs), Q -> q buffer, K -> K cache
+//                 at (slot[m], pos[m]), V -> transposed V cache.
 #include "common.h"
 
-enum { EPI_BF16 = 0, EPI_RESID = 1, EPI_F32 = 2, EPI_SILU = 3, EPI_GELU = 4 };
+enum { EPI_BF16 = 0, EPI_RESID_SS = 1, EPI_F32 = 2, EPI_SILU = 3, EPI_GELU = 4, EPI_QKV_ROPE = 5 };
 
-template <int NT, int NB, int WAVES, int U, int EPI>
-__global__ __launch_bounds__(WAVES * 64) void skinny_gemm_kernel(
-    const bf16x8* __restrict__ Wp, const __bf16* __restrict__ X, int ldx, int K, int N, int M,
-    void* __restrict__ Y, int ldy, const float* __restrict__ bias, const __bf16* __restrict__ resid, int ldr) {
+struct GemmArgs {
+  const bf16x8* Wp;
+  const __bf16* X;
+  int ldx, K, N, M;
+  void* Y;
+  int ldy;
+  const float* bias;
+  // NORM prologue
+  const float* ss_in;
+  const __bf16* gain;
+  float eps;
+  // RESID_SS
+  float* ss_out;
+  float* ss_zero;
+  // QKV_ROPE
+  const int* slot;
+  const int* pos;
+  const float* cos_t;
+  const float* sin_t;
+  __bf16* kc;
+  __bf16* vtc;
+  int H, Hkv, hd, T_max;
+};
+
+// Epilogue inputs of one (tile, column-tile, lane) unit, loaded BEFORE the main loop
+// so their latency hides under the weight stream (the residual row, bias, RoPE
+// position / tables).
+struct EpiIn {
+  bf16x4 r;      // EPI_RESID_SS: residual values
+  f32x4 b1, b2;  // bias (QKV: rows n1.. and n2..)
+  f32x4 c, sn;   // QKV: cos / sin of the 4 rotation pairs
+  int p, sl;     // QKV: position, cache slot
+};
+
+template <int NT, int NB, int EPI>
+__device__ __forceinline__ EpiIn epi_load(const GemmArgs& a, int tile0, int u) {
+  EpiIn e{};
+  const int lane = u & 63, tb = u >> 6, b = tb % NB, t = tb / NB;
+  const int m = b * 16 + (lane & 15);
+  const int nsub = (lane >> 4) * 4;
+  if (m >= a.M) return e;
+  if constexpr (EPI == EPI_RESID_SS) {
+    e.r = *reinterpret_cast<const bf16x4*>(reinterpret_cast<const __bf16*>(a.Y) + (size_t)m * a.ldy +
+                                           (tile0 + t) * 16 + nsub);
+  } else if constexpr (EPI == EPI_BF16) {
+    if (a.bias) e.b1 = *reinterpret_cast<const f32x4*>(a.bias + (tile0 + t) * 16 + nsub);
+  } else if constexpr (EPI == EPI_QKV_ROPE) {
+    const int gt = tile0 + t;
+    e.sl = a.slot[m];
+    e.p = a.pos[m];
+    if (a.bias) {
+      e.b1 = *reinterpret_cast<const f32x4*>(a.bias + gt * 16 + nsub);
+      e.b2 = *reinterpret_cast<const f32x4*>(a.bias + gt * 16 + ((nsub + 8) & 15));
+    }
+    const int tph = a.hd >> 4;
+    if (gt < (a.H + a.Hkv) * tph && (lane >> 4) < 2 && e.sl >= 0) {
+      const int half = a.hd >> 1;
+      const int j0 = (gt - (gt / tph) * tph) * 8 + nsub;
+      e.c = *reinterpret_cast<const f32x4*>(a.cos_t + (size_t)e.p * half + j0);
+      e.sn = *reinterpret_cast<const f32x4*>(a.sin_t + (size_t)e.p * half + j0);
+    }
+  }
+  return e;
+}
+
+template <int NT, int NB, int WAVES, int U, int EPI, bool NORM>
+__global__ __launch_bounds__(WAVES * 64) void skinny_gemm_kernel(const GemmArgs a) {
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
+  const int K = a.K;
   const int KS = K >> 5;
   const int tile0 = blockIdx.x * NT;
   const int s_beg = (wave * KS) / WAVES;
   const int s_end = ((wave + 1) * KS) / WAVES;
+  constexpr int UNITS = NT * NB * 64;
+  constexpr bool PRE = UNITS <= WAVES * 64;  // each wave finalises at most one 64-unit chunk
+
+  EpiIn pre{};
+  if constexpr (PRE) {
+    if (wave * 64 < UNITS) pre = epi_load<NT, NB, EPI>(a, tile0, wave * 64 + lane);
+  }
 
   f32x4 acc[NT][NB];
 #pragma unroll
@@ -46,182 +129,305 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_gemm_kernel(
 
   const bf16x8* wbase[NT];
 #pragma unroll
-  for (int t = 0; t < NT; ++t) wbase[t] = Wp + (size_t)(tile0 + t) * KS * 64 + lane;
-  // B fragment: column m = lane & 15 of column tile b, k group g = lane >> 4
+  for (int t = 0; t < NT; ++t) wbase[t] = a.Wp + (size_t)(tile0 + t) * KS * 64 + lane;
   const __bf16* xbase[NB];
+  float inv[NB];
 #pragma unroll
-  for (int b = 0; b < NB; ++b) xbase[b] = X + (size_t)(b * 16 + (lane & 15)) * ldx + ((lane >> 4) << 3);
+  for (int b = 0; b < NB; ++b) {
+    const int m = b * 16 + (lane & 15);
+    xbase[b] = a.X + (size_t)m * a.ldx + ((lane >> 4) << 3);
+    if constexpr (NORM) inv[b] = rsqrtf(a.ss_in[m] / float(K) + a.eps);
+  }
+  const __bf16* gbase = NORM ? a.gain + ((lane >> 4) << 3) : nullptr;
 
-  int s = s_beg;
-  for (; s + U <= s_end; s += U) {
-    bf16x8 a[U][NT], xb[U][NB];
+  // raw fragment loads (issued early); normalisation happens at use, after the data landed
+  auto load_w = [&](int s, int t) -> bf16x8 { return __builtin_nontemporal_load(wbase[t] + (size_t)s * 64); };
+  auto load_x = [&](int s, int b) -> bf16x8 { return *reinterpret_cast<const bf16x8*>(xbase[b] + s * 32); };
+  auto load_g = [&](int s) -> bf16x8 {
+    if constexpr (NORM) return *reinterpret_cast<const bf16x8*>(gbase + s * 32);
+    else return bf16x8{};
+  };
+  auto norm_x = [&](bf16x8 v, bf16x8 g, int b) -> bf16x8 {
+    if constexpr (NORM) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = f2bf(bf2f(f2bf(bf2f(v[j]) * inv[b])) * bf2f(g[j]));
+    }
+    return v;
+  };
+  auto compute = [&](const bf16x8 (&w)[U][NT], const bf16x8 (&x)[U][NB], const bf16x8 (&g)[U]) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
+      bf16x8 xb[NB];
 #pragma unroll
-      for (int t = 0; t < NT; ++t) a[u][t] = __builtin_nontemporal_load(wbase[t] + (size_t)(s + u) * 64);
-#pragma unroll
-      for (int b = 0; b < NB; ++b) xb[u][b] = *reinterpret_cast<const bf16x8*>(xbase[b] + (s + u) * 32);
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u)
+      for (int b = 0; b < NB; ++b) xb[b] = norm_x(x[u][b], g[u], b);
 #pragma unroll
       for (int t = 0; t < NT; ++t)
 #pragma unroll
         for (int b = 0; b < NB; ++b)
-          acc[t][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[u][t], xb[u][b], acc[t][b], 0, 0, 0);
+          acc[t][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[u][t], xb[b], acc[t][b], 0, 0, 0);
+    }
+  };
+
+  // ---- software-pipelined main loop: chunk c+1's loads are in flight while chunk c computes
+  int s = s_beg;
+  const int nfull = (s_end - s_beg) / U;
+  if (nfull > 0) {
+    bf16x8 wa[U][NT], xa[U][NB], ga[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+#pragma unroll
+      for (int t = 0; t < NT; ++t) wa[u][t] = load_w(s + u, t);
+#pragma unroll
+      for (int b = 0; b < NB; ++b) xa[u][b] = load_x(s + u, b);
+      ga[u] = load_g(s + u);
+    }
+    for (int c = 0; c < nfull; ++c) {
+      bf16x8 wn[U][NT], xn[U][NB], gn[U];
+      const int sn = s + U;
+      const bool more = c + 1 < nfull;
+      if (more) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+#pragma unroll
+          for (int t = 0; t < NT; ++t) wn[u][t] = load_w(sn + u, t);
+#pragma unroll
+          for (int b = 0; b < NB; ++b) xn[u][b] = load_x(sn + u, b);
+          gn[u] = load_g(sn + u);
+        }
+      }
+      compute(wa, xa, ga);
+      if (more) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+#pragma unroll
+          for (int t = 0; t < NT; ++t) wa[u][t] = wn[u][t];
+#pragma unroll
+          for (int b = 0; b < NB; ++b) xa[u][b] = xn[u][b];
+          ga[u] = gn[u];
+        }
+      }
+      s = sn;
+    }
   }
   for (; s < s_end; ++s) {
+    const bf16x8 g = load_g(s);
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
-      bf16x8 a = __builtin_nontemporal_load(wbase[t] + (size_t)s * 64);
+      const bf16x8 w = load_w(s, t);
 #pragma unroll
-      for (int b = 0; b < NB; ++b) {
-        bf16x8 xb = *reinterpret_cast<const bf16x8*>(xbase[b] + s * 32);
-        acc[t][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, xb, acc[t][b], 0, 0, 0);
-      }
+      for (int b = 0; b < NB; ++b)
+        acc[t][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w, norm_x(load_x(s, b), g, b), acc[t][b], 0, 0, 0);
     }
   }
 
-  // ---- cross-wave reduction through LDS: red[wave][unit][4], unit = (t*NB + b)*64 + lane
-  constexpr int UNITS = NT * NB * 64;
+  // ---- cross-wave reduction through LDS: red[wave][unit], unit = (t*NB + b)*64 + lane
   __shared__ __attribute__((aligned(16))) f32x4 red[WAVES][UNITS];
-  if (WAVES > 1) {
 #pragma unroll
-    for (int t = 0; t < NT; ++t)
+  for (int t = 0; t < NT; ++t)
 #pragma unroll
-      for (int b = 0; b < NB; ++b) red[wave][(t * NB + b) * 64 + lane] = acc[t][b];
-    __syncthreads();
+    for (int b = 0; b < NB; ++b) red[wave][(t * NB + b) * 64 + lane] = acc[t][b];
+  if constexpr (EPI == EPI_RESID_SS) {
+    if (blockIdx.x == 0 && a.ss_zero && threadIdx.x < a.M) a.ss_zero[threadIdx.x] = 0.f;
   }
+  __syncthreads();
 
-  // each thread finalises 4 consecutive n of one (t, b, lane) unit
-  constexpr int NUNITS = (EPI == EPI_SILU || EPI == EPI_GELU) ? (NT / 2) * NB * 64 : UNITS;
-  for (int u = threadIdx.x; u < NUNITS; u += WAVES * 64) {
-    const int ln = u & 63;
-    const int tb = u >> 6;  // (t * NB + b) or ((t/2) * NB + b) for gate/up
+  auto unit_sum = [&](int u) -> f32x4 {
+    f32x4 v = red[0][u];
+#pragma unroll
+    for (int w = 1; w < WAVES; ++w) v += red[w][u];
+    return v;
+  };
+
+  // whole waves walk the units (shuffles below need full waves)
+  for (int ub = wave * 64; ub < UNITS; ub += WAVES * 64) {
+    const int u = ub + lane;
+    const int tb = u >> 6;
     const int b = tb % NB;
     const int t = tb / NB;
-    const int m = b * 16 + (ln & 15);
-    const int nsub = (ln >> 4) * 4;
-    if (m >= M) continue;
+    const int m = b * 16 + (lane & 15);
+    const int nsub = (lane >> 4) * 4;
+    const bool mvalid = m < a.M;
+    const EpiIn e = (PRE && ub == wave * 64) ? pre : epi_load<NT, NB, EPI>(a, tile0, u);
     if constexpr (EPI == EPI_SILU || EPI == EPI_GELU) {
-      const int tg = 2 * t, tu = 2 * t + 1;
-      f32x4 g = {0.f, 0.f, 0.f, 0.f}, up = {0.f, 0.f, 0.f, 0.f};
-      if (WAVES > 1) {
-#pragma unroll
-        for (int w = 0; w < WAVES; ++w) {
-          g += red[w][(tg * NB + b) * 64 + ln];
-          up += red[w][(tu * NB + b) * 64 + ln];
-        }
-      } else {
-        g = acc[tg][b];
-        up = acc[tu][b];
-      }
-      const int n = ((tile0 >> 1) + t) * 16 + nsub;  // output feature index (gate/up pairs)
-      bf16x4 o;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        float a = (EPI == EPI_SILU) ? silu_f(g[i]) : gelu_tanh_f(g[i]);
-        o[i] = f2bf(a * up[i]);
-      }
-      *reinterpret_cast<bf16x4*>(reinterpret_cast<__bf16*>(Y) + (size_t)m * ldy + n) = o;
-    } else {
-      f32x4 v = {0.f, 0.f, 0.f, 0.f};
-      if (WAVES > 1) {
-#pragma unroll
-        for (int w = 0; w < WAVES; ++w) v += red[w][u];
-      } else {
-        v = acc[t][b];
-      }
-      const int n = (tile0 + t) * 16 + nsub;
-      if constexpr (EPI == EPI_F32) {
-        *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(Y) + (size_t)m * ldy + n) = v;
-      } else {
-        if constexpr (EPI == EPI_BF16) {
-          if (bias) {
-#pragma unroll
-            for (int i = 0; i < 4; ++i) v[i] += bias[n + i];
-          }
-        } else {  // EPI_RESID
-          bf16x4 r = *reinterpret_cast<const bf16x4*>(resid + (size_t)m * ldr + n);
-#pragma unroll
-          for (int i = 0; i < 4; ++i) v[i] += bf2f(r[i]);
-        }
+      // 8-row interleave: rows 0..7 of a tile are gate rows, rows 8..15 the matching up rows
+      if ((lane >> 4) < 2) {
+        const f32x4 g = unit_sum(u);
+        const f32x4 up = unit_sum(u + 32);
+        const int n = (tile0 + t) * 8 + nsub;
         bf16x4 o;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) o[i] = f2bf(v[i]);
-        *reinterpret_cast<bf16x4*>(reinterpret_cast<__bf16*>(Y) + (size_t)m * ldy + n) = o;
+        for (int i = 0; i < 4; ++i) {
+          const float av = (EPI == EPI_SILU) ? silu_f(g[i]) : gelu_tanh_f(g[i]);
+          o[i] = f2bf(av * up[i]);
+        }
+        if (mvalid) *reinterpret_cast<bf16x4*>(reinterpret_cast<__bf16*>(a.Y) + (size_t)m * a.ldy + n) = o;
+      }
+    } else if constexpr (EPI == EPI_QKV_ROPE) {
+      const int gt = tile0 + t;
+      const int tph = a.hd >> 4;  // tiles per head
+      const int qt = a.H * tph, kt = a.Hkv * tph;
+      const int sl = mvalid ? e.sl : -1;
+      if (gt < qt + kt) {
+        // rows 0..7 of the tile = pair elements j (first half), rows 8..15 = j + hd/2
+        if ((lane >> 4) < 2 && sl >= 0) {
+          const f32x4 x1 = unit_sum(u);
+          const f32x4 x2 = unit_sum(u + 32);  // partner rows +8 live in lane + 32
+          const int head = gt / tph, it = gt - (gt / tph) * tph;
+          const int half = a.hd >> 1;
+          const int j0 = it * 8 + nsub;  // first pair element of this thread
+          bf16x4 y1, y2;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            // round to bf16 first: the unfused path stores the projection in bf16 before RoPE
+            const float v1 = bf2f(f2bf(x1[i] + e.b1[i]));
+            const float v2 = bf2f(f2bf(x2[i] + e.b2[i]));
+            y1[i] = f2bf(v1 * e.c[i] - v2 * e.sn[i]);
+            y2[i] = f2bf(v2 * e.c[i] + v1 * e.sn[i]);
+          }
+          __bf16* dst;
+          if (head < a.H)
+            dst = reinterpret_cast<__bf16*>(a.Y) + (size_t)m * a.ldy + head * a.hd;
+          else
+            dst = a.kc + (((size_t)sl * a.Hkv + (head - a.H)) * a.T_max + e.p) * a.hd;
+          *reinterpret_cast<bf16x4*>(dst + j0) = y1;
+          *reinterpret_cast<bf16x4*>(dst + j0 + half) = y2;
+        }
+      } else if (sl >= 0) {
+        const f32x4 v = unit_sum(u);
+        const int vr = (gt - qt - kt) * 16 + nsub;  // row within the V block
+        const int kh = vr / a.hd, d = vr - (vr / a.hd) * a.hd;
+        __bf16* dst = a.vtc + (((size_t)sl * a.Hkv + kh) * a.hd + d) * a.T_max + e.p;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) dst[(size_t)i * a.T_max] = f2bf(v[i] + e.b1[i]);
+      }
+    } else {
+      const f32x4 v = unit_sum(u);
+      const int n = (tile0 + t) * 16 + nsub;
+      if constexpr (EPI == EPI_F32) {
+        if (mvalid) *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(a.Y) + (size_t)m * a.ldy + n) = v;
+      } else if constexpr (EPI == EPI_BF16) {
+        bf16x4 o;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) o[i] = f2bf(v[i] + e.b1[i]);
+        if (mvalid) *reinterpret_cast<bf16x4*>(reinterpret_cast<__bf16*>(a.Y) + (size_t)m * a.ldy + n) = o;
+      } else {  // EPI_RESID_SS: in-place residual update + sum of squares for the next RMSNorm
+        float ss = 0.f;
+        if (mvalid) {
+          bf16x4 o;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            o[i] = f2bf(v[i] + bf2f(e.r[i]));
+            const float f = bf2f(o[i]);
+            ss += f * f;
+          }
+          *reinterpret_cast<bf16x4*>(reinterpret_cast<__bf16*>(a.Y) + (size_t)m * a.ldy + n) = o;
+        }
+        // lanes l, l^16, l^32, l^48 share m: reduce, then one atomic per (wave, m)
+        ss += __shfl_xor(ss, 16, 64);
+        ss += __shfl_xor(ss, 32, 64);
+        if (lane < 16 && mvalid && a.ss_out) atomicAdd(a.ss_out + m, ss);
       }
     }
   }
 }
 
-template <int NT, int NB, int WAVES, int EPI>
-static hipError_t launch_t(const void* Wp, const void* X, int ldx, int K, int N, int M, void* Y, int ldy,
-                           const float* bias, const void* resid, int ldr, hipStream_t st) {
-  constexpr int U = (NB >= 4) ? 4 : 8;
-  dim3 grid(N / (16 * NT)), block(WAVES * 64);
-  hipLaunchKernelGGL((skinny_gemm_kernel<NT, NB, WAVES, U, EPI>), grid, block, 0, st,
-                     reinterpret_cast<const bf16x8*>(Wp), reinterpret_cast<const __bf16*>(X), ldx, K, N, M, Y, ldy,
-                     bias, reinterpret_cast<const __bf16*>(resid), ldr);
+template <int NT, int NB, int WAVES, int EPI, bool NORM>
+static hipError_t launch_t(const GemmArgs& a, hipStream_t st) {
+  constexpr int U = (NB >= 2) ? 2 : 4;  // x2 register sets (pipelined)
+  hipLaunchKernelGGL((skinny_gemm_kernel<NT, NB, WAVES, U, EPI, NORM>), dim3(a.N / (16 * NT)), dim3(WAVES * 64), 0, st,
+                     a);
   return hipGetLastError();
 }
 
-template <int NT, int NB, int EPI>
-static hipError_t launch_w(int waves, const void* Wp, const void* X, int ldx, int K, int N, int M, void* Y, int ldy,
-                           const float* bias, const void* resid, int ldr, hipStream_t st) {
-  switch (waves) {
-    case 4: return launch_t<NT, NB, 4, EPI>(Wp, X, ldx, K, N, M, Y, ldy, bias, resid, ldr, st);
-    case 8: return launch_t<NT, NB, 8, EPI>(Wp, X, ldx, K, N, M, Y, ldy, bias, resid, ldr, st);
-    default: return launch_t<NT, NB, 16, EPI>(Wp, X, ldx, K, N, M, Y, ldy, bias, resid, ldr, st);
+template <int NT, int NB, int EPI, bool NORM>
+static hipError_t launch_w(int waves, const GemmArgs& a, hipStream_t st) {
+  // the LDS reduction buffer is WAVES * NT * NB KiB: cap it at 64 KiB at compile time
+  constexpr int WMAX = 64 / (NT * NB);
+  if constexpr (WMAX >= 16) {
+    if (waves >= 16) return launch_t<NT, NB, 16, EPI, NORM>(a, st);
+  }
+  if constexpr (WMAX >= 8) {
+    if (waves >= 8) return launch_t<NT, NB, 8, EPI, NORM>(a, st);
+  }
+  return launch_t<NT, NB, 4, EPI, NORM>(a, st);
+}
+
+template <int NT, int EPI, bool NORM>
+static hipError_t launch_b(int nb, int waves, const GemmArgs& a, hipStream_t st) {
+  switch (nb) {
+    case 1: return launch_w<NT, 1, EPI, NORM>(waves, a, st);
+    case 2: return launch_w<NT, 2, EPI, NORM>(waves, a, st);
+    default: return launch_w<NT, 4, EPI, NORM>(waves, a, st);
   }
 }
 
-template <int NT, int EPI>
-static hipError_t launch_b(int nb, int waves, const void* Wp, const void* X, int ldx, int K, int N, int M, void* Y,
-                           int ldy, const float* bias, const void* resid, int ldr, hipStream_t st) {
-  switch (nb) {
-    case 1: return launch_w<NT, 1, EPI>(waves, Wp, X, ldx, K, N, M, Y, ldy, bias, resid, ldr, st);
-    case 2: return launch_w<NT, 2, EPI>(waves, Wp, X, ldx, K, N, M, Y, ldy, bias, resid, ldr, st);
-    default: return launch_w<NT, 4, EPI>(waves, Wp, X, ldx, K, N, M, Y, ldy, bias, resid, ldr, st);
+template <int NT, bool NORM>
+static hipError_t launch_e(int epi, int nb, int waves, const GemmArgs& a, hipStream_t st) {
+  switch (epi) {
+    case EPI_BF16: return launch_b<NT, EPI_BF16, NORM>(nb, waves, a, st);
+    case EPI_RESID_SS: return launch_b<NT, EPI_RESID_SS, NORM>(nb, waves, a, st);
+    case EPI_F32: return launch_b<NT, EPI_F32, NORM>(nb, waves, a, st);
+    case EPI_QKV_ROPE: return launch_b<NT, EPI_QKV_ROPE, NORM>(nb, waves, a, st);
+    default: return hipErrorInvalidValue;
   }
 }
 
 // Pick the number of waves per workgroup so the grid carries enough waves to
 // keep ~8 waves of weight streams per CU (256 CUs).
+// Waves per workgroup: 8 (the tuned choice on every llama3.1:8b decode shape, profiles/gemm_tune.md)
+// unless the grid is small (then 16, to keep >= ~2k waves streaming) or K is too short to give each
+// wave two pipelined chunks.
 static int pick_waves(int n_wg, int ks) {
-  int w = 4;
-  while (w < 16 && n_wg * w < 2048 && ks / (w * 2) >= 4) w *= 2;
+  int w = 8;
+  if (n_wg * w < 1024 && ks / 16 >= 8) w = 16;
+  while (w > 4 && ks / w < 8) w /= 2;
   return w;
 }
 
-// epi: 0 bf16(+bias) 1 resid 2 f32 3 silu-gateup 4 gelu-gateup.  M <= 64.
-// Returns hipError_t; -1 on unsupported shape.
-CAIN_API int cain_skinny_gemm(const void* Wp, const void* X, int ldx, int K, int N, int M, void* Y, int ldy,
-                              const float* bias, const void* resid, int ldr, int epi, int waves, hipStream_t st) {
-  if (K % 32 || N % 16 || M < 1 || M > 64) return -1;
+static int gemm_dispatch(const GemmArgs& a, int epi, int norm, int waves, hipStream_t st) {
+  if (a.K % 32 || a.N % 16 || a.M < 1 || a.M > 64) return -1;
   const bool pair = (epi == EPI_SILU || epi == EPI_GELU);
-  int nt = pair ? 2 : ((N % 32 == 0 && N >= 32 * 256) ? 2 : 1);
-  if (N % (16 * nt)) return -1;
-  int nb = M <= 16 ? 1 : (M <= 32 ? 2 : 4);
-  int n_wg = N / (16 * nt);
-  if (waves <= 0) waves = pick_waves(n_wg, K / 32);
+  const int nb = a.M <= 16 ? 1 : (a.M <= 32 ? 2 : 4);
+  // NT row tiles per wave amortise the activation (B) loads: per k-step a wave loads NT weight
+  // fragments and NB activation fragments, so NB > NT makes the L1/TA path, not HBM, the limit.
+  const int nt = (nb >= 2 && a.N % 32 == 0 && a.N / 32 >= 128) ? 2 : 1;
+  if (a.N % (16 * nt)) return -1;
+  const int n_wg = a.N / (16 * nt);
+  if (waves <= 0) waves = pick_waves(n_wg, a.K / 32);
+  while (waves > 4 && waves * nt * nb > 64) waves /= 2;  // LDS reduction buffer <= 64 KiB
+  // 16-wave groups cap registers at 128/lane: the RoPE / norm-prologue / NB=4 bodies would spill
+  if (waves > 8 && (epi == EPI_QKV_ROPE || norm || nb >= 4)) waves = 8;
   hipError_t e;
-  if (nt == 1) {
-    switch (epi) {
-      case EPI_BF16: e = launch_b<1, EPI_BF16>(nb, waves, Wp, X, ldx, K, N, M, Y, ldy, bias, resid, ldr, st); break;
-      case EPI_RESID: e = launch_b<1, EPI_RESID>(nb, waves, Wp, X, ldx, K, N, M, Y, ldy, bias, resid, ldr, st); break;
-      case EPI_F32: e = launch_b<1, EPI_F32>(nb, waves, Wp, X, ldx, K, N, M, Y, ldy, bias, resid, ldr, st); break;
-      default: return -1;
-    }
+  if (pair) {
+    if (nt == 1)
+      e = norm ? ((epi == EPI_SILU) ? launch_b<1, EPI_SILU, true>(nb, waves, a, st) : launch_b<1, EPI_GELU, true>(nb, waves, a, st))
+               : ((epi == EPI_SILU) ? launch_b<1, EPI_SILU, false>(nb, waves, a, st) : launch_b<1, EPI_GELU, false>(nb, waves, a, st));
+    else
+      e = norm ? ((epi == EPI_SILU) ? launch_b<2, EPI_SILU, true>(nb, waves, a, st) : launch_b<2, EPI_GELU, true>(nb, waves, a, st))
+               : ((epi == EPI_SILU) ? launch_b<2, EPI_SILU, false>(nb, waves, a, st) : launch_b<2, EPI_GELU, false>(nb, waves, a, st));
+  } else if (nt == 1) {
+    e = norm ? launch_e<1, true>(epi, nb, waves, a, st) : launch_e<1, false>(epi, nb, waves, a, st);
   } else {
-    switch (epi) {
-      case EPI_BF16: e = launch_b<2, EPI_BF16>(nb, waves, Wp, X, ldx, K, N, M, Y, ldy, bias, resid, ldr, st); break;
-      case EPI_RESID: e = launch_b<2, EPI_RESID>(nb, waves, Wp, X, ldx, K, N, M, Y, ldy, bias, resid, ldr, st); break;
-      case EPI_F32: e = launch_b<2, EPI_F32>(nb, waves, Wp, X, ldx, K, N, M, Y, ldy, bias, resid, ldr, st); break;
-      case EPI_SILU: e = launch_b<2, EPI_SILU>(nb, waves, Wp, X, ldx, K, N, M, Y, ldy, bias, resid, ldr, st); break;
-      case EPI_GELU: e = launch_b<2, EPI_GELU>(nb, waves, Wp, X, ldx, K, N, M, Y, ldy, bias, resid, ldr, st); break;
-      default: return -1;
-    }
+    e = norm ? launch_e<2, true>(epi, nb, waves, a, st) : launch_e<2, false>(epi, nb, waves, a, st);
   }
   return int(e);
+}
+
+// Fully general entry used by the runtime (norm prologue and/or QKV-RoPE epilogue).
+CAIN_API int cain_skinny_gemm_ex(const void* Wp, const void* X, int ldx, int K, int N, int M, void* Y, int ldy,
+                                 const float* bias, const float* ss_in, const void* gain, float eps, float* ss_out,
+                                 float* ss_zero, const int* slot, const int* pos, const float* cos_t,
+                                 const float* sin_t, void* kc, void* vtc, int H, int Hkv, int hd, int T_max, int epi,
+                                 int waves, hipStream_t st) {
+  GemmArgs a{};
+  a.Wp = reinterpret_cast<const bf16x8*>(Wp);
+  a.X = reinterpret_cast<const __bf16*>(X);
+  a.ldx = ldx, a.K = K, a.N = N, a.M = M, a.Y = Y, a.ldy = ldy, a.bias = bias;
+  a.ss_in = ss_in, a.gain = reinterpret_cast<const __bf16*>(gain), a.eps = eps;
+  a.ss_out = ss_out, a.ss_zero = ss_zero;
+  a.slot = slot, a.pos = pos, a.cos_t = cos_t, a.sin_t = sin_t;
+  a.kc = reinterpret_cast<__bf16*>(kc), a.vtc = reinterpret_cast<__bf16*>(vtc);
+  a.H = H, a.Hkv = Hkv, a.hd = hd, a.T_max = T_max;
+  if (epi == EPI_QKV_ROPE && (hd % 16 || (hd / 2) % 8)) return -1;
+  return gemm_dispatch(a, epi, ss_in != nullptr, waves, st);
 }

@@ -1,0 +1,29 @@
+"""The native libraries build for gfx950 and expose every symbol the bindings use (CPU-only check)."""
+import ctypes
+
+from cain_amd import ops
+from cain_amd.energy import native
+
+
+def test_kernel_library_loads_and_binds():
+    lib = ops.load()
+    for sym in ("cain_skinny_gemm_ex", "cain_rmsnorm", "cain_embed", "cain_attention", "cain_sample",
+                "cain_plan_create", "cain_plan_forward", "cain_plan_capture", "cain_graph_launch",
+                "cain_graph_destroy", "cain_sample_params_size", "cain_rows_size", "cain_plan_desc_size"):
+        assert hasattr(lib, sym), sym
+
+
+def test_struct_layouts_match_native():
+    from cain_amd.engine.engine import _CainLayer, _CainPlanDesc, _CainRows
+
+    lib = ops.load()
+    assert lib.cain_plan_desc_size() == ctypes.sizeof(_CainPlanDesc)
+    assert lib.cain_rows_size() == ctypes.sizeof(_CainRows)
+    assert lib.cain_layer_size() == ctypes.sizeof(_CainLayer)
+    assert lib.cain_sample_params_size() == 32
+
+
+def test_energy_library_loads_without_gpu():
+    lib = native.load()
+    assert lib.es_sample_size() == ctypes.sizeof(native.ESample)
+    assert native.init() >= 0

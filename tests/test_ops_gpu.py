@@ -14,7 +14,7 @@ if not torch.cuda.is_available():  # pragma: no cover
     pytest.skip("needs a GPU", allow_module_level=True)
 
 from cain_amd import ops  # noqa: E402
-from cain_amd.models.weights import interleave_tiles, pack_mfma_a  # noqa: E402
+from cain_amd.models.weights import interleave_tiles, pack_mfma_a, rope_pair_order  # noqa: E402
 
 DEV = torch.device("cuda")
 
@@ -37,15 +37,32 @@ def test_skinny_gemm_plain_bias(M, N, K):
 
 
 @pytest.mark.parametrize("M", [1, 8, 32])
-def test_skinny_gemm_resid_inplace(M):
+def test_skinny_gemm_resid_inplace_and_sumsq(M):
     torch.manual_seed(1)
     N, K = 2048, 4096
     W = (torch.randn(N, K, device=DEV) * 0.02).bfloat16()
     x = torch.randn(M, K, device=DEV).bfloat16()
     r = torch.randn(M, N, device=DEV).bfloat16()
     ref = x.float() @ W.float().t() + r.float()
-    ops.skinny_gemm(pack_mfma_a(W), x, N, ops.EPI_RESID, resid=r, out=r)
+    ss = torch.zeros(64, device=DEV)
+    zero_me = torch.ones(64, device=DEV)
+    ops.skinny_gemm(pack_mfma_a(W), x, N, ops.EPI_RESID, out=r, ss_out=ss, ss_zero=zero_me)
     assert rel_err(r, ref) < 1e-2
+    assert torch.allclose(ss[:M], r.float().pow(2).sum(-1), rtol=1e-3)
+    assert float(zero_me[:M].abs().sum()) == 0.0 and float(zero_me[M:].sum()) == 64 - M
+
+
+@pytest.mark.parametrize("M", [1, 16, 64])
+def test_skinny_gemm_fused_rmsnorm_prologue(M):
+    torch.manual_seed(7)
+    N, K = 1024, 3584
+    W = (torch.randn(N, K, device=DEV) * 0.02).bfloat16()
+    x = (3 * torch.randn(M, K, device=DEV)).bfloat16()
+    g = (1 + 0.2 * torch.randn(K, device=DEV)).bfloat16()
+    ss = x.float().pow(2).sum(-1)
+    y = ops.skinny_gemm(pack_mfma_a(W), x, N, ops.EPI_F32, ss_in=ss, gain=g, eps=1e-6)
+    xn = x.float() * torch.rsqrt(x.float().pow(2).mean(-1, keepdim=True) + 1e-6) * g.float()
+    assert rel_err(y, xn @ W.float().t()) < 1e-2
 
 
 def test_skinny_gemm_f32_logits():
@@ -67,7 +84,7 @@ def test_skinny_gemm_gateup(act, M):
     Wu = (torch.randn(F, K, device=DEV) * 0.03).bfloat16()
     x = torch.randn(M, K, device=DEV).bfloat16()
     epi = ops.EPI_SILU if act == "silu" else ops.EPI_GELU
-    y = ops.skinny_gemm(pack_mfma_a(interleave_tiles(Wg, Wu)), x, 2 * F, epi)
+    y = ops.skinny_gemm(pack_mfma_a(interleave_tiles(Wg, Wu, tile=8)), x, 2 * F, epi)
     g = x.float() @ Wg.float().t()
     u = x.float() @ Wu.float().t()
     a = torch.nn.functional.silu(g) if act == "silu" else torch.nn.functional.gelu(g, approximate="tanh")
@@ -85,69 +102,88 @@ def test_rmsnorm(d):
     assert rel_err(y, ref) < 1e-2
 
 
-def test_embed_scale():
+def test_embed_scale_and_sumsq():
     E = torch.randn(1000, 2048, device=DEV).bfloat16()
     tok = torch.tensor([3, 999, 0, 3], device=DEV, dtype=torch.int32)
-    y = ops.embed(tok, E, 45.25)
+    ss = torch.zeros(4, device=DEV)
+    y = ops.embed(tok, E, 45.25, ss_out=ss)
     assert rel_err(y, E[tok.long()].float() * 45.25) < 1e-2
+    assert torch.allclose(ss, y.float().pow(2).sum(-1), rtol=1e-4)
+
+
+def _rope_tables(hd, T_max, theta=10000.0):
+    inv = 1.0 / (theta ** (torch.arange(0, hd, 2, dtype=torch.float64) / hd))
+    ang = torch.arange(T_max, dtype=torch.float64)[:, None] * inv[None]
+    return ang.cos().float().to(DEV), ang.sin().float().to(DEV)
+
+
+def _rot(x, c, s_):
+    half = x.shape[-1] // 2
+    return torch.cat([x[..., :half] * c - x[..., half:] * s_, x[..., half:] * c + x[..., :half] * s_], -1)
+
+
+@pytest.mark.parametrize("H,Hkv,hd", [(32, 8, 128), (12, 2, 128), (8, 1, 256), (32, 32, 96), (28, 4, 128)])
+@pytest.mark.parametrize("M", [1, 5, 40])
+def test_fused_qkv_rope_kv_append(H, Hkv, hd, M):
+    torch.manual_seed(8)
+    K, T_max, S = 512, 256, 64
+    qkv_dim = (H + 2 * Hkv) * hd
+    W = (torch.randn(qkv_dim, K, device=DEV) * 0.05).bfloat16()
+    bias = torch.randn(qkv_dim, device=DEV)
+    x = torch.randn(M, K, device=DEV).bfloat16()
+    per = rope_pair_order(hd).to(DEV)
+    perm = torch.cat([h * hd + per for h in range(H + Hkv)] + [torch.arange((H + Hkv) * hd, qkv_dim, device=DEV)])
+    kc = torch.zeros(S, Hkv, T_max, hd, device=DEV).bfloat16()
+    vt = torch.zeros(S, Hkv, hd, T_max, device=DEV).bfloat16()
+    q = torch.zeros(M, H * hd, device=DEV).bfloat16()
+    slot = torch.randperm(S, device=DEV)[:M].int()
+    pos = torch.randint(0, T_max, (M,), device=DEV).int()
+    cos_t, sin_t = _rope_tables(hd, T_max)
+    ops.qkv_rope(pack_mfma_a(W[perm]), x, qkv_dim, q, kc, vt, slot, pos, cos_t, sin_t, H, Hkv, hd, bias=bias[perm])
+    ref = (x.float() @ W.float().t() + bias).bfloat16().float()
+    for m in range(M):
+        p, sl = int(pos[m]), int(slot[m])
+        c, s_ = cos_t[p], sin_t[p]
+        qh = ref[m, : H * hd].view(H, hd)
+        kh = ref[m, H * hd:(H + Hkv) * hd].view(Hkv, hd)
+        vh = ref[m, (H + Hkv) * hd:].view(Hkv, hd)
+        assert rel_err(q[m].view(H, hd), _rot(qh, c, s_)) < 1e-2
+        assert rel_err(kc[sl, :, p], _rot(kh, c, s_)) < 1e-2
+        assert rel_err(vt[sl, :, :, p], vh) < 1e-2
 
 
 def _attn_ref(q, K, V, L, G):
-    # q [H, hd], K/V [L, hd] per kv head list
     H, hd = q.shape
     out = torch.empty(H, hd, device=q.device)
     for h in range(H):
         kh = h // G
         s = (q[h].float() @ K[kh][:L].float().t()) / math.sqrt(hd)
-        p = s.softmax(-1)
-        out[h] = p @ V[kh][:L].float()
+        out[h] = s.softmax(-1) @ V[kh][:L].float()
     return out
 
 
 @pytest.mark.parametrize("H,Hkv,hd", [(32, 8, 128), (12, 2, 128), (8, 1, 256), (32, 32, 96), (28, 4, 128),
                                       (16, 16, 256)])
 @pytest.mark.parametrize("lengths", [[1], [37, 130, 1, 600], [2048]])
-def test_rope_kv_and_attention(H, Hkv, hd, lengths):
+def test_attention_split_combine(H, Hkv, hd, lengths):
     torch.manual_seed(4)
-    T_max, S = 2048, len(lengths)
+    T_max = 2048
     M = len(lengths)
-    qkv_dim = (H + 2 * Hkv) * hd
-    kc = torch.zeros(S, Hkv, T_max, hd, device=DEV).bfloat16()
-    vt = torch.zeros(S, Hkv, hd, T_max, device=DEV).bfloat16()
-    # fill cache history directly
-    Kf = torch.randn(S, Hkv, T_max, hd, device=DEV).bfloat16()
-    Vf = torch.randn(S, Hkv, T_max, hd, device=DEV).bfloat16()
-    for s, L in enumerate(lengths):
-        kc[s, :, : L - 1] = Kf[s, :, : L - 1]
-        vt[s, :, :, : L - 1] = Vf[s, :, : L - 1].transpose(-1, -2)
-    qkv = torch.randn(M, qkv_dim, device=DEV).bfloat16()
+    kc = torch.randn(M, Hkv, T_max, hd, device=DEV).bfloat16()
+    vt = torch.randn(M, Hkv, hd, T_max, device=DEV).bfloat16()
+    q = torch.randn(M, H * hd, device=DEV).bfloat16()
     slot = torch.arange(M, device=DEV, dtype=torch.int32)
     pos = torch.tensor([L - 1 for L in lengths], device=DEV, dtype=torch.int32)
-    inv = 1.0 / (10000 ** (torch.arange(0, hd, 2, dtype=torch.float64) / hd))
-    ang = torch.arange(T_max, dtype=torch.float64)[:, None] * inv[None]
-    cos_t, sin_t = ang.cos().float().to(DEV), ang.sin().float().to(DEV)
-    q = torch.empty(M, H * hd, device=DEV).bfloat16()
-    ops.rope_kv(qkv, slot, pos, cos_t, sin_t, q, kc, vt, H, Hkv, hd)
-    # reference rope
-    half = hd // 2
-    for m, L in enumerate(lengths):
-        p = L - 1
-        c, s_ = cos_t[p], sin_t[p]
-        row = qkv[m].float()
-        qh = row[: H * hd].view(H, hd)
-        kh = row[H * hd:(H + Hkv) * hd].view(Hkv, hd)
-        vh = row[(H + Hkv) * hd:].view(Hkv, hd)
-        rot = lambda x: torch.cat([x[:, :half] * c - x[:, half:] * s_, x[:, half:] * c + x[:, :half] * s_], -1)  # noqa
-        assert rel_err(q[m].view(H, hd), rot(qh)) < 1e-2
-        assert rel_err(kc[m, :, p], rot(kh)) < 1e-2
-        assert rel_err(vt[m, :, :, p], vh) < 1e-2
-    for nsplit in (1, 7, 64):
-        out = ops.attention(q, kc, vt, slot, pos, H, Hkv, hd, nsplit, 1.0 / math.sqrt(hd))
+    counters = torch.zeros(M * Hkv, device=DEV, dtype=torch.int32)
+    ss = torch.ones(8, device=DEV)
+    for nsplit in (1, 3, 16, 64, 16):  # repeated nsplit: the in-kernel counters must reset
+        out = ops.attention(q, kc, vt, slot, pos, H, Hkv, hd, nsplit, 1.0 / math.sqrt(hd), counters=counters,
+                            ss_zero=ss)
         for m, L in enumerate(lengths):
-            K = kc[m].float()
-            V = vt[m].float().transpose(-1, -2)
-            ref = _attn_ref(q[m].view(H, hd), K, V, L, H // Hkv)
+            ref = _attn_ref(q[m].view(H, hd), kc[m].float(), vt[m].float().transpose(-1, -2), L, H // Hkv)
             assert rel_err(out[m].view(H, hd), ref) < 2e-2, (nsplit, m, L)
+        assert int(counters.abs().sum()) == 0
+    assert float(ss[:M].sum()) == 0.0
 
 
 def test_sample_greedy_and_topk():
