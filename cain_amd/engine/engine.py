@@ -109,7 +109,7 @@ class _CainPlanDesc(ctypes.Structure):
                 + [(n, ctypes.c_void_p) for n in ("embed", "final_norm", "lm_head", "layers", "kcache", "vtcache")]
                 + [("kv_layer_elems", ctypes.c_longlong)]
                 + [(n, ctypes.c_void_p) for n in ("cos_t", "sin_t", "x", "q", "attn", "act", "logits",
-                                                 "part_o", "part_ml", "counters", "ss_a", "ss_b")])
+                                                 "part_o", "part_ml", "counters")])
 
 
 class _CainRows(ctypes.Structure):
@@ -122,7 +122,9 @@ def _ptr(t: Optional[torch.Tensor]) -> Optional[int]:
 
 
 def attention_splits(M: int, Hkv: int, T_max: int) -> int:
-    """Position splits per (row, kv head): ~256 workgroups in flight, >= 4 blocks of 32 per split."""
+    """Position splits per (row, kv head): ~256 workgroups in flight, >= 4 blocks of 32 per split at
+    full context, <= 64 splits (measured: 1024-WG targets lose more to the split combine than they
+    gain in parallelism, profiles/kernels.md)."""
     return int(max(1, min(64, max(1, T_max // 128), math.ceil(256 / (M * Hkv)))))
 
 
@@ -181,8 +183,7 @@ class DecodeEngine:
         R = MAX_ROWS
         z = lambda *s, dt=bf: torch.zeros(*s, device=dev, dtype=dt)  # noqa: E731
         self.buf = dict(x=z(R, cfg.d_model), q=z(R, cfg.q_dim), attn=z(R, cfg.q_dim), act=z(R, cfg.ffn),
-                        logits=z(R, cfg.vocab, dt=torch.float32), ss_a=z(R, dt=torch.float32),
-                        ss_b=z(R, dt=torch.float32), counters=z(R * cfg.n_kv_heads, dt=torch.int32))
+                        logits=z(R, cfg.vocab, dt=torch.float32), counters=z(R * cfg.n_kv_heads, dt=torch.int32))
         max_ms = max(m * attention_splits(m, cfg.n_kv_heads, T) for m in range(1, R + 1))
         self.part_o = z(max_ms * cfg.n_heads * cfg.head_dim, dt=torch.float32)
         self.part_ml = z(max(ops.attention_ml_floats(m, cfg.n_heads, cfg.n_kv_heads,
@@ -213,7 +214,7 @@ class DecodeEngine:
         d.layers = ctypes.cast(self._layers, ctypes.c_void_p).value
         d.kcache, d.vtcache, d.kv_layer_elems = _ptr(self.kcache), _ptr(self.vtcache), kv_layer
         d.cos_t, d.sin_t = _ptr(self.cos_t), _ptr(self.sin_t)
-        for k in ("x", "q", "attn", "act", "logits", "ss_a", "ss_b", "counters"):
+        for k in ("x", "q", "attn", "act", "logits", "counters"):
             setattr(d, k, _ptr(self.buf[k]))
         d.part_o, d.part_ml = _ptr(self.part_o), _ptr(self.part_ml)
         self._desc = d

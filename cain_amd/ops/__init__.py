@@ -11,10 +11,10 @@ Kernel inventory:
 op                     source                      replaces (Ollama/llama.cpp)
 =====================  ==========================  =============================
 ``skinny_gemm``        csrc/gemm.hip               O / gate-up(+act) / down / LM head GEMV,
-                                                   fused RMSNorm prologue, residual(+sum-sq) epilogue
+                                                   fused RMSNorm, residual epilogue
 ``qkv_rope``           csrc/gemm.hip               QKV GEMV + bias + RoPE + KV-cache append
 ``rmsnorm``            csrc/norm.hip               RMSNorm (standalone; the engine fuses it)
-``embed``              csrc/norm.hip               embedding gather (+Gemma scale, +sum-sq)
+``embed``              csrc/norm.hip               embedding gather (+Gemma scale)
 ``attention``          csrc/attention.hip          decode / prefill attention (split-K, in-kernel combine)
 ``sample``             csrc/sample.hip             repeat-penalty/temperature/top-k/top-p
 ``Plan``               csrc/runtime.hip            per-step schedule + hipGraph replay
@@ -63,11 +63,11 @@ def load() -> ctypes.CDLL:
             lib = ctypes.CDLL(str(LIB_PATH))
         except OSError as exc:
             raise NativeOpsUnavailable(f"cannot load {LIB_PATH}: {exc}") from exc
-        lib.cain_skinny_gemm_ex.argtypes = ([vp, vp, ci, ci, ci, ci, vp, ci, vp, vp, vp, cf, vp, vp, vp, vp, vp, vp,
-                                             vp, vp] + [ci] * 6 + [vp])
+        lib.cain_skinny_gemm_ex.argtypes = ([vp, vp, ci, ci, ci, ci, vp, ci, vp, vp, cf, vp, vp, vp, vp, vp, vp]
+                                            + [ci] * 6 + [vp])
         lib.cain_rmsnorm.argtypes = [vp, ci, vp, vp, ci, ci, ci, cf, vp]
-        lib.cain_embed.argtypes = [vp, vp, vp, ci, ci, ci, cf, vp, vp]
-        lib.cain_attention.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp, ci, ci, ci, ci, ci, ci, ci, cf, vp, vp]
+        lib.cain_embed.argtypes = [vp, vp, vp, ci, ci, ci, cf, vp]
+        lib.cain_attention.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp, ci, ci, ci, ci, ci, ci, ci, cf, vp]
         lib.cain_sample.argtypes = [vp, ci, ci, vp, vp, vp, ci, vp, vp, vp, vp, vp, ci, ci, vp, vp]
         lib.cain_plan_create.restype = vp
         lib.cain_plan_create.argtypes = [vp]
@@ -110,12 +110,11 @@ def _gpu(*ts):
 
 # ---------------------------------------------------------------- ops
 def skinny_gemm(wp: torch.Tensor, x: torch.Tensor, n: int, epi: int = EPI_BF16, bias=None,
-                out: Optional[torch.Tensor] = None, waves: int = 0, ss_in=None, gain=None, eps: float = 1e-6,
-                ss_out=None, ss_zero=None) -> torch.Tensor:
+                out: Optional[torch.Tensor] = None, waves: int = 0, gain=None, eps: float = 1e-6) -> torch.Tensor:
     """y[M, n] = epi(B(x)[M, K] @ W^T) with W packed by ``pack_mfma_a`` (gate/up interleaved for act epis).
 
-    ``ss_in``/``gain``: fused RMSNorm prologue (B = x * rsqrt(ss_in/K + eps) * gain).
-    ``EPI_RESID``: ``out`` is the residual stream, updated in place; ``ss_out`` accumulates sum(y^2).
+    ``gain``: fused RMSNorm of x (y = rsqrt(mean(x^2) + eps) * (W (x * gain))).
+    ``EPI_RESID``: ``out`` is the residual stream, updated in place.
     """
     lib = load()
     _gpu(wp, x)
@@ -127,22 +126,21 @@ def skinny_gemm(wp: torch.Tensor, x: torch.Tensor, n: int, epi: int = EPI_BF16, 
         assert out is not None and out.shape == (M, n_out), "EPI_RESID updates `out` (the residual) in place"
     if out is None:
         out = torch.empty(M, n_out, device=x.device, dtype=torch.float32 if epi == EPI_F32 else torch.bfloat16)
-    rc = lib.cain_skinny_gemm_ex(_p(wp), _p(x), x.stride(0), K, n, M, _p(out), out.stride(0), _p(bias), _p(ss_in),
-                                 _p(gain), eps, _p(ss_out), _p(ss_zero), None, None, None, None, None, None,
-                                 0, 0, 0, 0, epi, waves, _stream())
+    rc = lib.cain_skinny_gemm_ex(_p(wp), _p(x), x.stride(0), K, n, M, _p(out), out.stride(0), _p(bias), _p(gain),
+                                 eps, None, None, None, None, None, None, 0, 0, 0, 0, epi, waves, _stream())
     _check(rc, "skinny_gemm")
     return out
 
 
-def qkv_rope(wp, x, n, q_out, kc, vtc, slot, pos, cos_t, sin_t, H, Hkv, hd, bias=None, ss_in=None, gain=None,
+def qkv_rope(wp, x, n, q_out, kc, vtc, slot, pos, cos_t, sin_t, H, Hkv, hd, bias=None, gain=None,
              eps: float = 1e-6, waves: int = 0) -> None:
-    """Fused QKV projection (+RMSNorm prologue, +bias) -> RoPE -> Q buffer / K cache / V^T cache."""
+    """Fused QKV projection (+RMSNorm, +bias) -> RoPE -> Q buffer / K cache / V^T cache."""
     lib = load()
     M, K = x.shape
     T_max = kc.shape[-2]
     rc = lib.cain_skinny_gemm_ex(_p(wp), _p(x), x.stride(0), K, n, M, _p(q_out), q_out.stride(0), _p(bias),
-                                 _p(ss_in), _p(gain), eps, None, None, _p(slot), _p(pos), _p(cos_t), _p(sin_t),
-                                 _p(kc), _p(vtc), H, Hkv, hd, T_max, EPI_QKV_ROPE, waves, _stream())
+                                 _p(gain), eps, _p(slot), _p(pos), _p(cos_t), _p(sin_t), _p(kc), _p(vtc), H, Hkv,
+                                 hd, T_max, EPI_QKV_ROPE, waves, _stream())
     _check(rc, "qkv_rope")
 
 
@@ -155,12 +153,12 @@ def rmsnorm(x: torch.Tensor, g: torch.Tensor, eps: float, out: Optional[torch.Te
     return out
 
 
-def embed(tok: torch.Tensor, table: torch.Tensor, scale: float = 1.0, out=None, ss_out=None) -> torch.Tensor:
+def embed(tok: torch.Tensor, table: torch.Tensor, scale: float = 1.0, out=None) -> torch.Tensor:
     lib = load()
     M = tok.shape[0]
     d = table.shape[1]
     out = torch.empty(M, d, device=table.device, dtype=table.dtype) if out is None else out
-    _check(lib.cain_embed(_p(tok), _p(table), _p(out), out.stride(0), M, d, scale, _p(ss_out), _stream()), "embed")
+    _check(lib.cain_embed(_p(tok), _p(table), _p(out), out.stride(0), M, d, scale, _stream()), "embed")
     return out
 
 
@@ -171,7 +169,7 @@ def attention_ml_floats(M: int, H: int, Hkv: int, nsplit: int) -> int:
 
 
 def attention(q, kc, vtc, slot, pos, H, Hkv, hd, nsplit, scale, out=None, part_o=None, part_ml=None,
-              counters=None, ss_zero=None):
+              counters=None):
     lib = load()
     M = q.shape[0]
     T_max = kc.shape[-2]
@@ -182,7 +180,7 @@ def attention(q, kc, vtc, slot, pos, H, Hkv, hd, nsplit, scale, out=None, part_o
         counters = torch.zeros(M * Hkv, device=q.device, dtype=torch.int32)
     out = torch.empty(M, H * hd, device=q.device, dtype=torch.bfloat16) if out is None else out
     _check(lib.cain_attention(_p(q), _p(kc), _p(vtc), _p(slot), _p(pos), _p(part_o), _p(part_ml), _p(counters),
-                              _p(out), out.stride(0), M, H, Hkv, hd, T_max, nsplit, scale, _p(ss_zero), _stream()),
+                              _p(out), out.stride(0), M, H, Hkv, hd, T_max, nsplit, scale, _stream()),
            "attention")
     return out
 

@@ -22,8 +22,6 @@
 // barrier -> relaxed agent ticket; no release/acquire fences, counter reset by the
 // reducer: cdna_hip_programming.md §5 'In-launch split-K reduction'), so there
 // is no separate combine launch.
-// The launch also zeroes the RMSNorm sum-of-squares buffer the QKV GEMM just
-// consumed (ss_zero), keeping the fused-norm protocol launch-ordered.
 #include "common.h"
 
 constexpr float LOG2E = 1.4426950408889634f;
@@ -34,7 +32,7 @@ __global__ __launch_bounds__(AW * 64) void attn_decode_kernel(
     const __bf16* __restrict__ q, const __bf16* __restrict__ kc, const __bf16* __restrict__ vtc,
     const int* __restrict__ slot, const int* __restrict__ pos, float* __restrict__ part_o,
     float* __restrict__ part_ml, unsigned* __restrict__ counters, __bf16* __restrict__ out, int ldo, int M, int H,
-    int Hkv, int T_max, int nsplit, float scale, float* __restrict__ ss_zero) {
+    int Hkv, int T_max, int nsplit, float scale) {
   constexpr int NKS = HD / 32;  // MFMAs per S tile
   constexpr int NDT = HD / 16;  // O^T d-tiles
   const int lane = threadIdx.x & 63;
@@ -44,7 +42,6 @@ __global__ __launch_bounds__(AW * 64) void attn_decode_kernel(
   const int sp = blockIdx.y;
   const int G = H / Hkv;
   const int g = lane & 15, hq = lane >> 4;
-  if (ss_zero && mk == 0 && sp == 0 && threadIdx.x < M) ss_zero[threadIdx.x] = 0.f;
   const int s = slot[m];
   const int L = (s >= 0) ? pos[m] + 1 : 0;
   const int nblk = (L + 31) >> 5;
@@ -73,24 +70,36 @@ __global__ __launch_bounds__(AW * 64) void attn_decode_kernel(
     const float sl2 = scale * LOG2E;
     const __bf16* kbase = kc + ((size_t)s * Hkv + kh) * T_max * HD;
     const __bf16* vbase = vtc + ((size_t)s * Hkv + kh) * HD * T_max;
-    for (int blk = b0 + wave; blk < b1; blk += AW) {
+    // K/V fragments of one 32-position block; with HD <= 128 the next block's loads are
+    // issued before the current block computes (register double buffer)
+    constexpr bool PREF = HD <= 128;
+    bf16x8 ka[NKS], kb[NKS];
+    u16x4 va[NDT], vb[NDT];
+    auto load_blk = [&](int blk, bf16x8 (&k_a)[NKS], bf16x8 (&k_b)[NKS], u16x4 (&v_a)[NDT], u16x4 (&v_b)[NDT]) {
       const int t0 = blk * 32;
-      f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = {0.f, 0.f, 0.f, 0.f};
       const __bf16* k0 = kbase + (size_t)(t0 + g) * HD + hq * 8;
       const __bf16* k1 = k0 + 16 * HD;
-      bf16x8 ka[NKS], kb[NKS];
 #pragma unroll
       for (int i = 0; i < NKS; ++i) {
-        ka[i] = *reinterpret_cast<const bf16x8*>(k0 + i * 32);
-        kb[i] = *reinterpret_cast<const bf16x8*>(k1 + i * 32);
+        k_a[i] = *reinterpret_cast<const bf16x8*>(k0 + i * 32);
+        k_b[i] = *reinterpret_cast<const bf16x8*>(k1 + i * 32);
       }
-      u16x4 va[NDT], vb[NDT];
 #pragma unroll
       for (int dt = 0; dt < NDT; ++dt) {
         const __bf16* vr = vbase + (size_t)(dt * 16 + g) * T_max + t0 + hq * 4;
-        va[dt] = *reinterpret_cast<const u16x4*>(vr);
-        vb[dt] = *reinterpret_cast<const u16x4*>(vr + 16);
+        v_a[dt] = *reinterpret_cast<const u16x4*>(vr);
+        v_b[dt] = *reinterpret_cast<const u16x4*>(vr + 16);
       }
+    };
+    if (b0 + wave < b1) load_blk(b0 + wave, ka, kb, va, vb);
+    for (int blk = b0 + wave; blk < b1; blk += AW) {
+      const int t0 = blk * 32;
+      bf16x8 nka[PREF ? NKS : 1], nkb[PREF ? NKS : 1];
+      u16x4 nva[PREF ? NDT : 1], nvb[PREF ? NDT : 1];
+      if constexpr (PREF) {
+        if (blk + AW < b1) load_blk(blk + AW, nka, nkb, nva, nvb);
+      }
+      f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int i = 0; i < NKS; ++i) {
         s0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ka[i], qf[i], s0, 0, 0, 0);
@@ -129,6 +138,14 @@ __global__ __launch_bounds__(AW * 64) void attn_decode_kernel(
           vv[4 + j] = vb[dt][j];
         }
         o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, vv), pf, o[dt], 0, 0, 0);
+      }
+      if constexpr (PREF) {
+#pragma unroll
+        for (int i = 0; i < NKS; ++i) { ka[i] = nka[i]; kb[i] = nkb[i]; }
+#pragma unroll
+        for (int dt = 0; dt < NDT; ++dt) { va[dt] = nva[dt]; vb[dt] = nvb[dt]; }
+      } else {
+        if (blk + AW < b1) load_blk(blk + AW, ka, kb, va, vb);
       }
     }
   }
@@ -231,10 +248,10 @@ __global__ __launch_bounds__(AW * 64) void attn_decode_kernel(
 template <int HD>
 static hipError_t launch_attn(const void* q, const void* kc, const void* vtc, const int* slot, const int* pos,
                               float* part_o, float* part_ml, unsigned* counters, void* out, int ldo, int M, int H,
-                              int Hkv, int T_max, int nsplit, float scale, float* ss_zero, hipStream_t st) {
+                              int Hkv, int T_max, int nsplit, float scale, hipStream_t st) {
   hipLaunchKernelGGL(attn_decode_kernel<HD>, dim3(M * Hkv, nsplit), dim3(AW * 64), 0, st, (const __bf16*)q,
                      (const __bf16*)kc, (const __bf16*)vtc, slot, pos, part_o, part_ml, counters, (__bf16*)out, ldo, M,
-                     H, Hkv, T_max, nsplit, scale, ss_zero);
+                     H, Hkv, T_max, nsplit, scale);
   return hipGetLastError();
 }
 
@@ -242,13 +259,13 @@ static hipError_t launch_attn(const void* q, const void* kc, const void* vtc, co
 // (zeroed once; the reducer resets them).
 CAIN_API int cain_attention(const void* q, const void* kc, const void* vtc, const int* slot, const int* pos,
                             float* part_o, float* part_ml, unsigned* counters, void* out, int ldo, int M, int H,
-                            int Hkv, int hd, int T_max, int nsplit, float scale, float* ss_zero, hipStream_t st) {
+                            int Hkv, int hd, int T_max, int nsplit, float scale, hipStream_t st) {
   if (H % Hkv || H / Hkv > 16 || T_max % 32 || nsplit < 1 || nsplit > 64 || M > 256) return -1;
   switch (hd) {
-    case 64: return int(launch_attn<64>(q, kc, vtc, slot, pos, part_o, part_ml, counters, out, ldo, M, H, Hkv, T_max, nsplit, scale, ss_zero, st));
-    case 96: return int(launch_attn<96>(q, kc, vtc, slot, pos, part_o, part_ml, counters, out, ldo, M, H, Hkv, T_max, nsplit, scale, ss_zero, st));
-    case 128: return int(launch_attn<128>(q, kc, vtc, slot, pos, part_o, part_ml, counters, out, ldo, M, H, Hkv, T_max, nsplit, scale, ss_zero, st));
-    case 256: return int(launch_attn<256>(q, kc, vtc, slot, pos, part_o, part_ml, counters, out, ldo, M, H, Hkv, T_max, nsplit, scale, ss_zero, st));
+    case 64: return int(launch_attn<64>(q, kc, vtc, slot, pos, part_o, part_ml, counters, out, ldo, M, H, Hkv, T_max, nsplit, scale, st));
+    case 96: return int(launch_attn<96>(q, kc, vtc, slot, pos, part_o, part_ml, counters, out, ldo, M, H, Hkv, T_max, nsplit, scale, st));
+    case 128: return int(launch_attn<128>(q, kc, vtc, slot, pos, part_o, part_ml, counters, out, ldo, M, H, Hkv, T_max, nsplit, scale, st));
+    case 256: return int(launch_attn<256>(q, kc, vtc, slot, pos, part_o, part_ml, counters, out, ldo, M, H, Hkv, T_max, nsplit, scale, st));
     default: return -1;
   }
 }

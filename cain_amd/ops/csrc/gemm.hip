@@ -12,10 +12,11 @@
 // reads X[m][32s+8g .. +8]); neither operand goes through LDS
 // (cdna_hip_programming.md §5, 'GEMV / M <= 16' row).
 //
-// Prologue (NORM): RMSNorm is applied to the B fragment on the fly,
-//   B = bf16( X[m][k] * rsqrt(ss[m]/K + eps) * gain[k] ),
-// where ss[m] (sum of squares of row m) was accumulated by the PREVIOUS GEMM's
-// epilogue — so no separate normalisation kernel (or its launch gap) exists.
+// Fused RMSNorm (NORM): W.(x * inv * g) = inv * W.(x * g) with inv a per-row
+// scalar, so the B fragment is bf16(x * gain), every workgroup accumulates the
+// row's sum of squares from the x fragments it streams anyway (its waves cover
+// all of K), and the epilogue scales by rsqrt(mean(x^2) + eps): no separate
+// normalisation kernel, no launch gap, no cross-kernel state.
 //
 // Parallelism: a workgroup owns NT 16-row tiles; its WAVES waves split the
 // K-slices and run a register double-buffered loop (the next U slices' loads
@@ -25,10 +26,7 @@
 //
 // Epilogues (SURVEY §2.4 rows QKV / RoPE / KV-append / O / gate-up / down / LM head):
 //   EPI_BF16      y = bf16(acc + bias)
-//   EPI_RESID_SS  y = bf16(acc + resid) (in place on the residual stream) and
-//                 ss_out[m] += sum_n y^2 (for the next layer's fused RMSNorm);
-//                 block 0 zeroes ss_zero[0..M) (the buffer the previous GEMM
-//                 consumed), keeping the double-buffered ss protocol launch-ordered
+//   EPI_RESID     y = bf16(acc + resid) (in place on the residual stream)
 //   EPI_F32       y = acc (fp32 LM-head logits)
 //   EPI_SILU/GELU gate/up rows interleaved by 8 inside each 16-row tile
 //                 -> y = bf16(act(gate) * up)
@@ -37,22 +35,19 @@
 //                 at (slot[m], pos[m]), V -> transposed V cache.
 #include "common.h"
 
-enum { EPI_BF16 = 0, EPI_RESID_SS = 1, EPI_F32 = 2, EPI_SILU = 3, EPI_GELU = 4, EPI_QKV_ROPE = 5 };
+enum { EPI_BF16 = 0, EPI_RESID = 1, EPI_F32 = 2, EPI_SILU = 3, EPI_GELU = 4, EPI_QKV_ROPE = 5 };
 
 struct GemmArgs {
   const bf16x8* Wp;
   const __bf16* X;
   int ldx, K, N, M;
+  int msplit;  // workgroups per row tile, each owning 16*NB of the M rows
   void* Y;
   int ldy;
   const float* bias;
-  // NORM prologue
-  const float* ss_in;
+  // NORM (fused RMSNorm): B = bf16(x * gain), acc *= rsqrt(mean(x^2) + eps)
   const __bf16* gain;
   float eps;
-  // RESID_SS
-  float* ss_out;
-  float* ss_zero;
   // QKV_ROPE
   const int* slot;
   const int* pos;
@@ -67,20 +62,20 @@ struct GemmArgs {
 // so their latency hides under the weight stream (the residual row, bias, RoPE
 // position / tables).
 struct EpiIn {
-  bf16x4 r;      // EPI_RESID_SS: residual values
+  bf16x4 r;      // EPI_RESID: residual values
   f32x4 b1, b2;  // bias (QKV: rows n1.. and n2..)
   f32x4 c, sn;   // QKV: cos / sin of the 4 rotation pairs
   int p, sl;     // QKV: position, cache slot
 };
 
 template <int NT, int NB, int EPI>
-__device__ __forceinline__ EpiIn epi_load(const GemmArgs& a, int tile0, int u) {
+__device__ __forceinline__ EpiIn epi_load(const GemmArgs& a, int tile0, int mo, int u) {
   EpiIn e{};
   const int lane = u & 63, tb = u >> 6, b = tb % NB, t = tb / NB;
-  const int m = b * 16 + (lane & 15);
+  const int m = mo + b * 16 + (lane & 15);
   const int nsub = (lane >> 4) * 4;
   if (m >= a.M) return e;
-  if constexpr (EPI == EPI_RESID_SS) {
+  if constexpr (EPI == EPI_RESID) {
     e.r = *reinterpret_cast<const bf16x4*>(reinterpret_cast<const __bf16*>(a.Y) + (size_t)m * a.ldy +
                                            (tile0 + t) * 16 + nsub);
   } else if constexpr (EPI == EPI_BF16) {
@@ -110,7 +105,25 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_gemm_kernel(const GemmArgs 
   const int wave = threadIdx.x >> 6;
   const int K = a.K;
   const int KS = K >> 5;
-  const int tile0 = blockIdx.x * NT;
+  // XCD-aware block -> (row tile, M split) mapping: blocks b and b + 8 share an XCD under the
+  // round-robin dispatch, so the msplit workgroups of one weight tile are given ids that differ by
+  // multiples of 8 and their repeated tile reads hit the same L2 (speed only: any placement is correct).
+  int tg, ms;
+  {
+    const int bid = blockIdx.x, msp = a.msplit;
+    const int ntg = gridDim.x / msp;
+    if (msp == 1) {
+      tg = bid, ms = 0;
+    } else if ((ntg & 7) == 0) {
+      const int r = bid >> 3;
+      ms = r % msp;
+      tg = (r / msp) * 8 + (bid & 7);
+    } else {
+      tg = bid / msp, ms = bid - (bid / msp) * msp;
+    }
+  }
+  const int tile0 = tg * NT;
+  const int mo = ms * 16 * NB;  // first row of this workgroup
   const int s_beg = (wave * KS) / WAVES;
   const int s_end = ((wave + 1) * KS) / WAVES;
   constexpr int UNITS = NT * NB * 64;
@@ -118,7 +131,7 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_gemm_kernel(const GemmArgs 
 
   EpiIn pre{};
   if constexpr (PRE) {
-    if (wave * 64 < UNITS) pre = epi_load<NT, NB, EPI>(a, tile0, wave * 64 + lane);
+    if (wave * 64 < UNITS) pre = epi_load<NT, NB, EPI>(a, tile0, mo, wave * 64 + lane);
   }
 
   f32x4 acc[NT][NB];
@@ -131,26 +144,38 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_gemm_kernel(const GemmArgs 
 #pragma unroll
   for (int t = 0; t < NT; ++t) wbase[t] = a.Wp + (size_t)(tile0 + t) * KS * 64 + lane;
   const __bf16* xbase[NB];
-  float inv[NB];
+  float ssq[NB];  // NORM: this lane's partial sum of x^2 of row m (its k-group of each slice)
 #pragma unroll
   for (int b = 0; b < NB; ++b) {
-    const int m = b * 16 + (lane & 15);
+    const int m = min(mo + b * 16 + (lane & 15), a.M - 1);  // rows past M re-read a valid row
     xbase[b] = a.X + (size_t)m * a.ldx + ((lane >> 4) << 3);
-    if constexpr (NORM) inv[b] = rsqrtf(a.ss_in[m] / float(K) + a.eps);
+    ssq[b] = 0.f;
   }
   const __bf16* gbase = NORM ? a.gain + ((lane >> 4) << 3) : nullptr;
 
   // raw fragment loads (issued early); normalisation happens at use, after the data landed
-  auto load_w = [&](int s, int t) -> bf16x8 { return __builtin_nontemporal_load(wbase[t] + (size_t)s * 64); };
+  // non-temporal weight loads when this workgroup is the tile's only reader; with msplit > 1 the
+  // tile-mates re-read it, so keep the default policy and let them hit L2
+  const bool ntl = a.msplit == 1;
+  auto load_w = [&](int s, int t) -> bf16x8 {
+    return ntl ? __builtin_nontemporal_load(wbase[t] + (size_t)s * 64) : wbase[t][(size_t)s * 64];
+  };
   auto load_x = [&](int s, int b) -> bf16x8 { return *reinterpret_cast<const bf16x8*>(xbase[b] + s * 32); };
   auto load_g = [&](int s) -> bf16x8 {
     if constexpr (NORM) return *reinterpret_cast<const bf16x8*>(gbase + s * 32);
     else return bf16x8{};
   };
+  // RMSNorm factorisation: W (x * inv * g) = inv * (W (x * g)); the per-row inv is applied in the
+  // epilogue and the sum of squares is accumulated from the x fragments this WG streams anyway
+  // (its waves cover all of K), so no separate norm kernel and no cross-kernel sum-of-squares buffer.
   auto norm_x = [&](bf16x8 v, bf16x8 g, int b) -> bf16x8 {
     if constexpr (NORM) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = f2bf(bf2f(f2bf(bf2f(v[j]) * inv[b])) * bf2f(g[j]));
+      for (int j = 0; j < 8; ++j) {
+        const float f = bf2f(v[j]);
+        ssq[b] += f * f;
+        v[j] = f2bf(f * bf2f(g[j]));
+      }
     }
     return v;
   };
@@ -222,12 +247,19 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_gemm_kernel(const GemmArgs 
 
   // ---- cross-wave reduction through LDS: red[wave][unit], unit = (t*NB + b)*64 + lane
   __shared__ __attribute__((aligned(16))) f32x4 red[WAVES][UNITS];
+  __shared__ float red_ss[NORM ? WAVES : 1][NORM ? NB * 16 : 1];
 #pragma unroll
   for (int t = 0; t < NT; ++t)
 #pragma unroll
     for (int b = 0; b < NB; ++b) red[wave][(t * NB + b) * 64 + lane] = acc[t][b];
-  if constexpr (EPI == EPI_RESID_SS) {
-    if (blockIdx.x == 0 && a.ss_zero && threadIdx.x < a.M) a.ss_zero[threadIdx.x] = 0.f;
+  if constexpr (NORM) {
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      float v = ssq[b];
+      v += __shfl_xor(v, 16, 64);  // the 4 k-groups of row m
+      v += __shfl_xor(v, 32, 64);
+      if (lane < 16) red_ss[wave][b * 16 + lane] = v;
+    }
   }
   __syncthreads();
 
@@ -235,6 +267,13 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_gemm_kernel(const GemmArgs 
     f32x4 v = red[0][u];
 #pragma unroll
     for (int w = 1; w < WAVES; ++w) v += red[w][u];
+    if constexpr (NORM) {
+      const int b = (u >> 6) % NB, m16 = b * 16 + (u & 15);
+      float ss = 0.f;
+#pragma unroll
+      for (int w = 0; w < WAVES; ++w) ss += red_ss[w][m16];
+      v *= rsqrtf(ss / float(a.K) + a.eps);
+    }
     return v;
   };
 
@@ -244,10 +283,10 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_gemm_kernel(const GemmArgs 
     const int tb = u >> 6;
     const int b = tb % NB;
     const int t = tb / NB;
-    const int m = b * 16 + (lane & 15);
+    const int m = mo + b * 16 + (lane & 15);
     const int nsub = (lane >> 4) * 4;
     const bool mvalid = m < a.M;
-    const EpiIn e = (PRE && ub == wave * 64) ? pre : epi_load<NT, NB, EPI>(a, tile0, u);
+    const EpiIn e = (PRE && ub == wave * 64) ? pre : epi_load<NT, NB, EPI>(a, tile0, mo, u);
     if constexpr (EPI == EPI_SILU || EPI == EPI_GELU) {
       // 8-row interleave: rows 0..7 of a tile are gate rows, rows 8..15 the matching up rows
       if ((lane >> 4) < 2) {
@@ -310,22 +349,13 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_gemm_kernel(const GemmArgs 
 #pragma unroll
         for (int i = 0; i < 4; ++i) o[i] = f2bf(v[i] + e.b1[i]);
         if (mvalid) *reinterpret_cast<bf16x4*>(reinterpret_cast<__bf16*>(a.Y) + (size_t)m * a.ldy + n) = o;
-      } else {  // EPI_RESID_SS: in-place residual update + sum of squares for the next RMSNorm
-        float ss = 0.f;
+      } else {  // EPI_RESID: in-place residual update
         if (mvalid) {
           bf16x4 o;
 #pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            o[i] = f2bf(v[i] + bf2f(e.r[i]));
-            const float f = bf2f(o[i]);
-            ss += f * f;
-          }
+          for (int i = 0; i < 4; ++i) o[i] = f2bf(v[i] + bf2f(e.r[i]));
           *reinterpret_cast<bf16x4*>(reinterpret_cast<__bf16*>(a.Y) + (size_t)m * a.ldy + n) = o;
         }
-        // lanes l, l^16, l^32, l^48 share m: reduce, then one atomic per (wave, m)
-        ss += __shfl_xor(ss, 16, 64);
-        ss += __shfl_xor(ss, 32, 64);
-        if (lane < 16 && mvalid && a.ss_out) atomicAdd(a.ss_out + m, ss);
       }
     }
   }
@@ -334,8 +364,8 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_gemm_kernel(const GemmArgs 
 template <int NT, int NB, int WAVES, int EPI, bool NORM>
 static hipError_t launch_t(const GemmArgs& a, hipStream_t st) {
   constexpr int U = (NB >= 2) ? 2 : 4;  // x2 register sets (pipelined)
-  hipLaunchKernelGGL((skinny_gemm_kernel<NT, NB, WAVES, U, EPI, NORM>), dim3(a.N / (16 * NT)), dim3(WAVES * 64), 0, st,
-                     a);
+  hipLaunchKernelGGL((skinny_gemm_kernel<NT, NB, WAVES, U, EPI, NORM>), dim3(a.N / (16 * NT) * a.msplit),
+                     dim3(WAVES * 64), 0, st, a);
   return hipGetLastError();
 }
 
@@ -352,28 +382,19 @@ static hipError_t launch_w(int waves, const GemmArgs& a, hipStream_t st) {
   return launch_t<NT, NB, 4, EPI, NORM>(a, st);
 }
 
-template <int NT, int EPI, bool NORM>
-static hipError_t launch_b(int nb, int waves, const GemmArgs& a, hipStream_t st) {
-  switch (nb) {
-    case 1: return launch_w<NT, 1, EPI, NORM>(waves, a, st);
-    case 2: return launch_w<NT, 2, EPI, NORM>(waves, a, st);
-    default: return launch_w<NT, 4, EPI, NORM>(waves, a, st);
-  }
-}
-
-template <int NT, bool NORM>
-static hipError_t launch_e(int epi, int nb, int waves, const GemmArgs& a, hipStream_t st) {
+template <bool NORM>
+static hipError_t launch_e(int epi, int waves, const GemmArgs& a, hipStream_t st) {
   switch (epi) {
-    case EPI_BF16: return launch_b<NT, EPI_BF16, NORM>(nb, waves, a, st);
-    case EPI_RESID_SS: return launch_b<NT, EPI_RESID_SS, NORM>(nb, waves, a, st);
-    case EPI_F32: return launch_b<NT, EPI_F32, NORM>(nb, waves, a, st);
-    case EPI_QKV_ROPE: return launch_b<NT, EPI_QKV_ROPE, NORM>(nb, waves, a, st);
+    case EPI_BF16: return launch_w<1, 1, EPI_BF16, NORM>(waves, a, st);
+    case EPI_RESID: return launch_w<1, 1, EPI_RESID, NORM>(waves, a, st);
+    case EPI_F32: return launch_w<1, 1, EPI_F32, NORM>(waves, a, st);
+    case EPI_SILU: return launch_w<1, 1, EPI_SILU, NORM>(waves, a, st);
+    case EPI_GELU: return launch_w<1, 1, EPI_GELU, NORM>(waves, a, st);
+    case EPI_QKV_ROPE: return launch_w<1, 1, EPI_QKV_ROPE, NORM>(waves, a, st);
     default: return hipErrorInvalidValue;
   }
 }
 
-// Pick the number of waves per workgroup so the grid carries enough waves to
-// keep ~8 waves of weight streams per CU (256 CUs).
 // Waves per workgroup: 8 (the tuned choice on every llama3.1:8b decode shape, profiles/gemm_tune.md)
 // unless the grid is small (then 16, to keep >= ~2k waves streaming) or K is too short to give each
 // wave two pipelined chunks.
@@ -384,50 +405,39 @@ static int pick_waves(int n_wg, int ks) {
   return w;
 }
 
-static int gemm_dispatch(const GemmArgs& a, int epi, int norm, int waves, hipStream_t st) {
+static int gemm_dispatch(GemmArgs a, int epi, int norm, int waves, hipStream_t st) {
   if (a.K % 32 || a.N % 16 || a.M < 1 || a.M > 64) return -1;
   const bool pair = (epi == EPI_SILU || epi == EPI_GELU);
-  const int nb = a.M <= 16 ? 1 : (a.M <= 32 ? 2 : 4);
-  // NT row tiles per wave amortise the activation (B) loads: per k-step a wave loads NT weight
-  // fragments and NB activation fragments, so NB > NT makes the L1/TA path, not HBM, the limit.
-  const int nt = (nb >= 2 && a.N % 32 == 0 && a.N / 32 >= 128) ? 2 : 1;
-  if (a.N % (16 * nt)) return -1;
-  const int n_wg = a.N / (16 * nt);
+  // Rows beyond 16 are split over workgroups (msplit) rather than widening a workgroup's
+  // B operand: per k-step a wave then loads one weight and one activation fragment, and
+  // the grid keeps N/16 * msplit workgroups (a wider NB would need NT > 1 to amortise the
+  // activation loads, which halves the grid — measured 1.4-2.7 TB/s at M = 32-64).
+  const int nb = 1;
+  const int nt = 1;
+  a.msplit = (a.M + 15) / 16;
+  const int n_wg = a.N / 16 * a.msplit;
   if (waves <= 0) waves = pick_waves(n_wg, a.K / 32);
   while (waves > 4 && waves * nt * nb > 64) waves /= 2;  // LDS reduction buffer <= 64 KiB
   // 16-wave groups cap registers at 128/lane: the RoPE / norm-prologue / NB=4 bodies would spill
   if (waves > 8 && (epi == EPI_QKV_ROPE || norm || nb >= 4)) waves = 8;
-  hipError_t e;
-  if (pair) {
-    if (nt == 1)
-      e = norm ? ((epi == EPI_SILU) ? launch_b<1, EPI_SILU, true>(nb, waves, a, st) : launch_b<1, EPI_GELU, true>(nb, waves, a, st))
-               : ((epi == EPI_SILU) ? launch_b<1, EPI_SILU, false>(nb, waves, a, st) : launch_b<1, EPI_GELU, false>(nb, waves, a, st));
-    else
-      e = norm ? ((epi == EPI_SILU) ? launch_b<2, EPI_SILU, true>(nb, waves, a, st) : launch_b<2, EPI_GELU, true>(nb, waves, a, st))
-               : ((epi == EPI_SILU) ? launch_b<2, EPI_SILU, false>(nb, waves, a, st) : launch_b<2, EPI_GELU, false>(nb, waves, a, st));
-  } else if (nt == 1) {
-    e = norm ? launch_e<1, true>(epi, nb, waves, a, st) : launch_e<1, false>(epi, nb, waves, a, st);
-  } else {
-    e = norm ? launch_e<2, true>(epi, nb, waves, a, st) : launch_e<2, false>(epi, nb, waves, a, st);
-  }
+  (void)pair;
+  const hipError_t e = norm ? launch_e<true>(epi, waves, a, st) : launch_e<false>(epi, waves, a, st);
   return int(e);
 }
 
-// Fully general entry used by the runtime (norm prologue and/or QKV-RoPE epilogue).
+// Entry used by the runtime and the bindings.  gain != null selects the fused RMSNorm.
 CAIN_API int cain_skinny_gemm_ex(const void* Wp, const void* X, int ldx, int K, int N, int M, void* Y, int ldy,
-                                 const float* bias, const float* ss_in, const void* gain, float eps, float* ss_out,
-                                 float* ss_zero, const int* slot, const int* pos, const float* cos_t,
-                                 const float* sin_t, void* kc, void* vtc, int H, int Hkv, int hd, int T_max, int epi,
-                                 int waves, hipStream_t st) {
+                                 const float* bias, const void* gain, float eps, const int* slot, const int* pos,
+                                 const float* cos_t, const float* sin_t, void* kc, void* vtc, int H, int Hkv, int hd,
+                                 int T_max, int epi, int waves, hipStream_t st) {
   GemmArgs a{};
   a.Wp = reinterpret_cast<const bf16x8*>(Wp);
   a.X = reinterpret_cast<const __bf16*>(X);
   a.ldx = ldx, a.K = K, a.N = N, a.M = M, a.Y = Y, a.ldy = ldy, a.bias = bias;
-  a.ss_in = ss_in, a.gain = reinterpret_cast<const __bf16*>(gain), a.eps = eps;
-  a.ss_out = ss_out, a.ss_zero = ss_zero;
+  a.gain = reinterpret_cast<const __bf16*>(gain), a.eps = eps;
   a.slot = slot, a.pos = pos, a.cos_t = cos_t, a.sin_t = sin_t;
   a.kc = reinterpret_cast<__bf16*>(kc), a.vtc = reinterpret_cast<__bf16*>(vtc);
   a.H = H, a.Hkv = Hkv, a.hd = hd, a.T_max = T_max;
   if (epi == EPI_QKV_ROPE && (hd % 16 || (hd / 2) % 8)) return -1;
-  return gemm_dispatch(a, epi, ss_in != nullptr, waves, st);
+  return gemm_dispatch(a, epi, gain != nullptr, waves, st);
 }

@@ -59,29 +59,19 @@ __global__ __launch_bounds__(THREADS) void rmsnorm_kernel(const __bf16* __restri
 }
 
 // out[m] = E[tok[m]] * scale   (scale = sqrt(d) rounded to bf16 for Gemma, else 1)
-// and ss_out[m] = sum(out[m]^2): the first layer's fused RMSNorm input.
 __global__ __launch_bounds__(256) void embed_kernel(const int* __restrict__ tok, const __bf16* __restrict__ E,
-                                                    __bf16* __restrict__ out, int ldo, int d, float scale,
-                                                    float* __restrict__ ss_out) {
-  __shared__ float sh[4];
+                                                    __bf16* __restrict__ out, int ldo, int d, float scale) {
   const int m = blockIdx.x;
   const int id = tok[m];
   const bf16x8* src = reinterpret_cast<const bf16x8*>(E + (size_t)id * d);
   bf16x8* dst = reinterpret_cast<bf16x8*>(out + (size_t)m * ldo);
-  float ss = 0.f;
   for (int i = threadIdx.x; i < (d >> 3); i += 256) {
     bf16x8 v = src[i];
+    if (scale != 1.0f) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      if (scale != 1.0f) v[j] = f2bf(bf2f(v[j]) * scale);
-      const float f = bf2f(v[j]);
-      ss += f * f;
+      for (int j = 0; j < 8; ++j) v[j] = f2bf(bf2f(v[j]) * scale);
     }
     dst[i] = v;
-  }
-  if (ss_out) {
-    const float t = block_sum<256>(ss, sh);
-    if (threadIdx.x == 0) ss_out[m] = t;
   }
 }
 
@@ -97,10 +87,8 @@ CAIN_API int cain_rmsnorm(const void* x, int ldx, const void* g, void* y, int ld
   return int(hipGetLastError());
 }
 
-CAIN_API int cain_embed(const int* tok, const void* E, void* out, int ldo, int M, int d, float scale, float* ss_out,
-                        hipStream_t st) {
+CAIN_API int cain_embed(const int* tok, const void* E, void* out, int ldo, int M, int d, float scale, hipStream_t st) {
   if (d % 8) return -1;
-  hipLaunchKernelGGL(embed_kernel, dim3(M), dim3(256), 0, st, tok, (const __bf16*)E, (__bf16*)out, ldo, d, scale,
-                     ss_out);
+  hipLaunchKernelGGL(embed_kernel, dim3(M), dim3(256), 0, st, tok, (const __bf16*)E, (__bf16*)out, ldo, d, scale);
   return int(hipGetLastError());
 }

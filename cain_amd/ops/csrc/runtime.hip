@@ -6,10 +6,10 @@
 // forward over M rows (decode: one row per live sequence; prefill: one row per
 // prompt token, each with its own cache slot and position):
 //
-//   embed(+ss) -> L x [QKV GEMM(+RMSNorm prologue, +bias, RoPE, KV append)
-//                 -> attention(+split combine) -> O GEMM(+residual, +ss)
-//                 -> gate/up GEMM(+RMSNorm prologue, act*mul) -> down GEMM(+residual, +ss)]
-//                 -> LM-head GEMM(+RMSNorm prologue) -> sample
+//   embed -> L x [QKV GEMM(+RMSNorm, +bias, RoPE, KV append)
+//                 -> attention(+split combine) -> O GEMM(+residual)
+//                 -> gate/up GEMM(+RMSNorm, act*mul) -> down GEMM(+residual)]
+//                 -> LM-head GEMM(+RMSNorm) -> sample
 //
 // = 5 launches per layer (the unfused schedule had 9).  `cain_plan_capture` records `steps` consecutive
 // decode steps into ONE hipGraph; since the sampler advances tok/pos/n_gen on
@@ -21,15 +21,13 @@
 #include "common.h"
 
 CAIN_API int cain_skinny_gemm_ex(const void* Wp, const void* X, int ldx, int K, int N, int M, void* Y, int ldy,
-                                 const float* bias, const float* ss_in, const void* gain, float eps, float* ss_out,
-                                 float* ss_zero, const int* slot, const int* pos, const float* cos_t,
-                                 const float* sin_t, void* kc, void* vtc, int H, int Hkv, int hd, int T_max, int epi,
-                                 int waves, hipStream_t st);
-CAIN_API int cain_embed(const int* tok, const void* E, void* out, int ldo, int M, int d, float scale, float* ss_out,
-                        hipStream_t st);
+                                 const float* bias, const void* gain, float eps, const int* slot, const int* pos,
+                                 const float* cos_t, const float* sin_t, void* kc, void* vtc, int H, int Hkv, int hd,
+                                 int T_max, int epi, int waves, hipStream_t st);
+CAIN_API int cain_embed(const int* tok, const void* E, void* out, int ldo, int M, int d, float scale, hipStream_t st);
 CAIN_API int cain_attention(const void* q, const void* kc, const void* vtc, const int* slot, const int* pos,
                             float* part_o, float* part_ml, unsigned* counters, void* out, int ldo, int M, int H,
-                            int Hkv, int hd, int T_max, int nsplit, float scale, float* ss_zero, hipStream_t st);
+                            int Hkv, int hd, int T_max, int nsplit, float scale, hipStream_t st);
 CAIN_API int cain_sample(float* logits, int ldl, int V, int* tok, int* pos, int* gen, int ldg, int* n_gen,
                          const int* max_new, int* done, int* hist, const int* slot, int T_max, int M,
                          const void* params, hipStream_t st);
@@ -66,8 +64,6 @@ struct CainPlanDesc {
   float* part_o;
   float* part_ml;
   unsigned* counters;
-  float* ss_a;  // sum of squares feeding the attention-side RMSNorm (and the final norm)
-  float* ss_b;  // ... feeding the MLP-side RMSNorm
 };
 
 struct CainRows {
@@ -99,37 +95,32 @@ struct Plan {
     if (_e != 0) return _e;       \
   } while (0)
 
-// 5 launches per layer: QKV(+norm, rope, KV append) -> attention(+combine) ->
-// O(+residual, ss) -> gate/up(+norm, act*mul) -> down(+residual, ss).
+// 5 launches per layer: QKV(+RMSNorm, bias, RoPE, KV append) -> attention(+combine) ->
+// O(+residual) -> gate/up(+RMSNorm, act*mul) -> down(+residual).
 int forward(const Plan& p, int M, const CainRows& r, int want_logits, int want_sample, hipStream_t st) {
   const CainPlanDesc& d = p.d;
   const int qkv_dim = (d.H + 2 * d.Hkv) * d.hd;
   const int q_dim = d.H * d.hd;
   const int epi_act = d.act_kind == 1 ? 4 : 3;
-  CK(cain_embed(r.tok, d.embed, d.x, d.d, M, d.d, d.embed_scale, d.ss_a, st));
+  CK(cain_embed(r.tok, d.embed, d.x, d.d, M, d.d, d.embed_scale, st));
   for (int l = 0; l < d.n_layers; ++l) {
     const CainLayer& L = p.layers[l];
     __bf16* kc = reinterpret_cast<__bf16*>(d.kcache) + (size_t)l * d.kv_layer_elems;
     __bf16* vc = reinterpret_cast<__bf16*>(d.vtcache) + (size_t)l * d.kv_layer_elems;
-    CK(cain_skinny_gemm_ex(L.wqkv, d.x, d.d, d.d, qkv_dim, M, d.q, q_dim, L.bqkv, d.ss_a, L.attn_norm, d.eps,
-                           nullptr, nullptr, r.slot, r.pos, d.cos_t, d.sin_t, kc, vc, d.H, d.Hkv, d.hd, d.T_max,
-                           /*EPI_QKV_ROPE*/ 5, d.waves, st));
+    CK(cain_skinny_gemm_ex(L.wqkv, d.x, d.d, d.d, qkv_dim, M, d.q, q_dim, L.bqkv, L.attn_norm, d.eps, r.slot, r.pos,
+                           d.cos_t, d.sin_t, kc, vc, d.H, d.Hkv, d.hd, d.T_max, /*EPI_QKV_ROPE*/ 5, d.waves, st));
     CK(cain_attention(d.q, kc, vc, r.slot, r.pos, d.part_o, d.part_ml, d.counters, d.attn, q_dim, M, d.H, d.Hkv,
-                      d.hd, d.T_max, d.nsplit, d.attn_scale, d.ss_a, st));
-    CK(cain_skinny_gemm_ex(L.wo, d.attn, q_dim, q_dim, d.d, M, d.x, d.d, nullptr, nullptr, nullptr, 0.f, d.ss_b,
-                           nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0, 0, 0,
-                           /*EPI_RESID_SS*/ 1, d.waves, st));
-    CK(cain_skinny_gemm_ex(L.wgu, d.x, d.d, d.d, 2 * d.ffn, M, d.act, d.ffn, nullptr, d.ss_b, L.mlp_norm, d.eps,
-                           nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0, 0, 0,
-                           epi_act, d.waves, st));
-    CK(cain_skinny_gemm_ex(L.wdown, d.act, d.ffn, d.ffn, d.d, M, d.x, d.d, nullptr, nullptr, nullptr, 0.f, d.ss_a,
-                           d.ss_b, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0, 0, 0,
-                           /*EPI_RESID_SS*/ 1, d.waves, st));
+                      d.hd, d.T_max, d.nsplit, d.attn_scale, st));
+    CK(cain_skinny_gemm_ex(L.wo, d.attn, q_dim, q_dim, d.d, M, d.x, d.d, nullptr, nullptr, 0.f, nullptr, nullptr,
+                           nullptr, nullptr, nullptr, nullptr, 0, 0, 0, 0, /*EPI_RESID*/ 1, d.waves, st));
+    CK(cain_skinny_gemm_ex(L.wgu, d.x, d.d, d.d, 2 * d.ffn, M, d.act, d.ffn, nullptr, L.mlp_norm, d.eps, nullptr,
+                           nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0, 0, 0, epi_act, d.waves, st));
+    CK(cain_skinny_gemm_ex(L.wdown, d.act, d.ffn, d.ffn, d.d, M, d.x, d.d, nullptr, nullptr, 0.f, nullptr, nullptr,
+                           nullptr, nullptr, nullptr, nullptr, 0, 0, 0, 0, /*EPI_RESID*/ 1, d.waves, st));
   }
   if (want_logits) {
-    CK(cain_skinny_gemm_ex(d.lm_head, d.x, d.d, d.d, d.V, M, d.logits, d.V, nullptr, d.ss_a, d.final_norm, d.eps,
-                           nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0, 0, 0,
-                           /*EPI_F32*/ 2, d.waves, st));
+    CK(cain_skinny_gemm_ex(d.lm_head, d.x, d.d, d.d, d.V, M, d.logits, d.V, nullptr, d.final_norm, d.eps, nullptr,
+                           nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0, 0, 0, /*EPI_F32*/ 2, d.waves, st));
   }
   if (want_sample) {
     CK(cain_sample(d.logits, d.V, d.V, r.tok, r.pos, r.gen, r.ldg, r.n_gen, r.max_new, r.done, r.hist, r.slot,

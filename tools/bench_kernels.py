@@ -72,7 +72,7 @@ def main():
                 def run():
                     w = W[role][it[0] % len(W[role])]
                     it[0] += 1
-                    ops.skinny_gemm(w, x, n, epi, out=out, waves=wv, ss_out=ss if epi == ops.EPI_RESID else None)
+                    ops.skinny_gemm(w, x, n, epi, out=out, waves=wv)
                 us = timeit(run)
                 gbs = n * k * 2 / us / 1e3
                 r = dict(kind="gemm", model=cfg.name, role=role, M=M, N=n, K=k, waves=wv, us=round(us, 2),
