@@ -159,6 +159,7 @@ class DecodeEngine:
             torch.cuda.synchronize(self.device)
         self.load_duration_ns = time.perf_counter_ns() - t0
         self._first_call = True
+        self.last_ttft_ns = 0
 
     # ---------------------------------------------------------------- hip setup
     def _init_hip(self) -> None:
@@ -282,8 +283,10 @@ class DecodeEngine:
         return [int(t) for t in prompt]
 
     def generate(self, prompts: Sequence[Union[str, Sequence[int]]], num_predict: Union[int, Sequence[int]] = 128,
-                 options: Union[None, Dict, Sequence[Optional[Dict]]] = None, use_graph: bool = True
-                 ) -> List[GenResult]:
+                 options: Union[None, Dict, Sequence[Optional[Dict]]] = None, use_graph: bool = True,
+                 on_tokens=None) -> List[GenResult]:
+        """Generate for a batch of prompts (ids or text).  ``on_tokens(list_per_row)`` streams newly
+        generated ids every ``steps_per_graph`` decode steps (and stops early once every row is done)."""
         prompts = list(prompts)
         B = len(prompts)
         if B == 0:
@@ -294,7 +297,7 @@ class DecodeEngine:
                 sl = slice(i, i + self.max_batch)
                 nps = num_predict[sl] if not isinstance(num_predict, int) else num_predict
                 ops_ = options[sl] if isinstance(options, (list, tuple)) else options
-                out += self.generate(prompts[sl], nps, ops_, use_graph)
+                out += self.generate(prompts[sl], nps, ops_, use_graph, on_tokens)
             return out
         ids = [self.encode(p) or [self.cfg.bos_id] for p in prompts]
         nps = [int(num_predict)] * B if isinstance(num_predict, int) else [int(x) for x in num_predict]
@@ -308,12 +311,15 @@ class DecodeEngine:
         t0 = time.perf_counter_ns()
         if self.backend == "torch":
             gen, t_pref, t_dec = self._generate_torch(ids, nps, row_opts)
+            if on_tokens is not None:
+                on_tokens(gen)
         else:
-            gen, t_pref, t_dec = self._generate_hip(ids, nps, row_opts, use_graph)
+            gen, t_pref, t_dec = self._generate_hip(ids, nps, row_opts, use_graph, on_tokens)
         total = time.perf_counter_ns() - t0
         load = self.load_duration_ns if self._first_call else 0
         self._first_call = False
         steps = max(nps)
+        self.last_prefill_ns, self.last_decode_ns = t_pref, t_dec
         out = []
         for i in range(B):
             toks = gen[i]
@@ -325,7 +331,7 @@ class DecodeEngine:
                                  total_duration_ns=total + load))
         return out
 
-    def _generate_hip(self, ids, nps, row_opts, use_graph):
+    def _generate_hip(self, ids, nps, row_opts, use_graph, on_tokens=None, check_every: int = 1):
         from .. import ops
 
         dev = self.device
@@ -346,24 +352,57 @@ class DecodeEngine:
             self.stream.synchronize()
             t1 = time.perf_counter_ns()
             steps = max(nps)
-            if use_graph:
+            stream_h = ctypes.c_void_p(self.stream.cuda_stream)
+
+            def launch(nsteps: int) -> None:
+                if not use_graph:
+                    for _ in range(nsteps):
+                        self._forward(B, r, want_logits=True, want_sample=True)
+                    return
                 k = self.steps_per_graph
-                g = self._graph(B, k)
-                for _ in range(steps // k):
-                    rc = self.lib.cain_graph_launch(ctypes.c_void_p(g), ctypes.c_void_p(self.stream.cuda_stream))
+                g = self._graph(B, k) if nsteps >= k else None
+                for _ in range(nsteps // k):
+                    rc = self.lib.cain_graph_launch(ctypes.c_void_p(g), stream_h)
                     if rc != 0:
                         raise RuntimeError(f"hipGraphLaunch failed rc={rc}")
-                rem = steps % k
-                if rem:
+                if nsteps % k:
                     g1 = self._graph(B, 1)
-                    for _ in range(rem):
-                        self.lib.cain_graph_launch(ctypes.c_void_p(g1), ctypes.c_void_p(self.stream.cuda_stream))
-            else:
-                for _ in range(steps):
-                    self._forward(B, r, want_logits=True, want_sample=True)
+                    for _ in range(nsteps % k):
+                        self.lib.cain_graph_launch(ctypes.c_void_p(g1), stream_h)
+
+            # first token on its own so time-to-first-token is measured exactly
+            launch(1)
+            self.stream.synchronize()
+            t_first = time.perf_counter_ns()
+            done_steps = 1
+            emitted = [0] * B
+            watch = on_tokens is not None or any(o["eos_id"] >= 0 for o in row_opts)
+            chunk = self.steps_per_graph * max(1, int(check_every))
+
+            def poll() -> bool:
+                ng = r["n_gen"][:B].cpu().tolist()
+                if on_tokens is not None:
+                    new = [self.gen[i, emitted[i]: ng[i]].cpu().tolist() if ng[i] > emitted[i] else []
+                           for i in range(B)]
+                    for i in range(B):
+                        emitted[i] = ng[i]
+                    on_tokens(new)
+                return bool(r["done"][:B].all())
+
+            if watch and poll():
+                done_steps = steps
+            while done_steps < steps:
+                n = min(chunk if watch else steps, steps - done_steps)
+                launch(n)
+                done_steps += n
+                if watch and done_steps < steps and poll():
+                    break
             n_gen = r["n_gen"][:B].cpu().tolist()
             gen = self.gen[:B].cpu()
+            if on_tokens is not None:
+                on_tokens([gen[i, emitted[i]: n_gen[i]].tolist() for i in range(B)])
             t2 = time.perf_counter_ns()
+        self.last_ttft_ns = t_first - t0
         return [gen[i, : n_gen[i]].tolist() for i in range(B)], t1 - t0, t2 - t1
 
     @torch.no_grad()

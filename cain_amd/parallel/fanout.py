@@ -1,0 +1,192 @@
+"""Data-parallel trial fan-out across the GPUs of one node (SURVEY §2.5 row DP, §5.8).
+
+The reference runs its 1,260 trials strictly one after another
+(experiment-runner/ExperimentOrchestrator/Experiment/ExperimentController.py:119-137)
+with a 90 s cooldown each — 31.5 h of sleep.  Trials are independent, so here
+they are sharded over N worker processes, one per GPU:
+
+* every rank builds the same ``RunnerConfig`` (the config file is re-imported in
+  each spawned worker — HIP state never crosses a fork);
+* rank 0 owns ``run_table.csv`` / ``metadata.json`` (creation, resume, md5 check)
+  and ``broadcast_object_list``s the TODO run ids; the shard of rank r is every
+  world-th TODO row starting at r, recomputed from the TODO rows on every start,
+  so a resume works with a different GPU count;
+* BEFORE_EXPERIMENT runs on every rank (per-GPU setup such as starting that
+  rank's local server); AFTER_EXPERIMENT — the reference's run-table
+  post-processing — on the writer only, then ``config.teardown_rank()`` if defined;
+* work proceeds in waves: each rank runs one row (hooks see
+  ``context.rank`` / ``context.device``; the energy plugin measures that
+  rank's GPU), then ``gather_object`` brings the finished rows to rank 0, which
+  commits them in ONE atomic rewrite (single writer), and the
+  cooldown overlaps across GPUs;
+* the collectives are a few hundred bytes (RCCL over xGMI when the process
+  group is ``nccl``; ``gloo`` on CPU), i.e. latency-bound: there is nothing to
+  tune for bandwidth here.
+
+Failure handling: an exception in a run leaves that row TODO (reference
+semantics) and is logged to ``errors.jsonl``; ``retry_failed`` re-runs such rows
+in extra waves.  A rank that dies takes the job down via the process-group
+timeout; its rows are still TODO and the next start resumes them on however
+many GPUs are available.
+"""
+from __future__ import annotations
+
+import datetime
+import os
+import socket
+import traceback
+from typing import Any, Dict, List, Optional
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _backend() -> str:
+    forced = os.environ.get("CAIN_DIST_BACKEND")
+    if forced:
+        return forced
+    try:
+        import torch
+        return "nccl" if torch.cuda.is_available() and torch.cuda.device_count() > 0 else "gloo"
+    except Exception:  # pragma: no cover
+        return "gloo"
+
+
+def run_rank(config_path: str, rank: int, world: int, isolation: Optional[str] = None,
+             timeout: Optional[float] = None, assume_yes: Optional[bool] = None, retry_failed: int = 0,
+             pg_timeout_s: float = 3600.0) -> int:
+    """Body of one worker; the process group must already be initialisable from the environment."""
+    import torch
+    import torch.distributed as dist
+
+    from ..runner.cli import build_config
+    from ..runner.controller import ExperimentController
+    from ..runner.events import EventSubscriptionController, RunnerEvents
+    from ..runner.models import OperationType, RunProgress
+    from ..runner.output import OutputProcedure as output
+    from ..runner.store import CSVOutputManager
+    from ..runner.validator import ConfigValidator
+
+    backend = _backend()
+    local = int(os.environ.get("LOCAL_RANK", rank))
+    device = None
+    if backend == "nccl":
+        torch.cuda.set_device(local)
+        device = f"cuda:{local}"
+        dist.init_process_group("nccl", rank=rank, world_size=world,
+                                timeout=datetime.timedelta(seconds=pg_timeout_s),
+                                device_id=torch.device("cuda", local))
+    else:
+        dist.init_process_group("gloo", rank=rank, world_size=world,
+                                timeout=datetime.timedelta(seconds=pg_timeout_s))
+    output.tag = f"[rank {rank}/{world}]"
+    try:
+        config, metadata, source = build_config(config_path)
+        config.dp_rank, config.dp_world = rank, world
+        if device is not None and not hasattr(config, "energy_devices"):
+            config.energy_devices = [local]
+        ConfigValidator.validate_config(config, quiet=rank != 0)
+        writer = rank == 0
+        ctrl = None
+        if writer:
+            ctrl = ExperimentController(config, metadata, source=source, source_name=config_path,
+                                        assume_yes=assume_yes, isolation=isolation, run_timeout_s=timeout,
+                                        writer=True, rank=rank, device=device)
+        dist.barrier()
+        if not writer:
+            ctrl = ExperimentController(config, metadata, isolation=isolation, run_timeout_s=timeout, writer=False,
+                                        rank=rank, device=device)
+            # adopt the writer's (possibly resumed, re-ordered) table
+            ctrl.run_table = CSVOutputManager(ctrl.path).read_run_table()
+        todo_ids = [[v["__run_id"] for v in ctrl.pending()] if writer else None]
+        dist.broadcast_object_list(todo_ids, src=0)
+        todo_ids = todo_ids[0]
+        by_id = {v["__run_id"]: v for v in ctrl.run_table}
+        output.console_log_OK(f"{len(todo_ids)} TODO runs over {world} ranks")
+        EventSubscriptionController.raise_event(RunnerEvents.BEFORE_EXPERIMENT)
+        passes = 1 + max(0, int(retry_failed))
+        for p in range(passes):
+            n_waves = (len(todo_ids) + world - 1) // world
+            failed: List[str] = []
+            for w in range(n_waves):
+                idx = w * world + rank
+                row: Optional[Dict[str, Any]] = None
+                if idx < len(todo_ids):
+                    rid = todo_ids[idx]
+                    row = ctrl.run_variation(by_id[rid], commit=lambda r: None)
+                    if row is None:
+                        failed.append(rid)
+                rows: List[Optional[Dict[str, Any]]] = [None] * world if writer else None
+                dist.gather_object(row, rows, dst=0)
+                if writer:
+                    done = [dict(r) for r in rows if r is not None]
+                    for r in done:
+                        r["__done"] = RunProgress.DONE
+                    if done:
+                        CSVOutputManager(ctrl.path).update_rows(done)
+                        output.console_log_WARNING(f"CSVManager: committed {len(done)} rows (wave {w + 1}/{n_waves})")
+                if w + 1 < n_waves:
+                    ctrl.cooldown()
+                if config.operation_type is OperationType.SEMI:
+                    EventSubscriptionController.raise_event(RunnerEvents.CONTINUE)
+            all_failed: List[List[str]] = [None] * world if writer else None
+            dist.gather_object(failed, all_failed, dst=0)
+            retry = [[rid for lst in all_failed for rid in lst] if writer else None]
+            dist.broadcast_object_list(retry, src=0)
+            todo_ids = retry[0]
+            if not todo_ids or p + 1 >= passes:
+                break
+            output.console_log_WARNING(f"retrying {len(todo_ids)} failed runs (pass {p + 2}/{passes})")
+        dist.barrier()
+        if writer:
+            output.console_log_OK("Experiment completed...")
+            EventSubscriptionController.raise_event(RunnerEvents.AFTER_EXPERIMENT)
+        dist.barrier()
+        # per-rank teardown (e.g. the rank's local Ollama-compatible server); AFTER_EXPERIMENT is the
+        # reference's post-processing of run_table.csv and runs on the single writer only
+        if hasattr(config, "teardown_rank"):
+            config.teardown_rank()
+        return 0
+    except Exception:
+        traceback.print_exc()
+        return 1
+    finally:
+        try:
+            dist.destroy_process_group()
+        except Exception:
+            pass
+
+
+def _spawn_entry(rank, world, port, config_path, isolation, timeout, assume_yes, retry_failed, rcs):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    rcs[rank] = run_rank(config_path, rank, world, isolation, timeout, assume_yes, retry_failed)
+
+
+def launch(config_path: str, n_gpus: int, isolation: Optional[str] = None, timeout: Optional[float] = None,
+           assume_yes: Optional[bool] = None, retry_failed: int = 0) -> int:
+    """Run ``config_path`` data-parallel on ``n_gpus`` ranks (spawned here, or the current torchrun job)."""
+    if "RANK" in os.environ and "WORLD_SIZE" in os.environ:
+        return run_rank(config_path, int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"]), isolation, timeout,
+                        assume_yes, retry_failed)
+    import multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    with ctx.Manager() as mgr:
+        rcs = mgr.dict()
+        procs = [ctx.Process(target=_spawn_entry, args=(r, n_gpus, port, os.path.abspath(config_path), isolation,
+                                                        timeout, assume_yes, retry_failed, rcs))
+                 for r in range(n_gpus)]
+        for p in procs:
+            p.start()
+        for p in procs:
+            p.join()
+        codes = [rcs.get(r, p.exitcode if p.exitcode else 1) for r, p in enumerate(procs)]
+    return 0 if all(c == 0 for c in codes) else 1

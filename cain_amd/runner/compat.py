@@ -83,4 +83,16 @@ def install() -> None:
             setattr(leaf, k, v)
     # `from Plugins.Profilers import CodecarbonWrapper` needs the attribute on the package
     sys.modules["Plugins.Profilers"].CodecarbonWrapper = sys.modules["Plugins.Profilers.CodecarbonWrapper"]
+    # python-dotenv is not installed in this image; the reference config imports it
+    # (experiment/RunnerConfig.py:22) — serve the same two names from cain_amd.utils.env
+    try:
+        import dotenv  # noqa: F401
+    except ImportError:
+        from ..utils import env as _env
+
+        mod = types.ModuleType("dotenv")
+        mod.load_dotenv = _env.load_dotenv
+        mod.dotenv_values = _env.dotenv_values
+        mod.__cain_alias__ = True
+        sys.modules["dotenv"] = mod
     _installed = True

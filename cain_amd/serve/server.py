@@ -1,0 +1,460 @@
+"""Ollama-compatible HTTP server over the decode engine.
+
+The reference's both arms talk to an Ollama server on port 11434
+(experiment/RunnerConfig.py:122-131; ``POST /api/generate`` with
+``{"model", "prompt", "stream": false}``).  This module is that server, backed
+by ``cain_amd.engine.DecodeEngine`` (HIP kernels on the GPU this process owns),
+so the on-device arm (localhost) and the remote arm (another GPU / host) speak
+the same protocol as the reference.  SURVEY §2.3 row 1, §5.8.
+
+Endpoints: ``POST /api/generate`` (stream NDJSON or one JSON), ``POST /api/chat``,
+``GET /api/tags``, ``POST /api/show``, ``GET /api/ps``, ``GET /api/version``,
+``POST /api/pull`` (no-op: weights are random-init, nothing is downloaded),
+``GET /`` ("Ollama is running").  Response statistics use Ollama's field names
+and units (ns): ``total_duration``, ``load_duration``, ``prompt_eval_count``,
+``prompt_eval_duration``, ``eval_count``, ``eval_duration``.
+
+Concurrency: requests for the same model that arrive within ``batch_window_ms``
+are decoded together as one batch (up to the engine's ``max_batch``) — trial
+batching on the server side.  One worker thread per model owns
+the GPU work; HTTP handler threads only enqueue and stream results back.
+
+Length policy: random weights rarely emit EOS, so when a request does not set
+``options.num_predict`` the server derives it from the prompt: "In N words ..."
+(the study's prompt template, experiment/RunnerConfig.py:120) maps to
+⌈4/3·N⌉ tokens; anything else gets 128 tokens.
+"""
+from __future__ import annotations
+
+import argparse
+import datetime
+import json
+import queue
+import re
+import sys
+import threading
+import time
+from dataclasses import dataclass, field
+from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
+from typing import Any, Callable, Dict, List, Optional
+
+from ..models.tokenizer import tokens_for_words
+
+VERSION = "0.5.0-cain-amd"
+_WORDS = re.compile(r"\bin\s+(\d+)\s+words\b", re.IGNORECASE)
+DEFAULT_NUM_PREDICT = 128
+
+
+def default_num_predict(prompt: str) -> int:
+    m = _WORDS.search(prompt or "")
+    return tokens_for_words(int(m.group(1))) if m else DEFAULT_NUM_PREDICT
+
+
+def _now() -> str:
+    return datetime.datetime.now(datetime.timezone.utc).isoformat().replace("+00:00", "Z")
+
+
+@dataclass
+class Job:
+    model: str
+    prompt: Any                      # str or token ids
+    num_predict: int
+    options: Dict[str, Any]
+    stream: Optional[Callable[[str], None]] = None   # receives text pieces
+    done: threading.Event = field(default_factory=threading.Event)
+    result: Any = None
+    error: Optional[BaseException] = None
+    t_submit: float = field(default_factory=time.perf_counter)
+
+
+class Backend:
+    """Interface: decode a batch of jobs for one model."""
+
+    def models(self) -> List[str]:
+        raise NotImplementedError
+
+    def run(self, model: str, jobs: List[Job]) -> None:
+        raise NotImplementedError
+
+    def max_batch(self, model: str) -> int:
+        return 1
+
+    def model_info(self, model: str) -> Dict[str, Any]:
+        return {}
+
+
+class EngineBackend(Backend):
+    """Backed by one DecodeEngine per model on ``device`` (created on first use, then resident)."""
+
+    def __init__(self, models: List[str], device: str = "cuda:0", max_batch: int = 16, max_context: int = 2048,
+                 backend: Optional[str] = None, seed: int = 0, preload: bool = False, steps_per_graph: int = 8):
+        self._models = list(models)
+        self.device = device
+        self._max_batch = max_batch
+        self.max_context = max_context
+        self.backend = backend
+        self.seed = seed
+        self.steps_per_graph = steps_per_graph
+        self.engines: Dict[str, Any] = {}
+        self._lock = threading.Lock()
+        if preload:
+            for m in self._models:
+                self.engine(m)
+
+    def models(self) -> List[str]:
+        return list(self._models)
+
+    def max_batch(self, model: str) -> int:
+        return self._max_batch
+
+    def engine(self, model: str):
+        from ..engine import DecodeEngine
+
+        with self._lock:
+            eng = self.engines.get(model)
+            if eng is None:
+                if model not in self._models:
+                    raise KeyError(f"model '{model}' not found, try pulling it first")
+                eng = DecodeEngine(model, device=self.device, max_batch=self._max_batch,
+                                   max_context=self.max_context, backend=self.backend, seed=self.seed,
+                                   steps_per_graph=self.steps_per_graph)
+                self.engines[model] = eng
+            return eng
+
+    def model_info(self, model: str) -> Dict[str, Any]:
+        from ..models import get_config
+
+        cfg = get_config(model)
+        return {"details": {"family": cfg.name.split(":")[0], "parameter_size": f"{cfg.n_params() / 1e9:.1f}B",
+                            "quantization_level": "BF16", "format": "cain-packed"},
+                "model_info": cfg.as_dict()}
+
+    def run(self, model: str, jobs: List[Job]) -> None:
+        eng = self.engine(model)
+        tok = eng.tokenizer
+        streams = [j.stream for j in jobs]
+
+        def on_tokens(new_per_row: List[List[int]]) -> None:
+            for j, ids in zip(jobs, new_per_row):
+                if j.stream is not None and ids:
+                    j.stream("".join(tok.piece(t) for t in ids))
+
+        res = eng.generate([j.prompt for j in jobs], [j.num_predict for j in jobs], [j.options for j in jobs],
+                           on_tokens=on_tokens if any(streams) else None)
+        ttft = getattr(eng, "last_ttft_ns", 0)
+        for j, r in zip(jobs, res):
+            j.result = r
+            j.ttft_ns = ttft
+
+
+class FakeBackend(Backend):
+    """Canned generations with controllable latency (tests / plumbing runs without a GPU).
+    ``fail`` makes every request raise; ``hang_s`` sleeps before answering (timeout tests)."""
+
+    def __init__(self, models=("qwen2:1.5b",), tokens_per_s: float = 2000.0, prefill_s: float = 0.0,
+                 fail: bool = False, hang_s: float = 0.0):
+        self._models = list(models)
+        self.tokens_per_s = tokens_per_s
+        self.prefill_s = prefill_s
+        self.fail = fail
+        self.hang_s = hang_s
+        self.calls: List[Dict[str, Any]] = []
+
+    def models(self) -> List[str]:
+        return list(self._models)
+
+    def max_batch(self, model: str) -> int:
+        return 8
+
+    def run(self, model: str, jobs: List[Job]) -> None:
+        from ..engine.engine import GenResult
+        from ..models.tokenizer import SyntheticTokenizer
+
+        if self.hang_s:
+            time.sleep(self.hang_s)
+        if self.fail:
+            raise RuntimeError("fake backend failure")
+        tok = SyntheticTokenizer(32000)
+        t0 = time.perf_counter_ns()
+        time.sleep(self.prefill_s)
+        n = max(j.num_predict for j in jobs)
+        time.sleep(n / self.tokens_per_s)
+        dt = time.perf_counter_ns() - t0
+        for i, j in enumerate(jobs):
+            ids = [16 + (i * 131 + k * 7919) % 31000 for k in range(j.num_predict)]
+            text = tok.decode(ids)
+            if j.stream:
+                j.stream(text)
+            prompt_ids = tok.encode(j.prompt) if isinstance(j.prompt, str) else list(j.prompt)
+            j.result = GenResult(model, prompt_ids, ids, text, "length", 0, int(self.prefill_s * 1e9), dt, dt)
+            j.ttft_ns = int(self.prefill_s * 1e9)
+            self.calls.append({"model": model, "prompt": j.prompt, "num_predict": j.num_predict})
+
+
+class Scheduler:
+    """Per-model job queues; a worker thread per model batches jobs that arrive together."""
+
+    def __init__(self, backend: Backend, batch_window_ms: float = 5.0):
+        self.backend = backend
+        self.window = batch_window_ms / 1000.0
+        self.queues: Dict[str, "queue.Queue[Job]"] = {}
+        self.threads: Dict[str, threading.Thread] = {}
+        self.lock = threading.Lock()
+        self.loaded_at: Dict[str, float] = {}
+
+    def submit(self, job: Job) -> Job:
+        if job.model not in self.backend.models():
+            raise KeyError(f"model '{job.model}' not found, try pulling it first")
+        with self.lock:
+            q = self.queues.get(job.model)
+            if q is None:
+                q = self.queues[job.model] = queue.Queue()
+                t = threading.Thread(target=self._worker, args=(job.model, q), daemon=True,
+                                     name=f"cain-sched-{job.model}")
+                self.threads[job.model] = t
+                self.loaded_at[job.model] = time.time()
+                t.start()
+        q.put(job)
+        return job
+
+    def _worker(self, model: str, q: "queue.Queue[Job]") -> None:
+        while True:
+            first = q.get()
+            batch = [first]
+            deadline = time.perf_counter() + self.window
+            cap = self.backend.max_batch(model)
+            while len(batch) < cap:
+                rem = deadline - time.perf_counter()
+                if rem <= 0:
+                    break
+                try:
+                    batch.append(q.get(timeout=rem))
+                except queue.Empty:
+                    break
+            try:
+                self.backend.run(model, batch)
+            except BaseException as exc:  # noqa: BLE001 - reported per job
+                for j in batch:
+                    j.error = exc
+            for j in batch:
+                j.done.set()
+
+
+def _result_json(job: Job, created: Optional[str] = None) -> Dict[str, Any]:
+    r = job.result
+    d = r.ollama_json(created or _now())
+    d["cain_ttft_ns"] = int(getattr(job, "ttft_ns", 0))
+    return d
+
+
+class OllamaHandler(BaseHTTPRequestHandler):
+    server_version = "cain-amd-ollama/" + VERSION
+    protocol_version = "HTTP/1.1"
+    scheduler: Scheduler = None  # set by make_server
+
+    def log_message(self, fmt, *args):  # keep stdout for the experiment logs
+        if getattr(self.server, "verbose", False):
+            sys.stderr.write("[serve] " + (fmt % args) + "\n")
+
+    # -- helpers -------------------------------------------------------------
+    def _send_json(self, code: int, obj: Any) -> None:
+        body = json.dumps(obj).encode()
+        self.send_response(code)
+        self.send_header("Content-Type", "application/json; charset=utf-8")
+        self.send_header("Content-Length", str(len(body)))
+        self.end_headers()
+        self.wfile.write(body)
+
+    def _body(self) -> Dict[str, Any]:
+        n = int(self.headers.get("Content-Length") or 0)
+        raw = self.rfile.read(n) if n else b""
+        if not raw:
+            return {}
+        return json.loads(raw.decode("utf-8"))
+
+    # -- routes ----------------------------------------------------------------
+    def do_GET(self):  # noqa: N802
+        if self.path in ("/", ""):
+            body = b"Ollama is running"
+            self.send_response(200)
+            self.send_header("Content-Type", "text/plain")
+            self.send_header("Content-Length", str(len(body)))
+            self.end_headers()
+            self.wfile.write(body)
+        elif self.path == "/api/version":
+            self._send_json(200, {"version": VERSION})
+        elif self.path == "/api/tags":
+            be = self.scheduler.backend
+            self._send_json(200, {"models": [{"name": m, "model": m, "modified_at": _now(), "size": 0,
+                                              "details": be.model_info(m).get("details", {})} for m in be.models()]})
+        elif self.path == "/api/ps":
+            self._send_json(200, {"models": [{"name": m, "model": m,
+                                              "expires_at": "2999-01-01T00:00:00Z"}
+                                             for m in self.scheduler.queues]})
+        else:
+            self._send_json(404, {"error": "not found"})
+
+    def do_POST(self):  # noqa: N802
+        try:
+            body = self._body()
+        except (ValueError, UnicodeDecodeError) as exc:
+            return self._send_json(400, {"error": f"invalid JSON: {exc}"})
+        if self.path == "/api/generate":
+            return self._generate(body, chat=False)
+        if self.path == "/api/chat":
+            return self._generate(body, chat=True)
+        if self.path == "/api/show":
+            m = body.get("model") or body.get("name")
+            if m not in self.scheduler.backend.models():
+                return self._send_json(404, {"error": f"model '{m}' not found"})
+            return self._send_json(200, self.scheduler.backend.model_info(m))
+        if self.path == "/api/pull":
+            m = body.get("model") or body.get("name")
+            ok = m in self.scheduler.backend.models()
+            return self._send_json(200 if ok else 404, {"status": "success"} if ok else {"error": "unknown model"})
+        return self._send_json(404, {"error": "not found"})
+
+    def _generate(self, body: Dict[str, Any], chat: bool) -> None:
+        model = body.get("model")
+        if not model:
+            return self._send_json(400, {"error": "model is required"})
+        if chat:
+            msgs = body.get("messages") or []
+            prompt = "\n".join(f"{m.get('role', 'user')}: {m.get('content', '')}" for m in msgs)
+        else:
+            prompt = body.get("prompt", "")
+            if body.get("system"):
+                prompt = f"{body['system']}\n{prompt}"
+        opts = dict(body.get("options") or {})
+        n = opts.get("num_predict")
+        num_predict = int(n) if n is not None and int(n) > 0 else default_num_predict(prompt)
+        stream = body.get("stream", True)
+        created = _now()
+        chunks: "queue.Queue[str]" = queue.Queue()
+        job = Job(model, prompt, num_predict, opts, stream=chunks.put if stream else None)
+        try:
+            self.scheduler.submit(job)
+        except KeyError as exc:
+            return self._send_json(404, {"error": str(exc).strip("'\"")})
+        if not stream:
+            job.done.wait()
+            if job.error is not None:
+                return self._send_json(500, {"error": str(job.error)})
+            d = _result_json(job, created)
+            if chat:
+                d["message"] = {"role": "assistant", "content": d.pop("response")}
+            return self._send_json(200, d)
+        # NDJSON streaming (chunked transfer encoding)
+        self.send_response(200)
+        self.send_header("Content-Type", "application/x-ndjson")
+        self.send_header("Transfer-Encoding", "chunked")
+        self.end_headers()
+
+        def emit(obj) -> None:
+            data = (json.dumps(obj) + "\n").encode()
+            self.wfile.write(f"{len(data):x}\r\n".encode() + data + b"\r\n")
+            self.wfile.flush()
+
+        while not (job.done.is_set() and chunks.empty()):
+            try:
+                piece = chunks.get(timeout=0.05)
+            except queue.Empty:
+                continue
+            part = {"model": model, "created_at": _now(), "done": False}
+            if chat:
+                part["message"] = {"role": "assistant", "content": piece}
+            else:
+                part["response"] = piece
+            emit(part)
+        if job.error is not None:
+            emit({"error": str(job.error)})
+        else:
+            d = _result_json(job, created)
+            d["response"] = ""
+            if chat:
+                d.pop("response")
+                d["message"] = {"role": "assistant", "content": ""}
+            emit(d)
+        self.wfile.write(b"0\r\n\r\n")
+        self.wfile.flush()
+
+
+def make_server(backend: Backend, host: str = "127.0.0.1", port: int = 11434, batch_window_ms: float = 5.0,
+                verbose: bool = False) -> ThreadingHTTPServer:
+    sched = Scheduler(backend, batch_window_ms)
+    handler = type("BoundOllamaHandler", (OllamaHandler,), {"scheduler": sched})
+    srv = ThreadingHTTPServer((host, port), handler)
+    srv.daemon_threads = True
+    srv.verbose = verbose
+    srv.scheduler = sched
+    return srv
+
+
+class ServerThread:
+    """Run a server in a background thread (tests, in-process remote arm)."""
+
+    def __init__(self, backend: Backend, host: str = "127.0.0.1", port: int = 0, **kw):
+        self.server = make_server(backend, host, port, **kw)
+        self.thread = threading.Thread(target=self.server.serve_forever, daemon=True, name="cain-ollama")
+
+    @property
+    def url(self) -> str:
+        h, p = self.server.server_address[:2]
+        return f"http://{h}:{p}"
+
+    def __enter__(self):
+        self.thread.start()
+        return self
+
+    def __exit__(self, *exc):
+        self.server.shutdown()
+        self.server.server_close()
+
+
+def main(argv: Optional[List[str]] = None) -> None:
+    from ..models import MODELS, TINY
+
+    ap = argparse.ArgumentParser(prog="python -m cain_amd serve")
+    ap.add_argument("--host", default="127.0.0.1")
+    ap.add_argument("--port", type=int, default=11434)
+    ap.add_argument("--models", default=",".join(MODELS), help="comma-separated model tags to serve")
+    ap.add_argument("--device", default="cuda:0")
+    ap.add_argument("--max-batch", type=int, default=16)
+    ap.add_argument("--max-context", type=int, default=2048)
+    ap.add_argument("--batch-window-ms", type=float, default=5.0)
+    ap.add_argument("--backend", choices=["hip", "torch", "fake"], default=None)
+    ap.add_argument("--preload", action="store_true", help="load every model at startup (all stay resident)")
+    ap.add_argument("-v", "--verbose", action="store_true")
+    ns = ap.parse_args(argv)
+    models = [m for m in ns.models.split(",") if m]
+    for m in models:
+        if m not in MODELS and m not in TINY:
+            raise SystemExit(f"unknown model {m}")
+    if ns.backend == "fake":
+        be: Backend = FakeBackend(models)
+    else:
+        be = EngineBackend(models, device=ns.device, max_batch=ns.max_batch, max_context=ns.max_context,
+                           backend=ns.backend, preload=ns.preload)
+    srv = make_server(be, ns.host, ns.port, ns.batch_window_ms, ns.verbose)
+    print(f"[serve] Ollama-compatible API on http://{ns.host}:{srv.server_address[1]} models={models}", flush=True)
+    try:
+        srv.serve_forever()
+    except KeyboardInterrupt:  # pragma: no cover
+        pass
+
+
+def generate_main(argv: Optional[List[str]] = None) -> None:
+    """``python -m cain_amd generate --model M --prompt P``: one local generation, Ollama JSON on stdout."""
+    ap = argparse.ArgumentParser(prog="python -m cain_amd generate")
+    ap.add_argument("--model", required=True)
+    ap.add_argument("--prompt", required=True)
+    ap.add_argument("--num-predict", type=int, default=None)
+    ap.add_argument("--device", default="cuda:0")
+    ap.add_argument("--temperature", type=float, default=None)
+    ap.add_argument("--seed", type=int, default=None)
+    ns = ap.parse_args(argv)
+    be = EngineBackend([ns.model], device=ns.device, max_batch=1)
+    opts = {k: v for k, v in (("temperature", ns.temperature), ("seed", ns.seed)) if v is not None}
+    job = Job(ns.model, ns.prompt, ns.num_predict or default_num_predict(ns.prompt), opts)
+    be.run(ns.model, [job])
+    print(json.dumps(_result_json(job)))

@@ -1,0 +1,108 @@
+"""Energy sampler / meter / plugin on hosts without a GPU (the amd-smi path runs in the GPU tests)."""
+import math
+import time
+from pathlib import Path
+
+import pytest
+
+from cain_amd.energy import DataColumns, EnergyMeter, emission_tracker, native
+from cain_amd.energy.meter import EnergyReading
+from cain_amd.energy.plugin import column_values
+from cain_amd.energy.wattsup import WattsUpPro, parse_frame
+from cain_amd.runner.models import FactorModel, RunnerContext, RunTableModel
+
+
+def test_native_sampler_host_metrics():
+    s = native.NativeSampler([], period_ms=10, fast_period_ms=1)
+    s.start()
+    x = 0
+    t_end = time.time() + 0.15
+    while time.time() < t_end:  # keep one core busy so cpu% > 0
+        x += 1
+    s.stop()
+    smp = s.drain()
+    s.close()
+    assert len(smp) >= 5
+    assert all(sm["gpu"] == -1 for sm in smp)
+    mem = [sm["mem_pct"] for sm in smp]
+    assert all(0 < m < 100 for m in mem)
+    assert any(sm["cpu_pct"] > 0 for sm in smp if not math.isnan(sm["cpu_pct"]))
+
+
+def test_meter_window_cpu_model_without_gpu():
+    m = EnergyMeter(smi_indices=[], period_ms=10, cpu_tdp_w=100.0, sources=("gpu", "cpu"))
+    m.start()
+    time.sleep(0.2)
+    r = m.stop(settle_ms=0)
+    m.close()
+    assert 0.19 < r.duration_s < 0.5
+    assert r.gpu_energy_j == 0.0 and r.cpu_energy_source in ("model", "rapl")
+    assert r.total_energy_j == pytest.approx(r.gpu_energy_j + r.cpu_energy_j + r.ram_energy_j)
+    assert 0 < r.memory_usage < 100
+
+
+def test_column_values_units():
+    r = EnergyReading(0, int(2e9), 2.0, gpu_energy_j=360.0, cpu_energy_j=36.0, ram_energy_j=0.0,
+                      total_energy_j=396.0, cpu_energy_source="model", gpu_usage=50.0, cpu_usage=5.0,
+                      memory_usage=40.0, gpu_power_w=180.0, vram_usage=1.0, idle_power_w=100.0,
+                      idle_subtracted_j=196.0)
+    v = column_values(r, [DataColumns.ENERGY_CONSUMED, DataColumns.ENERGY_USAGE_J, DataColumns.GPU_ENERGY,
+                          DataColumns.IDLE_SUBTRACTED_J, DataColumns.EMISSIONS], country="NLD")
+    assert v["codecarbon__energy_consumed"] == pytest.approx(396.0 / 3.6e6)
+    assert v["energy_usage_J"] == 396.0 and v["idle_subtracted_J"] == 196.0
+    assert v["codecarbon__gpu_energy"] == pytest.approx(1e-4)
+    assert v["codecarbon__emissions"] == pytest.approx(396.0 / 3.6e6 * 0.328)
+
+
+def test_plugin_decorator_adds_and_fills_columns(tmp_path):
+    @emission_tracker(data_columns=[DataColumns.ENERGY_CONSUMED, DataColumns.ENERGY_USAGE_J],
+                      country_iso_code="NLD", smi_indices=[], period_ms=10, cpu_tdp_w=50.0)
+    class Cfg:
+        name = "x"
+
+        def create_run_table_model(self):
+            self.run_table_model = RunTableModel([FactorModel("f", [1])], data_columns=["topic"])
+            return self.run_table_model
+
+        def start_measurement(self, ctx):
+            self.started = True
+
+        def stop_measurement(self, ctx):
+            self.stopped = True
+
+        def populate_run_data(self, ctx):
+            return {"topic": "t"}
+
+    c = Cfg()
+    m = c.create_run_table_model()
+    assert m.get_data_columns() == ["topic", "codecarbon__energy_consumed", "energy_usage_J"]
+    ctx = RunnerContext({"__run_id": "r"}, 1, tmp_path)
+    c.start_measurement(ctx)
+    time.sleep(0.05)
+    c.stop_measurement(ctx)
+    d = c.populate_run_data(ctx)
+    assert d["topic"] == "t" and d["energy_usage_J"] >= 0 and "codecarbon__energy_consumed" in d
+    assert (Path(tmp_path) / "energy.json").exists()
+    c.__energy_meter__.close()
+
+
+class _FakeSerial:
+    def __init__(self, lines):
+        self.lines = list(lines)
+        self.written = []
+
+    def write(self, b):
+        self.written.append(b)
+
+    def readline(self):
+        return self.lines.pop(0) if self.lines else b""
+
+
+def test_wattsup_parsing_and_integration():
+    assert parse_frame(b"#d,-,18,1234,2301,567,x;\n").watts == pytest.approx(123.4)
+    assert parse_frame(b"garbage") is None
+    frames = [b"#d,-,18,1000,2300,500;\n", b"#d,-,18,1000,2300,500;\n"]
+    w = WattsUpPro(serial_port=_FakeSerial(frames), interval=1.0)
+    s = w.log(timeout=0.05)
+    assert len(s) == 2 and w.energy_j() >= 0.0
+    assert w.s.written[0].startswith(b"#L,W,3,E")

@@ -1,0 +1,80 @@
+"""Data-parallel fan-out on CPU ranks (gloo): shard, gather to the single writer, failure, resume with
+a different world size."""
+import csv
+import os
+import subprocess
+import sys
+import textwrap
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+
+CFG = textwrap.dedent('''
+    import os
+    from pathlib import Path
+    from EventManager.Models.RunnerEvents import RunnerEvents
+    from EventManager.EventSubscriptionController import EventSubscriptionController
+    from ConfigValidator.Config.Models.RunTableModel import RunTableModel
+    from ConfigValidator.Config.Models.FactorModel import FactorModel
+    from ConfigValidator.Config.Models.OperationType import OperationType
+
+    OUT = Path(os.environ["CAIN_TEST_OUT"])
+
+    class RunnerConfig:
+        name = "dp"
+        results_output_path = OUT
+        operation_type = OperationType.AUTO
+        time_between_runs_in_ms = 0
+
+        def __init__(self):
+            EventSubscriptionController.subscribe_to_multiple_events([
+                (RunnerEvents.START_RUN, self.start_run),
+                (RunnerEvents.POPULATE_RUN_DATA, self.populate),
+                (RunnerEvents.AFTER_EXPERIMENT, self.after)])
+
+        def create_run_table_model(self):
+            self.run_table_model = RunTableModel([FactorModel("model", ["a", "b", "c"]),
+                                                  FactorModel("length", ["100", "500"])],
+                                                 repetitions=2, data_columns=["rank", "pid"], shuffle=True, seed=7)
+            return self.run_table_model
+
+        def start_run(self, ctx):
+            flag = OUT / "failed_once"
+            if ctx.run_variation["__run_id"] == "run_3_repetition_1" and not flag.exists():
+                flag.touch()
+                raise RuntimeError("injected")
+
+        def populate(self, ctx):
+            return {"rank": ctx.rank, "pid": os.getpid()}
+
+        def after(self):
+            (OUT / "after_ran").write_text(str(self.dp_rank))
+
+        experiment_path = None
+''')
+
+
+def _run(cfg, gpus, out):
+    env = dict(os.environ, PYTHONPATH=str(ROOT), CAIN_TEST_OUT=str(out), CAIN_DIST_BACKEND="gloo",
+               CAIN_ASSUME_YES="1", NO_COLOR="1")
+    return subprocess.run([sys.executable, "-m", "cain_amd", str(cfg), "--gpus", str(gpus)], capture_output=True,
+                          text=True, env=env, timeout=240)
+
+
+def test_fanout_two_ranks_then_resume_on_one(tmp_path):
+    cfg = tmp_path / "cfg.py"
+    cfg.write_text(CFG)
+    r = _run(cfg, 2, tmp_path)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    rows = list(csv.DictReader(open(tmp_path / "dp" / "run_table.csv")))
+    assert len(rows) == 12
+    done = [x for x in rows if x["__done"] == "DONE"]
+    assert len(done) == 11 and {x["rank"] for x in done} == {"0", "1"}
+    assert [x["__run_id"] for x in rows if x["__done"] == "TODO"] == ["run_3_repetition_1"]
+    assert (tmp_path / "after_ran").read_text() == "0"  # AFTER_EXPERIMENT on the writer only
+    r = _run(cfg, 1, tmp_path)
+    assert r.returncode == 0, r.stdout[-2000:]
+    rows2 = list(csv.DictReader(open(tmp_path / "dp" / "run_table.csv")))
+    assert all(x["__done"] == "DONE" for x in rows2)
+    assert [x["__run_id"] for x in rows2] == [x["__run_id"] for x in rows]  # order preserved
+    assert r.stdout.count("NEW RUN") == 1
