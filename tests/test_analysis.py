@@ -1,0 +1,125 @@
+"""Golden test of the analysis module against every published number of the paper's R notebook
+(`data-analysis/analysis-visualization.ipynb:524-531, 1062-1067, 1307-1311, 1714-1720`),
+recomputed from the reference's own run table (tests/fixtures/run_table.csv, data only)."""
+import itertools
+import subprocess
+import sys
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+from cain_amd.analysis import stats as S
+from cain_amd.analysis.report import analyze, load_run_table, make_subsets
+
+FIX = Path(__file__).parent / "fixtures" / "run_table.csv"
+
+# (length, method) -> n, energy mean/median/sd, time mean/median/sd (ipynb:524-531)
+SUMMARY = {
+    ("short", "on_device"): (167, 52.82, 55.00, 20.94, 15.07, 15.47, 3.44),
+    ("short", "remote"): (175, 15.18, 14.30, 5.86, 8.90, 8.76, 0.97),
+    ("medium", "on_device"): (182, 349.34, 403.80, 179.15, 35.99, 38.77, 12.16),
+    ("medium", "remote"): (160, 41.01, 47.55, 14.18, 13.17, 14.21, 2.35),
+    ("long", "on_device"): (191, 431.97, 462.50, 246.92, 43.35, 43.19, 18.50),
+    ("long", "remote"): (162, 48.56, 47.80, 19.86, 14.38, 14.30, 3.29),
+}
+H1 = {"short": ("28370", 0.941, 0.905, 0.964), "medium": ("28486", 0.956, 0.920, 0.976),
+      "long": ("29587", 0.912, 0.868, 0.942)}
+H2 = {  # rho time, cpu, gpu, memory (ipynb:1714-1720)
+    "on_device_short": (0.991, -0.708, -0.176, 0.541), "on_device_medium": (0.928, -0.284, 0.153, 0.520),
+    "on_device_long": (0.986, -0.276, 0.315, 0.536), "remote_short": (0.891, -0.785, -0.647, 0.010),
+    "remote_medium": (0.963, -0.645, -0.723, -0.032), "remote_long": (0.983, -0.710, -0.640, -0.045)}
+SHAPIRO_W = {"on_device_short": 0.9547488, "on_device_medium": 0.8745747, "on_device_long": 0.9290627,
+             "remote_short": 0.8594111, "remote_medium": 0.9094642, "remote_long": 0.9322779}
+
+
+@pytest.fixture(scope="module")
+def result(tmp_path_factory):
+    return analyze(FIX, tmp_path_factory.mktemp("an"), quiet=True)
+
+
+def test_summary_table_matches_paper(result):
+    for r in result["summary"]:
+        exp = SUMMARY[(r["length"], r["method"])]
+        got = (r["n"], r["energy_usage_J"]["mean"], r["energy_usage_J"]["median"], r["energy_usage_J"]["sd"],
+               r["execution_time"]["mean"], r["execution_time"]["median"], r["execution_time"]["sd"])
+        assert got[0] == exp[0]
+        assert [f"{v:.2f}" for v in got[1:]] == [f"{v:.2f}" for v in exp[1:]]
+
+
+def test_h1_wilcoxon_and_cliff(result):
+    for r in result["h1"]:
+        w, d, lo, hi = H1[r["length"]]
+        assert f"{r['W']:.0f}" == w and r["p"] < 2.2e-16 and r["magnitude"] == "Large"
+        assert (f"{r['cliffs_delta']:.3f}", f"{r['lower_ci']:.3f}", f"{r['upper_ci']:.3f}") == \
+            (f"{d:.3f}", f"{lo:.3f}", f"{hi:.3f}")
+    assert [r["W"] for r in result["h1"]] == [28370.0, 28485.5, 29587.0]
+
+
+def test_h2_spearman(result):
+    for r in result["h2"]:
+        exp = H2[f"{r['method']}_{r['length']}"]
+        got = tuple(round(r[k]["rho"], 3) for k in ("execution_time", "cpu_usage", "gpu_usage", "memory_usage"))
+        assert got == pytest.approx(exp, abs=1e-9)
+    rs = {f"{r['method']}_{r['length']}": r for r in result["h2"]}
+    assert rs["on_device_short"]["gpu_usage"]["stars"] == "*"
+    assert f"{rs['remote_short']['memory_usage']['p']:.3f}" == "0.893"
+    assert f"{rs['remote_long']['memory_usage']['p']:.3f}" == "0.570"
+
+
+def test_shapiro_and_skew(result):
+    for r in result["shapiro"]:
+        if "W" in r:
+            assert round(r["W"], 7) == SHAPIRO_W[r["subset"]] and r["p"] <= 3.3e-5
+    sk = {r["subset"]: r for r in result["shapiro"] if "skew_on_device" in r}
+    assert sk["short"]["transforms"] == []  # arms skew differently -> no transformation (ipynb output)
+    assert [t["name"] for t in sk["medium"]["transforms"]] == ["Original", "Power 2", "Power 3"]
+    assert sk["medium"]["transforms"][0]["p_on_device"] == pytest.approx(3.521535e-11, rel=1e-4)
+
+
+def test_outputs_written(result, tmp_path):
+    out = Path(result["source"]).parent
+    res = analyze(FIX, tmp_path, quiet=True)
+    tex = (tmp_path / "h1.tex").read_text()
+    assert "\\textbf{Short (100 words)} & 28370 & < 2.2e-16 & 0.941 & 0.905 & 0.964 & Large" in tex
+    assert "52.82 & 55.00 & 20.94" in (tmp_path / "summary.tex").read_text()
+    assert len(res["per_model"]) == 42 and (tmp_path / "results.json").exists()
+    llama = [r for r in res["per_model"] if r["model"] == "llama3.1:8b" and r["method"] == "on_device"
+             and r["length"] == 1000][0]
+    assert round(llama["energy_J"], 1) == 764.7 and round(llama["time_s"], 2) == 69.27
+
+
+def test_quantile_type7_and_iqr():
+    x = [1, 2, 3, 4, 100]
+    assert S.quantile7(x, 0.25) == 2 and S.quantile7(x, 0.75) == 4
+    assert S.quantile7([1, 2], 0.25) == 1.25
+
+
+def test_wilcox_exact_small_sample():
+    x = [1.83, 0.50, 1.62, 2.48, 1.68, 1.88, 1.55, 3.06, 1.30]
+    y = [0.878, 0.647, 0.598, 2.05, 1.06, 1.29, 1.07, 3.14, 1.28]
+    r = S.wilcox_test(x, y)
+    # W counts pairs x>y; 9 x 9 without ties -> exact distribution (R: n < 50 and no ties)
+    assert r.statistic == sum(a > b for a in x for b in y) and r.warning is None and "exact" in r.method
+    x2 = [1.0, 2.0, 2.0, 3.0]
+    r2 = S.wilcox_test(x2, [2.0, 4.0, 5.0])
+    assert r2.warning  # ties force the normal approximation, like R
+
+
+def test_spearman_edgeworth_matches_enumeration():
+    n = 10
+    perms = np.array(list(itertools.permutations(range(1, n + 1))), dtype=np.int16)
+    ss = np.sum((perms - np.arange(1, n + 1)) ** 2, axis=1)
+    for s in (100, 150, 200, 260):
+        assert S._spearman_upper_edgeworth(s, n) == pytest.approx(np.mean(ss >= s), abs=1e-3)
+    r = S.spearman_test([1, 2, 3, 4, 5], [5, 6, 7, 8, 7.5])
+    assert r.statistic == pytest.approx(0.9) and r.warning is None
+
+
+def test_cli_analyze(tmp_path):
+    r = subprocess.run([sys.executable, "-m", "cain_amd", "analyze", str(FIX), "--out", str(tmp_path), "--plots"],
+                       capture_output=True, text=True, timeout=300, cwd=Path(__file__).parent.parent)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "28370" in r.stdout
+    assert (tmp_path / "scatter_plots" / "cpu_usage_vs_energy_usage_J.pdf").exists()
+    assert (tmp_path / "violin_plots" / "combined_violin_plots_llms_energy_usage_J.pdf").exists()
