@@ -109,7 +109,8 @@ class _CainPlanDesc(ctypes.Structure):
                 + [(n, ctypes.c_void_p) for n in ("embed", "final_norm", "lm_head", "layers", "kcache", "vtcache")]
                 + [("kv_layer_elems", ctypes.c_longlong)]
                 + [(n, ctypes.c_void_p) for n in ("cos_t", "sin_t", "x", "q", "attn", "act", "logits",
-                                                 "part_o", "part_ml", "counters")])
+                                                 "part_o", "part_ml", "counters", "gemm_ws")]
+                + [("gemm_ws_bytes", ctypes.c_longlong)])
 
 
 class _CainRows(ctypes.Structure):
@@ -218,6 +219,12 @@ class DecodeEngine:
         for k in ("x", "q", "attn", "act", "logits", "counters"):
             setattr(d, k, _ptr(self.buf[k]))
         d.part_o, d.part_ml = _ptr(self.part_o), _ptr(self.part_ml)
+        # batched GEMM (16 < M <= 64) split-K workspace: largest need over this model's GEMM shapes
+        shapes = [(cfg.qkv_dim, cfg.d_model), (cfg.d_model, cfg.q_dim), (2 * cfg.ffn, cfg.d_model),
+                  (cfg.d_model, cfg.ffn), (cfg.vocab, cfg.d_model)]
+        ws = max([ops.gemm_ws_bytes(n, k, m) for n, k in shapes for m in range(17, R + 1)] + [0])
+        self.gemm_ws = torch.zeros(max(ws, 16) // 4 + 1, device=dev, dtype=torch.int32)
+        d.gemm_ws, d.gemm_ws_bytes = _ptr(self.gemm_ws), ws
         self._desc = d
         self._plans: Dict[int, int] = {}
         self._graphs: Dict[tuple, int] = {}

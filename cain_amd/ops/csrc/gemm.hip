@@ -33,6 +33,9 @@
 //   EPI_QKV_ROPE  fused QKV epilogue: + bias, RoPE (rows pre-permuted so each
 //                 16-row tile holds 8 rotation pairs), Q -> q buffer, K -> K cache
 //                 at (slot[m], pos[m]), V -> transposed V cache.
+#include <algorithm>
+#include <cstdlib>
+
 #include "common.h"
 
 enum { EPI_BF16 = 0, EPI_RESID = 1, EPI_F32 = 2, EPI_SILU = 3, EPI_GELU = 4, EPI_QKV_ROPE = 5 };
@@ -68,20 +71,17 @@ struct EpiIn {
   int p, sl;     // QKV: position, cache slot
 };
 
-template <int NT, int NB, int EPI>
-__device__ __forceinline__ EpiIn epi_load(const GemmArgs& a, int tile0, int mo, int u) {
+// gt = global 16-row tile of N, m = output row of this lane
+template <int EPI>
+__device__ __forceinline__ EpiIn epi_load_at(const GemmArgs& a, int gt, int m, int lane) {
   EpiIn e{};
-  const int lane = u & 63, tb = u >> 6, b = tb % NB, t = tb / NB;
-  const int m = mo + b * 16 + (lane & 15);
   const int nsub = (lane >> 4) * 4;
   if (m >= a.M) return e;
   if constexpr (EPI == EPI_RESID) {
-    e.r = *reinterpret_cast<const bf16x4*>(reinterpret_cast<const __bf16*>(a.Y) + (size_t)m * a.ldy +
-                                           (tile0 + t) * 16 + nsub);
+    e.r = *reinterpret_cast<const bf16x4*>(reinterpret_cast<const __bf16*>(a.Y) + (size_t)m * a.ldy + gt * 16 + nsub);
   } else if constexpr (EPI == EPI_BF16) {
-    if (a.bias) e.b1 = *reinterpret_cast<const f32x4*>(a.bias + (tile0 + t) * 16 + nsub);
+    if (a.bias) e.b1 = *reinterpret_cast<const f32x4*>(a.bias + gt * 16 + nsub);
   } else if constexpr (EPI == EPI_QKV_ROPE) {
-    const int gt = tile0 + t;
     e.sl = a.slot[m];
     e.p = a.pos[m];
     if (a.bias) {
@@ -97,6 +97,91 @@ __device__ __forceinline__ EpiIn epi_load(const GemmArgs& a, int tile0, int mo, 
     }
   }
   return e;
+}
+
+template <int NT, int NB, int EPI>
+__device__ __forceinline__ EpiIn epi_load(const GemmArgs& a, int tile0, int mo, int u) {
+  const int lane = u & 63, tb = u >> 6, b = tb % NB, t = tb / NB;
+  return epi_load_at<EPI>(a, tile0 + t, mo + b * 16 + (lane & 15), lane);
+}
+
+// Finish and store one 64-unit chunk (one 16x16 output block: n in tile gt, 16 rows m).
+// get(off) returns the final fp32 accumulator of the unit held by lane (lane + off) of the
+// chunk; the pair epilogues read their partner rows (+8 of the tile) at off = 32.
+template <int EPI, class Get>
+__device__ __forceinline__ void epi_store(const GemmArgs& a, int gt, int m, int lane, const EpiIn& e, Get get) {
+  const int nsub = (lane >> 4) * 4;
+  const bool mvalid = m < a.M;
+  if constexpr (EPI == EPI_SILU || EPI == EPI_GELU) {
+    // 8-row interleave: rows 0..7 of a tile are gate rows, rows 8..15 the matching up rows
+    if ((lane >> 4) < 2) {
+      const f32x4 g = get(0);
+      const f32x4 up = get(32);
+      const int n = gt * 8 + nsub;
+      bf16x4 o;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float av = (EPI == EPI_SILU) ? silu_f(g[i]) : gelu_tanh_f(g[i]);
+        o[i] = f2bf(av * up[i]);
+      }
+      if (mvalid) *reinterpret_cast<bf16x4*>(reinterpret_cast<__bf16*>(a.Y) + (size_t)m * a.ldy + n) = o;
+    }
+  } else if constexpr (EPI == EPI_QKV_ROPE) {
+    const int tph = a.hd >> 4;  // tiles per head
+    const int qt = a.H * tph, kt = a.Hkv * tph;
+    const int sl = mvalid ? e.sl : -1;
+    if (gt < qt + kt) {
+      // rows 0..7 of the tile = pair elements j (first half), rows 8..15 = j + hd/2
+      if ((lane >> 4) < 2 && sl >= 0) {
+        const f32x4 x1 = get(0);
+        const f32x4 x2 = get(32);  // partner rows +8 live in lane + 32
+        const int head = gt / tph, it = gt - (gt / tph) * tph;
+        const int half = a.hd >> 1;
+        const int j0 = it * 8 + nsub;  // first pair element of this thread
+        bf16x4 y1, y2;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          // round to bf16 first: the unfused path stores the projection in bf16 before RoPE
+          const float v1 = bf2f(f2bf(x1[i] + e.b1[i]));
+          const float v2 = bf2f(f2bf(x2[i] + e.b2[i]));
+          y1[i] = f2bf(v1 * e.c[i] - v2 * e.sn[i]);
+          y2[i] = f2bf(v2 * e.c[i] + v1 * e.sn[i]);
+        }
+        __bf16* dst;
+        if (head < a.H)
+          dst = reinterpret_cast<__bf16*>(a.Y) + (size_t)m * a.ldy + head * a.hd;
+        else
+          dst = a.kc + (((size_t)sl * a.Hkv + (head - a.H)) * a.T_max + e.p) * a.hd;
+        *reinterpret_cast<bf16x4*>(dst + j0) = y1;
+        *reinterpret_cast<bf16x4*>(dst + j0 + half) = y2;
+      }
+    } else if (sl >= 0) {
+      const f32x4 v = get(0);
+      const int vr = (gt - qt - kt) * 16 + nsub;  // row within the V block
+      const int kh = vr / a.hd, d = vr - (vr / a.hd) * a.hd;
+      __bf16* dst = a.vtc + (((size_t)sl * a.Hkv + kh) * a.hd + d) * a.T_max + e.p;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) dst[(size_t)i * a.T_max] = f2bf(v[i] + e.b1[i]);
+    }
+  } else {
+    const f32x4 v = get(0);
+    const int n = gt * 16 + nsub;
+    if constexpr (EPI == EPI_F32) {
+      if (mvalid) *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(a.Y) + (size_t)m * a.ldy + n) = v;
+    } else if constexpr (EPI == EPI_BF16) {
+      bf16x4 o;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) o[i] = f2bf(v[i] + e.b1[i]);
+      if (mvalid) *reinterpret_cast<bf16x4*>(reinterpret_cast<__bf16*>(a.Y) + (size_t)m * a.ldy + n) = o;
+    } else {  // EPI_RESID: in-place residual update
+      if (mvalid) {
+        bf16x4 o;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) o[i] = f2bf(v[i] + bf2f(e.r[i]));
+        *reinterpret_cast<bf16x4*>(reinterpret_cast<__bf16*>(a.Y) + (size_t)m * a.ldy + n) = o;
+      }
+    }
+  }
 }
 
 template <int NT, int NB, int WAVES, int U, int EPI, bool NORM>
@@ -284,80 +369,8 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_gemm_kernel(const GemmArgs 
     const int b = tb % NB;
     const int t = tb / NB;
     const int m = mo + b * 16 + (lane & 15);
-    const int nsub = (lane >> 4) * 4;
-    const bool mvalid = m < a.M;
     const EpiIn e = (PRE && ub == wave * 64) ? pre : epi_load<NT, NB, EPI>(a, tile0, mo, u);
-    if constexpr (EPI == EPI_SILU || EPI == EPI_GELU) {
-      // 8-row interleave: rows 0..7 of a tile are gate rows, rows 8..15 the matching up rows
-      if ((lane >> 4) < 2) {
-        const f32x4 g = unit_sum(u);
-        const f32x4 up = unit_sum(u + 32);
-        const int n = (tile0 + t) * 8 + nsub;
-        bf16x4 o;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const float av = (EPI == EPI_SILU) ? silu_f(g[i]) : gelu_tanh_f(g[i]);
-          o[i] = f2bf(av * up[i]);
-        }
-        if (mvalid) *reinterpret_cast<bf16x4*>(reinterpret_cast<__bf16*>(a.Y) + (size_t)m * a.ldy + n) = o;
-      }
-    } else if constexpr (EPI == EPI_QKV_ROPE) {
-      const int gt = tile0 + t;
-      const int tph = a.hd >> 4;  // tiles per head
-      const int qt = a.H * tph, kt = a.Hkv * tph;
-      const int sl = mvalid ? e.sl : -1;
-      if (gt < qt + kt) {
-        // rows 0..7 of the tile = pair elements j (first half), rows 8..15 = j + hd/2
-        if ((lane >> 4) < 2 && sl >= 0) {
-          const f32x4 x1 = unit_sum(u);
-          const f32x4 x2 = unit_sum(u + 32);  // partner rows +8 live in lane + 32
-          const int head = gt / tph, it = gt - (gt / tph) * tph;
-          const int half = a.hd >> 1;
-          const int j0 = it * 8 + nsub;  // first pair element of this thread
-          bf16x4 y1, y2;
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            // round to bf16 first: the unfused path stores the projection in bf16 before RoPE
-            const float v1 = bf2f(f2bf(x1[i] + e.b1[i]));
-            const float v2 = bf2f(f2bf(x2[i] + e.b2[i]));
-            y1[i] = f2bf(v1 * e.c[i] - v2 * e.sn[i]);
-            y2[i] = f2bf(v2 * e.c[i] + v1 * e.sn[i]);
-          }
-          __bf16* dst;
-          if (head < a.H)
-            dst = reinterpret_cast<__bf16*>(a.Y) + (size_t)m * a.ldy + head * a.hd;
-          else
-            dst = a.kc + (((size_t)sl * a.Hkv + (head - a.H)) * a.T_max + e.p) * a.hd;
-          *reinterpret_cast<bf16x4*>(dst + j0) = y1;
-          *reinterpret_cast<bf16x4*>(dst + j0 + half) = y2;
-        }
-      } else if (sl >= 0) {
-        const f32x4 v = unit_sum(u);
-        const int vr = (gt - qt - kt) * 16 + nsub;  // row within the V block
-        const int kh = vr / a.hd, d = vr - (vr / a.hd) * a.hd;
-        __bf16* dst = a.vtc + (((size_t)sl * a.Hkv + kh) * a.hd + d) * a.T_max + e.p;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) dst[(size_t)i * a.T_max] = f2bf(v[i] + e.b1[i]);
-      }
-    } else {
-      const f32x4 v = unit_sum(u);
-      const int n = (tile0 + t) * 16 + nsub;
-      if constexpr (EPI == EPI_F32) {
-        if (mvalid) *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(a.Y) + (size_t)m * a.ldy + n) = v;
-      } else if constexpr (EPI == EPI_BF16) {
-        bf16x4 o;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) o[i] = f2bf(v[i] + e.b1[i]);
-        if (mvalid) *reinterpret_cast<bf16x4*>(reinterpret_cast<__bf16*>(a.Y) + (size_t)m * a.ldy + n) = o;
-      } else {  // EPI_RESID: in-place residual update
-        if (mvalid) {
-          bf16x4 o;
-#pragma unroll
-          for (int i = 0; i < 4; ++i) o[i] = f2bf(v[i] + bf2f(e.r[i]));
-          *reinterpret_cast<bf16x4*>(reinterpret_cast<__bf16*>(a.Y) + (size_t)m * a.ldy + n) = o;
-        }
-      }
-    }
+    epi_store<EPI>(a, tile0 + t, m, lane, e, [&](int off) { return unit_sum(u + off); });
   }
 }
 
@@ -425,6 +438,410 @@ static int gemm_dispatch(GemmArgs a, int epi, int norm, int waves, hipStream_t s
   return int(e);
 }
 
+// =====================================================================================================
+// Batched weight-streaming GEMM, 16 < M <= 64 (batched decode, prefill chunks).
+//
+// The skinny kernel's waves split K and each wave reads its own activation fragments straight from L2:
+// at M = 64 that is 4 B of activation traffic per weight byte and the CU's vector-memory path, not HBM,
+// becomes the limit.  Here the waves of a workgroup split N instead (each owns NTW 16-row tiles) and
+// walk the SAME k-range, so the activation chunk X[0..M)[k0..k0+256) is staged ONCE per workgroup into
+// LDS (bf16, already multiplied by the RMSNorm gain, MFMA-B-fragment-major so both the staging write
+// and every ds_read_b128 of a wave are 1 KiB contiguous, conflict-free) and double-buffered: chunk c+1
+// streams in from L2 while chunk c feeds the MFMAs; one barrier per chunk.  Weights still stream from
+// HBM as 1 KiB non-temporal fragment loads, prefetched one slice group ahead in registers.
+//
+// Parallelism: N/(16*NTW*8) row blocks x ksplit k-ranges.  With ksplit > 1 every workgroup publishes
+// its fp32 16x16 blocks (and the RMSNorm partial sums of squares) with write-through stores and the
+// LAST arriving workgroup of a row block adds them up and runs the fused epilogue (same ticket protocol
+// as the attention combine).  Traffic per weight byte: M/(16*NTW*8) activation (L2) + 2M/k_range
+// partials (MALL), against 4 for the skinny kernel at M = 64.
+// =====================================================================================================
+constexpr int BG_WAVES = 8;
+constexpr int BG_CK = 8;  // 32-wide k-slices per LDS chunk (256 k)
+
+struct BgArgs {
+  int ksplit;  // workgroups per row block
+  int kspl;    // k-slices per workgroup (multiple of BG_CK)
+  float* part;       // [nblk][ksplit][BG_WAVES*NTW*NB][64] f32x4  (ksplit > 1)
+  float* part_ss;    // [nblk][ksplit][NB*16]                   (ksplit > 1 && NORM)
+  unsigned* counters;  // [nblk], zero between launches (the reducer resets its own)
+};
+
+__device__ __forceinline__ void st_wt(float* p, const f32x4& v) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) __hip_atomic_store(p + i, v[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ f32x4 ld_wt(const float* p) {
+  f32x4 v;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) v[i] = __hip_atomic_load(p + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return v;
+}
+
+template <int NB, int NTW, int U, int EPI, bool NORM>
+__global__ __launch_bounds__(BG_WAVES * 64) void bgemm_kernel(const GemmArgs a, const BgArgs bg) {
+  constexpr int W = BG_WAVES;
+  constexpr int FR = BG_CK * NB;        // B fragments per chunk
+  constexpr int FPW = FR / W;           // staged per wave per chunk
+  constexpr int NGRP = BG_CK / U;       // weight prefetch groups per chunk
+  constexpr int UNITS = W * NTW * NB;   // 64-lane output blocks per workgroup
+  static_assert(FR % W == 0 && BG_CK % U == 0, "tiling");
+  static_assert(UNITS * 1024 <= 2 * FR * 1024, "epilogue buffer must fit in the staging buffer");
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int KS = a.K >> 5, ntiles = a.N >> 4;
+  int blk, kc;
+  {
+    const int bid = blockIdx.x, ks = bg.ksplit, nblk = gridDim.x / ks;
+    if (ks == 1) {
+      blk = bid, kc = 0;
+    } else if ((nblk & 7) == 0) {  // k-range partners share an XCD (ids differ by multiples of 8)
+      const int r = bid >> 3;
+      kc = r % ks;
+      blk = (r / ks) * 8 + (bid & 7);
+    } else {
+      blk = bid / ks, kc = bid - (bid / ks) * ks;
+    }
+  }
+  const int s_beg = kc * bg.kspl;
+  const int nch = (min(KS, s_beg + bg.kspl) - s_beg) / BG_CK;
+
+  __shared__ __attribute__((aligned(16))) bf16x8 xs[2][FR][64];
+  __shared__ float ss_red[NORM ? W : 1][NORM ? NB * 16 : 1];
+  __shared__ float s_inv[NB * 16];
+  __shared__ unsigned s_ticket;
+
+  int gt[NTW];
+  const bf16x8* wb[NTW];
+#pragma unroll
+  for (int t = 0; t < NTW; ++t) {
+    gt[t] = (blk * W + wave) * NTW + t;
+    wb[t] = a.Wp + (size_t)min(gt[t], ntiles - 1) * KS * 64 + lane;  // idle tiles re-read a valid one
+  }
+  auto load_w = [&](int s, int t) -> bf16x8 { return __builtin_nontemporal_load(wb[t] + (size_t)s * 64); };
+
+  // staging: fragment f = wave + W*i of a chunk is (slice f / NB, row block f % NB); lane reads
+  // X[16*rb + (lane & 15)][32*slice + 8*(lane >> 4) .. +8]  (rows past M re-read row M-1)
+  const __bf16* xrow[FPW];
+  float ssq[FPW];
+#pragma unroll
+  for (int i = 0; i < FPW; ++i) {
+    const int f = wave + W * i, rb = f % NB, sl = f / NB;
+    const int m = min(rb * 16 + (lane & 15), a.M - 1);
+    xrow[i] = a.X + (size_t)m * a.ldx + sl * 32 + ((lane >> 4) << 3);
+    ssq[i] = 0.f;
+  }
+  auto stage_load = [&](int c, bf16x8 (&xr)[FPW], bf16x8 (&gr)[FPW]) {
+    const int k0 = (s_beg + c * BG_CK) * 32;
+#pragma unroll
+    for (int i = 0; i < FPW; ++i) {
+      xr[i] = *reinterpret_cast<const bf16x8*>(xrow[i] + k0);
+      if constexpr (NORM) {
+        const int sl = (wave + W * i) / NB;
+        gr[i] = *reinterpret_cast<const bf16x8*>(a.gain + k0 + sl * 32 + ((lane >> 4) << 3));
+      }
+    }
+  };
+  auto stage_store = [&](int buf, const bf16x8 (&xr)[FPW], const bf16x8 (&gr)[FPW]) {
+#pragma unroll
+    for (int i = 0; i < FPW; ++i) {
+      bf16x8 v = xr[i];
+      if constexpr (NORM) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float f = bf2f(v[j]);
+          ssq[i] += f * f;
+          v[j] = f2bf(f * bf2f(gr[i][j]));
+        }
+      }
+      xs[buf][wave + W * i][lane] = v;
+    }
+  };
+
+  f32x4 acc[NTW][NB];
+#pragma unroll
+  for (int t = 0; t < NTW; ++t)
+#pragma unroll
+    for (int b = 0; b < NB; ++b) acc[t][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  bf16x8 wa[U][NTW];
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+#pragma unroll
+    for (int t = 0; t < NTW; ++t) wa[u][t] = load_w(s_beg + u, t);
+  {
+    bf16x8 xr[FPW], gr[FPW];
+    stage_load(0, xr, gr);
+    stage_store(0, xr, gr);
+  }
+  __syncthreads();
+
+  for (int c = 0; c < nch; ++c) {
+    const int buf = c & 1;
+    const bool more = c + 1 < nch;
+    bf16x8 xr[FPW], gr[FPW];
+    if (more) stage_load(c + 1, xr, gr);
+#pragma unroll
+    for (int h = 0; h < NGRP; ++h) {
+      const int sn = s_beg + c * BG_CK + (h + 1) * U;  // first slice of the next group
+      const bool has = (h + 1 < NGRP) || more;
+      bf16x8 wn[U][NTW];
+      if (has) {
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+          for (int t = 0; t < NTW; ++t) wn[u][t] = load_w(sn + u, t);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        bf16x8 xb[NB];
+#pragma unroll
+        for (int b = 0; b < NB; ++b) xb[b] = xs[buf][(h * U + u) * NB + b][lane];
+#pragma unroll
+        for (int t = 0; t < NTW; ++t)
+#pragma unroll
+          for (int b = 0; b < NB; ++b)
+            acc[t][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[u][t], xb[b], acc[t][b], 0, 0, 0);
+      }
+      if (has) {
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+          for (int t = 0; t < NTW; ++t) wa[u][t] = wn[u][t];
+      }
+    }
+    if (more) stage_store(buf ^ 1, xr, gr);
+    __syncthreads();
+  }
+
+  // ---- per-row sum of squares of this workgroup's k-range (NORM)
+  if constexpr (NORM) {
+    float v[NB];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) v[b] = 0.f;
+#pragma unroll
+    for (int i = 0; i < FPW; ++i) {
+      const int rb = (wave + W * i) % NB;
+#pragma unroll
+      for (int b = 0; b < NB; ++b)
+        if (b == rb) v[b] += ssq[i];
+    }
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      float x = v[b];
+      x += __shfl_xor(x, 16, 64);
+      x += __shfl_xor(x, 32, 64);
+      if (lane < 16) ss_red[wave][b * 16 + lane] = x;
+    }
+  }
+  // the staging buffer becomes the epilogue buffer: red[unit][lane], unit = (wave*NTW + t)*NB + b
+  f32x4* red = reinterpret_cast<f32x4*>(&xs[0][0][0]);
+  if (bg.ksplit == 1) {
+#pragma unroll
+    for (int t = 0; t < NTW; ++t)
+#pragma unroll
+      for (int b = 0; b < NB; ++b) red[((wave * NTW + t) * NB + b) * 64 + lane] = acc[t][b];
+    __syncthreads();
+    if constexpr (NORM) {
+      if (threadIdx.x < NB * 16) {
+        float x = 0.f;
+#pragma unroll
+        for (int w = 0; w < W; ++w) x += ss_red[w][threadIdx.x];
+        s_inv[threadIdx.x] = rsqrtf(x / float(a.K) + a.eps);
+      }
+      __syncthreads();
+    }
+  } else {
+    const size_t pb = (size_t)blk * bg.ksplit;
+    float* mine = bg.part + (pb + kc) * (size_t)UNITS * 256;
+#pragma unroll
+    for (int t = 0; t < NTW; ++t)
+#pragma unroll
+      for (int b = 0; b < NB; ++b) st_wt(mine + ((size_t)((wave * NTW + t) * NB + b) * 64 + lane) * 4, acc[t][b]);
+    if constexpr (NORM) {
+      __syncthreads();  // ss_red complete
+      if (threadIdx.x < NB * 16) {
+        float x = 0.f;
+#pragma unroll
+        for (int w = 0; w < W; ++w) x += ss_red[w][threadIdx.x];
+        __hip_atomic_store(bg.part_ss + (pb + kc) * (NB * 16) + threadIdx.x, x, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    // every storing wave drains, one lane takes a ticket; the last arriver of the row block reduces
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0)
+      s_ticket = __hip_atomic_fetch_add(bg.counters + blk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    if (s_ticket != unsigned(bg.ksplit - 1)) return;
+    // sum the k-range partials, 4 ranges x NTW*NB units of loads in flight per round trip
+    const float* base = bg.part + pb * (size_t)UNITS * 256;
+    f32x4 sum[NTW][NB];
+#pragma unroll
+    for (int t = 0; t < NTW; ++t)
+#pragma unroll
+      for (int b = 0; b < NB; ++b) sum[t][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int k0 = 0; k0 < bg.ksplit; k0 += 4) {
+      f32x4 l[4][NTW][NB];
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int t = 0; t < NTW; ++t)
+#pragma unroll
+          for (int b = 0; b < NB; ++b) {
+            const size_t off = ((size_t)((wave * NTW + t) * NB + b) * 64 + lane) * 4;
+            l[j][t][b] = (k0 + j < bg.ksplit) ? ld_wt(base + (size_t)(k0 + j) * UNITS * 256 + off)
+                                              : f32x4{0.f, 0.f, 0.f, 0.f};
+          }
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int t = 0; t < NTW; ++t)
+#pragma unroll
+          for (int b = 0; b < NB; ++b) sum[t][b] += l[j][t][b];
+    }
+#pragma unroll
+    for (int t = 0; t < NTW; ++t)
+#pragma unroll
+      for (int b = 0; b < NB; ++b) red[((wave * NTW + t) * NB + b) * 64 + lane] = sum[t][b];
+    if constexpr (NORM) {
+      if (threadIdx.x < NB * 16) {
+        float x = 0.f;
+        for (int k = 0; k < bg.ksplit; ++k)
+          x += __hip_atomic_load(bg.part_ss + (pb + k) * (NB * 16) + threadIdx.x, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
+        s_inv[threadIdx.x] = rsqrtf(x / float(a.K) + a.eps);
+      }
+    }
+    if (threadIdx.x == 0) bg.counters[blk] = 0u;  // ready for the next launch (launch-ordered)
+    __syncthreads();
+  }
+
+  // ---- fused epilogue: each wave finishes its own tiles
+#pragma unroll
+  for (int t = 0; t < NTW; ++t) {
+    if (gt[t] >= ntiles) continue;
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      const int ub = ((wave * NTW + t) * NB + b) * 64;
+      const int m = b * 16 + (lane & 15);
+      const EpiIn e = epi_load_at<EPI>(a, gt[t], m, lane);
+      epi_store<EPI>(a, gt[t], m, lane, e, [&](int off) {
+        f32x4 v = red[ub + lane + off];
+        if constexpr (NORM) v *= s_inv[b * 16 + ((lane + off) & 15)];
+        return v;
+      });
+    }
+  }
+}
+
+struct BgPlan {
+  int nb, ntw, nblk, ksplit, kspl;
+  size_t part_floats, ss_floats;
+};
+
+// Launch shape (profiles/bgemm_sweep.md, llama3.1:8b decode shapes at M = 32 / 64):
+//  * NTW = 2 tiles per wave when the grid has >= 512 row blocks anyway (LM head): halves the LDS
+//    fragment reads per weight byte;
+//  * no k-split once >= 128 row blocks exist (gate/up, LM head): the fp32 partials + combine cost more
+//    than the idle CUs;
+//  * otherwise ceil(target / row blocks) k-ranges, target 128 workgroups for K <= 4096 and 256 for longer
+//    K (down projection), at most 8.  Env overrides: CAIN_BGEMM_NTW, CAIN_BGEMM_WG, CAIN_BGEMM_KSMAX.
+static int env_int(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e ? atoi(e) : dflt;
+}
+
+static BgPlan bgemm_plan(int N, int K, int M, int ntw_req) {
+  static const int target_env = env_int("CAIN_BGEMM_WG", 0);
+  static const int ksmax = env_int("CAIN_BGEMM_KSMAX", 8);
+  BgPlan p{};
+  p.nb = M <= 32 ? 2 : 4;
+  const int rows1 = 16 * BG_WAVES;
+  p.ntw = ntw_req > 0 ? ntw_req : ((N + rows1 - 1) / rows1 >= 512 ? 2 : 1);
+  const int rows = rows1 * p.ntw;
+  p.nblk = (N + rows - 1) / rows;
+  const int nchunk = (K / 32) / BG_CK;
+  const int target = target_env > 0 ? target_env : (K > 4096 ? 256 : 128);
+  int ks = p.nblk >= 128 && target_env <= 0 ? 1 : std::max(1, std::min(std::min(nchunk, ksmax), (target + p.nblk - 1) / p.nblk));
+  const int cpw = (nchunk + ks - 1) / ks;
+  ks = (nchunk + cpw - 1) / cpw;
+  p.ksplit = ks;
+  p.kspl = cpw * BG_CK;
+  if (ks > 1) {
+    p.part_floats = (size_t)p.nblk * ks * BG_WAVES * p.ntw * p.nb * 64 * 4;
+    p.ss_floats = (size_t)p.nblk * ks * p.nb * 16;
+  }
+  return p;
+}
+
+constexpr size_t BG_COUNTER_BYTES = 64 * 1024;  // counters live at the start of the workspace
+
+static size_t bgemm_ws_bytes(const BgPlan& p) {
+  return BG_COUNTER_BYTES + (p.part_floats + p.ss_floats) * sizeof(float);
+}
+
+template <int NB, int NTW, int EPI, bool NORM>
+static hipError_t bg_launch(const GemmArgs& a, const BgArgs& b, int nblk, hipStream_t st) {
+  constexpr int U = NTW == 1 ? 8 : 4;
+  hipLaunchKernelGGL((bgemm_kernel<NB, NTW, U, EPI, NORM>), dim3(nblk * b.ksplit), dim3(BG_WAVES * 64), 0, st, a,
+                     b);
+  return hipGetLastError();
+}
+
+template <int NB, int NTW, bool NORM>
+static hipError_t bg_launch_e(int epi, const GemmArgs& a, const BgArgs& b, int nblk, hipStream_t st) {
+  switch (epi) {
+    case EPI_BF16: return bg_launch<NB, NTW, EPI_BF16, NORM>(a, b, nblk, st);
+    case EPI_RESID: return bg_launch<NB, NTW, EPI_RESID, NORM>(a, b, nblk, st);
+    case EPI_F32: return bg_launch<NB, NTW, EPI_F32, NORM>(a, b, nblk, st);
+    case EPI_SILU: return bg_launch<NB, NTW, EPI_SILU, NORM>(a, b, nblk, st);
+    case EPI_GELU: return bg_launch<NB, NTW, EPI_GELU, NORM>(a, b, nblk, st);
+    case EPI_QKV_ROPE: return bg_launch<NB, NTW, EPI_QKV_ROPE, NORM>(a, b, nblk, st);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+static int bgemm_dispatch(const GemmArgs& a, int epi, bool norm, const BgPlan& p, void* ws, hipStream_t st) {
+  BgArgs b{};
+  b.ksplit = p.ksplit;
+  b.kspl = p.kspl;
+  b.counters = reinterpret_cast<unsigned*>(ws);
+  b.part = reinterpret_cast<float*>(reinterpret_cast<char*>(ws) + BG_COUNTER_BYTES);
+  b.part_ss = b.part + p.part_floats;
+  hipError_t e;
+  if (p.nb == 2) {
+    if (p.ntw == 2) e = norm ? bg_launch_e<2, 2, true>(epi, a, b, p.nblk, st) : bg_launch_e<2, 2, false>(epi, a, b, p.nblk, st);
+    else e = norm ? bg_launch_e<2, 1, true>(epi, a, b, p.nblk, st) : bg_launch_e<2, 1, false>(epi, a, b, p.nblk, st);
+  } else {
+    if (p.ntw == 2) e = norm ? bg_launch_e<4, 2, true>(epi, a, b, p.nblk, st) : bg_launch_e<4, 2, false>(epi, a, b, p.nblk, st);
+    else e = norm ? bg_launch_e<4, 1, true>(epi, a, b, p.nblk, st) : bg_launch_e<4, 1, false>(epi, a, b, p.nblk, st);
+  }
+  return int(e);
+}
+
+// Batched path is used for M > CAIN_BGEMM_MIN_M (default 16) when K is a multiple of 256.
+static int bgemm_min_m() {
+  static const int v = env_int("CAIN_BGEMM_MIN_M", 16);
+  return v;
+}
+static int bgemm_ntw() {
+  static const int v = env_int("CAIN_BGEMM_NTW", 0);
+  return v;
+}
+
+// M <= 32 on narrow outputs (N < 8192: O / QKV projections) stays on the skinny kernel, which measured
+// faster there (its whole grid streams from the first cycle; no staging, no combine).
+static bool bgemm_eligible(int N, int K, int M) {
+  return M > bgemm_min_m() && M <= 64 && K % (32 * BG_CK) == 0 && (M > 32 || N >= 8192);
+}
+
+// Workspace the batched path needs for a GEMM of this shape (0 when the skinny kernel runs it).
+CAIN_API long long cain_gemm_ws_bytes(int N, int K, int M) {
+  if (!bgemm_eligible(N, K, M)) return 0;
+  return (long long)bgemm_ws_bytes(bgemm_plan(N, K, M, bgemm_ntw()));
+}
+
 // Entry used by the runtime and the bindings.  gain != null selects the fused RMSNorm.
 CAIN_API int cain_skinny_gemm_ex(const void* Wp, const void* X, int ldx, int K, int N, int M, void* Y, int ldy,
                                  const float* bias, const void* gain, float eps, const int* slot, const int* pos,
@@ -441,3 +858,29 @@ CAIN_API int cain_skinny_gemm_ex(const void* Wp, const void* X, int ldx, int K, 
   if (epi == EPI_QKV_ROPE && (hd % 16 || (hd / 2) % 8)) return -1;
   return gemm_dispatch(a, epi, gain != nullptr, waves, st);
 }
+
+// Full entry: batched path for 16 < M <= 64 when a workspace of cain_gemm_ws_bytes() (zeroed once) is
+// given, the skinny kernel otherwise.
+CAIN_API int cain_gemm(const void* Wp, const void* X, int ldx, int K, int N, int M, void* Y, int ldy,
+                       const float* bias, const void* gain, float eps, const int* slot, const int* pos,
+                       const float* cos_t, const float* sin_t, void* kc, void* vtc, int H, int Hkv, int hd, int T_max,
+                       void* ws, long long ws_bytes, int epi, int waves, hipStream_t st) {
+  if (ws && bgemm_eligible(N, K, M) && K % 32 == 0 && N % 16 == 0) {
+    const BgPlan p = bgemm_plan(N, K, M, bgemm_ntw());
+    if ((long long)bgemm_ws_bytes(p) <= ws_bytes && p.nblk * 4 <= (int)BG_COUNTER_BYTES) {
+      GemmArgs a{};
+      a.Wp = reinterpret_cast<const bf16x8*>(Wp);
+      a.X = reinterpret_cast<const __bf16*>(X);
+      a.ldx = ldx, a.K = K, a.N = N, a.M = M, a.Y = Y, a.ldy = ldy, a.bias = bias;
+      a.gain = reinterpret_cast<const __bf16*>(gain), a.eps = eps;
+      a.slot = slot, a.pos = pos, a.cos_t = cos_t, a.sin_t = sin_t;
+      a.kc = reinterpret_cast<__bf16*>(kc), a.vtc = reinterpret_cast<__bf16*>(vtc);
+      a.H = H, a.Hkv = Hkv, a.hd = hd, a.T_max = T_max;
+      if (epi == EPI_QKV_ROPE && (hd % 16 || (hd / 2) % 8)) return -1;
+      return bgemm_dispatch(a, epi, gain != nullptr, p, ws, st);
+    }
+  }
+  return cain_skinny_gemm_ex(Wp, X, ldx, K, N, M, Y, ldy, bias, gain, eps, slot, pos, cos_t, sin_t, kc, vtc, H, Hkv,
+                             hd, T_max, epi, waves, st);
+}
+

@@ -20,10 +20,10 @@
 
 #include "common.h"
 
-CAIN_API int cain_skinny_gemm_ex(const void* Wp, const void* X, int ldx, int K, int N, int M, void* Y, int ldy,
-                                 const float* bias, const void* gain, float eps, const int* slot, const int* pos,
-                                 const float* cos_t, const float* sin_t, void* kc, void* vtc, int H, int Hkv, int hd,
-                                 int T_max, int epi, int waves, hipStream_t st);
+CAIN_API int cain_gemm(const void* Wp, const void* X, int ldx, int K, int N, int M, void* Y, int ldy,
+                       const float* bias, const void* gain, float eps, const int* slot, const int* pos,
+                       const float* cos_t, const float* sin_t, void* kc, void* vtc, int H, int Hkv, int hd, int T_max,
+                       void* ws, long long ws_bytes, int epi, int waves, hipStream_t st);
 CAIN_API int cain_embed(const int* tok, const void* E, void* out, int ldo, int M, int d, float scale, hipStream_t st);
 CAIN_API int cain_attention(const void* q, const void* kc, const void* vtc, const int* slot, const int* pos,
                             float* part_o, float* part_ml, unsigned* counters, void* out, int ldo, int M, int H,
@@ -64,6 +64,8 @@ struct CainPlanDesc {
   float* part_o;
   float* part_ml;
   unsigned* counters;
+  void* gemm_ws;  // batched-GEMM workspace (counters zeroed once + split-K partials), see gemm.hip
+  long long gemm_ws_bytes;
 };
 
 struct CainRows {
@@ -107,20 +109,20 @@ int forward(const Plan& p, int M, const CainRows& r, int want_logits, int want_s
     const CainLayer& L = p.layers[l];
     __bf16* kc = reinterpret_cast<__bf16*>(d.kcache) + (size_t)l * d.kv_layer_elems;
     __bf16* vc = reinterpret_cast<__bf16*>(d.vtcache) + (size_t)l * d.kv_layer_elems;
-    CK(cain_skinny_gemm_ex(L.wqkv, d.x, d.d, d.d, qkv_dim, M, d.q, q_dim, L.bqkv, L.attn_norm, d.eps, r.slot, r.pos,
-                           d.cos_t, d.sin_t, kc, vc, d.H, d.Hkv, d.hd, d.T_max, /*EPI_QKV_ROPE*/ 5, d.waves, st));
+    CK(cain_gemm(L.wqkv, d.x, d.d, d.d, qkv_dim, M, d.q, q_dim, L.bqkv, L.attn_norm, d.eps, r.slot, r.pos,
+                           d.cos_t, d.sin_t, kc, vc, d.H, d.Hkv, d.hd, d.T_max, d.gemm_ws, d.gemm_ws_bytes, /*EPI_QKV_ROPE*/ 5, d.waves, st));
     CK(cain_attention(d.q, kc, vc, r.slot, r.pos, d.part_o, d.part_ml, d.counters, d.attn, q_dim, M, d.H, d.Hkv,
                       d.hd, d.T_max, d.nsplit, d.attn_scale, st));
-    CK(cain_skinny_gemm_ex(L.wo, d.attn, q_dim, q_dim, d.d, M, d.x, d.d, nullptr, nullptr, 0.f, nullptr, nullptr,
-                           nullptr, nullptr, nullptr, nullptr, 0, 0, 0, 0, /*EPI_RESID*/ 1, d.waves, st));
-    CK(cain_skinny_gemm_ex(L.wgu, d.x, d.d, d.d, 2 * d.ffn, M, d.act, d.ffn, nullptr, L.mlp_norm, d.eps, nullptr,
-                           nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0, 0, 0, epi_act, d.waves, st));
-    CK(cain_skinny_gemm_ex(L.wdown, d.act, d.ffn, d.ffn, d.d, M, d.x, d.d, nullptr, nullptr, 0.f, nullptr, nullptr,
-                           nullptr, nullptr, nullptr, nullptr, 0, 0, 0, 0, /*EPI_RESID*/ 1, d.waves, st));
+    CK(cain_gemm(L.wo, d.attn, q_dim, q_dim, d.d, M, d.x, d.d, nullptr, nullptr, 0.f, nullptr, nullptr,
+                           nullptr, nullptr, nullptr, nullptr, 0, 0, 0, 0, d.gemm_ws, d.gemm_ws_bytes, /*EPI_RESID*/ 1, d.waves, st));
+    CK(cain_gemm(L.wgu, d.x, d.d, d.d, 2 * d.ffn, M, d.act, d.ffn, nullptr, L.mlp_norm, d.eps, nullptr,
+                           nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0, 0, 0, d.gemm_ws, d.gemm_ws_bytes, epi_act, d.waves, st));
+    CK(cain_gemm(L.wdown, d.act, d.ffn, d.ffn, d.d, M, d.x, d.d, nullptr, nullptr, 0.f, nullptr, nullptr,
+                           nullptr, nullptr, nullptr, nullptr, 0, 0, 0, 0, d.gemm_ws, d.gemm_ws_bytes, /*EPI_RESID*/ 1, d.waves, st));
   }
   if (want_logits) {
-    CK(cain_skinny_gemm_ex(d.lm_head, d.x, d.d, d.d, d.V, M, d.logits, d.V, nullptr, d.final_norm, d.eps, nullptr,
-                           nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0, 0, 0, /*EPI_F32*/ 2, d.waves, st));
+    CK(cain_gemm(d.lm_head, d.x, d.d, d.d, d.V, M, d.logits, d.V, nullptr, d.final_norm, d.eps, nullptr,
+                           nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0, 0, 0, d.gemm_ws, d.gemm_ws_bytes, /*EPI_F32*/ 2, d.waves, st));
   }
   if (want_sample) {
     CK(cain_sample(d.logits, d.V, d.V, r.tok, r.pos, r.gen, r.ldg, r.n_gen, r.max_new, r.done, r.hist, r.slot,

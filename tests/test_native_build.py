@@ -7,7 +7,7 @@ from cain_amd.energy import native
 
 def test_kernel_library_loads_and_binds():
     lib = ops.load()
-    for sym in ("cain_skinny_gemm_ex", "cain_rmsnorm", "cain_embed", "cain_attention", "cain_sample",
+    for sym in ("cain_skinny_gemm_ex", "cain_gemm", "cain_gemm_ws_bytes", "cain_rmsnorm", "cain_embed", "cain_attention", "cain_sample",
                 "cain_plan_create", "cain_plan_forward", "cain_plan_capture", "cain_graph_launch",
                 "cain_graph_destroy", "cain_sample_params_size", "cain_rows_size", "cain_plan_desc_size"):
         assert hasattr(lib, sym), sym

@@ -101,6 +101,30 @@ def test_skinny_gemm_gateup(act, M):
     assert rel_err(y, a * u) < 1.5e-2
 
 
+@pytest.mark.parametrize("M", [17, 32, 48, 64])
+@pytest.mark.parametrize("N,K,norm", [(32064, 3072, True), (256, 14336, False), (4096, 4096, True),
+                                      (1920, 8960, False)])
+def test_batched_gemm_matches_skinny_and_reference(M, N, K, norm):
+    """The LDS-staged split-K path (16 < M <= 64): N not a multiple of the 128-row block, deep k-splits
+    (N=256, K=14336 -> 56 partial ranges), fused norm; repeated launches check the self-resetting tickets."""
+    torch.manual_seed(11)
+    W = (torch.randn(N, K, device=DEV) * 0.02).bfloat16()
+    x = (2 * torch.randn(M, K, device=DEV)).bfloat16()
+    g = (1 + 0.2 * torch.randn(K, device=DEV)).bfloat16() if norm else None
+    assert ops.gemm_ws_bytes(N, K, M) > 0 or (M <= 32 and N < 8192)  # narrow N at M <= 32: skinny path
+    wp = pack_mfma_a(W)
+    ys = [ops.skinny_gemm(wp, x, N, ops.EPI_F32, gain=g, eps=1e-6) for _ in range(3)]
+    y0 = ops.skinny_gemm(wp, x, N, ops.EPI_F32, gain=g, eps=1e-6, batched=False)
+    xr = x.float()
+    if norm:
+        xr = xr * torch.rsqrt(xr.pow(2).mean(-1, keepdim=True) + 1e-6) * g.float()
+    ref = xr @ W.float().t()
+    for y in ys:
+        assert rel_err(y, ref) < 2e-3
+        assert torch.equal(y, ys[0])  # deterministic reduction order
+    assert rel_err(ys[0], y0) < 2e-3
+
+
 @pytest.mark.parametrize("d", [1536, 2048, 3584, 4096])
 def test_rmsnorm(d):
     x = torch.randn(7, d, device=DEV).bfloat16()

@@ -41,6 +41,8 @@ def main():
     ap.add_argument("--model", default="llama3.1:8b")
     ap.add_argument("--rows", default="1,16,64")
     ap.add_argument("--waves", default="0,4,8,16")
+    ap.add_argument("--gemm-only", action="store_true")
+    ap.add_argument("--roles", default="qkv,o,gateup,down,lm_head")
     ns = ap.parse_args()
     cfg = get_config(ns.model)
     dev = torch.device("cuda")
@@ -59,6 +61,8 @@ def main():
     for k, (n, k_, _) in roles.items():
         ncopy = max(1, math.ceil(600e6 / (n * k_ * 2)))
         W[k] = [torch.randn(n // 16, k_ // 32, 64, 8, device=dev).bfloat16() for _ in range(ncopy)]
+    roles = {r: v for r, v in roles.items() if r in ns.roles.split(",")}
+    W = {r: W[r] for r in roles}
     res = []
     for M in [int(x) for x in ns.rows.split(",")]:
         for role, (n, k, epi) in roles.items():
@@ -66,19 +70,24 @@ def main():
             out = torch.zeros(M, n // 2 if epi == ops.EPI_SILU else n, device=dev,
                               dtype=torch.float32 if epi == ops.EPI_F32 else torch.bfloat16)
             ss = torch.zeros(64, device=dev)
-            for wv in [int(x) for x in ns.waves.split(",")]:
+            variants = [(False, int(w)) for w in ns.waves.split(",")]
+            if ops.gemm_ws_bytes(n, k, M) > 0:
+                variants = [(False, 0), (True, 0)]
+            for batched, wv in variants:
                 it = [0]
 
                 def run():
                     w = W[role][it[0] % len(W[role])]
                     it[0] += 1
-                    ops.skinny_gemm(w, x, n, epi, out=out, waves=wv)
+                    ops.skinny_gemm(w, x, n, epi, out=out, waves=wv, batched=batched)
                 us = timeit(run)
                 gbs = n * k * 2 / us / 1e3
                 r = dict(kind="gemm", model=cfg.name, role=role, M=M, N=n, K=k, waves=wv, us=round(us, 2),
-                         TBps=round(gbs / 1e3, 3))
+                         TBps=round(gbs / 1e3, 3), path="batched" if batched else "skinny")
                 res.append(r)
                 print(json.dumps(r), flush=True)
+    if ns.gemm_only:
+        return
     # attention
     T_max = 2048
     for M, L in [(1, 128), (1, 1400), (16, 700), (64, 1400)]:
