@@ -456,13 +456,13 @@ static int gemm_dispatch(GemmArgs a, int epi, int norm, int waves, hipStream_t s
 // as the attention combine).  Traffic per weight byte: M/(16*NTW*8) activation (L2) + 2M/k_range
 // partials (MALL), against 4 for the skinny kernel at M = 64.
 // =====================================================================================================
-constexpr int BG_WAVES = 8;
-constexpr int BG_CK = 8;  // 32-wide k-slices per LDS chunk (256 k)
+constexpr int BG_WAVES = 8;  // default waves per workgroup (template W: 4 or 8)
+constexpr int BG_CK = 8;     // default 32-wide k-slices per LDS chunk (template CK: 8 or 16)
 
 struct BgArgs {
   int ksplit;  // workgroups per row block
-  int kspl;    // k-slices per workgroup (multiple of BG_CK)
-  float* part;       // [nblk][ksplit][BG_WAVES*NTW*NB][64] f32x4  (ksplit > 1)
+  int kspl;    // k-slices per workgroup (multiple of CK)
+  float* part;       // [nblk][ksplit][W*NTW*NB][64] f32x4  (ksplit > 1)
   float* part_ss;    // [nblk][ksplit][NB*16]                   (ksplit > 1 && NORM)
   unsigned* counters;  // [nblk], zero between launches (the reducer resets its own)
 };
@@ -478,9 +478,9 @@ __device__ __forceinline__ f32x4 ld_wt(const float* p) {
   return v;
 }
 
-template <int NB, int NTW, int U, int EPI, bool NORM>
-__global__ __launch_bounds__(BG_WAVES * 64) void bgemm_kernel(const GemmArgs a, const BgArgs bg) {
-  constexpr int W = BG_WAVES;
+template <int NB, int NTW, int W, int CK, int U, int EPI, bool NORM>
+__global__ __launch_bounds__(W * 64) void bgemm_kernel(const GemmArgs a, const BgArgs bg) {
+  constexpr int BG_CK = CK;
   constexpr int FR = BG_CK * NB;        // B fragments per chunk
   constexpr int FPW = FR / W;           // staged per wave per chunk
   constexpr int NGRP = BG_CK / U;       // weight prefetch groups per chunk
@@ -736,7 +736,7 @@ __global__ __launch_bounds__(BG_WAVES * 64) void bgemm_kernel(const GemmArgs a, 
 }
 
 struct BgPlan {
-  int nb, ntw, nblk, ksplit, kspl;
+  int nb, ntw, w, ck, nblk, ksplit, kspl;
   size_t part_floats, ss_floats;
 };
 
@@ -755,21 +755,28 @@ static int env_int(const char* name, int dflt) {
 static BgPlan bgemm_plan(int N, int K, int M, int ntw_req) {
   static const int target_env = env_int("CAIN_BGEMM_WG", 0);
   static const int ksmax = env_int("CAIN_BGEMM_KSMAX", 8);
+  static const int w_env = env_int("CAIN_BGEMM_W", 0);
+  static const int ck_env = env_int("CAIN_BGEMM_CK", 0);
   BgPlan p{};
   p.nb = M <= 32 ? 2 : 4;
   const int rows1 = 16 * BG_WAVES;
   p.ntw = ntw_req > 0 ? ntw_req : ((N + rows1 - 1) / rows1 >= 512 ? 2 : 1);
-  const int rows = rows1 * p.ntw;
+  // the 4-wave and 16-slice-chunk variants exist for NTW = 1 only; 4-wave workgroups (64-row blocks)
+  // measured faster on N <= 4096 (O / down projections: 23.2 vs 25.8 us, 41.5 vs 46.7 us at M = 64)
+  const bool narrow = N <= 4096 && p.ntw == 1;
+  p.w = (w_env == 4 || (w_env == 0 && narrow)) && p.ntw == 1 ? 4 : BG_WAVES;
+  p.ck = (ck_env == 16 && p.ntw == 1 && p.w == 8 && (K / 32) % 16 == 0) ? 16 : BG_CK;
+  const int rows = 16 * p.w * p.ntw;
   p.nblk = (N + rows - 1) / rows;
-  const int nchunk = (K / 32) / BG_CK;
+  const int nchunk = (K / 32) / p.ck;
   const int target = target_env > 0 ? target_env : (K > 4096 ? 256 : 128);
   int ks = p.nblk >= 128 && target_env <= 0 ? 1 : std::max(1, std::min(std::min(nchunk, ksmax), (target + p.nblk - 1) / p.nblk));
   const int cpw = (nchunk + ks - 1) / ks;
   ks = (nchunk + cpw - 1) / cpw;
   p.ksplit = ks;
-  p.kspl = cpw * BG_CK;
+  p.kspl = cpw * p.ck;
   if (ks > 1) {
-    p.part_floats = (size_t)p.nblk * ks * BG_WAVES * p.ntw * p.nb * 64 * 4;
+    p.part_floats = (size_t)p.nblk * ks * p.w * p.ntw * p.nb * 64 * 4;
     p.ss_floats = (size_t)p.nblk * ks * p.nb * 16;
   }
   return p;
@@ -781,25 +788,32 @@ static size_t bgemm_ws_bytes(const BgPlan& p) {
   return BG_COUNTER_BYTES + (p.part_floats + p.ss_floats) * sizeof(float);
 }
 
-template <int NB, int NTW, int EPI, bool NORM>
+template <int NB, int NTW, int W, int CK, int EPI, bool NORM>
 static hipError_t bg_launch(const GemmArgs& a, const BgArgs& b, int nblk, hipStream_t st) {
   constexpr int U = NTW == 1 ? 8 : 4;
-  hipLaunchKernelGGL((bgemm_kernel<NB, NTW, U, EPI, NORM>), dim3(nblk * b.ksplit), dim3(BG_WAVES * 64), 0, st, a,
-                     b);
+  hipLaunchKernelGGL((bgemm_kernel<NB, NTW, W, CK, U, EPI, NORM>), dim3(nblk * b.ksplit), dim3(W * 64), 0, st, a, b);
   return hipGetLastError();
 }
 
-template <int NB, int NTW, bool NORM>
+template <int NB, int NTW, int W, int CK, bool NORM>
 static hipError_t bg_launch_e(int epi, const GemmArgs& a, const BgArgs& b, int nblk, hipStream_t st) {
   switch (epi) {
-    case EPI_BF16: return bg_launch<NB, NTW, EPI_BF16, NORM>(a, b, nblk, st);
-    case EPI_RESID: return bg_launch<NB, NTW, EPI_RESID, NORM>(a, b, nblk, st);
-    case EPI_F32: return bg_launch<NB, NTW, EPI_F32, NORM>(a, b, nblk, st);
-    case EPI_SILU: return bg_launch<NB, NTW, EPI_SILU, NORM>(a, b, nblk, st);
-    case EPI_GELU: return bg_launch<NB, NTW, EPI_GELU, NORM>(a, b, nblk, st);
-    case EPI_QKV_ROPE: return bg_launch<NB, NTW, EPI_QKV_ROPE, NORM>(a, b, nblk, st);
+    case EPI_BF16: return bg_launch<NB, NTW, W, CK, EPI_BF16, NORM>(a, b, nblk, st);
+    case EPI_RESID: return bg_launch<NB, NTW, W, CK, EPI_RESID, NORM>(a, b, nblk, st);
+    case EPI_F32: return bg_launch<NB, NTW, W, CK, EPI_F32, NORM>(a, b, nblk, st);
+    case EPI_SILU: return bg_launch<NB, NTW, W, CK, EPI_SILU, NORM>(a, b, nblk, st);
+    case EPI_GELU: return bg_launch<NB, NTW, W, CK, EPI_GELU, NORM>(a, b, nblk, st);
+    case EPI_QKV_ROPE: return bg_launch<NB, NTW, W, CK, EPI_QKV_ROPE, NORM>(a, b, nblk, st);
     default: return hipErrorInvalidValue;
   }
+}
+
+template <int NB, bool NORM>
+static hipError_t bg_launch_shape(int epi, const BgPlan& p, const GemmArgs& a, const BgArgs& b, hipStream_t st) {
+  if (p.ntw == 2) return bg_launch_e<NB, 2, 8, 8, NORM>(epi, a, b, p.nblk, st);
+  if (p.w == 4) return bg_launch_e<NB, 1, 4, 8, NORM>(epi, a, b, p.nblk, st);
+  if (p.ck == 16) return bg_launch_e<NB, 1, 8, 16, NORM>(epi, a, b, p.nblk, st);
+  return bg_launch_e<NB, 1, 8, 8, NORM>(epi, a, b, p.nblk, st);
 }
 
 static int bgemm_dispatch(const GemmArgs& a, int epi, bool norm, const BgPlan& p, void* ws, hipStream_t st) {
@@ -810,13 +824,8 @@ static int bgemm_dispatch(const GemmArgs& a, int epi, bool norm, const BgPlan& p
   b.part = reinterpret_cast<float*>(reinterpret_cast<char*>(ws) + BG_COUNTER_BYTES);
   b.part_ss = b.part + p.part_floats;
   hipError_t e;
-  if (p.nb == 2) {
-    if (p.ntw == 2) e = norm ? bg_launch_e<2, 2, true>(epi, a, b, p.nblk, st) : bg_launch_e<2, 2, false>(epi, a, b, p.nblk, st);
-    else e = norm ? bg_launch_e<2, 1, true>(epi, a, b, p.nblk, st) : bg_launch_e<2, 1, false>(epi, a, b, p.nblk, st);
-  } else {
-    if (p.ntw == 2) e = norm ? bg_launch_e<4, 2, true>(epi, a, b, p.nblk, st) : bg_launch_e<4, 2, false>(epi, a, b, p.nblk, st);
-    else e = norm ? bg_launch_e<4, 1, true>(epi, a, b, p.nblk, st) : bg_launch_e<4, 1, false>(epi, a, b, p.nblk, st);
-  }
+  if (p.nb == 2) e = norm ? bg_launch_shape<2, true>(epi, p, a, b, st) : bg_launch_shape<2, false>(epi, p, a, b, st);
+  else e = norm ? bg_launch_shape<4, true>(epi, p, a, b, st) : bg_launch_shape<4, false>(epi, p, a, b, st);
   return int(e);
 }
 
@@ -830,10 +839,10 @@ static int bgemm_ntw() {
   return v;
 }
 
-// M <= 32 on narrow outputs (N < 8192: O / QKV projections) stays on the skinny kernel, which measured
-// faster there (its whole grid streams from the first cycle; no staging, no combine).
+// M <= 32 on narrow outputs with short K (N < 8192, K <= 4096: O / QKV projections) stays on the skinny
+// kernel, which measured faster there (its whole grid streams from the first cycle; no staging, no combine).
 static bool bgemm_eligible(int N, int K, int M) {
-  return M > bgemm_min_m() && M <= 64 && K % (32 * BG_CK) == 0 && (M > 32 || N >= 8192);
+  return M > bgemm_min_m() && M <= 64 && K % (32 * BG_CK) == 0 && (M > 32 || N >= 8192 || K > 4096);
 }
 
 // Workspace the batched path needs for a GEMM of this shape (0 when the skinny kernel runs it).

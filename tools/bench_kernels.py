@@ -42,6 +42,7 @@ def main():
     ap.add_argument("--rows", default="1,16,64")
     ap.add_argument("--waves", default="0,4,8,16")
     ap.add_argument("--gemm-only", action="store_true")
+    ap.add_argument("--norm", action="store_true", help="fused RMSNorm on qkv/gateup/lm_head (as in the model)")
     ap.add_argument("--roles", default="qkv,o,gateup,down,lm_head")
     ns = ap.parse_args()
     cfg = get_config(ns.model)
@@ -70,6 +71,7 @@ def main():
             out = torch.zeros(M, n // 2 if epi == ops.EPI_SILU else n, device=dev,
                               dtype=torch.float32 if epi == ops.EPI_F32 else torch.bfloat16)
             ss = torch.zeros(64, device=dev)
+            g = torch.ones(k, device=dev).bfloat16() if ns.norm and role in ("qkv", "gateup", "lm_head") else None
             variants = [(False, int(w)) for w in ns.waves.split(",")]
             if ops.gemm_ws_bytes(n, k, M) > 0:
                 variants = [(False, 0), (True, 0)]
@@ -79,7 +81,7 @@ def main():
                 def run():
                     w = W[role][it[0] % len(W[role])]
                     it[0] += 1
-                    ops.skinny_gemm(w, x, n, epi, out=out, waves=wv, batched=batched)
+                    ops.skinny_gemm(w, x, n, epi, out=out, waves=wv, batched=batched, gain=g)
                 us = timeit(run)
                 gbs = n * k * 2 / us / 1e3
                 r = dict(kind="gemm", model=cfg.name, role=role, M=M, N=n, K=k, waves=wv, us=round(us, 2),
