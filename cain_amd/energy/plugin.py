@@ -22,7 +22,9 @@ Decorator kwargs: ``devices`` (HIP ordinals of the *measured device*),
 ``cpu_tdp_w``, ``ram_w_per_gb``, ``sources``, ``country_iso_code`` (carbon
 intensity for the EMISSIONS columns), ``save_samples`` (write
 ``energy_samples.csv`` into the run dir), ``idle_baseline_s`` (measure idle
-power once in the first window's process).  Unknown codecarbon kwargs are
+power once in the first window's process).  A config may define
+``energy_sources_for(context) -> ("gpu", "cpu", ...)`` to choose the measured
+sources per run.  Unknown codecarbon kwargs are
 accepted and ignored so reference configs load unchanged.
 """
 from __future__ import annotations
@@ -108,6 +110,8 @@ def emission_tracker(online: bool = False, *decargs, **deckwargs):
         cls.stop_measurement = _stop(cls.stop_measurement)
         cls.populate_run_data = _populate(data_columns, country, carbon, save_samples)(cls.populate_run_data)
         cls.__energy_columns__ = [c.value for c in data_columns]
+        cls.__energy_meter_kwargs__ = dict(meter_kwargs)
+        cls.__energy_idle_s__ = idle_s
         return cls
 
     return decorate
@@ -130,15 +134,32 @@ def _add_columns(cols):
 def _meter_for(self, meter_kwargs, idle_s) -> EnergyMeter:
     meter = getattr(self, "__energy_meter__", None)
     if meter is None:
-        kw = dict(meter_kwargs)
+        kw = dict(getattr(self, "__energy_meter_kwargs__", None) or meter_kwargs)
         kw.setdefault("devices", getattr(self, "energy_devices", None))
         meter = EnergyMeter(**kw)
-        if idle_s:
-            meter.measure_idle(idle_s)
-        elif getattr(self, "idle_power_w", None) is not None:
+        if getattr(self, "idle_power_w", None) is not None:
             meter.idle_power_w = float(self.idle_power_w)
+        elif idle_s:
+            meter.measure_idle(idle_s)
+            self.idle_power_w = meter.idle_power_w
         self.__energy_meter__ = meter
     return meter
+
+
+def ensure_meter(config) -> EnergyMeter:
+    """Create the decorated config's meter now (e.g. at START_RUN, so its start-up is not inside a window)."""
+    return _meter_for(config, {}, getattr(config, "__energy_idle_s__", 0.0))
+
+
+def measure_idle_baseline(config, seconds: float = 2.0) -> float:
+    """Idle board power of the config's measured GPUs (W), measured with a short-lived meter and stored
+    as ``config.idle_power_w`` — call it from BEFORE_EXPERIMENT, before any run and without leaving a
+    sampler thread behind (forked run children could not use it)."""
+    kw = dict(getattr(config, "__energy_meter_kwargs__", None) or {})
+    kw.setdefault("devices", getattr(config, "energy_devices", None))
+    with EnergyMeter(**kw) as m:
+        config.idle_power_w = m.measure_idle(seconds)
+    return config.idle_power_w
 
 
 def _start(meter_kwargs, idle_s):
@@ -146,6 +167,9 @@ def _start(meter_kwargs, idle_s):
         @functools.wraps(fn)
         def wrapper(self, context, *a, **kw):
             meter = _meter_for(self, meter_kwargs, idle_s)
+            pick = getattr(self, "energy_sources_for", None)
+            if callable(pick):  # per-run measured sources (e.g. the remote arm: client CPU only)
+                meter.sources = tuple(pick(context))
             meter.start()
             return fn(self, context, *a, **kw)
         return wrapper

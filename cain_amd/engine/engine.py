@@ -153,7 +153,7 @@ class DecodeEngine:
             self._init_hip()
         elif backend == "torch":
             from ..models.reference import ReferenceModel
-            self.ref = ReferenceModel(weights)
+            self.ref = ReferenceModel(weights, memo_weights=self.device.type == "cpu")
         else:
             raise ValueError(f"unknown backend {backend!r}")
         if self.device.type == "cuda":
@@ -447,19 +447,20 @@ class DecodeEngine:
             self._forward(n, pr, want_logits=False, want_sample=False)
 
     def _generate_torch(self, ids, nps, row_opts):
-        """Oracle backend: full recompute per step, greedy or sampled on the host."""
+        """Oracle backend with a KV cache (one token of compute per step), sampled on the host."""
         t0 = time.perf_counter_ns()
         gens = []
         for i, p in enumerate(ids):
             o = row_opts[i]
             rng = np.random.default_rng(o["seed"])
-            toks = list(p)
             out = []
+            cache: list = []
+            step = torch.tensor([list(p)], device=self.device)
             for _ in range(nps[i]):
-                logits = self.ref.forward(torch.tensor([toks], device=self.device))[0, -1].float().cpu()
+                logits = self.ref.forward(step, cache=cache, last_only=True)[0, -1].float().cpu()
                 nxt = sample_host(logits, out, o, rng)
                 out.append(nxt)
-                toks.append(nxt)
+                step = torch.tensor([[nxt]], device=self.device)
                 if o["eos_id"] >= 0 and nxt == o["eos_id"]:
                     break
             gens.append(out)

@@ -1,0 +1,445 @@
+"""The CAIN'25 study as a native RunnerConfig: on-device vs remote LLM content fetching.
+
+Behaviour of the reference study (`experiment/RunnerConfig.py`):
+
+* factors ``model`` (7 Ollama tags) × ``method`` ∈ {remote, on_device} × ``length`` ∈ {'100','500','1000'},
+  30 repetitions, shuffled (:66-87);
+* a run picks a topic from ``experiment/topics.csv`` and asks ``"In {length} words, please give me
+  information about {topic}"`` over ``POST /api/generate`` with ``stream: false`` — to localhost for the
+  on-device arm, to ``SERVER_IP`` (from ``.env``) for the remote arm (:106-131);
+* the measurement window is the request (:133-175); ``execution_time`` runs from BEFORE_RUN to STOP_RUN
+  (:98-103, :189-193, :224); CPU % / memory % are sampled while it runs, GPU % from powermetrics (:195-221);
+* energy comes from the emission-tracker plugin (:28-31), converted to Joules (:239-259).
+
+MI355X-native differences:
+
+* the on-device arm is this framework's own decode engine behind an Ollama-compatible server started per
+  data-parallel rank on that rank's GPU (``python -m cain_amd serve``, port ``port_base + 1 + rank``);
+* energy is the amd-smi hardware accumulator of the measured GPU plus host CPU (RAPL or a TDP model), on a
+  native sampler thread (``cain_amd.energy``); the remote arm measures the client only (the rank's GPU
+  when the server lives on another device, otherwise host CPU only);
+* the response JSON is captured (the reference's curl printed it and dropped it), so the run table gains
+  ``tokens_generated``, ``J_per_token``, ``tok_per_s``, ``ttft_s`` ... after the reference's columns;
+* topics are drawn with a per-run seeded RNG (reproducible), prompts/lengths are the reference's.
+
+Every setting can be overridden with ``CAIN_STUDY_<FIELD>`` environment variables (lists comma-separated),
+e.g. ``CAIN_STUDY_MODELS=gemma:2b CAIN_STUDY_REPETITIONS=3 python -m cain_amd experiments/study.py``.
+"""
+from __future__ import annotations
+
+import csv
+import dataclasses
+import json
+import os
+import random
+import shutil
+import signal
+import subprocess
+import sys
+import threading
+import time
+from dataclasses import dataclass, field
+from datetime import datetime
+from pathlib import Path
+from typing import Any, Dict, List, Optional
+
+from ..client import CurlRequest, OllamaClient, OllamaError
+from ..energy import DataColumns, emission_tracker
+from ..energy.plugin import ensure_meter, measure_idle_baseline
+from ..models import STUDY_ORDER
+from ..runner.events import EventSubscriptionController, RunnerEvents
+from ..runner.models import FactorModel, OperationType, RunnerContext, RunTableModel
+from ..runner.output import OutputProcedure as output
+from ..utils.env import server_url
+
+REPO_ROOT = Path(__file__).resolve().parents[2]
+DEFAULT_TOPICS = REPO_ROOT / "experiments" / "topics.csv"
+
+REFERENCE_COLUMNS = ["topic", "execution_time", "cpu_usage", "gpu_usage", "memory_usage"]
+EXTRA_COLUMNS = ["tokens_generated", "prompt_tokens", "J_per_token", "tok_per_s", "ttft_s", "server_total_s",
+                 "server_eval_s", "client_wall_s", "device", "server"]
+ENERGY_COLUMNS = [DataColumns.ENERGY_CONSUMED, DataColumns.ENERGY_USAGE_J, DataColumns.GPU_ENERGY_J,
+                  DataColumns.CPU_ENERGY_J, DataColumns.IDLE_SUBTRACTED_J, DataColumns.AVG_GPU_POWER_W,
+                  DataColumns.WINDOW_S]
+
+
+@dataclass
+class StudySettings:
+    name: str = "new_runner_experiment"
+    models: List[str] = field(default_factory=lambda: list(STUDY_ORDER))
+    methods: List[str] = field(default_factory=lambda: ["remote", "on_device"])
+    lengths: List[str] = field(default_factory=lambda: ["100", "500", "1000"])
+    repetitions: int = 30
+    shuffle: bool = True
+    seed: Optional[int] = None
+    cooldown_ms: int = 90000
+    results_dir: str = str(REPO_ROOT / "experiments" / "experiments_output")
+    topics_csv: str = str(DEFAULT_TOPICS)
+    # on-device arm: a local server per rank
+    device_backend: str = "auto"          # auto (hip on GPU, torch on CPU) | hip | torch | fake
+    port_base: int = 11434
+    max_batch: int = 4
+    max_context: int = 2048
+    preload: bool = True
+    # remote arm: "" -> SERVER_IP from .env, else "fake" (modelled remote GPU server on this host's CPU),
+    # "local:<device>" (an engine server on another device of this host) or an explicit URL
+    remote: str = ""
+    remote_fake_tok_s: float = 70.0       # RTX 4070-class llama-8B decode rate for the modelled server
+    remote_fake_prefill_s: float = 0.15
+    client: str = "curl"                  # curl (reference parity) | http (in-process client)
+    stream: bool = False
+    request_timeout_s: float = 900.0
+    server_start_timeout_s: float = 900.0
+    # energy: idle board power measured once per rank after the servers are up (0 disables)
+    idle_baseline_s: float = 2.0
+
+    @classmethod
+    def from_env(cls, base: Optional["StudySettings"] = None) -> "StudySettings":
+        s = dataclasses.replace(base) if base is not None else cls()
+        for f in dataclasses.fields(cls):
+            raw = os.environ.get(f"CAIN_STUDY_{f.name.upper()}")
+            if raw is None:
+                continue
+            cur = getattr(s, f.name)
+            if isinstance(cur, list):
+                val: Any = [x.strip() for x in raw.split(",") if x.strip()]
+            elif isinstance(cur, bool):
+                val = raw.lower() in ("1", "true", "yes", "on")
+            elif isinstance(cur, int) and f.name != "seed":
+                val = int(raw)
+            elif isinstance(cur, float):
+                val = float(raw)
+            elif f.name == "seed":
+                val = int(raw) if raw else None
+            else:
+                val = raw
+            setattr(s, f.name, val)
+        return s
+
+
+def load_topics(path) -> List[str]:
+    with open(path, newline="", encoding="utf-8") as fh:
+        return [row["Topic"] for row in csv.DictReader(fh) if row.get("Topic")]
+
+
+def prompt_for(length: str, topic: str) -> str:
+    return f"In {length} words, please give me information about " + topic
+
+
+def _wait_alive(url: str, timeout_s: float, proc: Optional[subprocess.Popen] = None) -> None:
+    client = OllamaClient(url, timeout=5.0)
+    t_end = time.time() + timeout_s
+    while time.time() < t_end:
+        if proc is not None and proc.poll() is not None:
+            raise RuntimeError(f"server for {url} exited with {proc.returncode}")
+        if client.alive():
+            return
+        time.sleep(0.5)
+    raise RuntimeError(f"server {url} not up after {timeout_s:.0f} s")
+
+
+class _ServerProc:
+    """``python -m cain_amd serve ...`` as a child process in its own process group."""
+
+    def __init__(self, args: List[str], log_path: Path, env: Optional[Dict[str, str]] = None):
+        log_path.parent.mkdir(parents=True, exist_ok=True)
+        self.log = open(log_path, "ab")
+        e = dict(os.environ)
+        e.setdefault("PYTHONPATH", str(REPO_ROOT))
+        if env:
+            e.update(env)
+        self.proc = subprocess.Popen([sys.executable, "-m", "cain_amd", "serve", *args], stdout=self.log,
+                                     stderr=subprocess.STDOUT, cwd=str(REPO_ROOT), env=e, start_new_session=True)
+
+    def stop(self) -> None:
+        if self.proc.poll() is None:
+            try:
+                os.killpg(self.proc.pid, signal.SIGTERM)
+                self.proc.wait(timeout=20)
+            except (ProcessLookupError, subprocess.TimeoutExpired):
+                try:
+                    os.killpg(self.proc.pid, signal.SIGKILL)
+                except ProcessLookupError:
+                    pass
+                self.proc.wait()
+        self.log.close()
+
+
+class _HttpRequest:
+    """In-process client request on a thread (when curl is unavailable or client='http')."""
+
+    def __init__(self, url: str, model: str, prompt: str, stream: bool, timeout_s: float):
+        self.client = OllamaClient(url, timeout=timeout_s)
+        self.args = (model, prompt, stream)
+        self.result = None
+        self.error: Optional[BaseException] = None
+        self.thread = threading.Thread(target=self._run, daemon=True)
+
+    def _run(self):
+        try:
+            m, p, st = self.args
+            self.result = self.client.generate(m, p, stream=st)
+        except BaseException as exc:  # noqa: BLE001
+            self.error = exc
+
+    def start(self):
+        self.thread.start()
+        return self
+
+    def running(self) -> bool:
+        return self.thread.is_alive()
+
+    def wait(self, timeout=None):
+        self.thread.join(timeout)
+        if self.thread.is_alive():
+            raise OllamaError("request timed out")
+        if self.error is not None:
+            raise self.error
+        return self.result
+
+    def kill(self):
+        pass
+
+
+class _StudyBase:
+    """Reference columns only; the energy plugin decorates this layer so its columns follow them."""
+
+    SETTINGS = StudySettings()
+
+    def __init__(self):
+        self.settings = StudySettings.from_env(type(self).SETTINGS)
+        s = self.settings
+        self.name = s.name
+        self.results_output_path = Path(s.results_dir)
+        self.operation_type = OperationType.AUTO
+        self.time_between_runs_in_ms = int(s.cooldown_ms)
+        self.idle_power_w = None
+        EventSubscriptionController.subscribe_to_multiple_events([
+            (RunnerEvents.BEFORE_EXPERIMENT, self.before_experiment),
+            (RunnerEvents.BEFORE_RUN, self.before_run),
+            (RunnerEvents.START_RUN, self.start_run),
+            (RunnerEvents.START_MEASUREMENT, self.start_measurement),
+            (RunnerEvents.INTERACT, self.interact),
+            (RunnerEvents.STOP_MEASUREMENT, self.stop_measurement),
+            (RunnerEvents.STOP_RUN, self.stop_run),
+            (RunnerEvents.POPULATE_RUN_DATA, self.populate_run_data),
+            (RunnerEvents.AFTER_EXPERIMENT, self.after_experiment),
+        ])
+        self.run_table_model = None
+        self._servers: List[_ServerProc] = []
+        self._threads = []
+        self.local_url: Optional[str] = None
+        self.remote_url: Optional[str] = None
+        self.remote_shares_gpu = False
+        self.topics = load_topics(s.topics_csv)
+        self.request = None
+        self.response = None
+        self.error: Optional[str] = None
+
+    # ------------------------------------------------------------------ table
+    def create_run_table_model(self) -> RunTableModel:
+        s = self.settings
+        self.run_table_model = RunTableModel(
+            factors=[FactorModel("model", list(s.models)), FactorModel("method", list(s.methods)),
+                     FactorModel("length", list(s.lengths))],
+            data_columns=list(REFERENCE_COLUMNS), repetitions=int(s.repetitions), shuffle=s.shuffle, seed=s.seed)
+        return self.run_table_model
+
+    # ------------------------------------------------------------------ rank setup / teardown
+    @property
+    def rank(self) -> int:
+        return int(getattr(self, "dp_rank", 0))
+
+    def _gpu_index(self) -> Optional[int]:
+        devs = getattr(self, "energy_devices", None)
+        if devs:
+            return int(devs[0])
+        try:
+            import torch
+
+            return 0 if torch.cuda.device_count() > 0 else None  # device_count does not initialise HIP
+        except Exception:  # pragma: no cover
+            return None
+
+    def before_experiment(self) -> None:
+        s = self.settings
+        log_dir = self.results_output_path / s.name / "servers"
+        gpu = self._gpu_index()
+        if "on_device" in s.methods:
+            port = s.port_base + 1 + self.rank
+            backend = s.device_backend
+            device = f"cuda:{gpu}" if gpu is not None else "cpu"
+            if backend == "auto":
+                backend = "hip" if gpu is not None else "torch"
+            args = ["--host", "127.0.0.1", "--port", str(port), "--models", ",".join(s.models),
+                    "--device", device, "--max-batch", str(s.max_batch), "--max-context", str(s.max_context),
+                    "--backend", backend]
+            if s.preload and backend != "fake":
+                args.append("--preload")
+            env = {}
+            if gpu is not None:
+                # the server sees only this rank's GPU; the rank keeps addressing it by its own ordinal
+                env = {"HIP_VISIBLE_DEVICES": str(gpu)}
+                args[args.index("--device") + 1] = "cuda:0"
+            srv = _ServerProc(args, log_dir / f"on_device_rank{self.rank}.log", env)
+            self._servers.append(srv)
+            self.local_url = f"http://127.0.0.1:{port}"
+            output.console_log(f"starting on-device server {self.local_url} on {device} ({backend})")
+            _wait_alive(self.local_url, s.server_start_timeout_s, srv.proc)
+        if "remote" in s.methods:
+            self.remote_url = self._start_remote(log_dir)
+        output.console_log_OK(f"servers up: on_device={self.local_url} remote={self.remote_url}")
+        if s.idle_baseline_s > 0 and self.idle_power_w is None:
+            # models resident, nothing running: the idle_subtracted_J baseline of every later window
+            w = measure_idle_baseline(self, s.idle_baseline_s)
+            output.console_log(f"idle baseline {w:.1f} W over {s.idle_baseline_s:.1f} s")
+
+    def _start_remote(self, log_dir: Path) -> str:
+        s = self.settings
+        spec = s.remote or ""
+        if not spec:
+            try:
+                return server_url("remote")  # SERVER_IP from the environment / .env, as the reference
+            except RuntimeError:
+                output.console_log_WARNING("SERVER_IP not set: the remote arm uses a modelled server on this host")
+                spec = "fake"
+        if spec == "fake":
+            from ..serve import FakeBackend, ServerThread
+
+            th = ServerThread(FakeBackend(list(s.models), tokens_per_s=s.remote_fake_tok_s,
+                                          prefill_s=s.remote_fake_prefill_s), port=0).__enter__()
+            self._threads.append(th)
+            return th.url
+        if spec.startswith("local:"):
+            dev = spec.split(":", 1)[1]
+            port = s.port_base + 101 + self.rank
+            env = {"HIP_VISIBLE_DEVICES": dev} if dev.isdigit() else {}
+            device = "cuda:0" if dev.isdigit() else dev
+            self.remote_shares_gpu = dev.isdigit() and self._gpu_index() == int(dev)
+            srv = _ServerProc(["--host", "127.0.0.1", "--port", str(port), "--models", ",".join(s.models),
+                               "--device", device, "--max-batch", str(s.max_batch), "--max-context",
+                               str(s.max_context), "--preload"], log_dir / f"remote_rank{self.rank}.log", env)
+            self._servers.append(srv)
+            url = f"http://127.0.0.1:{port}"
+            _wait_alive(url, s.server_start_timeout_s, srv.proc)
+            return url
+        return spec if "://" in spec else f"http://{spec}"
+
+    def teardown_rank(self) -> None:
+        for srv in self._servers:
+            srv.stop()
+        for th in self._threads:
+            th.__exit__(None, None, None)
+        self._servers, self._threads = [], []
+
+    # ------------------------------------------------------------------ per-run hooks
+    def before_run(self) -> None:
+        self.timestamp_start = datetime.now()
+
+    def start_run(self, context: RunnerContext) -> None:
+        ensure_meter(self)  # sampler start-up stays outside the measurement window
+        v = context.run_variation
+        rng = random.Random(f"{self.settings.seed}:{v['__run_id']}")
+        self.topic = rng.choice(self.topics)
+        self.prompt = prompt_for(str(v["length"]), self.topic)
+        url = self.local_url if v["method"] == "on_device" else self.remote_url
+        if url is None:
+            raise RuntimeError(f"no server for method {v['method']} (before_experiment not run?)")
+        self.url = url
+        self.response, self.error = None, None
+        s = self.settings
+        if s.client == "curl" and shutil.which("curl"):
+            self.request = CurlRequest(url, v["model"], self.prompt, stream=s.stream,
+                                       timeout_s=s.request_timeout_s).start()
+        else:
+            self.request = _HttpRequest(url, v["model"], self.prompt, s.stream, s.request_timeout_s).start()
+
+    def energy_sources_for(self, context: RunnerContext):
+        if context.run_variation.get("method") == "remote" and self.remote_shares_gpu:
+            return ("cpu",)
+        return ("gpu", "cpu")
+
+    def start_measurement(self, context: RunnerContext) -> None:
+        # the window is the request (reference: a psutil poll loop until curl exits)
+        try:
+            self.response = self.request.wait(self.settings.request_timeout_s + 30)
+        except OllamaError as exc:
+            self.error = str(exc)
+
+    def interact(self, context: RunnerContext) -> None:
+        pass
+
+    def stop_measurement(self, context: RunnerContext) -> None:
+        if self.request is not None and self.request.running():
+            self.request.kill()
+
+    def stop_run(self, context: RunnerContext) -> None:
+        self.timestamp_end = datetime.now()
+        if self.error is not None:
+            raise RuntimeError(f"request failed: {self.error}")
+
+    def populate_run_data(self, context: RunnerContext) -> Optional[Dict[str, Any]]:
+        r = getattr(self, "__energy_reading__", None)
+        data: Dict[str, Any] = {
+            "topic": self.topic,
+            "execution_time": (self.timestamp_end - self.timestamp_start).total_seconds(),
+            "cpu_usage": round(r.cpu_usage, 3) if r is not None else "",
+            "gpu_usage": round(r.gpu_usage, 3) if r is not None and r.gpu_usage == r.gpu_usage else 0.0,
+            "memory_usage": round(r.memory_usage, 3) if r is not None else "",
+        }
+        self._last_stats = self.response.stats() if self.response is not None else {}
+        try:
+            (context.run_dir / "response.json").write_text(json.dumps(self.response.data if self.response else {},
+                                                                      indent=1))
+        except OSError:  # pragma: no cover
+            pass
+        return data
+
+    def after_experiment(self) -> None:
+        """Writer only: derive ``energy_usage_J`` where missing (reference :239-259) and write the paper
+        tables next to the run table (cain_amd.analysis)."""
+        from ..analysis import analyze
+
+        path = self.results_output_path / self.settings.name / "run_table.csv"
+        try:
+            analyze(path, path.parent / "analysis", quiet=True)
+            output.console_log_OK(f"analysis tables written to {path.parent / 'analysis'}")
+        except Exception as exc:  # noqa: BLE001 - analysis needs both arms / enough rows
+            output.console_log_WARNING(f"analysis skipped: {exc}")
+
+
+@emission_tracker(data_columns=ENERGY_COLUMNS, country_iso_code="NLD")
+class _MeasuredStudy(_StudyBase):
+    pass
+
+
+class StudyConfig(_MeasuredStudy):
+    """Reference columns, then the energy columns, then the measured-token columns."""
+
+    def create_run_table_model(self) -> RunTableModel:
+        m = super().create_run_table_model()
+        dc = m.get_data_columns()
+        for c in EXTRA_COLUMNS:
+            if c not in dc:
+                dc.append(c)
+        return m
+
+    def populate_run_data(self, context: RunnerContext) -> Optional[Dict[str, Any]]:
+        data = super().populate_run_data(context)  # + energy columns (plugin)
+        st = getattr(self, "_last_stats", {}) or {}
+        tok = int(st.get("tokens_generated") or 0)
+        e = data.get(DataColumns.ENERGY_USAGE_J.value)
+        wall = st.get("client_wall_s") or 0.0
+        data.update({
+            "tokens_generated": tok,
+            "prompt_tokens": int(st.get("prompt_tokens") or 0),
+            "J_per_token": round(float(e) / tok, 6) if tok and e not in (None, "") else "",
+            "tok_per_s": round(tok / wall, 3) if tok and wall else "",
+            "ttft_s": round(st["ttft_s"], 6) if st.get("ttft_s") is not None else "",
+            "server_total_s": round(st.get("server_total_s", 0.0), 6),
+            "server_eval_s": round(st.get("server_eval_s", 0.0), 6),
+            "client_wall_s": round(wall, 6),
+            "device": str(getattr(self, "energy_devices", [""])[0]) if getattr(self, "energy_devices", None) else "",
+            "server": self.url,
+        })
+        return data

@@ -46,12 +46,26 @@ def activation(cfg: ModelConfig, g: torch.Tensor) -> torch.Tensor:
 
 
 class ReferenceModel:
-    """Full-sequence causal forward: tokens [B, T] → logits [B, T, V] (fp32)."""
+    """Causal forward: tokens [B, T] → logits [B, T, V] (fp32).
 
-    def __init__(self, mw: ModelWeights, compute_dtype=torch.float32):
+    ``cache`` (a list, one ``[k, v]`` per layer, filled on first use) turns it into an incremental decoder:
+    the CPU serving path of the engine uses it so a generation costs one token of compute per step.
+    ``memo_weights`` keeps the compute-dtype copies of the weights (CPU serving: no per-call conversion)."""
+
+    def __init__(self, mw: ModelWeights, compute_dtype=torch.float32, memo_weights: bool = False):
         self.mw = mw
         self.cfg = mw.cfg
         self.dt = compute_dtype
+        self._memo = {} if memo_weights else None
+
+    def _w(self, t: torch.Tensor) -> torch.Tensor:
+        if self._memo is None:
+            return t.to(self.dt)
+        key = id(t)
+        w = self._memo.get(key)
+        if w is None:
+            w = self._memo[key] = t.to(self.dt)
+        return w
 
     def embed(self, tokens: torch.Tensor) -> torch.Tensor:
         x = self.mw.embed[tokens].to(self.dt)
@@ -59,11 +73,12 @@ class ReferenceModel:
             x = x * torch.tensor(math.sqrt(self.cfg.d_model), dtype=torch.bfloat16).to(self.dt)
         return x
 
-    def layer(self, x: torch.Tensor, li: int, positions: torch.Tensor, attn_mask: Optional[torch.Tensor] = None):
+    def layer(self, x: torch.Tensor, li: int, positions: torch.Tensor, attn_mask: Optional[torch.Tensor] = None,
+              cache: Optional[list] = None):
         cfg, lw = self.cfg, self.mw.layers[li]
         B, T, _ = x.shape
         h = rms_norm(x, effective_gain(cfg, lw.attn_norm), cfg.norm_eps).to(self.dt)
-        qkv = h @ lw.wqkv.to(self.dt).t()
+        qkv = h @ self._w(lw.wqkv).t()
         if lw.bqkv is not None:
             qkv = qkv + lw.bqkv.to(self.dt)
         q, k, v = qkv.split([cfg.q_dim, cfg.kv_dim, cfg.kv_dim], dim=-1)
@@ -73,30 +88,43 @@ class ReferenceModel:
         cos, sin = rope_cos_sin(cfg, positions)                     # [B, T, hd/2]
         q = apply_rope(q.float(), cos[:, :, None], sin[:, :, None]).to(self.dt)
         k = apply_rope(k.float(), cos[:, :, None], sin[:, :, None]).to(self.dt)
+        past = 0
+        if cache is not None:
+            if len(cache) > li:
+                past = cache[li][0].shape[1]
+                k = torch.cat([cache[li][0], k], dim=1)
+                v = torch.cat([cache[li][1], v], dim=1)
+                cache[li] = [k, v]
+            else:
+                cache.append([k, v])
         k = k.repeat_interleave(cfg.group, dim=2)
         v = v.repeat_interleave(cfg.group, dim=2)
         att = torch.einsum("bqhd,bkhd->bhqk", q.float(), k.float()) / math.sqrt(cfg.head_dim)
-        causal = torch.ones(T, T, dtype=torch.bool, device=x.device).tril()
+        causal = torch.ones(T, past + T, dtype=torch.bool, device=x.device).tril(diagonal=past)
         mask = causal if attn_mask is None else causal & attn_mask
         att = att.masked_fill(~mask, float("-inf")).softmax(-1)
         o = torch.einsum("bhqk,bkhd->bqhd", att, v.float()).reshape(B, T, cfg.q_dim).to(self.dt)
-        x = x + (o @ lw.wo.to(self.dt).t())
+        x = x + (o @ self._w(lw.wo).t())
         h = rms_norm(x, effective_gain(cfg, lw.mlp_norm), cfg.norm_eps).to(self.dt)
-        g = h @ lw.w_gate.to(self.dt).t()
-        u = h @ lw.w_up.to(self.dt).t()
+        g = h @ self._w(lw.w_gate).t()
+        u = h @ self._w(lw.w_up).t()
         a = (activation(cfg, g.float()) * u.float()).to(self.dt)
-        return x + a @ lw.w_down.to(self.dt).t()
+        return x + a @ self._w(lw.w_down).t()
 
     @torch.no_grad()
-    def forward(self, tokens: torch.Tensor, positions: Optional[torch.Tensor] = None) -> torch.Tensor:
+    def forward(self, tokens: torch.Tensor, positions: Optional[torch.Tensor] = None,
+                cache: Optional[list] = None, last_only: bool = False) -> torch.Tensor:
         B, T = tokens.shape
         if positions is None:
-            positions = torch.arange(T, device=tokens.device).expand(B, T)
+            past = cache[0][0].shape[1] if cache else 0
+            positions = torch.arange(past, past + T, device=tokens.device).expand(B, T)
         x = self.embed(tokens)
         for li in range(self.cfg.n_layers):
-            x = self.layer(x, li, positions)
+            x = self.layer(x, li, positions, cache=cache)
+        if last_only:
+            x = x[:, -1:]
         x = rms_norm(x, effective_gain(self.cfg, self.mw.final_norm), self.cfg.norm_eps).to(self.dt)
-        return (x @ self.mw.lm_head.to(self.dt).t()).float()
+        return (x @ self._w(self.mw.lm_head).t()).float()
 
     @torch.no_grad()
     def greedy(self, prompt: torch.Tensor, n_new: int) -> torch.Tensor:

@@ -424,6 +424,8 @@ def main(argv: Optional[List[str]] = None) -> None:
     ap.add_argument("--batch-window-ms", type=float, default=5.0)
     ap.add_argument("--backend", choices=["hip", "torch", "fake"], default=None)
     ap.add_argument("--preload", action="store_true", help="load every model at startup (all stay resident)")
+    ap.add_argument("--fake-tok-s", type=float, default=2000.0, help="fake backend: modelled decode rate")
+    ap.add_argument("--fake-prefill-s", type=float, default=0.0, help="fake backend: modelled time to first token")
     ap.add_argument("-v", "--verbose", action="store_true")
     ns = ap.parse_args(argv)
     models = [m for m in ns.models.split(",") if m]
@@ -431,7 +433,7 @@ def main(argv: Optional[List[str]] = None) -> None:
         if m not in MODELS and m not in TINY:
             raise SystemExit(f"unknown model {m}")
     if ns.backend == "fake":
-        be: Backend = FakeBackend(models)
+        be: Backend = FakeBackend(models, tokens_per_s=ns.fake_tok_s, prefill_s=ns.fake_prefill_s)
     else:
         be = EngineBackend(models, device=ns.device, max_batch=ns.max_batch, max_context=ns.max_context,
                            backend=ns.backend, preload=ns.preload)

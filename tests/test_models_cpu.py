@@ -90,3 +90,16 @@ def test_sample_host_pipeline():
     assert sample_host(logits, [1], o, rng) == 2  # repeat penalty demotes the recent token
     o.update(temperature=1.0, top_k=1)
     assert sample_host(logits, [], o, rng) == 1
+
+
+@pytest.mark.parametrize("name", ["tiny-gemma:2b", "tiny-qwen2:7b", "tiny-llama3.1:8b"])
+def test_reference_model_kv_cache_matches_full_forward(name):
+    cfg = TINY[name]
+    m = ReferenceModel(random_weights(cfg, seed=1), memo_weights=True)
+    t = torch.randint(0, cfg.vocab, (1, 12))
+    full = m.forward(t)
+    cache: list = []
+    inc = torch.cat([m.forward(t[:, :7], cache=cache), m.forward(t[:, 7:9], cache=cache),
+                     m.forward(t[:, 9:], cache=cache)], 1)
+    assert torch.allclose(inc, full, atol=1e-4)
+    assert len(cache) == cfg.n_layers and cache[0][0].shape[1] == 12

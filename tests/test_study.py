@@ -1,0 +1,68 @@
+"""The study RunnerConfig end to end on CPU: runner → per-rank Ollama-compatible server (tiny model, torch
+backend) + modelled remote server → HTTP client → energy plugin → run_table.csv with the reference's columns
+first and the measured-token columns after them."""
+import csv
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parent.parent
+
+
+def _env(tmp_path, **kw):
+    env = dict(os.environ, PYTHONPATH=str(ROOT), CAIN_ASSUME_YES="1", NO_COLOR="1", CAIN_DIST_BACKEND="gloo",
+               CAIN_STUDY_MODELS="tiny-qwen2:1.5b", CAIN_STUDY_LENGTHS="6", CAIN_STUDY_REPETITIONS="2",
+               CAIN_STUDY_COOLDOWN_MS="0", CAIN_STUDY_RESULTS_DIR=str(tmp_path), CAIN_STUDY_SEED="5",
+               CAIN_STUDY_REMOTE="fake", CAIN_STUDY_REMOTE_FAKE_TOK_S="500", CAIN_STUDY_CLIENT="http",
+               CAIN_STUDY_PORT_BASE=str(20000 + os.getpid() % 20000))
+    env.update(kw)
+    return env
+
+
+@pytest.mark.parametrize("gpus", [0, 2])
+def test_study_config_runs_both_arms(tmp_path, gpus):
+    cmd = [sys.executable, "-m", "cain_amd", str(ROOT / "experiments" / "study.py")]
+    if gpus:
+        cmd += ["--gpus", str(gpus)]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=ROOT,
+                       env=_env(tmp_path, CAIN_STUDY_PORT_BASE=str(21000 + gpus * 500 + os.getpid() % 400)))
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    rows = list(csv.DictReader(open(tmp_path / "full_factorial" / "run_table.csv")))
+    assert len(rows) == 4 and all(x["__done"] == "DONE" for x in rows)
+    cols = list(rows[0].keys())
+    assert cols[:11] == ["__run_id", "__done", "model", "method", "length", "topic", "execution_time", "cpu_usage",
+                         "gpu_usage", "memory_usage", "codecarbon__energy_consumed"]
+    assert cols[11] == "energy_usage_J" and "J_per_token" in cols and cols.index("J_per_token") > 11
+    for x in rows:
+        assert int(x["tokens_generated"]) == 8  # "In 6 words" -> ceil(6 * 4/3) tokens
+        assert float(x["execution_time"]) > 0 and float(x["tok_per_s"]) > 0
+        assert x["topic"] and x["server"].startswith("http://127.0.0.1:")
+    methods = sorted(x["method"] for x in rows)
+    assert methods == ["on_device", "on_device", "remote", "remote"]
+    if gpus:
+        assert "rank 1/2" in r.stdout
+    # the writer post-processed the table into the paper's tables
+    assert (tmp_path / "full_factorial" / "analysis" / "results.json").exists()
+
+
+@pytest.mark.gpu
+def test_study_on_device_arm_on_gpu_measures_energy(tmp_path):
+    """On the GPU box: the per-rank server runs the HIP engine, the window reads the amd-smi accumulator."""
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    r = subprocess.run([sys.executable, "-m", "cain_amd", str(ROOT / "experiments" / "study.py")],
+                       capture_output=True, text=True, timeout=900, cwd=ROOT,
+                       env=_env(tmp_path, CAIN_STUDY_MODELS="gemma:2b", CAIN_STUDY_LENGTHS="100",
+                                CAIN_STUDY_REPETITIONS="2", CAIN_STUDY_METHODS="on_device", CAIN_STUDY_CLIENT="curl"))
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    rows = list(csv.DictReader(open(tmp_path / "full_factorial" / "run_table.csv")))
+    assert len(rows) == 2
+    for x in rows:
+        assert int(x["tokens_generated"]) == 134
+        assert float(x["gpu_energy_J"]) > 0 and float(x["avg_gpu_power_W"]) > 50
+        assert float(x["J_per_token"]) > 0 and x["idle_subtracted_J"] != ""
