@@ -27,6 +27,7 @@ e.g. ``CAIN_STUDY_MODELS=gemma:2b CAIN_STUDY_REPETITIONS=3 python -m cain_amd ex
 """
 from __future__ import annotations
 
+import atexit
 import csv
 import dataclasses
 import json
@@ -90,8 +91,9 @@ class StudySettings:
     stream: bool = False
     request_timeout_s: float = 900.0
     server_start_timeout_s: float = 900.0
-    # energy: idle board power measured once per rank after the servers are up (0 disables)
-    idle_baseline_s: float = 2.0
+    # energy: idle board power measured once per rank after the servers are up and have settled (0 disables)
+    idle_baseline_s: float = 3.0
+    idle_settle_s: float = 5.0
 
     @classmethod
     def from_env(cls, base: Optional["StudySettings"] = None) -> "StudySettings":
@@ -126,13 +128,18 @@ def prompt_for(length: str, topic: str) -> str:
     return f"In {length} words, please give me information about " + topic
 
 
-def _wait_alive(url: str, timeout_s: float, proc: Optional[subprocess.Popen] = None) -> None:
+def _wait_alive(url: str, timeout_s: float, proc: Optional[subprocess.Popen] = None,
+                models: Optional[List[str]] = None) -> None:
+    """Wait until OUR server answers: the child must still run (a stale server of an earlier experiment on
+    the same port answers too, and its bind failure kills ours) and it must list the expected models."""
     client = OllamaClient(url, timeout=5.0)
     t_end = time.time() + timeout_s
     while time.time() < t_end:
         if proc is not None and proc.poll() is not None:
-            raise RuntimeError(f"server for {url} exited with {proc.returncode}")
+            raise RuntimeError(f"server for {url} exited with {proc.returncode} (port in use? see its log)")
         if client.alive():
+            if models and not set(models) <= set(client.tags()):
+                raise RuntimeError(f"{url} serves {client.tags()}, expected {models}: another server owns the port")
             return
         time.sleep(0.5)
     raise RuntimeError(f"server {url} not up after {timeout_s:.0f} s")
@@ -152,6 +159,8 @@ class _ServerProc:
                                      stderr=subprocess.STDOUT, cwd=str(REPO_ROOT), env=e, start_new_session=True)
 
     def stop(self) -> None:
+        if self.log.closed:
+            return
         if self.proc.poll() is None:
             try:
                 os.killpg(self.proc.pid, signal.SIGTERM)
@@ -283,14 +292,17 @@ class _StudyBase:
                 args[args.index("--device") + 1] = "cuda:0"
             srv = _ServerProc(args, log_dir / f"on_device_rank{self.rank}.log", env)
             self._servers.append(srv)
+            atexit.register(srv.stop)  # never leave a server behind, even if the experiment dies
             self.local_url = f"http://127.0.0.1:{port}"
             output.console_log(f"starting on-device server {self.local_url} on {device} ({backend})")
-            _wait_alive(self.local_url, s.server_start_timeout_s, srv.proc)
+            _wait_alive(self.local_url, s.server_start_timeout_s, srv.proc, list(s.models))
         if "remote" in s.methods:
             self.remote_url = self._start_remote(log_dir)
         output.console_log_OK(f"servers up: on_device={self.local_url} remote={self.remote_url}")
         if s.idle_baseline_s > 0 and self.idle_power_w is None:
-            # models resident, nothing running: the idle_subtracted_J baseline of every later window
+            # models resident, nothing running: the idle_subtracted_J baseline of every later window (after
+            # a settle period: right after loading, board power is still ~15 % above its idle floor)
+            time.sleep(s.idle_settle_s)
             w = measure_idle_baseline(self, s.idle_baseline_s)
             output.console_log(f"idle baseline {w:.1f} W over {s.idle_baseline_s:.1f} s")
 
@@ -320,8 +332,9 @@ class _StudyBase:
                                "--device", device, "--max-batch", str(s.max_batch), "--max-context",
                                str(s.max_context), "--preload"], log_dir / f"remote_rank{self.rank}.log", env)
             self._servers.append(srv)
+            atexit.register(srv.stop)
             url = f"http://127.0.0.1:{port}"
-            _wait_alive(url, s.server_start_timeout_s, srv.proc)
+            _wait_alive(url, s.server_start_timeout_s, srv.proc, list(s.models))
             return url
         return spec if "://" in spec else f"http://{spec}"
 

@@ -217,14 +217,21 @@ class ExperimentController:
     def do_experiment(self) -> None:
         output.console_log_OK("Experiment setup completed...")
         output.console_log_WARNING("Calling before_experiment config hook")
-        EventSubscriptionController.raise_event(RunnerEvents.BEFORE_EXPERIMENT)
-        todo = self.pending()
-        for n, variation in enumerate(todo):
-            self.run_variation(variation)
-            if n + 1 < len(todo):
-                self.cooldown()
-            if self.config.operation_type is OperationType.SEMI:
-                EventSubscriptionController.raise_event(RunnerEvents.CONTINUE)
-        output.console_log_OK("Experiment completed...")
-        output.console_log_WARNING("Calling after_experiment config hook")
-        EventSubscriptionController.raise_event(RunnerEvents.AFTER_EXPERIMENT)
+        try:
+            EventSubscriptionController.raise_event(RunnerEvents.BEFORE_EXPERIMENT)
+            todo = self.pending()
+            for n, variation in enumerate(todo):
+                self.run_variation(variation)
+                if n + 1 < len(todo):
+                    self.cooldown()
+                if self.config.operation_type is OperationType.SEMI:
+                    EventSubscriptionController.raise_event(RunnerEvents.CONTINUE)
+            output.console_log_OK("Experiment completed...")
+            output.console_log_WARNING("Calling after_experiment config hook")
+            EventSubscriptionController.raise_event(RunnerEvents.AFTER_EXPERIMENT)
+        finally:
+            # per-process resources a config started in BEFORE_EXPERIMENT (e.g. its local servers); the
+            # data-parallel path calls the same hook once per rank (parallel/fanout.py)
+            teardown = getattr(self.config, "teardown_rank", None)
+            if callable(teardown):
+                teardown()

@@ -17,7 +17,8 @@ def _env(tmp_path, **kw):
                CAIN_STUDY_MODELS="tiny-qwen2:1.5b", CAIN_STUDY_LENGTHS="6", CAIN_STUDY_REPETITIONS="2",
                CAIN_STUDY_COOLDOWN_MS="0", CAIN_STUDY_RESULTS_DIR=str(tmp_path), CAIN_STUDY_SEED="5",
                CAIN_STUDY_REMOTE="fake", CAIN_STUDY_REMOTE_FAKE_TOK_S="500", CAIN_STUDY_CLIENT="http",
-               CAIN_STUDY_PORT_BASE=str(20000 + os.getpid() % 20000))
+               CAIN_STUDY_PORT_BASE=str(20000 + os.getpid() % 20000), CAIN_STUDY_IDLE_SETTLE_S="0",
+               CAIN_STUDY_IDLE_BASELINE_S="0.5")
     env.update(kw)
     return env
 
