@@ -16,7 +16,7 @@ from typing import Dict
 
 
 def _aliases() -> Dict[str, Dict[str, object]]:
-    from . import errors, events, isolation, models, output, store
+    from . import controller, errors, events, isolation, misc, models, output, paths, store, validator
     from ..energy import plugin as energy_plugin
     from ..energy import wattsup
     from . import template
@@ -52,6 +52,17 @@ def _aliases() -> Dict[str, Dict[str, object]]:
         "ExtendedTyping.Typing": {"SupportsStr": models.SupportsStr},
         "ExperimentOrchestrator.Architecture.Processify": {"processify": isolation.processify},
         "ExperimentOrchestrator.Misc.BashHeaders": {"BashHeaders": output.BashHeaders},
+        "ExperimentOrchestrator.Misc.PathValidation": {
+            n: getattr(paths, n) for n in ("is_pathname_valid", "is_path_creatable", "is_path_exists_or_creatable",
+                                           "is_path_sibling_creatable", "is_path_exists_or_creatable_portable")},
+        "ExperimentOrchestrator.Misc.DictConversion": {
+            "class_to_dict": validator.class_to_dict, "pop_from_each_dict_in_list": misc.pop_from_each_dict_in_list},
+        "ExperimentOrchestrator.Architecture.Singleton": {
+            "Singleton": misc.Singleton, "SingletonABCMeta": misc.SingletonABCMeta},
+        "ExperimentOrchestrator.Experiment.ExperimentController": {
+            "ExperimentController": controller.ExperimentController},
+        "ExperimentOrchestrator.Experiment.Run.RunController": {"RunController": controller.RunController},
+        "ConfigValidator.Config.Validation.ConfigValidator": {"ConfigValidator": validator.ConfigValidator},
         "Plugins.Profilers.CodecarbonWrapper": {
             "DataColumns": energy_plugin.DataColumns, "emission_tracker": energy_plugin.emission_tracker},
         "Plugins.Profilers.WattsUpPro": {"WattsUpPro": wattsup.WattsUpPro},

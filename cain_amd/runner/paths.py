@@ -1,8 +1,9 @@
 """Path validity / writability checks (reference ExperimentOrchestrator/Misc/PathValidation.py:14-149).
 
-Simplified to what the framework needs: a pathname is valid if every
-component is ≤ NAME_MAX bytes and free of NUL, and creatable if the nearest
-existing ancestor is a writable directory.
+A pathname is valid if every component is ≤ NAME_MAX bytes and free of NUL, and creatable if the
+nearest existing ancestor is a writable directory.  The reference's five public names exist here too
+(``is_path_creatable``, ``is_path_sibling_creatable`` and the ``_portable`` variant included); unlike the
+reference they accept ``Path`` objects, which is what made its writability check a no-op.
 """
 from __future__ import annotations
 
@@ -50,3 +51,36 @@ def ensure_dir(path: Path) -> Path:
         if exc.errno != errno.EEXIST:
             raise
     return Path(path)
+
+
+def is_path_creatable(pathname: str) -> bool:
+    """True if the nearest existing ancestor directory of ``pathname`` is writable."""
+    if not is_pathname_valid(pathname):
+        return False
+    anc = nearest_existing_ancestor(Path(os.path.expanduser(os.fspath(pathname))))
+    return anc.is_dir() and os.access(anc, os.W_OK | os.X_OK)
+
+
+def is_path_sibling_creatable(pathname: str) -> bool:
+    """True if a file next to ``pathname`` could be created (its directory is writable)."""
+    if not is_pathname_valid(pathname):
+        return False
+    parent = Path(os.path.abspath(os.path.expanduser(os.fspath(pathname)))).parent
+    anc = nearest_existing_ancestor(parent)
+    return anc.is_dir() and os.access(anc, os.W_OK | os.X_OK)
+
+
+def is_path_exists_or_creatable_portable(pathname: str) -> bool:
+    """Same answer as :func:`is_path_exists_or_creatable` by actually probing with a temporary file."""
+    import tempfile
+
+    if not is_pathname_valid(pathname):
+        return False
+    p = Path(os.path.abspath(os.path.expanduser(os.fspath(pathname))))
+    if p.exists():
+        return True
+    try:
+        with tempfile.TemporaryFile(dir=nearest_existing_ancestor(p)):
+            return True
+    except OSError:
+        return False

@@ -357,3 +357,29 @@ def test_compat_modules_expose_reference_names():
     assert OT is OperationType
     assert CodecarbonWrapper.DataColumns.ENERGY_CONSUMED.name == "codecarbon__energy_consumed"
     assert callable(OutputProcedure.console_log) and callable(dotenv.load_dotenv)
+
+
+def test_reference_utility_modules_import_by_reference_names(tmp_path):
+    from cain_amd.runner import compat
+
+    compat.install()
+    from ExperimentOrchestrator.Architecture.Singleton import Singleton, SingletonABCMeta  # noqa: F401
+    from ExperimentOrchestrator.Misc.DictConversion import class_to_dict, pop_from_each_dict_in_list
+    from ExperimentOrchestrator.Misc.PathValidation import (is_path_creatable, is_path_exists_or_creatable,
+                                                             is_path_exists_or_creatable_portable,
+                                                             is_path_sibling_creatable, is_pathname_valid)
+
+    class One(metaclass=Singleton):
+        pass
+
+    assert One() is One()
+    assert pop_from_each_dict_in_list([{"a": 1, "b": 2}], "a") == [{"b": 2}]
+    assert is_pathname_valid(str(tmp_path / "x")) and not is_pathname_valid("")
+    assert is_path_creatable(str(tmp_path / "new" / "dir")) and is_path_sibling_creatable(str(tmp_path / "f"))
+    assert is_path_exists_or_creatable(tmp_path / "p") and is_path_exists_or_creatable_portable(str(tmp_path / "q"))
+
+    class Cfg:
+        name = "n"
+        x = 3
+
+    assert class_to_dict(Cfg())["x"] == 3
