@@ -15,11 +15,11 @@ Backends
            device, one host sync per generation.
 ``torch``  torch-eager oracle (``models/reference.py``): CPU tests / debugging.
 
-Batching: up to ``max_batch`` (≤ 64) sequences decode together ("trial
+Batching: up to ``max_batch`` (≤ 128) sequences decode together ("trial
 batching") — each row has its own cache slot, position, budget
 and sampling options; rows that finish early idle until the batch ends.
 Prefill: every prompt token but the last goes through the same forward as
-≤64-row chunks (rows carry their own slot/position, so the decode attention
+≤128-row chunks (rows carry their own slot/position, so the decode attention
 kernel doubles as causal prefill attention); the last prompt token is the
 first decode step's input, so no separate prefill LM-head path exists.
 """
@@ -41,7 +41,7 @@ from ..models.weights import ModelWeights, pack_for_engine, random_weights
 #: Ollama's default sampling options (SURVEY §2.4 "Sampling" row)
 OLLAMA_DEFAULTS = dict(temperature=0.8, top_k=40, top_p=0.9, repeat_penalty=1.1, repeat_last_n=64, seed=None)
 
-MAX_ROWS = 64
+MAX_ROWS = 128  # rows per forward: decode batch / prefill chunk (runtime.hip CAIN_MAX_ROWS)
 
 
 @dataclass
@@ -219,7 +219,7 @@ class DecodeEngine:
         for k in ("x", "q", "attn", "act", "logits", "counters"):
             setattr(d, k, _ptr(self.buf[k]))
         d.part_o, d.part_ml = _ptr(self.part_o), _ptr(self.part_ml)
-        # batched GEMM (16 < M <= 64) split-K workspace: largest need over this model's GEMM shapes
+        # batched GEMM (16 < M <= 128) split-K workspace: largest need over this model's GEMM shapes
         shapes = [(cfg.qkv_dim, cfg.d_model), (cfg.d_model, cfg.q_dim), (2 * cfg.ffn, cfg.d_model),
                   (cfg.d_model, cfg.ffn), (cfg.vocab, cfg.d_model)]
         ws = max([ops.gemm_ws_bytes(n, k, m) for n, k in shapes for m in range(17, R + 1)] + [0])
@@ -344,7 +344,7 @@ class DecodeEngine:
         dev = self.device
         B = len(ids)
         with torch.cuda.stream(self.stream):
-            # ---- prefill: all prompt tokens except the last, in <=64-row chunks
+            # ---- prefill: all prompt tokens except the last, in <=MAX_ROWS-row chunks
             t0 = time.perf_counter_ns()
             self._prefill(ids)
             # ---- decode rows

@@ -439,7 +439,7 @@ static int gemm_dispatch(GemmArgs a, int epi, int norm, int waves, hipStream_t s
 }
 
 // =====================================================================================================
-// Batched weight-streaming GEMM, 16 < M <= 64 (batched decode, prefill chunks).
+// Batched weight-streaming GEMM, 16 < M <= 128 (batched decode, prefill chunks).
 //
 // The skinny kernel's waves split K and each wave reads its own activation fragments straight from L2:
 // at M = 64 that is 4 B of activation traffic per weight byte and the CU's vector-memory path, not HBM,
@@ -758,14 +758,17 @@ static BgPlan bgemm_plan(int N, int K, int M, int ntw_req) {
   static const int w_env = env_int("CAIN_BGEMM_W", 0);
   static const int ck_env = env_int("CAIN_BGEMM_CK", 0);
   BgPlan p{};
-  p.nb = M <= 32 ? 2 : 4;
+  p.nb = M <= 32 ? 2 : (M <= 64 ? 4 : 8);
   const int rows1 = 16 * BG_WAVES;
-  p.ntw = ntw_req > 0 ? ntw_req : ((N + rows1 - 1) / rows1 >= 512 ? 2 : 1);
+  p.ntw = p.nb == 8 ? 1 : (ntw_req > 0 ? ntw_req : ((N + rows1 - 1) / rows1 >= 512 ? 2 : 1));
   // the 4-wave and 16-slice-chunk variants exist for NTW = 1 only; 4-wave workgroups (64-row blocks)
   // measured faster on N <= 4096 (O / down projections: 23.2 vs 25.8 us, 41.5 vs 46.7 us at M = 64)
   const bool narrow = N <= 4096 && p.ntw == 1;
   p.w = (w_env == 4 || (w_env == 0 && narrow)) && p.ntw == 1 ? 4 : BG_WAVES;
-  p.ck = (ck_env == 16 && p.ntw == 1 && p.w == 8 && (K / 32) % 16 == 0) ? 16 : BG_CK;
+  if (p.nb == 8)  // 128 rows: 4-slice chunks keep the double-buffered stage at 64 KiB (2 workgroups per CU)
+    p.ck = (ck_env == 8 && p.w == 8) ? 8 : 4;
+  else
+    p.ck = (ck_env == 16 && p.ntw == 1 && p.w == 8 && (K / 32) % 16 == 0) ? 16 : BG_CK;
   const int rows = 16 * p.w * p.ntw;
   p.nblk = (N + rows - 1) / rows;
   const int nchunk = (K / 32) / p.ck;
@@ -790,7 +793,7 @@ static size_t bgemm_ws_bytes(const BgPlan& p) {
 
 template <int NB, int NTW, int W, int CK, int EPI, bool NORM>
 static hipError_t bg_launch(const GemmArgs& a, const BgArgs& b, int nblk, hipStream_t st) {
-  constexpr int U = NTW == 1 ? 8 : 4;
+  constexpr int U = NTW == 1 ? (CK < 8 ? CK : 8) : 4;
   hipLaunchKernelGGL((bgemm_kernel<NB, NTW, W, CK, U, EPI, NORM>), dim3(nblk * b.ksplit), dim3(W * 64), 0, st, a, b);
   return hipGetLastError();
 }
@@ -810,10 +813,16 @@ static hipError_t bg_launch_e(int epi, const GemmArgs& a, const BgArgs& b, int n
 
 template <int NB, bool NORM>
 static hipError_t bg_launch_shape(int epi, const BgPlan& p, const GemmArgs& a, const BgArgs& b, hipStream_t st) {
-  if (p.ntw == 2) return bg_launch_e<NB, 2, 8, 8, NORM>(epi, a, b, p.nblk, st);
-  if (p.w == 4) return bg_launch_e<NB, 1, 4, 8, NORM>(epi, a, b, p.nblk, st);
-  if (p.ck == 16) return bg_launch_e<NB, 1, 8, 16, NORM>(epi, a, b, p.nblk, st);
-  return bg_launch_e<NB, 1, 8, 8, NORM>(epi, a, b, p.nblk, st);
+  if constexpr (NB == 8) {
+    if (p.w == 4) return bg_launch_e<8, 1, 4, 4, NORM>(epi, a, b, p.nblk, st);
+    if (p.ck == 8) return bg_launch_e<8, 1, 8, 8, NORM>(epi, a, b, p.nblk, st);
+    return bg_launch_e<8, 1, 8, 4, NORM>(epi, a, b, p.nblk, st);
+  } else {
+    if (p.ntw == 2) return bg_launch_e<NB, 2, 8, 8, NORM>(epi, a, b, p.nblk, st);
+    if (p.w == 4) return bg_launch_e<NB, 1, 4, 8, NORM>(epi, a, b, p.nblk, st);
+    if (p.ck == 16) return bg_launch_e<NB, 1, 8, 16, NORM>(epi, a, b, p.nblk, st);
+    return bg_launch_e<NB, 1, 8, 8, NORM>(epi, a, b, p.nblk, st);
+  }
 }
 
 static int bgemm_dispatch(const GemmArgs& a, int epi, bool norm, const BgPlan& p, void* ws, hipStream_t st) {
@@ -825,7 +834,8 @@ static int bgemm_dispatch(const GemmArgs& a, int epi, bool norm, const BgPlan& p
   b.part_ss = b.part + p.part_floats;
   hipError_t e;
   if (p.nb == 2) e = norm ? bg_launch_shape<2, true>(epi, p, a, b, st) : bg_launch_shape<2, false>(epi, p, a, b, st);
-  else e = norm ? bg_launch_shape<4, true>(epi, p, a, b, st) : bg_launch_shape<4, false>(epi, p, a, b, st);
+  else if (p.nb == 4) e = norm ? bg_launch_shape<4, true>(epi, p, a, b, st) : bg_launch_shape<4, false>(epi, p, a, b, st);
+  else e = norm ? bg_launch_shape<8, true>(epi, p, a, b, st) : bg_launch_shape<8, false>(epi, p, a, b, st);
   return int(e);
 }
 
@@ -842,7 +852,7 @@ static int bgemm_ntw() {
 // M <= 32 on narrow outputs with short K (N < 8192, K <= 4096: O / QKV projections) stays on the skinny
 // kernel, which measured faster there (its whole grid streams from the first cycle; no staging, no combine).
 static bool bgemm_eligible(int N, int K, int M) {
-  return M > bgemm_min_m() && M <= 64 && K % (32 * BG_CK) == 0 && (M > 32 || N >= 8192 || K > 4096);
+  return M > bgemm_min_m() && M <= 128 && K % (32 * BG_CK) == 0 && (M > 32 || N >= 8192 || K > 4096);
 }
 
 // Workspace the batched path needs for a GEMM of this shape (0 when the skinny kernel runs it).
@@ -868,7 +878,7 @@ CAIN_API int cain_skinny_gemm_ex(const void* Wp, const void* X, int ldx, int K, 
   return gemm_dispatch(a, epi, gain != nullptr, waves, st);
 }
 
-// Full entry: batched path for 16 < M <= 64 when a workspace of cain_gemm_ws_bytes() (zeroed once) is
+// Full entry: batched path for 16 < M <= 128 when a workspace of cain_gemm_ws_bytes() (zeroed once) is
 // given, the skinny kernel otherwise.
 CAIN_API int cain_gemm(const void* Wp, const void* X, int ldx, int K, int N, int M, void* Y, int ldy,
                        const float* bias, const void* gain, float eps, const int* slot, const int* pos,

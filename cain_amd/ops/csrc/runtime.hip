@@ -20,6 +20,8 @@
 
 #include "common.h"
 
+constexpr int CAIN_MAX_ROWS = 128;  // rows per forward (decode batch / prefill chunk)
+
 CAIN_API int cain_gemm(const void* Wp, const void* X, int ldx, int K, int N, int M, void* Y, int ldy,
                        const float* bias, const void* gain, float eps, const int* slot, const int* pos,
                        const float* cos_t, const float* sin_t, void* kc, void* vtc, int H, int Hkv, int hd, int T_max,
@@ -148,7 +150,7 @@ CAIN_API void cain_plan_destroy(void* plan) { delete static_cast<Plan*>(plan); }
 CAIN_API int cain_plan_forward(void* plan, int M, const CainRows* rows, int want_logits, int want_sample,
                                hipStream_t st) {
   auto* p = static_cast<Plan*>(plan);
-  if (M < 1 || M > 64 || M > p->d.Mpad) return -1;
+  if (M < 1 || M > CAIN_MAX_ROWS || M > p->d.Mpad) return -1;
   return forward(*p, M, *rows, want_logits, want_sample, st);
 }
 
@@ -156,7 +158,7 @@ CAIN_API int cain_plan_forward(void* plan, int M, const CainRows* rows, int want
 CAIN_API void* cain_plan_capture(void* plan, int M, const CainRows* rows, int steps, hipStream_t st, int* err) {
   auto* p = static_cast<Plan*>(plan);
   *err = 0;
-  if (M < 1 || M > 64 || M > p->d.Mpad || steps < 1) {
+  if (M < 1 || M > CAIN_MAX_ROWS || M > p->d.Mpad || steps < 1) {
     *err = -1;
     return nullptr;
   }

@@ -85,7 +85,7 @@ def test_skinny_gemm_f32_logits():
 
 
 @pytest.mark.parametrize("act", ["silu", "gelu"])
-@pytest.mark.parametrize("M", [1, 16, 40])
+@pytest.mark.parametrize("M", [1, 16, 40, 120])
 def test_skinny_gemm_gateup(act, M):
     torch.manual_seed(3)
     F, K = 1536, 1024
@@ -101,7 +101,7 @@ def test_skinny_gemm_gateup(act, M):
     assert rel_err(y, a * u) < 1.5e-2
 
 
-@pytest.mark.parametrize("M", [17, 32, 48, 64])
+@pytest.mark.parametrize("M", [17, 32, 48, 64, 65, 100, 128])
 @pytest.mark.parametrize("N,K,norm", [(32064, 3072, True), (256, 14336, False), (4096, 4096, True),
                                       (1920, 8960, False)])
 def test_batched_gemm_matches_skinny_and_reference(M, N, K, norm):
@@ -114,7 +114,7 @@ def test_batched_gemm_matches_skinny_and_reference(M, N, K, norm):
     assert ops.gemm_ws_bytes(N, K, M) > 0 or (M <= 32 and N < 8192)  # narrow N at M <= 32: skinny path
     wp = pack_mfma_a(W)
     ys = [ops.skinny_gemm(wp, x, N, ops.EPI_F32, gain=g, eps=1e-6) for _ in range(3)]
-    y0 = ops.skinny_gemm(wp, x, N, ops.EPI_F32, gain=g, eps=1e-6, batched=False)
+    y0 = ops.skinny_gemm(wp, x, N, ops.EPI_F32, gain=g, eps=1e-6, batched=False) if M <= 64 else None
     xr = x.float()
     if norm:
         xr = xr * torch.rsqrt(xr.pow(2).mean(-1, keepdim=True) + 1e-6) * g.float()
@@ -122,7 +122,8 @@ def test_batched_gemm_matches_skinny_and_reference(M, N, K, norm):
     for y in ys:
         assert rel_err(y, ref) < 2e-3
         assert torch.equal(y, ys[0])  # deterministic reduction order
-    assert rel_err(ys[0], y0) < 2e-3
+    if y0 is not None:  # the skinny kernel covers M <= 64
+        assert rel_err(ys[0], y0) < 2e-3
 
 
 @pytest.mark.parametrize("d", [1536, 2048, 3584, 4096])
@@ -154,11 +155,11 @@ def _rot(x, c, s_):
 
 
 @pytest.mark.parametrize("H,Hkv,hd", [(32, 8, 128), (12, 2, 128), (8, 1, 256), (32, 32, 96), (28, 4, 128)])
-@pytest.mark.parametrize("M", [1, 5, 40])
+@pytest.mark.parametrize("M", [1, 5, 40, 128])
 @pytest.mark.parametrize("norm", [False, True])
 def test_fused_qkv_rope_kv_append(H, Hkv, hd, M, norm):
     torch.manual_seed(8)
-    K, T_max, S = 512, 256, 64
+    K, T_max, S = 512, 256, max(64, M)
     qkv_dim = (H + 2 * Hkv) * hd
     W = (torch.randn(qkv_dim, K, device=DEV) * 0.05).bfloat16()
     bias = torch.randn(qkv_dim, device=DEV)
