@@ -267,7 +267,7 @@ struct Sampler {
   std::vector<es_sample_t> ring;
   size_t ring_cap = 1 << 16;
   size_t head = 0, count = 0;  // ring of slow samples
-  uint64_t dropped = 0;
+  std::atomic<uint64_t> dropped{0};  // written under mu by the sampler, read lock-free by es_dropped
   uint64_t t_start = 0;
   CpuTimes last_cpu;
   std::vector<std::string> rapl;
@@ -279,7 +279,7 @@ struct Sampler {
     size_t idx = (head + count) % ring_cap;
     if (count == ring_cap) {  // overwrite oldest
       head = (head + 1) % ring_cap;
-      ++dropped;
+      dropped.fetch_add(1, std::memory_order_relaxed);
     } else {
       ++count;
     }
@@ -578,7 +578,7 @@ int es_drain(void* h, es_sample_t* out, int max) {
   return n;
 }
 
-uint64_t es_dropped(void* h) { return h ? static_cast<Sampler*>(h)->dropped : 0; }
+uint64_t es_dropped(void* h) { return h ? static_cast<Sampler*>(h)->dropped.load(std::memory_order_relaxed) : 0; }
 
 int es_sample_size(void) { return int(sizeof(es_sample_t)); }
 

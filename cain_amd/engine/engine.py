@@ -99,14 +99,14 @@ def _row_options(opts: Optional[Dict], cfg: ModelConfig, index: int, base_seed: 
 
 # ============================================================== ctypes structs
 class _CainLayer(ctypes.Structure):
-    _fields_ = [(n, ctypes.c_void_p) for n in ("attn_norm", "wqkv", "bqkv", "wo", "mlp_norm", "wgu", "wdown")]
+    _fields_ = [(n, ctypes.c_void_p) for n in ("wqkv", "bqkv", "wo", "wgu", "wdown")]
 
 
 class _CainPlanDesc(ctypes.Structure):
     _fields_ = ([(n, ctypes.c_int) for n in ("n_layers", "d", "H", "Hkv", "hd", "ffn", "V", "act_kind", "T_max",
                                             "Mpad", "nsplit", "waves")]
                 + [(n, ctypes.c_float) for n in ("eps", "embed_scale", "attn_scale")]
-                + [(n, ctypes.c_void_p) for n in ("embed", "final_norm", "lm_head", "layers", "kcache", "vtcache")]
+                + [(n, ctypes.c_void_p) for n in ("embed", "lm_head", "layers", "kcache", "vtcache")]
                 + [("kv_layer_elems", ctypes.c_longlong)]
                 + [(n, ctypes.c_void_p) for n in ("cos_t", "sin_t", "x", "q", "attn", "act", "logits",
                                                  "part_o", "part_ml", "counters", "gemm_ws")]
@@ -202,8 +202,8 @@ class DecodeEngine:
             dev)
         self._layers = (_CainLayer * L)()
         for i, lp in enumerate(packed["layers"]):
-            self._layers[i] = _CainLayer(_ptr(lp["attn_norm"]), _ptr(lp["wqkv"]), _ptr(lp["bqkv"]), _ptr(lp["wo"]),
-                                         _ptr(lp["mlp_norm"]), _ptr(lp["wgu"]), _ptr(lp["wdown"]))
+            self._layers[i] = _CainLayer(_ptr(lp["wqkv"]), _ptr(lp["bqkv"]), _ptr(lp["wo"]), _ptr(lp["wgu"]),
+                                         _ptr(lp["wdown"]))
         self._packed = packed
         d = _CainPlanDesc()
         d.n_layers, d.d, d.H, d.Hkv, d.hd = L, cfg.d_model, cfg.n_heads, cfg.n_kv_heads, cfg.head_dim
@@ -212,7 +212,7 @@ class DecodeEngine:
         d.eps = cfg.norm_eps
         d.embed_scale = float(torch.tensor(math.sqrt(cfg.d_model), dtype=bf).float()) if cfg.embed_scale else 1.0
         d.attn_scale = 1.0 / math.sqrt(cfg.head_dim)
-        d.embed, d.final_norm, d.lm_head = _ptr(self.weights.embed), _ptr(packed["final_norm"]), _ptr(packed["lm_head"])
+        d.embed, d.lm_head = _ptr(self.weights.embed), _ptr(packed["lm_head"])
         d.layers = ctypes.cast(self._layers, ctypes.c_void_p).value
         d.kcache, d.vtcache, d.kv_layer_elems = _ptr(self.kcache), _ptr(self.vtcache), kv_layer
         d.cos_t, d.sin_t = _ptr(self.cos_t), _ptr(self.sin_t)

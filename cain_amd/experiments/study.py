@@ -401,6 +401,15 @@ class _StudyBase:
             "memory_usage": round(r.memory_usage, 3) if r is not None else "",
         }
         self._last_stats = self.response.stats() if self.response is not None else {}
+        if r is not None and r.samples:  # reference run_dir/cpu_mem_usage.csv (RunnerConfig.py:146-168)
+            try:
+                with open(context.run_dir / "cpu_mem_usage.csv", "w") as fh:
+                    fh.write("timestamp,cpu_usage,memory_usage\n")
+                    for smp in r.samples:
+                        if smp.get("gpu", -1) <= 0:  # one row per sampler tick (host-only or first GPU)
+                            fh.write(f"{smp['t_ns'] / 1e9:.6f},{smp['cpu_pct']:.3f},{smp['mem_pct']:.3f}\n")
+            except OSError:  # pragma: no cover
+                pass
         try:
             (context.run_dir / "response.json").write_text(json.dumps(self.response.data if self.response else {},
                                                                       indent=1))

@@ -133,27 +133,34 @@ def effective_gain(cfg: ModelConfig, w: torch.Tensor) -> torch.Tensor:
     return (w.float() + 1.0).to(w.dtype) if cfg.norm_add_one else w
 
 
+def fold_gain(w: torch.Tensor, g: torch.Tensor) -> torch.Tensor:
+    """W diag(g): the RMSNorm gain that feeds a GEMM folded into its weight columns (fp32 product, one
+    bf16 rounding).  RMSNorm(x) W^T = inv(x) * (x (W diag(g))^T), so the fused kernels only need the
+    per-row sum of squares of x (gemm.hip, NORM)."""
+    return (w.float() * g.float()[None, :]).to(w.dtype)
+
+
 def pack_for_engine(mw: ModelWeights, free_natural: bool = False) -> Dict[str, object]:
-    """Build the decode engine's packed tensors (see module doc)."""
+    """Build the decode engine's packed tensors (see module doc); norm gains are folded into the GEMM
+    weights they feed (attn_norm -> wqkv, mlp_norm -> gate/up, final_norm -> lm_head)."""
     cfg = mw.cfg
     perm = qkv_row_permutation(cfg).to(mw.device)
     layers = []
     for lw in mw.layers:
+        ga = effective_gain(cfg, lw.attn_norm)
+        gm = effective_gain(cfg, lw.mlp_norm)
         layers.append({
-            "attn_norm": effective_gain(cfg, lw.attn_norm).contiguous(),
-            "wqkv": pack_mfma_a(lw.wqkv[perm]),
+            "wqkv": pack_mfma_a(fold_gain(lw.wqkv[perm], ga)),
             "bqkv": None if lw.bqkv is None else lw.bqkv.float()[perm].contiguous(),
             "wo": pack_mfma_a(lw.wo),
-            "mlp_norm": effective_gain(cfg, lw.mlp_norm).contiguous(),
-            "wgu": pack_mfma_a(interleave_tiles(lw.w_gate, lw.w_up, tile=8)),
+            "wgu": pack_mfma_a(interleave_tiles(fold_gain(lw.w_gate, gm), fold_gain(lw.w_up, gm), tile=8)),
             "wdown": pack_mfma_a(lw.w_down),
         })
         if free_natural:
             lw.wqkv = lw.wo = lw.w_gate = lw.w_up = lw.w_down = None
     packed = {
         "layers": layers,
-        "final_norm": effective_gain(cfg, mw.final_norm).contiguous(),
-        "lm_head": pack_mfma_a(mw.lm_head),
+        "lm_head": pack_mfma_a(fold_gain(mw.lm_head, effective_gain(cfg, mw.final_norm))),
     }
     if free_natural and not cfg.tie_embeddings:
         mw.lm_head = None

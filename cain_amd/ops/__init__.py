@@ -63,9 +63,9 @@ def load() -> ctypes.CDLL:
             lib = ctypes.CDLL(str(LIB_PATH))
         except OSError as exc:
             raise NativeOpsUnavailable(f"cannot load {LIB_PATH}: {exc}") from exc
-        lib.cain_skinny_gemm_ex.argtypes = ([vp, vp, ci, ci, ci, ci, vp, ci, vp, vp, cf, vp, vp, vp, vp, vp, vp]
+        lib.cain_skinny_gemm_ex.argtypes = ([vp, vp, ci, ci, ci, ci, vp, ci, vp, ci, cf, vp, vp, vp, vp, vp, vp]
                                             + [ci] * 6 + [vp])
-        lib.cain_gemm.argtypes = ([vp, vp, ci, ci, ci, ci, vp, ci, vp, vp, cf, vp, vp, vp, vp, vp, vp]
+        lib.cain_gemm.argtypes = ([vp, vp, ci, ci, ci, ci, vp, ci, vp, ci, cf, vp, vp, vp, vp, vp, vp]
                                   + [ci] * 4 + [vp, ctypes.c_longlong, ci, ci, vp])
         lib.cain_gemm_ws_bytes.restype = ctypes.c_longlong
         lib.cain_gemm_ws_bytes.argtypes = [ci, ci, ci]
@@ -133,21 +133,22 @@ def _workspace(device, nbytes: int) -> Optional[torch.Tensor]:
     return ws
 
 
-def _gemm_call(lib, wp, x, K, n, M, out, bias, gain, eps, slot, pos, cos_t, sin_t, kc, vtc, H, Hkv, hd, T_max, epi,
+def _gemm_call(lib, wp, x, K, n, M, out, bias, norm, eps, slot, pos, cos_t, sin_t, kc, vtc, H, Hkv, hd, T_max, epi,
                waves, batched: bool):
     nbytes = gemm_ws_bytes(n, K, M) if batched else 0
     ws = _workspace(x.device, nbytes)
-    return lib.cain_gemm(_p(wp), _p(x), x.stride(0), K, n, M, _p(out), out.stride(0), _p(bias), _p(gain), eps,
+    return lib.cain_gemm(_p(wp), _p(x), x.stride(0), K, n, M, _p(out), out.stride(0), _p(bias), int(bool(norm)), eps,
                          _p(slot), _p(pos), _p(cos_t), _p(sin_t), _p(kc), _p(vtc), H, Hkv, hd, T_max, _p(ws),
                          nbytes, epi, waves, _stream())
 
 
 def skinny_gemm(wp: torch.Tensor, x: torch.Tensor, n: int, epi: int = EPI_BF16, bias=None,
-                out: Optional[torch.Tensor] = None, waves: int = 0, gain=None, eps: float = 1e-6,
+                out: Optional[torch.Tensor] = None, waves: int = 0, norm: bool = False, eps: float = 1e-6,
                 batched: bool = True) -> torch.Tensor:
     """y[M, n] = epi(B(x)[M, K] @ W^T) with W packed by ``pack_mfma_a`` (gate/up interleaved for act epis).
 
-    ``gain``: fused RMSNorm of x (y = rsqrt(mean(x^2) + eps) * (W (x * gain))).
+    ``norm``: fused RMSNorm of x, y = rsqrt(mean(x^2) + eps) * (x @ W^T) where the norm gain must already
+    be folded into W (``models.weights.fold_gain``).
     ``EPI_RESID``: ``out`` is the residual stream, updated in place.
     ``batched``: 16 < M <= 64 runs the LDS-staged split-K kernel (False forces the skinny kernel).
     """
@@ -161,19 +162,19 @@ def skinny_gemm(wp: torch.Tensor, x: torch.Tensor, n: int, epi: int = EPI_BF16, 
         assert out is not None and out.shape == (M, n_out), "EPI_RESID updates `out` (the residual) in place"
     if out is None:
         out = torch.empty(M, n_out, device=x.device, dtype=torch.float32 if epi == EPI_F32 else torch.bfloat16)
-    rc = _gemm_call(lib, wp, x, K, n, M, out, bias, gain, eps, None, None, None, None, None, None, 0, 0, 0, 0, epi,
+    rc = _gemm_call(lib, wp, x, K, n, M, out, bias, norm, eps, None, None, None, None, None, None, 0, 0, 0, 0, epi,
                     waves, batched)
     _check(rc, "skinny_gemm")
     return out
 
 
-def qkv_rope(wp, x, n, q_out, kc, vtc, slot, pos, cos_t, sin_t, H, Hkv, hd, bias=None, gain=None,
+def qkv_rope(wp, x, n, q_out, kc, vtc, slot, pos, cos_t, sin_t, H, Hkv, hd, bias=None, norm: bool = False,
              eps: float = 1e-6, waves: int = 0, batched: bool = True) -> None:
     """Fused QKV projection (+RMSNorm, +bias) -> RoPE -> Q buffer / K cache / V^T cache."""
     lib = load()
     M, K = x.shape
     T_max = kc.shape[-2]
-    rc = _gemm_call(lib, wp, x, K, n, M, q_out, bias, gain, eps, slot, pos, cos_t, sin_t, kc, vtc, H, Hkv, hd,
+    rc = _gemm_call(lib, wp, x, K, n, M, q_out, bias, norm, eps, slot, pos, cos_t, sin_t, kc, vtc, H, Hkv, hd,
                     T_max, EPI_QKV_ROPE, waves, batched)
     _check(rc, "qkv_rope")
 

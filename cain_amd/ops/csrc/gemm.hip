@@ -12,8 +12,9 @@
 // reads X[m][32s+8g .. +8]); neither operand goes through LDS
 // (cdna_hip_programming.md §5, 'GEMV / M <= 16' row).
 //
-// Fused RMSNorm (NORM): W.(x * inv * g) = inv * W.(x * g) with inv a per-row
-// scalar, so the B fragment is bf16(x * gain), every workgroup accumulates the
+// Fused RMSNorm (NORM): W.(x * inv * g) = inv * (W diag(g)).x with inv a per-row
+// scalar; the gain g is folded into the weight columns at pack time
+// (cain_amd/models/weights.py fold_gain), so the B fragment is x itself, every workgroup accumulates the
 // row's sum of squares from the x fragments it streams anyway (its waves cover
 // all of K), and the epilogue scales by rsqrt(mean(x^2) + eps): no separate
 // normalisation kernel, no launch gap, no cross-kernel state.
@@ -48,8 +49,7 @@ struct GemmArgs {
   void* Y;
   int ldy;
   const float* bias;
-  // NORM (fused RMSNorm): B = bf16(x * gain), acc *= rsqrt(mean(x^2) + eps)
-  const __bf16* gain;
+  // NORM (fused RMSNorm, gain folded into W): acc *= rsqrt(mean(x^2) + eps)
   float eps;
   // QKV_ROPE
   const int* slot;
@@ -236,7 +236,6 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_gemm_kernel(const GemmArgs 
     xbase[b] = a.X + (size_t)m * a.ldx + ((lane >> 4) << 3);
     ssq[b] = 0.f;
   }
-  const __bf16* gbase = NORM ? a.gain + ((lane >> 4) << 3) : nullptr;
 
   // raw fragment loads (issued early); normalisation happens at use, after the data landed
   // non-temporal weight loads when this workgroup is the tile's only reader; with msplit > 1 the
@@ -246,30 +245,25 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_gemm_kernel(const GemmArgs 
     return ntl ? __builtin_nontemporal_load(wbase[t] + (size_t)s * 64) : wbase[t][(size_t)s * 64];
   };
   auto load_x = [&](int s, int b) -> bf16x8 { return *reinterpret_cast<const bf16x8*>(xbase[b] + s * 32); };
-  auto load_g = [&](int s) -> bf16x8 {
-    if constexpr (NORM) return *reinterpret_cast<const bf16x8*>(gbase + s * 32);
-    else return bf16x8{};
-  };
-  // RMSNorm factorisation: W (x * inv * g) = inv * (W (x * g)); the per-row inv is applied in the
-  // epilogue and the sum of squares is accumulated from the x fragments this WG streams anyway
+  // RMSNorm factorisation: (W diag(g)) (x * inv) = inv * ((W diag(g)) x); the per-row inv is applied in
+  // the epilogue and the sum of squares is accumulated from the x fragments this WG streams anyway
   // (its waves cover all of K), so no separate norm kernel and no cross-kernel sum-of-squares buffer.
-  auto norm_x = [&](bf16x8 v, bf16x8 g, int b) -> bf16x8 {
+  auto norm_x = [&](bf16x8 v, int b) -> bf16x8 {
     if constexpr (NORM) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const float f = bf2f(v[j]);
         ssq[b] += f * f;
-        v[j] = f2bf(f * bf2f(g[j]));
       }
     }
     return v;
   };
-  auto compute = [&](const bf16x8 (&w)[U][NT], const bf16x8 (&x)[U][NB], const bf16x8 (&g)[U]) {
+  auto compute = [&](const bf16x8 (&w)[U][NT], const bf16x8 (&x)[U][NB]) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       bf16x8 xb[NB];
 #pragma unroll
-      for (int b = 0; b < NB; ++b) xb[b] = norm_x(x[u][b], g[u], b);
+      for (int b = 0; b < NB; ++b) xb[b] = norm_x(x[u][b], b);
 #pragma unroll
       for (int t = 0; t < NT; ++t)
 #pragma unroll
@@ -282,17 +276,16 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_gemm_kernel(const GemmArgs 
   int s = s_beg;
   const int nfull = (s_end - s_beg) / U;
   if (nfull > 0) {
-    bf16x8 wa[U][NT], xa[U][NB], ga[U];
+    bf16x8 wa[U][NT], xa[U][NB];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
 #pragma unroll
       for (int t = 0; t < NT; ++t) wa[u][t] = load_w(s + u, t);
 #pragma unroll
       for (int b = 0; b < NB; ++b) xa[u][b] = load_x(s + u, b);
-      ga[u] = load_g(s + u);
     }
     for (int c = 0; c < nfull; ++c) {
-      bf16x8 wn[U][NT], xn[U][NB], gn[U];
+      bf16x8 wn[U][NT], xn[U][NB];
       const int sn = s + U;
       const bool more = c + 1 < nfull;
       if (more) {
@@ -302,10 +295,9 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_gemm_kernel(const GemmArgs 
           for (int t = 0; t < NT; ++t) wn[u][t] = load_w(sn + u, t);
 #pragma unroll
           for (int b = 0; b < NB; ++b) xn[u][b] = load_x(sn + u, b);
-          gn[u] = load_g(sn + u);
         }
       }
-      compute(wa, xa, ga);
+      compute(wa, xa);
       if (more) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -313,20 +305,18 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_gemm_kernel(const GemmArgs 
           for (int t = 0; t < NT; ++t) wa[u][t] = wn[u][t];
 #pragma unroll
           for (int b = 0; b < NB; ++b) xa[u][b] = xn[u][b];
-          ga[u] = gn[u];
         }
       }
       s = sn;
     }
   }
   for (; s < s_end; ++s) {
-    const bf16x8 g = load_g(s);
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
       const bf16x8 w = load_w(s, t);
 #pragma unroll
       for (int b = 0; b < NB; ++b)
-        acc[t][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w, norm_x(load_x(s, b), g, b), acc[t][b], 0, 0, 0);
+        acc[t][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w, norm_x(load_x(s, b), b), acc[t][b], 0, 0, 0);
     }
   }
 
@@ -445,7 +435,7 @@ static int gemm_dispatch(GemmArgs a, int epi, int norm, int waves, hipStream_t s
 // at M = 64 that is 4 B of activation traffic per weight byte and the CU's vector-memory path, not HBM,
 // becomes the limit.  Here the waves of a workgroup split N instead (each owns NTW 16-row tiles) and
 // walk the SAME k-range, so the activation chunk X[0..M)[k0..k0+256) is staged ONCE per workgroup into
-// LDS (bf16, already multiplied by the RMSNorm gain, MFMA-B-fragment-major so both the staging write
+// LDS (bf16, MFMA-B-fragment-major so both the staging write
 // and every ds_read_b128 of a wave are 1 KiB contiguous, conflict-free) and double-buffered: chunk c+1
 // streams in from L2 while chunk c feeds the MFMAs; one barrier per chunk.  Weights still stream from
 // HBM as 1 KiB non-temporal fragment loads, prefetched one slice group ahead in registers.
@@ -479,7 +469,7 @@ __device__ __forceinline__ f32x4 ld_wt(const float* p) {
 }
 
 template <int NB, int NTW, int W, int CK, int U, int EPI, bool NORM>
-__global__ __launch_bounds__(W * 64) void bgemm_kernel(const GemmArgs a, const BgArgs bg) {
+__global__ __launch_bounds__(W * 64, (W == 8 && NTW == 1 && CK * NB <= 32) ? 4 : 2) void bgemm_kernel(const GemmArgs a, const BgArgs bg) {
   constexpr int BG_CK = CK;
   constexpr int FR = BG_CK * NB;        // B fragments per chunk
   constexpr int FPW = FR / W;           // staged per wave per chunk
@@ -530,30 +520,22 @@ __global__ __launch_bounds__(W * 64) void bgemm_kernel(const GemmArgs a, const B
     xrow[i] = a.X + (size_t)m * a.ldx + sl * 32 + ((lane >> 4) << 3);
     ssq[i] = 0.f;
   }
-  auto stage_load = [&](int c, bf16x8 (&xr)[FPW], bf16x8 (&gr)[FPW]) {
+  auto stage_load = [&](int c, bf16x8 (&xr)[FPW]) {
     const int k0 = (s_beg + c * BG_CK) * 32;
 #pragma unroll
-    for (int i = 0; i < FPW; ++i) {
-      xr[i] = *reinterpret_cast<const bf16x8*>(xrow[i] + k0);
-      if constexpr (NORM) {
-        const int sl = (wave + W * i) / NB;
-        gr[i] = *reinterpret_cast<const bf16x8*>(a.gain + k0 + sl * 32 + ((lane >> 4) << 3));
-      }
-    }
+    for (int i = 0; i < FPW; ++i) xr[i] = *reinterpret_cast<const bf16x8*>(xrow[i] + k0);
   };
-  auto stage_store = [&](int buf, const bf16x8 (&xr)[FPW], const bf16x8 (&gr)[FPW]) {
+  auto stage_store = [&](int buf, const bf16x8 (&xr)[FPW]) {
 #pragma unroll
     for (int i = 0; i < FPW; ++i) {
-      bf16x8 v = xr[i];
-      if constexpr (NORM) {
+      if constexpr (NORM) {  // the gain is folded into W: only the row's sum of squares is needed
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          const float f = bf2f(v[j]);
+          const float f = bf2f(xr[i][j]);
           ssq[i] += f * f;
-          v[j] = f2bf(f * bf2f(gr[i][j]));
         }
       }
-      xs[buf][wave + W * i][lane] = v;
+      xs[buf][wave + W * i][lane] = xr[i];
     }
   };
 
@@ -569,17 +551,17 @@ __global__ __launch_bounds__(W * 64) void bgemm_kernel(const GemmArgs a, const B
 #pragma unroll
     for (int t = 0; t < NTW; ++t) wa[u][t] = load_w(s_beg + u, t);
   {
-    bf16x8 xr[FPW], gr[FPW];
-    stage_load(0, xr, gr);
-    stage_store(0, xr, gr);
+    bf16x8 xr[FPW];
+    stage_load(0, xr);
+    stage_store(0, xr);
   }
   __syncthreads();
 
   for (int c = 0; c < nch; ++c) {
     const int buf = c & 1;
     const bool more = c + 1 < nch;
-    bf16x8 xr[FPW], gr[FPW];
-    if (more) stage_load(c + 1, xr, gr);
+    bf16x8 xr[FPW];
+    if (more) stage_load(c + 1, xr);
 #pragma unroll
     for (int h = 0; h < NGRP; ++h) {
       const int sn = s_beg + c * BG_CK + (h + 1) * U;  // first slice of the next group
@@ -601,6 +583,9 @@ __global__ __launch_bounds__(W * 64) void bgemm_kernel(const GemmArgs a, const B
 #pragma unroll
           for (int b = 0; b < NB; ++b)
             acc[t][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[u][t], xb[b], acc[t][b], 0, 0, 0);
+        // keep the scheduler from hoisting the next slices' LDS fragments above these MFMAs: with
+        // NB = 8 that would hold 4 x 8 fragments live and spill under the 128-VGPR budget
+        if constexpr (NB >= 8) __builtin_amdgcn_sched_barrier(0);
       }
       if (has) {
 #pragma unroll
@@ -609,7 +594,7 @@ __global__ __launch_bounds__(W * 64) void bgemm_kernel(const GemmArgs a, const B
           for (int t = 0; t < NTW; ++t) wa[u][t] = wn[u][t];
       }
     }
-    if (more) stage_store(buf ^ 1, xr, gr);
+    if (more) stage_store(buf ^ 1, xr);
     __syncthreads();
   }
 
@@ -674,17 +659,19 @@ __global__ __launch_bounds__(W * 64) void bgemm_kernel(const GemmArgs a, const B
       s_ticket = __hip_atomic_fetch_add(bg.counters + blk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
     if (s_ticket != unsigned(bg.ksplit - 1)) return;
-    // sum the k-range partials, 4 ranges x NTW*NB units of loads in flight per round trip
+    // sum the k-range partials, RB ranges x NTW*NB units of loads in flight per round trip (RB x NTW*NB
+    // f32x4 registers: 2 ranges at 8 units keeps the 128-row variants inside 128 VGPRs)
+    constexpr int RB = NTW * NB >= 8 ? 2 : 4;
     const float* base = bg.part + pb * (size_t)UNITS * 256;
     f32x4 sum[NTW][NB];
 #pragma unroll
     for (int t = 0; t < NTW; ++t)
 #pragma unroll
       for (int b = 0; b < NB; ++b) sum[t][b] = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int k0 = 0; k0 < bg.ksplit; k0 += 4) {
-      f32x4 l[4][NTW][NB];
+    for (int k0 = 0; k0 < bg.ksplit; k0 += RB) {
+      f32x4 l[RB][NTW][NB];
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
+      for (int j = 0; j < RB; ++j)
 #pragma unroll
         for (int t = 0; t < NTW; ++t)
 #pragma unroll
@@ -694,7 +681,7 @@ __global__ __launch_bounds__(W * 64) void bgemm_kernel(const GemmArgs a, const B
                                               : f32x4{0.f, 0.f, 0.f, 0.f};
           }
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
+      for (int j = 0; j < RB; ++j)
 #pragma unroll
         for (int t = 0; t < NTW; ++t)
 #pragma unroll
@@ -762,11 +749,17 @@ static BgPlan bgemm_plan(int N, int K, int M, int ntw_req) {
   const int rows1 = 16 * BG_WAVES;
   p.ntw = p.nb == 8 ? 1 : (ntw_req > 0 ? ntw_req : ((N + rows1 - 1) / rows1 >= 512 ? 2 : 1));
   // the 4-wave and 16-slice-chunk variants exist for NTW = 1 only; 4-wave workgroups (64-row blocks)
-  // measured faster on N <= 4096 (O / down projections: 23.2 vs 25.8 us, 41.5 vs 46.7 us at M = 64)
-  const bool narrow = N <= 4096 && p.ntw == 1;
+  // measured faster on N <= 6144 (O / QKV / down projections at M = 64: 23.1 vs 25.6, 27.0 vs 30.0,
+  // 41.1 vs 46.5 us; profiles/bgemm_sweep.md)
+  const bool narrow = N <= 6144 && p.ntw == 1;
   p.w = (w_env == 4 || (w_env == 0 && narrow)) && p.ntw == 1 ? 4 : BG_WAVES;
-  if (p.nb == 8)  // 128 rows: 4-slice chunks keep the double-buffered stage at 64 KiB (2 workgroups per CU)
-    p.ck = (ck_env == 8 && p.w == 8) ? 8 : 4;
+  if (p.nb == 8) {
+    // 128 rows: 4-slice chunks keep the double-buffered stage at 64 KiB (2 workgroups per CU); the
+    // mid-width gate/up projection (128 <= row blocks < 512) measured faster with 8-slice chunks
+    const int nblk8 = (N + 16 * BG_WAVES - 1) / (16 * BG_WAVES);
+    const bool mid = nblk8 >= 128 && nblk8 < 512;
+    p.ck = p.w == 8 && (ck_env == 8 || (ck_env == 0 && mid)) ? 8 : 4;
+  }
   else
     p.ck = (ck_env == 16 && p.ntw == 1 && p.w == 8 && (K / 32) % 16 == 0) ? 16 : BG_CK;
   const int rows = 16 * p.w * p.ntw;
@@ -861,27 +854,27 @@ CAIN_API long long cain_gemm_ws_bytes(int N, int K, int M) {
   return (long long)bgemm_ws_bytes(bgemm_plan(N, K, M, bgemm_ntw()));
 }
 
-// Entry used by the runtime and the bindings.  gain != null selects the fused RMSNorm.
+// Entry used by the runtime and the bindings.  norm != 0 selects the fused RMSNorm (gain pre-folded into Wp).
 CAIN_API int cain_skinny_gemm_ex(const void* Wp, const void* X, int ldx, int K, int N, int M, void* Y, int ldy,
-                                 const float* bias, const void* gain, float eps, const int* slot, const int* pos,
+                                 const float* bias, int norm, float eps, const int* slot, const int* pos,
                                  const float* cos_t, const float* sin_t, void* kc, void* vtc, int H, int Hkv, int hd,
                                  int T_max, int epi, int waves, hipStream_t st) {
   GemmArgs a{};
   a.Wp = reinterpret_cast<const bf16x8*>(Wp);
   a.X = reinterpret_cast<const __bf16*>(X);
   a.ldx = ldx, a.K = K, a.N = N, a.M = M, a.Y = Y, a.ldy = ldy, a.bias = bias;
-  a.gain = reinterpret_cast<const __bf16*>(gain), a.eps = eps;
+  a.eps = eps;
   a.slot = slot, a.pos = pos, a.cos_t = cos_t, a.sin_t = sin_t;
   a.kc = reinterpret_cast<__bf16*>(kc), a.vtc = reinterpret_cast<__bf16*>(vtc);
   a.H = H, a.Hkv = Hkv, a.hd = hd, a.T_max = T_max;
   if (epi == EPI_QKV_ROPE && (hd % 16 || (hd / 2) % 8)) return -1;
-  return gemm_dispatch(a, epi, gain != nullptr, waves, st);
+  return gemm_dispatch(a, epi, norm != 0, waves, st);
 }
 
 // Full entry: batched path for 16 < M <= 128 when a workspace of cain_gemm_ws_bytes() (zeroed once) is
 // given, the skinny kernel otherwise.
 CAIN_API int cain_gemm(const void* Wp, const void* X, int ldx, int K, int N, int M, void* Y, int ldy,
-                       const float* bias, const void* gain, float eps, const int* slot, const int* pos,
+                       const float* bias, int norm, float eps, const int* slot, const int* pos,
                        const float* cos_t, const float* sin_t, void* kc, void* vtc, int H, int Hkv, int hd, int T_max,
                        void* ws, long long ws_bytes, int epi, int waves, hipStream_t st) {
   if (ws && bgemm_eligible(N, K, M) && K % 32 == 0 && N % 16 == 0) {
@@ -891,15 +884,15 @@ CAIN_API int cain_gemm(const void* Wp, const void* X, int ldx, int K, int N, int
       a.Wp = reinterpret_cast<const bf16x8*>(Wp);
       a.X = reinterpret_cast<const __bf16*>(X);
       a.ldx = ldx, a.K = K, a.N = N, a.M = M, a.Y = Y, a.ldy = ldy, a.bias = bias;
-      a.gain = reinterpret_cast<const __bf16*>(gain), a.eps = eps;
+      a.eps = eps;
       a.slot = slot, a.pos = pos, a.cos_t = cos_t, a.sin_t = sin_t;
       a.kc = reinterpret_cast<__bf16*>(kc), a.vtc = reinterpret_cast<__bf16*>(vtc);
       a.H = H, a.Hkv = Hkv, a.hd = hd, a.T_max = T_max;
       if (epi == EPI_QKV_ROPE && (hd % 16 || (hd / 2) % 8)) return -1;
-      return bgemm_dispatch(a, epi, gain != nullptr, p, ws, st);
+      return bgemm_dispatch(a, epi, norm != 0, p, ws, st);
     }
   }
-  return cain_skinny_gemm_ex(Wp, X, ldx, K, N, M, Y, ldy, bias, gain, eps, slot, pos, cos_t, sin_t, kc, vtc, H, Hkv,
+  return cain_skinny_gemm_ex(Wp, X, ldx, K, N, M, Y, ldy, bias, norm, eps, slot, pos, cos_t, sin_t, kc, vtc, H, Hkv,
                              hd, T_max, epi, waves, st);
 }
 

@@ -23,7 +23,7 @@
 constexpr int CAIN_MAX_ROWS = 128;  // rows per forward (decode batch / prefill chunk)
 
 CAIN_API int cain_gemm(const void* Wp, const void* X, int ldx, int K, int N, int M, void* Y, int ldy,
-                       const float* bias, const void* gain, float eps, const int* slot, const int* pos,
+                       const float* bias, int norm, float eps, const int* slot, const int* pos,
                        const float* cos_t, const float* sin_t, void* kc, void* vtc, int H, int Hkv, int hd, int T_max,
                        void* ws, long long ws_bytes, int epi, int waves, hipStream_t st);
 CAIN_API int cain_embed(const int* tok, const void* E, void* out, int ldo, int M, int d, float scale, hipStream_t st);
@@ -36,12 +36,12 @@ CAIN_API int cain_sample(float* logits, int ldl, int V, int* tok, int* pos, int*
 
 extern "C" {
 
+// RMSNorm gains are folded into the weight columns of the GEMM each norm feeds (attn_norm -> wqkv,
+// mlp_norm -> wgu, final_norm -> lm_head; models/weights.py fold_gain), so a norm is just a flag here.
 struct CainLayer {
-  const void* attn_norm;
   const void* wqkv;
   const float* bqkv;
   const void* wo;
-  const void* mlp_norm;
   const void* wgu;
   const void* wdown;
 };
@@ -50,7 +50,6 @@ struct CainPlanDesc {
   int n_layers, d, H, Hkv, hd, ffn, V, act_kind, T_max, Mpad, nsplit, waves;
   float eps, embed_scale, attn_scale;
   const void* embed;
-  const void* final_norm;
   const void* lm_head;
   const CainLayer* layers;
   void* kcache;  // [L][S][Hkv][T_max][hd]
@@ -111,19 +110,19 @@ int forward(const Plan& p, int M, const CainRows& r, int want_logits, int want_s
     const CainLayer& L = p.layers[l];
     __bf16* kc = reinterpret_cast<__bf16*>(d.kcache) + (size_t)l * d.kv_layer_elems;
     __bf16* vc = reinterpret_cast<__bf16*>(d.vtcache) + (size_t)l * d.kv_layer_elems;
-    CK(cain_gemm(L.wqkv, d.x, d.d, d.d, qkv_dim, M, d.q, q_dim, L.bqkv, L.attn_norm, d.eps, r.slot, r.pos,
+    CK(cain_gemm(L.wqkv, d.x, d.d, d.d, qkv_dim, M, d.q, q_dim, L.bqkv, 1, d.eps, r.slot, r.pos,
                            d.cos_t, d.sin_t, kc, vc, d.H, d.Hkv, d.hd, d.T_max, d.gemm_ws, d.gemm_ws_bytes, /*EPI_QKV_ROPE*/ 5, d.waves, st));
     CK(cain_attention(d.q, kc, vc, r.slot, r.pos, d.part_o, d.part_ml, d.counters, d.attn, q_dim, M, d.H, d.Hkv,
                       d.hd, d.T_max, d.nsplit, d.attn_scale, st));
-    CK(cain_gemm(L.wo, d.attn, q_dim, q_dim, d.d, M, d.x, d.d, nullptr, nullptr, 0.f, nullptr, nullptr,
+    CK(cain_gemm(L.wo, d.attn, q_dim, q_dim, d.d, M, d.x, d.d, nullptr, 0, 0.f, nullptr, nullptr,
                            nullptr, nullptr, nullptr, nullptr, 0, 0, 0, 0, d.gemm_ws, d.gemm_ws_bytes, /*EPI_RESID*/ 1, d.waves, st));
-    CK(cain_gemm(L.wgu, d.x, d.d, d.d, 2 * d.ffn, M, d.act, d.ffn, nullptr, L.mlp_norm, d.eps, nullptr,
+    CK(cain_gemm(L.wgu, d.x, d.d, d.d, 2 * d.ffn, M, d.act, d.ffn, nullptr, 1, d.eps, nullptr,
                            nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0, 0, 0, d.gemm_ws, d.gemm_ws_bytes, epi_act, d.waves, st));
-    CK(cain_gemm(L.wdown, d.act, d.ffn, d.ffn, d.d, M, d.x, d.d, nullptr, nullptr, 0.f, nullptr, nullptr,
+    CK(cain_gemm(L.wdown, d.act, d.ffn, d.ffn, d.d, M, d.x, d.d, nullptr, 0, 0.f, nullptr, nullptr,
                            nullptr, nullptr, nullptr, nullptr, 0, 0, 0, 0, d.gemm_ws, d.gemm_ws_bytes, /*EPI_RESID*/ 1, d.waves, st));
   }
   if (want_logits) {
-    CK(cain_gemm(d.lm_head, d.x, d.d, d.d, d.V, M, d.logits, d.V, nullptr, d.final_norm, d.eps, nullptr,
+    CK(cain_gemm(d.lm_head, d.x, d.d, d.d, d.V, M, d.logits, d.V, nullptr, 1, d.eps, nullptr,
                            nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0, 0, 0, d.gemm_ws, d.gemm_ws_bytes, /*EPI_F32*/ 2, d.waves, st));
   }
   if (want_sample) {

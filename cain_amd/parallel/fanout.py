@@ -25,9 +25,12 @@ they are sharded over N worker processes, one per GPU:
 
 Failure handling: an exception in a run leaves that row TODO (reference
 semantics) and is logged to ``errors.jsonl``; ``retry_failed`` re-runs such rows
-in extra waves.  A rank that dies takes the job down via the process-group
-timeout; its rows are still TODO and the next start resumes them on however
-many GPUs are available.
+in extra waves.  A rank that DIES (segfault, OOM kill, GPU fault) is detected by
+the launcher, which stops the surviving ranks at once (they would otherwise
+block in the next collective until the process-group timeout) and — with
+``max_restarts`` — starts a fresh job that resumes the TODO rows (the finished
+rows were committed wave by wave, so at most one wave is redone).  Under
+``torchrun`` its own ``--max-restarts`` plays that role.
 """
 from __future__ import annotations
 
@@ -162,31 +165,72 @@ def run_rank(config_path: str, rank: int, world: int, isolation: Optional[str] =
             pass
 
 
-def _spawn_entry(rank, world, port, config_path, isolation, timeout, assume_yes, retry_failed, rcs):
+def _spawn_entry(rank, world, port, config_path, isolation, timeout, assume_yes, retry_failed):
+    import signal
+    import sys
+
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank))
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-    rcs[rank] = run_rank(config_path, rank, world, isolation, timeout, assume_yes, retry_failed)
+    # SIGTERM from the launcher → SystemExit, so atexit handlers (e.g. a config's local servers) still run
+    signal.signal(signal.SIGTERM, lambda *_: sys.exit(143))
+    sys.exit(run_rank(config_path, rank, world, isolation, timeout, assume_yes, retry_failed))
+
+
+def _run_job(ctx, config_path, n_gpus, isolation, timeout, assume_yes, retry_failed, poll_s: float = 0.2) -> int:
+    """One job: spawn the ranks, and if any rank dies stop the others instead of letting them wait for
+    the process-group timeout.  Returns 0 when every rank exited 0."""
+    import time
+
+    port = _free_port()
+    procs = [ctx.Process(target=_spawn_entry, args=(r, n_gpus, port, os.path.abspath(config_path), isolation,
+                                                    timeout, assume_yes, retry_failed))
+             for r in range(n_gpus)]
+    for p in procs:
+        p.start()
+    failed = None
+    while any(p.is_alive() for p in procs):
+        bad = [r for r, p in enumerate(procs) if p.exitcode not in (None, 0)]
+        if bad:
+            failed = bad
+            break
+        time.sleep(poll_s)
+    if failed is not None:
+        from ..runner.output import OutputProcedure as output
+
+        output.console_log_FAIL(f"rank(s) {failed} died (exit {[procs[r].exitcode for r in failed]}): "
+                                f"stopping the surviving ranks")
+        for p in procs:
+            if p.is_alive():
+                p.terminate()
+        for p in procs:
+            p.join(30)
+            if p.is_alive():
+                p.kill()
+                p.join()
+    for p in procs:
+        p.join()
+    return 0 if all(p.exitcode == 0 for p in procs) else 1
 
 
 def launch(config_path: str, n_gpus: int, isolation: Optional[str] = None, timeout: Optional[float] = None,
-           assume_yes: Optional[bool] = None, retry_failed: int = 0) -> int:
-    """Run ``config_path`` data-parallel on ``n_gpus`` ranks (spawned here, or the current torchrun job)."""
+           assume_yes: Optional[bool] = None, retry_failed: int = 0, max_restarts: int = 0) -> int:
+    """Run ``config_path`` data-parallel on ``n_gpus`` ranks (spawned here, or the current torchrun job).
+    ``max_restarts``: after a rank dies, start up to that many fresh jobs; each resumes the TODO rows."""
     if "RANK" in os.environ and "WORLD_SIZE" in os.environ:
         return run_rank(config_path, int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"]), isolation, timeout,
                         assume_yes, retry_failed)
     import multiprocessing as mp
 
+    from ..runner.output import OutputProcedure as output
+
     ctx = mp.get_context("spawn")
-    port = _free_port()
-    with ctx.Manager() as mgr:
-        rcs = mgr.dict()
-        procs = [ctx.Process(target=_spawn_entry, args=(r, n_gpus, port, os.path.abspath(config_path), isolation,
-                                                        timeout, assume_yes, retry_failed, rcs))
-                 for r in range(n_gpus)]
-        for p in procs:
-            p.start()
-        for p in procs:
-            p.join()
-        codes = [rcs.get(r, p.exitcode if p.exitcode else 1) for r, p in enumerate(procs)]
-    return 0 if all(c == 0 for c in codes) else 1
+    rc = 1
+    for attempt in range(1 + max(0, int(max_restarts))):
+        if attempt:
+            output.console_log_WARNING(f"elastic restart {attempt}/{max_restarts}: resuming the TODO rows")
+            assume_yes = True  # the same config: the md5 prompt was answered by the first job
+        rc = _run_job(ctx, config_path, n_gpus, isolation, timeout, assume_yes, retry_failed)
+        if rc == 0:
+            break
+    return rc

@@ -11,7 +11,8 @@ libraries and HIP kernels in-tree), ``analyze <run_table.csv>`` (paper tables),
 (one local generation, prints Ollama-style JSON).
 
 Run options (new): ``--gpus N`` fans TODO rows out data-parallel over N GPU
-worker processes (``cain_amd.parallel``), ``--isolation``, ``--timeout``,
+worker processes (``cain_amd.parallel``; ``--max-restarts`` relaunches after a
+rank dies, ``--retry-failed`` re-runs failed rows), ``--isolation``, ``--timeout``,
 ``--cooldown-ms``, ``--yes`` (answer the md5 prompt), ``--seed``,
 ``--dry-run`` (validate and print the run table only).
 """
@@ -126,6 +127,9 @@ def run_experiment(argv: List[str]) -> None:
     ap.add_argument("--yes", action="store_true", help="continue on md5 mismatch without asking")
     ap.add_argument("--seed", type=int, default=None, help="seed for the run-table shuffle")
     ap.add_argument("--dry-run", action="store_true")
+    ap.add_argument("--max-restarts", type=int, default=0,
+                    help="with --gpus: relaunch after a rank dies, resuming the TODO rows (elastic restart)")
+    ap.add_argument("--retry-failed", type=int, default=0, help="with --gpus: extra passes over failed runs")
     ns = ap.parse_args(argv)
     if ns.cooldown_ms is not None:
         os.environ["CAIN_COOLDOWN_MS"] = str(ns.cooldown_ms)
@@ -135,7 +139,8 @@ def run_experiment(argv: List[str]) -> None:
         from ..parallel.fanout import launch
 
         sys.exit(launch(ns.config, ns.gpus, isolation=ns.isolation, timeout=ns.timeout,
-                        assume_yes=True if ns.yes else None))
+                        assume_yes=True if ns.yes else None, retry_failed=ns.retry_failed,
+                        max_restarts=ns.max_restarts))
     from .controller import ExperimentController
     from .validator import ConfigValidator
 

@@ -14,7 +14,7 @@ if not torch.cuda.is_available():  # pragma: no cover
     pytest.skip("needs a GPU", allow_module_level=True)
 
 from cain_amd import ops  # noqa: E402
-from cain_amd.models.weights import interleave_tiles, pack_mfma_a, rope_pair_order  # noqa: E402
+from cain_amd.models.weights import fold_gain, interleave_tiles, pack_mfma_a, rope_pair_order  # noqa: E402
 
 DEV = torch.device("cuda")
 
@@ -55,7 +55,7 @@ def test_skinny_gemm_fused_rmsnorm_prologue(M):
     W = (torch.randn(N, K, device=DEV) * 0.02).bfloat16()
     x = (3 * torch.randn(M, K, device=DEV)).bfloat16()
     g = (1 + 0.2 * torch.randn(K, device=DEV)).bfloat16()
-    y = ops.skinny_gemm(pack_mfma_a(W), x, N, ops.EPI_F32, gain=g, eps=1e-6)
+    y = ops.skinny_gemm(pack_mfma_a(fold_gain(W, g)), x, N, ops.EPI_F32, norm=True, eps=1e-6)
     xn = x.float() * torch.rsqrt(x.float().pow(2).mean(-1, keepdim=True) + 1e-6) * g.float()
     assert rel_err(y, xn @ W.float().t()) < 1e-2
 
@@ -68,7 +68,8 @@ def test_skinny_gemm_fused_rmsnorm_gateup(M):
     Wu = (torch.randn(F, K, device=DEV) * 0.02).bfloat16()
     x = (2 * torch.randn(M, K, device=DEV)).bfloat16()
     g = (1 + 0.3 * torch.randn(K, device=DEV)).bfloat16()
-    y = ops.skinny_gemm(pack_mfma_a(interleave_tiles(Wg, Wu, tile=8)), x, 2 * F, ops.EPI_SILU, gain=g, eps=1e-5)
+    y = ops.skinny_gemm(pack_mfma_a(interleave_tiles(fold_gain(Wg, g), fold_gain(Wu, g), tile=8)), x, 2 * F,
+                        ops.EPI_SILU, norm=True, eps=1e-5)
     xn = x.float() * torch.rsqrt(x.float().pow(2).mean(-1, keepdim=True) + 1e-5) * g.float()
     ref = torch.nn.functional.silu(xn @ Wg.float().t()) * (xn @ Wu.float().t())
     assert rel_err(y, ref) < 2e-2
@@ -112,13 +113,14 @@ def test_batched_gemm_matches_skinny_and_reference(M, N, K, norm):
     x = (2 * torch.randn(M, K, device=DEV)).bfloat16()
     g = (1 + 0.2 * torch.randn(K, device=DEV)).bfloat16() if norm else None
     assert ops.gemm_ws_bytes(N, K, M) > 0 or (M <= 32 and N < 8192)  # narrow N at M <= 32: skinny path
-    wp = pack_mfma_a(W)
-    ys = [ops.skinny_gemm(wp, x, N, ops.EPI_F32, gain=g, eps=1e-6) for _ in range(3)]
-    y0 = ops.skinny_gemm(wp, x, N, ops.EPI_F32, gain=g, eps=1e-6, batched=False) if M <= 64 else None
+    Wf = fold_gain(W, g) if norm else W
+    wp = pack_mfma_a(Wf)
+    ys = [ops.skinny_gemm(wp, x, N, ops.EPI_F32, norm=norm, eps=1e-6) for _ in range(3)]
+    y0 = ops.skinny_gemm(wp, x, N, ops.EPI_F32, norm=norm, eps=1e-6, batched=False) if M <= 64 else None
     xr = x.float()
     if norm:
-        xr = xr * torch.rsqrt(xr.pow(2).mean(-1, keepdim=True) + 1e-6) * g.float()
-    ref = xr @ W.float().t()
+        xr = xr * torch.rsqrt(xr.pow(2).mean(-1, keepdim=True) + 1e-6)
+    ref = xr @ Wf.float().t()
     for y in ys:
         assert rel_err(y, ref) < 2e-3
         assert torch.equal(y, ys[0])  # deterministic reduction order
@@ -173,8 +175,8 @@ def test_fused_qkv_rope_kv_append(H, Hkv, hd, M, norm):
     pos = torch.randint(0, T_max, (M,), device=DEV).int()
     cos_t, sin_t = _rope_tables(hd, T_max)
     g = (1 + 0.2 * torch.randn(K, device=DEV)).bfloat16() if norm else None
-    ops.qkv_rope(pack_mfma_a(W[perm]), x, qkv_dim, q, kc, vt, slot, pos, cos_t, sin_t, H, Hkv, hd, bias=bias[perm],
-                 gain=g, eps=1e-6)
+    Wp = pack_mfma_a(fold_gain(W[perm], g)) if norm else pack_mfma_a(W[perm])
+    ops.qkv_rope(Wp, x, qkv_dim, q, kc, vt, slot, pos, cos_t, sin_t, H, Hkv, hd, bias=bias[perm], norm=norm, eps=1e-6)
     xr = x.float()
     if norm:
         xr = xr * torch.rsqrt(xr.pow(2).mean(-1, keepdim=True) + 1e-6) * g.float()

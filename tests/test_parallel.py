@@ -78,3 +78,29 @@ def test_fanout_two_ranks_then_resume_on_one(tmp_path):
     assert all(x["__done"] == "DONE" for x in rows2)
     assert [x["__run_id"] for x in rows2] == [x["__run_id"] for x in rows]  # order preserved
     assert r.stdout.count("NEW RUN") == 1
+
+
+CRASH_CFG = CFG.replace("(RunnerEvents.START_RUN, self.start_run),",
+                        "(RunnerEvents.BEFORE_RUN, self.before_run), (RunnerEvents.START_RUN, self.start_run),"
+                        ).replace('''    def start_run(self, ctx):''', '''    def before_run(self):
+        # BEFORE_RUN runs in the rank process itself (not the per-run child): this kills the worker
+        crash = OUT / "crashed_once"
+        if self.dp_rank == 1 and not crash.exists():
+            crash.touch()
+            os._exit(9)
+
+    def start_run(self, ctx):''')
+assert CRASH_CFG != CFG
+
+
+def test_dead_rank_is_detected_and_job_restarts(tmp_path):
+    cfg = tmp_path / "cfg.py"
+    cfg.write_text(CRASH_CFG)
+    env = dict(os.environ, PYTHONPATH=str(ROOT), CAIN_TEST_OUT=str(tmp_path), CAIN_DIST_BACKEND="gloo",
+               CAIN_ASSUME_YES="1", NO_COLOR="1")
+    r = subprocess.run([sys.executable, "-m", "cain_amd", str(cfg), "--gpus", "2", "--max-restarts", "1",
+                        "--retry-failed", "1"], capture_output=True, text=True, env=env, timeout=240)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "died" in r.stdout and "elastic restart 1/1" in r.stdout
+    rows = list(csv.DictReader(open(tmp_path / "dp" / "run_table.csv")))
+    assert len(rows) == 12 and all(x["__done"] == "DONE" for x in rows)

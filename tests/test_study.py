@@ -45,6 +45,10 @@ def test_study_config_runs_both_arms(tmp_path, gpus):
     assert methods == ["on_device", "on_device", "remote", "remote"]
     if gpus:
         assert "rank 1/2" in r.stdout
+    run_dirs = [d for d in (tmp_path / "full_factorial").iterdir() if d.is_dir() and d.name.startswith("run_")]
+    assert len(run_dirs) == 4
+    assert all((d / "response.json").exists() for d in run_dirs)
+    assert any((d / "cpu_mem_usage.csv").exists() for d in run_dirs)
     # the writer post-processed the table into the paper's tables
     assert (tmp_path / "full_factorial" / "analysis" / "results.json").exists()
 

@@ -74,14 +74,14 @@ def main():
             g = torch.ones(k, device=dev).bfloat16() if ns.norm and role in ("qkv", "gateup", "lm_head") else None
             variants = [(False, int(w)) for w in ns.waves.split(",")]
             if ops.gemm_ws_bytes(n, k, M) > 0:
-                variants = [(False, 0), (True, 0)]
+                variants = [(False, 0), (True, 0)] if M <= 64 else [(True, 0)]  # skinny kernel: M <= 64
             for batched, wv in variants:
                 it = [0]
 
                 def run():
                     w = W[role][it[0] % len(W[role])]
                     it[0] += 1
-                    ops.skinny_gemm(w, x, n, epi, out=out, waves=wv, batched=batched, gain=g)
+                    ops.skinny_gemm(w, x, n, epi, out=out, waves=wv, batched=batched, norm=g is not None)
                 us = timeit(run)
                 gbs = n * k * 2 / us / 1e3
                 r = dict(kind="gemm", model=cfg.name, role=role, M=M, N=n, K=k, waves=wv, us=round(us, 2),
