@@ -184,7 +184,7 @@ __device__ __forceinline__ void epi_store(const GemmArgs& a, int gt, int m, int 
   }
 }
 
-template <int NT, int NB, int WAVES, int U, int EPI, bool NORM>
+template <int NT, int NB, int WAVES, int U, int EPI, bool NORM, bool PP>
 __global__ __launch_bounds__(WAVES * 64) void skinny_gemm_kernel(const GemmArgs a) {
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
@@ -238,44 +238,76 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_gemm_kernel(const GemmArgs 
   }
 
   // raw fragment loads (issued early); normalisation happens at use, after the data landed
-  // non-temporal weight loads when this workgroup is the tile's only reader; with msplit > 1 the
-  // tile-mates re-read it, so keep the default policy and let them hit L2
-  const bool ntl = a.msplit == 1;
-  auto load_w = [&](int s, int t) -> bf16x8 {
-    return ntl ? __builtin_nontemporal_load(wbase[t] + (size_t)s * 64) : wbase[t][(size_t)s * 64];
-  };
+  // (always non-temporal: a runtime choice of the cache policy put a branch around every load, which
+  // defeats the counted waits of the pipeline below; with msplit > 1 the tile-mates still hit L2/MALL)
+  auto load_w = [&](int s, int t) -> bf16x8 { return __builtin_nontemporal_load(wbase[t] + (size_t)s * 64); };
   auto load_x = [&](int s, int b) -> bf16x8 { return *reinterpret_cast<const bf16x8*>(xbase[b] + s * 32); };
   // RMSNorm factorisation: (W diag(g)) (x * inv) = inv * ((W diag(g)) x); the per-row inv is applied in
   // the epilogue and the sum of squares is accumulated from the x fragments this WG streams anyway
   // (its waves cover all of K), so no separate norm kernel and no cross-kernel sum-of-squares buffer.
-  auto norm_x = [&](bf16x8 v, int b) -> bf16x8 {
+  auto norm_x = [&](bf16x8 v, int b, float wgt) -> bf16x8 {
     if constexpr (NORM) {
+      float q = 0.f;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const float f = bf2f(v[j]);
-        ssq[b] += f * f;
+        q += f * f;
       }
+      ssq[b] += wgt * q;
     }
     return v;
   };
-  auto compute = [&](const bf16x8 (&w)[U][NT], const bf16x8 (&x)[U][NB]) {
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  auto compute = [&](const bf16x8 (&w)[U][NT], const bf16x8 (&x)[U][NB], bool valid) {
+    const uint32_t keep = valid ? 0xffffffffu : 0u;
+    const float wgt = valid ? 1.f : 0.f;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       bf16x8 xb[NB];
 #pragma unroll
-      for (int b = 0; b < NB; ++b) xb[b] = norm_x(x[u][b], b);
+      for (int b = 0; b < NB; ++b) xb[b] = norm_x(x[u][b], b, wgt);
 #pragma unroll
-      for (int t = 0; t < NT; ++t)
+      for (int t = 0; t < NT; ++t) {
+        const bf16x8 wm = __builtin_bit_cast(bf16x8, __builtin_bit_cast(u32x4, w[u][t]) & keep);
 #pragma unroll
         for (int b = 0; b < NB; ++b)
-          acc[t][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[u][t], xb[b], acc[t][b], 0, 0, 0);
+          acc[t][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wm, xb[b], acc[t][b], 0, 0, 0);
+      }
     }
   };
 
-  // ---- software-pipelined main loop: chunk c+1's loads are in flight while chunk c computes
+  // ---- software-pipelined main loop, branch-free and copy-free: group g+1's loads (clamped to the
+  // last full group) are issued before group g computes, into the other of two register sets that
+  // ping-pong (the loop is unrolled by two; an odd group count runs one masked dummy group).  A
+  // register copy of an in-flight load, or loads under a branch, made the compiler wait vmcnt(0).
   int s = s_beg;
   const int nfull = (s_end - s_beg) / U;
-  if (nfull > 0) {
+  if constexpr (PP) {
+    if (nfull > 0) {
+      const int s_lastf = s_beg + nfull * U - 1;
+      bf16x8 wa[U][NT], xa[U][NB], wb2[U][NT], xb2[U][NB];
+      auto load_group = [&](int s0, bf16x8 (&w)[U][NT], bf16x8 (&x)[U][NB]) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int si = min(s0 + u, s_lastf);
+#pragma unroll
+          for (int t = 0; t < NT; ++t) w[u][t] = load_w(si, t);
+#pragma unroll
+          for (int b = 0; b < NB; ++b) x[u][b] = load_x(si, b);
+        }
+      };
+      load_group(s, wa, xa);
+      for (int g = 0; g < nfull; g += 2) {
+        load_group(s_beg + (g + 1) * U, wb2, xb2);
+        __builtin_amdgcn_sched_barrier(0);
+        compute(wa, xa, true);
+        load_group(s_beg + (g + 2) * U, wa, xa);
+        __builtin_amdgcn_sched_barrier(0);
+        compute(wb2, xb2, g + 1 < nfull);
+      }
+      s = s_beg + nfull * U;
+    }
+  } else if (nfull > 0) {  // register-copy pipeline (the compiler schedules the loads itself)
     bf16x8 wa[U][NT], xa[U][NB];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -297,7 +329,7 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_gemm_kernel(const GemmArgs 
           for (int b = 0; b < NB; ++b) xn[u][b] = load_x(sn + u, b);
         }
       }
-      compute(wa, xa);
+      compute(wa, xa, true);
       if (more) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -316,7 +348,7 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_gemm_kernel(const GemmArgs 
       const bf16x8 w = load_w(s, t);
 #pragma unroll
       for (int b = 0; b < NB; ++b)
-        acc[t][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w, norm_x(load_x(s, b), b), acc[t][b], 0, 0, 0);
+        acc[t][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w, norm_x(load_x(s, b), b, 1.f), acc[t][b], 0, 0, 0);
     }
   }
 
@@ -367,8 +399,16 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_gemm_kernel(const GemmArgs 
 template <int NT, int NB, int WAVES, int EPI, bool NORM>
 static hipError_t launch_t(const GemmArgs& a, hipStream_t st) {
   constexpr int U = (NB >= 2) ? 2 : 4;  // x2 register sets (pipelined)
-  hipLaunchKernelGGL((skinny_gemm_kernel<NT, NB, WAVES, U, EPI, NORM>), dim3(a.N / (16 * NT) * a.msplit),
-                     dim3(WAVES * 64), 0, st, a);
+  static const int pp = [] {
+    const char* e = getenv("CAIN_SKINNY_PP");
+    return e ? atoi(e) : 0;
+  }();
+  if (pp)
+    hipLaunchKernelGGL((skinny_gemm_kernel<NT, NB, WAVES, U, EPI, NORM, true>), dim3(a.N / (16 * NT) * a.msplit),
+                       dim3(WAVES * 64), 0, st, a);
+  else
+    hipLaunchKernelGGL((skinny_gemm_kernel<NT, NB, WAVES, U, EPI, NORM, false>), dim3(a.N / (16 * NT) * a.msplit),
+                       dim3(WAVES * 64), 0, st, a);
   return hipGetLastError();
 }
 
@@ -525,15 +565,17 @@ __global__ __launch_bounds__(W * 64, (W == 8 && NTW == 1 && CK * NB <= 32) ? 4 :
 #pragma unroll
     for (int i = 0; i < FPW; ++i) xr[i] = *reinterpret_cast<const bf16x8*>(xrow[i] + k0);
   };
-  auto stage_store = [&](int buf, const bf16x8 (&xr)[FPW]) {
+  auto stage_store = [&](int buf, const bf16x8 (&xr)[FPW], float wgt) {
 #pragma unroll
     for (int i = 0; i < FPW; ++i) {
       if constexpr (NORM) {  // the gain is folded into W: only the row's sum of squares is needed
+        float q = 0.f;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const float f = bf2f(xr[i][j]);
-          ssq[i] += f * f;
+          q += f * f;
         }
+        ssq[i] += wgt * q;
       }
       xs[buf][wave + W * i][lane] = xr[i];
     }
@@ -553,49 +595,72 @@ __global__ __launch_bounds__(W * 64, (W == 8 && NTW == 1 && CK * NB <= 32) ? 4 :
   {
     bf16x8 xr[FPW];
     stage_load(0, xr);
-    stage_store(0, xr);
+    stage_store(0, xr, 1.f);
   }
   __syncthreads();
 
-  for (int c = 0; c < nch; ++c) {
+  // Steady state, branch-free and copy-free:
+  //  * the next chunk's activation loads and the next group's weight loads are issued unconditionally
+  //    (clamped to the last valid chunk / slice), so the compiler counts outstanding loads exactly;
+  //  * two weight register sets ping-pong (group g computes from one while the loads of group g+1 land
+  //    in the other), unrolled so neither is ever copied — a register copy of an in-flight load forces
+  //    s_waitcnt vmcnt(0) and exposed the full HBM latency once per group.
+  // With one group per chunk the chunk loop is unrolled by two; an odd chunk count runs one dummy
+  // chunk whose weights are masked to zero (its activations are the last real chunk: finite).
+  const int s_last = s_beg + nch * BG_CK - 1;
+  bf16x8 wb_[U][NTW];
+  auto run_group = [&](int c, int h, bool valid, bf16x8 (&cur)[U][NTW], bf16x8 (&nxt)[U][NTW]) {
     const int buf = c & 1;
-    const bool more = c + 1 < nch;
+    const int sn = s_beg + c * BG_CK + (h + 1) * U;  // first slice of the next group
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int t = 0; t < NTW; ++t) nxt[u][t] = load_w(min(sn + u, s_last), t);
+    __builtin_amdgcn_sched_barrier(0);  // issue the prefetch before this group's MFMAs, not after
+    const uint32_t keep = valid ? 0xffffffffu : 0u;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      bf16x8 xb[NB];
+#pragma unroll
+      for (int b = 0; b < NB; ++b) xb[b] = xs[buf][(h * U + u) * NB + b][lane];
+#pragma unroll
+      for (int t = 0; t < NTW; ++t) {
+        typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+        const bf16x8 w = __builtin_bit_cast(bf16x8, __builtin_bit_cast(u32x4, cur[u][t]) & keep);
+#pragma unroll
+        for (int b = 0; b < NB; ++b) acc[t][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w, xb[b], acc[t][b], 0, 0, 0);
+      }
+      // keep the scheduler from hoisting the next slices' LDS fragments above these MFMAs: with
+      // NB = 8 that would hold 4 x 8 fragments live and spill under the 128-VGPR budget
+      if constexpr (NB >= 8) __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  auto run_chunk = [&](int c, bool valid, bf16x8 (&A)[U][NTW], bf16x8 (&B)[U][NTW]) {
     bf16x8 xr[FPW];
-    if (more) stage_load(c + 1, xr);
+    stage_load(min(c + 1, nch - 1), xr);
+    // pin the activation loads ahead of the weight prefetch: issued later, they would be the youngest
+    // loads at the staging write and force a vmcnt(0) that drains the weight prefetch too
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (NGRP == 1) {
+      run_group(c, 0, valid, A, B);
+    } else {
 #pragma unroll
-    for (int h = 0; h < NGRP; ++h) {
-      const int sn = s_beg + c * BG_CK + (h + 1) * U;  // first slice of the next group
-      const bool has = (h + 1 < NGRP) || more;
-      bf16x8 wn[U][NTW];
-      if (has) {
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-#pragma unroll
-          for (int t = 0; t < NTW; ++t) wn[u][t] = load_w(sn + u, t);
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        bf16x8 xb[NB];
-#pragma unroll
-        for (int b = 0; b < NB; ++b) xb[b] = xs[buf][(h * U + u) * NB + b][lane];
-#pragma unroll
-        for (int t = 0; t < NTW; ++t)
-#pragma unroll
-          for (int b = 0; b < NB; ++b)
-            acc[t][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[u][t], xb[b], acc[t][b], 0, 0, 0);
-        // keep the scheduler from hoisting the next slices' LDS fragments above these MFMAs: with
-        // NB = 8 that would hold 4 x 8 fragments live and spill under the 128-VGPR budget
-        if constexpr (NB >= 8) __builtin_amdgcn_sched_barrier(0);
-      }
-      if (has) {
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-#pragma unroll
-          for (int t = 0; t < NTW; ++t) wa[u][t] = wn[u][t];
+      for (int h = 0; h < NGRP; h += 2) {
+        run_group(c, h, valid, A, B);
+        run_group(c, h + 1, valid, B, A);
       }
     }
-    if (more) stage_store(buf ^ 1, xr);
+    stage_store((c & 1) ^ 1, xr, (valid && c + 1 < nch) ? 1.f : 0.f);  // the final stage adds nothing to ssq
     __syncthreads();
+  };
+  static_assert(NGRP == 1 || NGRP % 2 == 0, "weight prefetch groups per chunk");
+  if constexpr (NGRP % 2 == 0) {
+    for (int c = 0; c < nch; ++c) run_chunk(c, true, wa, wb_);
+  } else {
+    for (int c = 0; c < nch; c += 2) {
+      run_chunk(c, true, wa, wb_);
+      run_chunk(c + 1, c + 1 < nch, wb_, wa);
+    }
   }
 
   // ---- per-row sum of squares of this workgroup's k-range (NORM)
@@ -754,14 +819,17 @@ static BgPlan bgemm_plan(int N, int K, int M, int ntw_req) {
   const bool narrow = N <= 6144 && p.ntw == 1;
   p.w = (w_env == 4 || (w_env == 0 && narrow)) && p.ntw == 1 ? 4 : BG_WAVES;
   if (p.nb == 8) {
-    // 128 rows: 4-slice chunks keep the double-buffered stage at 64 KiB (2 workgroups per CU); the
-    // mid-width gate/up projection (128 <= row blocks < 512) measured faster with 8-slice chunks
-    const int nblk8 = (N + 16 * BG_WAVES - 1) / (16 * BG_WAVES);
-    const bool mid = nblk8 >= 128 && nblk8 < 512;
-    p.ck = p.w == 8 && (ck_env == 8 || (ck_env == 0 && mid)) ? 8 : 4;
+    // 128 rows: 4-slice chunks keep the double-buffered stage at 64 KiB (2 workgroups per CU)
+    p.ck = p.w == 8 && ck_env == 8 ? 8 : 4;
   }
   else
-    p.ck = (ck_env == 16 && p.ntw == 1 && p.w == 8 && (K / 32) % 16 == 0) ? 16 : BG_CK;
+  {
+    // 64 rows: the mid-width gate/up projection measured faster with 4-slice chunks too (43.8 vs 47.0 us)
+    const int nblk8 = (N + 16 * BG_WAVES - 1) / (16 * BG_WAVES);
+    const bool mid = p.nb == 4 && nblk8 >= 128 && nblk8 < 512;
+    p.ck = (ck_env == 16 && p.ntw == 1 && p.w == 8 && (K / 32) % 16 == 0) ? 16
+           : (p.ntw == 1 && p.w == 8 && (ck_env == 4 || (ck_env == 0 && mid))) ? 4 : BG_CK;
+  }
   const int rows = 16 * p.w * p.ntw;
   p.nblk = (N + rows - 1) / rows;
   const int nchunk = (K / 32) / p.ck;
@@ -786,7 +854,7 @@ static size_t bgemm_ws_bytes(const BgPlan& p) {
 
 template <int NB, int NTW, int W, int CK, int EPI, bool NORM>
 static hipError_t bg_launch(const GemmArgs& a, const BgArgs& b, int nblk, hipStream_t st) {
-  constexpr int U = NTW == 1 ? (CK < 8 ? CK : 8) : 4;
+  constexpr int U = 4;  // slices per weight prefetch group (x2 register sets, ping-pong)
   hipLaunchKernelGGL((bgemm_kernel<NB, NTW, W, CK, U, EPI, NORM>), dim3(nblk * b.ksplit), dim3(W * 64), 0, st, a, b);
   return hipGetLastError();
 }
@@ -814,6 +882,7 @@ static hipError_t bg_launch_shape(int epi, const BgPlan& p, const GemmArgs& a, c
     if (p.ntw == 2) return bg_launch_e<NB, 2, 8, 8, NORM>(epi, a, b, p.nblk, st);
     if (p.w == 4) return bg_launch_e<NB, 1, 4, 8, NORM>(epi, a, b, p.nblk, st);
     if (p.ck == 16) return bg_launch_e<NB, 1, 8, 16, NORM>(epi, a, b, p.nblk, st);
+    if (p.ck == 4) return bg_launch_e<NB, 1, 8, 4, NORM>(epi, a, b, p.nblk, st);
     return bg_launch_e<NB, 1, 8, 8, NORM>(epi, a, b, p.nblk, st);
   }
 }
