@@ -58,7 +58,7 @@ def main() -> int:
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--model", default="llama3.1:8b")
     ap.add_argument("--words", type=int, default=1000)
-    ap.add_argument("--batch", type=int, default=64, help="concurrent trials per GPU (trial batching)")
+    ap.add_argument("--batch", type=int, default=128, help="concurrent trials per GPU (trial batching, <= 128)")
     ap.add_argument("--context", type=int, default=1536)
     ap.add_argument("--steps-per-graph", type=int, default=16)
     ap.add_argument("--no-energy", action="store_true")

@@ -508,7 +508,7 @@ __device__ __forceinline__ f32x4 ld_wt(const float* p) {
   return v;
 }
 
-template <int NB, int NTW, int W, int CK, int U, int EPI, bool NORM>
+template <int NB, int NTW, int W, int CK, int U, int D, int EPI, bool NORM>
 __global__ __launch_bounds__(W * 64, (W == 8 && NTW == 1 && CK * NB <= 32) ? 4 : 2) void bgemm_kernel(const GemmArgs a, const BgArgs bg) {
   constexpr int BG_CK = CK;
   constexpr int FR = BG_CK * NB;        // B fragments per chunk
@@ -552,7 +552,7 @@ __global__ __launch_bounds__(W * 64, (W == 8 && NTW == 1 && CK * NB <= 32) ? 4 :
   // staging: fragment f = wave + W*i of a chunk is (slice f / NB, row block f % NB); lane reads
   // X[16*rb + (lane & 15)][32*slice + 8*(lane >> 4) .. +8]  (rows past M re-read row M-1)
   const __bf16* xrow[FPW];
-  float ssq[FPW];
+  float ssq[FPW];  // NORM: partial sum of x^2 of the row of staged fragment i (its k-groups)
 #pragma unroll
   for (int i = 0; i < FPW; ++i) {
     const int f = wave + W * i, rb = f % NB, sl = f / NB;
@@ -609,9 +609,10 @@ __global__ __launch_bounds__(W * 64, (W == 8 && NTW == 1 && CK * NB <= 32) ? 4 :
   // chunk whose weights are masked to zero (its activations are the last real chunk: finite).
   const int s_last = s_beg + nch * BG_CK - 1;
   bf16x8 wb_[U][NTW];
-  auto run_group = [&](int c, int h, bool valid, bf16x8 (&cur)[U][NTW], bf16x8 (&nxt)[U][NTW]) {
+  // pf: prefetch distance in groups (1 for the ping-pong, D-1 for the register ring)
+  auto run_group = [&](int c, int h, bool valid, bf16x8 (&cur)[U][NTW], bf16x8 (&nxt)[U][NTW], int pf) {
     const int buf = c & 1;
-    const int sn = s_beg + c * BG_CK + (h + 1) * U;  // first slice of the next group
+    const int sn = s_beg + c * BG_CK + (h + pf) * U;  // first slice of the group being prefetched
 #pragma unroll
     for (int u = 0; u < U; ++u)
 #pragma unroll
@@ -635,31 +636,51 @@ __global__ __launch_bounds__(W * 64, (W == 8 && NTW == 1 && CK * NB <= 32) ? 4 :
       if constexpr (NB >= 8) __builtin_amdgcn_sched_barrier(0);
     }
   };
-  auto run_chunk = [&](int c, bool valid, bf16x8 (&A)[U][NTW], bf16x8 (&B)[U][NTW]) {
+  auto run_chunk = [&](int c, bool valid, bf16x8 (&A)[U][NTW], bf16x8 (&B)[U][NTW], int pf) {
     bf16x8 xr[FPW];
     stage_load(min(c + 1, nch - 1), xr);
     // pin the activation loads ahead of the weight prefetch: issued later, they would be the youngest
     // loads at the staging write and force a vmcnt(0) that drains the weight prefetch too
     __builtin_amdgcn_sched_barrier(0);
     if constexpr (NGRP == 1) {
-      run_group(c, 0, valid, A, B);
+      run_group(c, 0, valid, A, B, pf);
     } else {
 #pragma unroll
       for (int h = 0; h < NGRP; h += 2) {
-        run_group(c, h, valid, A, B);
-        run_group(c, h + 1, valid, B, A);
+        run_group(c, h, valid, A, B, 1);
+        run_group(c, h + 1, valid, B, A, 1);
       }
     }
-    stage_store((c & 1) ^ 1, xr, (valid && c + 1 < nch) ? 1.f : 0.f);  // the final stage adds nothing to ssq
+    stage_store((c & 1) ^ 1, xr, (valid && c + 1 < nch) ? 1.f : 0.f);  // the final stage adds nothing
     __syncthreads();
   };
   static_assert(NGRP == 1 || NGRP % 2 == 0, "weight prefetch groups per chunk");
+  static_assert(D == 2 || NGRP == 1, "the deep register ring needs one group per chunk");
   if constexpr (NGRP % 2 == 0) {
-    for (int c = 0; c < nch; ++c) run_chunk(c, true, wa, wb_);
-  } else {
+    for (int c = 0; c < nch; ++c) run_chunk(c, true, wa, wb_, 1);
+  } else if constexpr (D == 2) {
     for (int c = 0; c < nch; c += 2) {
-      run_chunk(c, true, wa, wb_);
-      run_chunk(c + 1, c + 1 < nch, wb_, wa);
+      run_chunk(c, true, wa, wb_, 1);
+      run_chunk(c + 1, c + 1 < nch, wb_, wa, 1);
+    }
+  } else {
+    // D-deep register ring (narrow outputs: few waves per CU, so each wave keeps D-1 groups of weight
+    // loads in flight): chunk c computes ring[c % D] and prefetches chunk c + D - 1 into the set that
+    // chunk c - 1 just finished; the loop is unrolled by D so every ring index is static.
+    bf16x8 ring[D][U][NTW];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int t = 0; t < NTW; ++t) ring[0][u][t] = wa[u][t];
+#pragma unroll
+    for (int j = 1; j < D - 1; ++j)
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int t = 0; t < NTW; ++t) ring[j][u][t] = load_w(min(s_beg + j * U + u, s_last), t);
+    for (int c = 0; c < nch; c += D) {
+#pragma unroll
+      for (int j = 0; j < D; ++j) run_chunk(c + j, c + j < nch, ring[j], ring[(j + D - 1) % D], D - 1);
     }
   }
 
@@ -827,8 +848,9 @@ static BgPlan bgemm_plan(int N, int K, int M, int ntw_req) {
     // 64 rows: the mid-width gate/up projection measured faster with 4-slice chunks too (43.8 vs 47.0 us)
     const int nblk8 = (N + 16 * BG_WAVES - 1) / (16 * BG_WAVES);
     const bool mid = p.nb == 4 && nblk8 >= 128 && nblk8 < 512;
-    p.ck = (ck_env == 16 && p.ntw == 1 && p.w == 8 && (K / 32) % 16 == 0) ? 16
-           : (p.ntw == 1 && p.w == 8 && (ck_env == 4 || (ck_env == 0 && mid))) ? 4 : BG_CK;
+    p.ck = p.w == 4 ? 4  // the 4-wave variants run the deep register ring: one prefetch group per chunk
+           : (ck_env == 16 && p.ntw == 1 && (K / 32) % 16 == 0) ? 16
+           : (p.ntw == 1 && (ck_env == 4 || (ck_env == 0 && mid))) ? 4 : BG_CK;
   }
   const int rows = 16 * p.w * p.ntw;
   p.nblk = (N + rows - 1) / rows;
@@ -854,8 +876,13 @@ static size_t bgemm_ws_bytes(const BgPlan& p) {
 
 template <int NB, int NTW, int W, int CK, int EPI, bool NORM>
 static hipError_t bg_launch(const GemmArgs& a, const BgArgs& b, int nblk, hipStream_t st) {
-  constexpr int U = 4;  // slices per weight prefetch group (x2 register sets, ping-pong)
-  hipLaunchKernelGGL((bgemm_kernel<NB, NTW, W, CK, U, EPI, NORM>), dim3(nblk * b.ksplit), dim3(W * 64), 0, st, a, b);
+  constexpr int U = 4;  // slices per weight prefetch group
+  // register sets of weight prefetch: 4-wave workgroups (narrow outputs, 2 waves per SIMD, 256-VGPR
+  // budget) keep 3 groups in flight, the rest ping-pong between 2 (so do the fused-norm 4-wave bodies,
+  // whose 8 staged fragments per wave leave no room for the deeper ring)
+  constexpr int D = (W == 4 && CK == U && !NORM) ? 4 : 2;
+  hipLaunchKernelGGL((bgemm_kernel<NB, NTW, W, CK, U, D, EPI, NORM>), dim3(nblk * b.ksplit), dim3(W * 64), 0, st, a,
+                     b);
   return hipGetLastError();
 }
 
@@ -880,7 +907,7 @@ static hipError_t bg_launch_shape(int epi, const BgPlan& p, const GemmArgs& a, c
     return bg_launch_e<8, 1, 8, 4, NORM>(epi, a, b, p.nblk, st);
   } else {
     if (p.ntw == 2) return bg_launch_e<NB, 2, 8, 8, NORM>(epi, a, b, p.nblk, st);
-    if (p.w == 4) return bg_launch_e<NB, 1, 4, 8, NORM>(epi, a, b, p.nblk, st);
+    if (p.w == 4) return bg_launch_e<NB, 1, 4, 4, NORM>(epi, a, b, p.nblk, st);
     if (p.ck == 16) return bg_launch_e<NB, 1, 8, 16, NORM>(epi, a, b, p.nblk, st);
     if (p.ck == 4) return bg_launch_e<NB, 1, 8, 4, NORM>(epi, a, b, p.nblk, st);
     return bg_launch_e<NB, 1, 8, 8, NORM>(epi, a, b, p.nblk, st);
