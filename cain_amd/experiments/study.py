@@ -57,8 +57,8 @@ REPO_ROOT = Path(__file__).resolve().parents[2]
 DEFAULT_TOPICS = REPO_ROOT / "experiments" / "topics.csv"
 
 REFERENCE_COLUMNS = ["topic", "execution_time", "cpu_usage", "gpu_usage", "memory_usage"]
-EXTRA_COLUMNS = ["tokens_generated", "prompt_tokens", "J_per_token", "tok_per_s", "ttft_s", "server_total_s",
-                 "server_eval_s", "client_wall_s", "device", "server"]
+EXTRA_COLUMNS = ["tokens_generated", "prompt_tokens", "J_per_token", "tok_per_s", "ttft_s", "gen_time_s",
+                 "server_total_s", "server_eval_s", "client_wall_s", "device", "server"]
 ENERGY_COLUMNS = [DataColumns.ENERGY_CONSUMED, DataColumns.ENERGY_USAGE_J, DataColumns.GPU_ENERGY_J,
                   DataColumns.CPU_ENERGY_J, DataColumns.IDLE_SUBTRACTED_J, DataColumns.AVG_GPU_POWER_W,
                   DataColumns.WINDOW_S]
@@ -88,6 +88,12 @@ class StudySettings:
     remote_fake_tok_s: float = 70.0       # RTX 4070-class llama-8B decode rate for the modelled server
     remote_fake_prefill_s: float = 0.15
     client: str = "curl"                  # curl (reference parity) | http (in-process client)
+    # measurement window: "request" opens the energy window, then issues the request;
+    # "reference" issues it in START_RUN first and opens the window afterwards, like the reference
+    window: str = "request"
+    # remote-arm trials on a shared host take a host-wide lock while measured, so concurrent ranks do
+    # not load the CPU whose energy they are charged
+    remote_exclusive: bool = True
     stream: bool = False
     request_timeout_s: float = 900.0
     server_start_timeout_s: float = 900.0
@@ -360,12 +366,42 @@ class _StudyBase:
             raise RuntimeError(f"no server for method {v['method']} (before_experiment not run?)")
         self.url = url
         self.response, self.error = None, None
+        self.request = None
+        self._model = v["model"]
+        self._lock_window(context)
+        if self.settings.window == "reference":
+            self._issue()
+
+    def _issue(self) -> None:
         s = self.settings
         if s.client == "curl" and shutil.which("curl"):
-            self.request = CurlRequest(url, v["model"], self.prompt, stream=s.stream,
+            self.request = CurlRequest(self.url, self._model, self.prompt, stream=s.stream,
                                        timeout_s=s.request_timeout_s).start()
         else:
-            self.request = _HttpRequest(url, v["model"], self.prompt, s.stream, s.request_timeout_s).start()
+            self.request = _HttpRequest(self.url, self._model, self.prompt, s.stream, s.request_timeout_s).start()
+
+    def _lock_window(self, context: RunnerContext) -> None:
+        """Host-wide exclusive lock for measured remote-arm windows when several ranks share the host
+        (taken at the end of START_RUN, i.e. before the plugin opens the window; released in STOP_RUN)."""
+        self._unlock_window()
+        if not (self.settings.remote_exclusive and context.run_variation.get("method") == "remote"
+                and int(getattr(self, "dp_world", 1)) > 1):
+            return
+        import fcntl
+
+        path = self.results_output_path / self.settings.name / ".remote_window.lock"
+        fh = open(path, "a")
+        fcntl.flock(fh, fcntl.LOCK_EX)
+        self._lock_fh = fh
+
+    def _unlock_window(self) -> None:
+        fh = getattr(self, "_lock_fh", None)
+        if fh is not None:
+            import fcntl
+
+            fcntl.flock(fh, fcntl.LOCK_UN)
+            fh.close()
+            self._lock_fh = None
 
     def energy_sources_for(self, context: RunnerContext):
         if context.run_variation.get("method") == "remote" and self.remote_shares_gpu:
@@ -373,7 +409,10 @@ class _StudyBase:
         return ("gpu", "cpu")
 
     def start_measurement(self, context: RunnerContext) -> None:
-        # the window is the request (reference: a psutil poll loop until curl exits)
+        # the energy window (opened by the plugin just before this body) covers the request; with
+        # window="request" the request is issued only now, so none of it runs outside the window
+        if self.request is None:
+            self._issue()
         try:
             self.response = self.request.wait(self.settings.request_timeout_s + 30)
         except OllamaError as exc:
@@ -388,6 +427,7 @@ class _StudyBase:
 
     def stop_run(self, context: RunnerContext) -> None:
         self.timestamp_end = datetime.now()
+        self._unlock_window()
         if self.error is not None:
             raise RuntimeError(f"request failed: {self.error}")
 
@@ -461,6 +501,7 @@ class StudyConfig(_MeasuredStudy):
             "server_total_s": round(st.get("server_total_s", 0.0), 6),
             "server_eval_s": round(st.get("server_eval_s", 0.0), 6),
             "client_wall_s": round(wall, 6),
+            "gen_time_s": round(st.get("server_eval_s", 0.0) + st.get("server_prompt_eval_s", 0.0), 6),
             "device": str(getattr(self, "energy_devices", [""])[0]) if getattr(self, "energy_devices", None) else "",
             "server": self.url,
         })

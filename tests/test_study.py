@@ -29,7 +29,8 @@ def test_study_config_runs_both_arms(tmp_path, gpus):
     if gpus:
         cmd += ["--gpus", str(gpus)]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=ROOT,
-                       env=_env(tmp_path, CAIN_STUDY_PORT_BASE=str(21000 + gpus * 500 + os.getpid() % 400)))
+                       env=_env(tmp_path, CAIN_STUDY_PORT_BASE=str(21000 + gpus * 500 + os.getpid() % 400),
+                                CAIN_STUDY_WINDOW="reference" if gpus else "request"))
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     rows = list(csv.DictReader(open(tmp_path / "full_factorial" / "run_table.csv")))
     assert len(rows) == 4 and all(x["__done"] == "DONE" for x in rows)
