@@ -508,7 +508,7 @@ __device__ __forceinline__ f32x4 ld_wt(const float* p) {
   return v;
 }
 
-template <int NB, int NTW, int W, int CK, int U, int D, int EPI, bool NORM>
+template <int NB, int NTW, int W, int CK, int U, int D, int XS, int EPI, bool NORM>
 __global__ __launch_bounds__(W * 64, (W == 8 && NTW == 1 && CK * NB <= 32) ? 4 : 2) void bgemm_kernel(const GemmArgs a, const BgArgs bg) {
   constexpr int BG_CK = CK;
   constexpr int FR = BG_CK * NB;        // B fragments per chunk
@@ -516,7 +516,8 @@ __global__ __launch_bounds__(W * 64, (W == 8 && NTW == 1 && CK * NB <= 32) ? 4 :
   constexpr int NGRP = BG_CK / U;       // weight prefetch groups per chunk
   constexpr int UNITS = W * NTW * NB;   // 64-lane output blocks per workgroup
   static_assert(FR % W == 0 && BG_CK % U == 0, "tiling");
-  static_assert(UNITS * 1024 <= 2 * FR * 1024, "epilogue buffer must fit in the staging buffer");
+  static_assert(UNITS * 1024 <= XS * FR * 1024, "epilogue buffer must fit in the staging buffer");
+  static_assert(XS == 2 || XS == 3, "activation stage depth");
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int KS = a.K >> 5, ntiles = a.N >> 4;
   int blk, kc;
@@ -535,7 +536,9 @@ __global__ __launch_bounds__(W * 64, (W == 8 && NTW == 1 && CK * NB <= 32) ? 4 :
   const int s_beg = kc * bg.kspl;
   const int nch = (min(KS, s_beg + bg.kspl) - s_beg) / BG_CK;
 
-  __shared__ __attribute__((aligned(16))) bf16x8 xs[2][FR][64];
+  // XS activation stages: chunk c is read from xs[c % XS]; with XS = 3 the loads of chunk c+2 are in
+  // flight while c computes (two chunk-times to land instead of one)
+  __shared__ __attribute__((aligned(16))) bf16x8 xs[XS][FR][64];
   __shared__ float ss_red[NORM ? W : 1][NORM ? NB * 16 : 1];
   __shared__ float s_inv[NB * 16];
   __shared__ unsigned s_ticket;
@@ -588,6 +591,7 @@ __global__ __launch_bounds__(W * 64, (W == 8 && NTW == 1 && CK * NB <= 32) ? 4 :
     for (int b = 0; b < NB; ++b) acc[t][b] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   bf16x8 wa[U][NTW];
+  bf16x8 xa_[FPW], xb_[FPW];  // activation staging registers (see run_chunk)
 #pragma unroll
   for (int u = 0; u < U; ++u)
 #pragma unroll
@@ -597,6 +601,7 @@ __global__ __launch_bounds__(W * 64, (W == 8 && NTW == 1 && CK * NB <= 32) ? 4 :
     stage_load(0, xr);
     stage_store(0, xr, 1.f);
   }
+  if constexpr (XS == 3) stage_load(min(1, nch - 1), xb_);  // chunk 1: stored at the end of chunk 0
   __syncthreads();
 
   // Steady state, branch-free and copy-free:
@@ -611,7 +616,7 @@ __global__ __launch_bounds__(W * 64, (W == 8 && NTW == 1 && CK * NB <= 32) ? 4 :
   bf16x8 wb_[U][NTW];
   // pf: prefetch distance in groups (1 for the ping-pong, D-1 for the register ring)
   auto run_group = [&](int c, int h, bool valid, bf16x8 (&cur)[U][NTW], bf16x8 (&nxt)[U][NTW], int pf) {
-    const int buf = c & 1;
+    const int buf = c % XS;
     const int sn = s_beg + c * BG_CK + (h + pf) * U;  // first slice of the group being prefetched
 #pragma unroll
     for (int u = 0; u < U; ++u)
@@ -636,9 +641,12 @@ __global__ __launch_bounds__(W * 64, (W == 8 && NTW == 1 && CK * NB <= 32) ? 4 :
       if constexpr (NB >= 8) __builtin_amdgcn_sched_barrier(0);
     }
   };
-  auto run_chunk = [&](int c, bool valid, bf16x8 (&A)[U][NTW], bf16x8 (&B)[U][NTW], int pf) {
-    bf16x8 xr[FPW];
-    stage_load(min(c + 1, nch - 1), xr);
+  // xa_/xb_: activation staging registers.  XS = 2: chunk c loads chunk c+1 into xa_ and stores it at
+  // its end.  XS = 3: chunk c loads chunk c+2 into one set and stores the other (chunk c+1, loaded one
+  // chunk earlier); the sets alternate, so the chunk loop runs unrolled by 2 (or D) and never copies.
+  auto run_chunk = [&](int c, bool valid, bf16x8 (&A)[U][NTW], bf16x8 (&B)[U][NTW], int pf, bf16x8 (&xl)[FPW],
+                       bf16x8 (&xw)[FPW]) {
+    stage_load(min(c + XS - 1, nch - 1), xl);
     // pin the activation loads ahead of the weight prefetch: issued later, they would be the youngest
     // loads at the staging write and force a vmcnt(0) that drains the weight prefetch too
     __builtin_amdgcn_sched_barrier(0);
@@ -651,22 +659,27 @@ __global__ __launch_bounds__(W * 64, (W == 8 && NTW == 1 && CK * NB <= 32) ? 4 :
         run_group(c, h + 1, valid, B, A, 1);
       }
     }
-    stage_store((c & 1) ^ 1, xr, (valid && c + 1 < nch) ? 1.f : 0.f);  // the final stage adds nothing
+    // stage chunk c+1 (XS = 2: just loaded into xl; XS = 3: loaded one chunk ago into xw); the final
+    // (clamped, redundant) stages add nothing to the sum of squares
+    if constexpr (XS == 2) stage_store((c + 1) % XS, xl, (valid && c + 1 < nch) ? 1.f : 0.f);
+    else stage_store((c + 1) % XS, xw, (valid && c + 1 < nch) ? 1.f : 0.f);
     __syncthreads();
   };
   static_assert(NGRP == 1 || NGRP % 2 == 0, "weight prefetch groups per chunk");
   static_assert(D == 2 || NGRP == 1, "the deep register ring needs one group per chunk");
+  static_assert(XS == 2 || NGRP == 1, "three activation stages need one group per chunk");
   if constexpr (NGRP % 2 == 0) {
-    for (int c = 0; c < nch; ++c) run_chunk(c, true, wa, wb_, 1);
+    for (int c = 0; c < nch; ++c) run_chunk(c, true, wa, wb_, 1, xa_, xb_);
   } else if constexpr (D == 2) {
     for (int c = 0; c < nch; c += 2) {
-      run_chunk(c, true, wa, wb_, 1);
-      run_chunk(c + 1, c + 1 < nch, wb_, wa, 1);
+      run_chunk(c, true, wa, wb_, 1, xa_, xb_);
+      run_chunk(c + 1, c + 1 < nch, wb_, wa, 1, xb_, xa_);
     }
   } else {
     // D-deep register ring (narrow outputs: few waves per CU, so each wave keeps D-1 groups of weight
     // loads in flight): chunk c computes ring[c % D] and prefetches chunk c + D - 1 into the set that
     // chunk c - 1 just finished; the loop is unrolled by D so every ring index is static.
+    static_assert(D % 2 == 0, "ring depth must keep the activation register sets alternating");
     bf16x8 ring[D][U][NTW];
 #pragma unroll
     for (int u = 0; u < U; ++u)
@@ -680,7 +693,10 @@ __global__ __launch_bounds__(W * 64, (W == 8 && NTW == 1 && CK * NB <= 32) ? 4 :
         for (int t = 0; t < NTW; ++t) ring[j][u][t] = load_w(min(s_beg + j * U + u, s_last), t);
     for (int c = 0; c < nch; c += D) {
 #pragma unroll
-      for (int j = 0; j < D; ++j) run_chunk(c + j, c + j < nch, ring[j], ring[(j + D - 1) % D], D - 1);
+      for (int j = 0; j < D; ++j) {
+        if (j % 2 == 0) run_chunk(c + j, c + j < nch, ring[j], ring[(j + D - 1) % D], D - 1, xa_, xb_);
+        else run_chunk(c + j, c + j < nch, ring[j], ring[(j + D - 1) % D], D - 1, xb_, xa_);
+      }
     }
   }
 
@@ -881,8 +897,10 @@ static hipError_t bg_launch(const GemmArgs& a, const BgArgs& b, int nblk, hipStr
   // budget) keep 3 groups in flight, the rest ping-pong between 2 (so do the fused-norm 4-wave bodies,
   // whose 8 staged fragments per wave leave no room for the deeper ring)
   constexpr int D = (W == 4 && CK == U && !NORM) ? 4 : 2;
-  hipLaunchKernelGGL((bgemm_kernel<NB, NTW, W, CK, U, D, EPI, NORM>), dim3(nblk * b.ksplit), dim3(W * 64), 0, st, a,
-                     b);
+  // three activation stages for the 4-wave bodies (one workgroup per CU on the narrow grids anyway)
+  constexpr int XS = (W == 4 && CK == U) ? 3 : 2;
+  hipLaunchKernelGGL((bgemm_kernel<NB, NTW, W, CK, U, D, XS, EPI, NORM>), dim3(nblk * b.ksplit), dim3(W * 64), 0, st,
+                     a, b);
   return hipGetLastError();
 }
 
