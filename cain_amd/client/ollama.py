@@ -63,6 +63,8 @@ class GenerateResponse:
             out["ttft_s"] = d["cain_ttft_ns"] * ns
         if out["server_eval_s"] > 0:
             out["server_tok_per_s"] = self.eval_count / out["server_eval_s"]
+        if d.get("cain_trace"):
+            out["trace_file"] = d["cain_trace"]
         return out
 
 

@@ -27,6 +27,7 @@ from __future__ import annotations
 
 import ctypes
 import math
+import os
 import time
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Sequence, Union
@@ -125,8 +126,13 @@ def _ptr(t: Optional[torch.Tensor]) -> Optional[int]:
 def attention_splits(M: int, Hkv: int, T_max: int) -> int:
     """Position splits per (row, kv head): ~256 workgroups in flight, >= 4 blocks of 32 per split at
     full context, <= 64 splits (measured: 1024-WG targets lose more to the split combine than they
-    gain in parallelism, profiles/kernels.md)."""
-    return int(max(1, min(64, max(1, T_max // 128), math.ceil(256 / (M * Hkv)))))
+    gain in parallelism, profiles/kernels.md).  ``CAIN_ATTN_SPLIT_BLOCKS`` = b > 0 additionally caps a
+    split at b blocks of 32 positions (bounds one workgroup's serial work at wide batches)."""
+    ns = max(1, min(T_max // 128, math.ceil(256 / (M * Hkv))))
+    per = int(os.environ.get("CAIN_ATTN_SPLIT_BLOCKS", "0") or 0)
+    if per > 0:
+        ns = max(ns, math.ceil((T_max // 32) / per))
+    return int(max(1, min(64, ns)))
 
 
 class DecodeEngine:

@@ -100,6 +100,9 @@ class StudySettings:
     # energy: idle board power measured once per rank after the servers are up and have settled (0 disables)
     idle_baseline_s: float = 3.0
     idle_settle_s: float = 5.0
+    # tracing: the on-device server records each generation with torch.profiler and the
+    # Chrome trace is filed as run_dir/kernel_trace.json (adds profiler overhead to the measured window)
+    trace: bool = False
 
     @classmethod
     def from_env(cls, base: Optional["StudySettings"] = None) -> "StudySettings":
@@ -291,6 +294,8 @@ class _StudyBase:
                     "--backend", backend]
             if s.preload and backend != "fake":
                 args.append("--preload")
+            if s.trace:
+                args += ["--trace-dir", str(self.results_output_path / s.name / "traces" / f"rank{self.rank}")]
             env = {}
             if gpu is not None:
                 # the server sees only this rank's GPU; the rank keeps addressing it by its own ordinal
@@ -455,6 +460,9 @@ class _StudyBase:
                                                                       indent=1))
         except OSError:  # pragma: no cover
             pass
+        trace = self._last_stats.get("trace_file")
+        if trace and os.path.exists(trace):  # server-side profiler trace of this request (settings.trace)
+            shutil.move(trace, context.run_dir / "kernel_trace.json")
         return data
 
     def after_experiment(self) -> None:

@@ -197,6 +197,55 @@ def embed(tok: torch.Tensor, table: torch.Tensor, scale: float = 1.0, out=None) 
     return out
 
 
+# ---------------------------------------------------------------- KV-cache layout (attention.hip header)
+def pack_kcache(k: torch.Tensor) -> torch.Tensor:
+    """Natural K ``[..., T, hd]`` -> the fragment-major K cache layout (same shape and element count):
+    per 16 positions x 32 head dims one 1-KiB MFMA A fragment, lane = (t & 15) + 16 * ((d & 31) >> 3)."""
+    *lead, T, hd = k.shape
+    n = len(lead)
+    t = k.reshape(*lead, T // 16, 16, hd // 32, 4, 8)                 # [u, r, s, q, e]
+    t = t.permute(*range(n), n, n + 2, n + 3, n + 1, n + 4)           # [u, s, q, r, e]
+    return t.contiguous().reshape(*lead, T, hd)
+
+
+def unpack_kcache(p: torch.Tensor) -> torch.Tensor:
+    *lead, T, hd = p.shape
+    n = len(lead)
+    t = p.reshape(*lead, T // 16, hd // 32, 4, 16, 8)                 # [u, s, q, r, e]
+    t = t.permute(*range(n), n, n + 3, n + 1, n + 2, n + 4)           # [u, r, s, q, e]
+    return t.contiguous().reshape(*lead, T, hd)
+
+
+def pack_vcache(v: torch.Tensor) -> torch.Tensor:
+    """Natural V ``[..., T, hd]`` -> the fragment-major V^T cache layout, returned as ``[..., hd, T]`` (the
+    engine's buffer shape): per 16 head dims x 32 positions one 1-KiB PV A fragment in the permuted k order
+    of P, lane = (d & 15) + 16 * ((t & 15) >> 2), element 4 * ((t >> 4) & 1) + (t & 3)."""
+    *lead, T, hd = v.shape
+    n = len(lead)
+    t = v.reshape(*lead, T // 32, 2, 4, 4, hd // 16, 16)              # [b, h, hq, j, c, dr]
+    t = t.permute(*range(n), n, n + 4, n + 2, n + 5, n + 1, n + 3)    # [b, c, hq, dr, h, j]
+    return t.contiguous().reshape(*lead, hd, T)
+
+
+def unpack_vcache(p: torch.Tensor) -> torch.Tensor:
+    """Inverse of ``pack_vcache``: ``[..., hd, T]`` buffer -> natural V ``[..., T, hd]``."""
+    *lead, hd, T = p.shape
+    n = len(lead)
+    t = p.reshape(*lead, T // 32, hd // 16, 4, 16, 2, 4)              # [b, c, hq, dr, h, j]
+    t = t.permute(*range(n), n, n + 4, n + 2, n + 5, n + 1, n + 3)    # [b, h, hq, j, c, dr]
+    return t.contiguous().reshape(*lead, T, hd)
+
+
+def kfrag_off(t: int, d: int, hd: int) -> int:
+    """Host mirror of common.h kfrag_off (element offset inside one (slot, kv head) block)."""
+    return ((t >> 4) * (hd >> 5) + (d >> 5)) * 512 + ((t & 15) + 16 * ((d & 31) >> 3)) * 8 + (d & 7)
+
+
+def vfrag_off(t: int, d: int, hd: int) -> int:
+    """Host mirror of common.h vfrag_off."""
+    return ((t >> 5) * (hd >> 4) + (d >> 4)) * 512 + ((d & 15) + 16 * ((t & 15) >> 2)) * 8 + 4 * ((t >> 4) & 1) + (t & 3)
+
+
 def attention_ml_floats(M: int, H: int, Hkv: int, nsplit: int) -> int:
     """Size of the (max, sum) partial workspace: one 128-B-aligned region per (row, kv head)."""
     G = H // Hkv

@@ -1,20 +1,31 @@
 // Decode / short-prefill attention over the KV cache, split over positions
 // (flash-decoding) with both products on MFMA (SURVEY §2.4 row "Decode attention").
 //
+// KV cache layout: fragment-major, written by the QKV GEMM epilogue (gemm.hip; element offsets
+// kfrag_off / vfrag_off in common.h, torch mirrors in cain_amd/ops pack_kcache / pack_vcache).
+// Per (slot, kv head):
+//   K    [T/16][hd/32][64 lanes][8]: the A fragment of v_mfma_f32_16x16x32_bf16 for positions
+//        16u..16u+15 x head dims 32s..32s+31 (lane = (t&15) + 16*((d&31)>>3), element d&7);
+//   V^T  [T/32][hd/16][64 lanes][8]: the A fragment of the PV product for head dims 16c..16c+15 x
+//        the 32 positions of block b in P's permuted k order below (lane = (d&15) + 16*((t&15)>>2),
+//        element 4*((t>>4)&1) + (t&3)).
+// A 32-position block of one (slot, kv head) is 2*hd*32 contiguous bytes of K and as many of V, and
+// every load instruction of a wave reads one contiguous 1 KiB (full 128-B lines; a row-major cache
+// made each K load touch 16 rows x 64 B and each V^T load 16 rows x 8 B).
+//
 // Workgroup = 4 waves = (row m, kv head kh, split sp).  The G = H/Hkv query
 // heads of the group are the 16 MFMA columns (G <= 16 covers MHA, GQA 4/6/7/8
 // and MQA).  The split's 32-position blocks are dealt to the 4 waves.  Per block:
 //   S^T[t][g] = K[t][:] . Q[g][:]     2 tiles of v_mfma_f32_16x16x32_bf16 x hd/32
-//       A = K rows (lane: row t = l&15, 16 B of K[t][32i+8(l>>4)..]) straight from HBM,
-//       B = Q^T (lane: col g) held in registers for the whole wave;
+//       A = K fragments straight from HBM, B = Q^T (lane: col g) held in registers
+//       for the whole wave;
 //   online softmax per column g in registers (exp2, scale*log2e folded);
 //   O^T[d][g] += V^T[d][t] P^T[t][g]   hd/16 MFMAs, k = the block's 32 positions
 //       B = P^T taken from the S accumulators WITHOUT moving data: lane (g, h)
 //       holds t = 4h..4h+3 (tile 0) and 16+4h..16+4h+3 (tile 1), which defines a
 //       permuted k order (cdna_hip_programming.md §3 'An accumulator tile as the
 //       next MFMA's operand');
-//       A = V^T rows in that same k order: two 8-byte loads from the transposed
-//       V cache (written by the QKV GEMM epilogue) — nothing is staged through LDS.
+//       A = V^T fragments stored in that same k order — nothing is staged through LDS.
 // The 4 waves merge their (m, l, O) in LDS.  With one split the workgroup
 // normalises and stores bf16 directly; otherwise each workgroup publishes an
 // unnormalised partial with write-through (sc1) stores and the LAST arriving
@@ -68,37 +79,23 @@ __global__ __launch_bounds__(AW * 64) void attn_decode_kernel(
       qf[i] = v;
     }
     const float sl2 = scale * LOG2E;
-    const __bf16* kbase = kc + ((size_t)s * Hkv + kh) * T_max * HD;
-    const __bf16* vbase = vtc + ((size_t)s * Hkv + kh) * HD * T_max;
-    // K/V fragments of one 32-position block; with HD <= 128 the next block's loads are
-    // issued before the current block computes (register double buffer)
-    constexpr bool PREF = HD <= 128;
-    bf16x8 ka[NKS], kb[NKS];
-    u16x4 va[NDT], vb[NDT];
-    auto load_blk = [&](int blk, bf16x8 (&k_a)[NKS], bf16x8 (&k_b)[NKS], u16x4 (&v_a)[NDT], u16x4 (&v_b)[NDT]) {
-      const int t0 = blk * 32;
-      const __bf16* k0 = kbase + (size_t)(t0 + g) * HD + hq * 8;
-      const __bf16* k1 = k0 + 16 * HD;
+    // fragment-major caches (layout at the top of this file): a 32-position block of one (slot, kv head) is
+    // 2*NKS contiguous 1-KiB K fragments and NDT contiguous 1-KiB V^T fragments; lane l's 16 B sit at 16*l
+    const __bf16* kbase = kc + ((size_t)s * Hkv + kh) * T_max * HD + lane * 8;
+    const __bf16* vbase = vtc + ((size_t)s * Hkv + kh) * HD * T_max + lane * 8;
+    auto load_blk = [&](int blk, bf16x8 (&k_a)[NKS], bf16x8 (&k_b)[NKS], bf16x8 (&v)[NDT]) {
+      const __bf16* k0 = kbase + (size_t)blk * (2 * NKS * 512);
 #pragma unroll
       for (int i = 0; i < NKS; ++i) {
-        k_a[i] = *reinterpret_cast<const bf16x8*>(k0 + i * 32);
-        k_b[i] = *reinterpret_cast<const bf16x8*>(k1 + i * 32);
+        k_a[i] = *reinterpret_cast<const bf16x8*>(k0 + i * 512);
+        k_b[i] = *reinterpret_cast<const bf16x8*>(k0 + (NKS + i) * 512);
       }
+      const __bf16* v0 = vbase + (size_t)blk * (NDT * 512);
 #pragma unroll
-      for (int dt = 0; dt < NDT; ++dt) {
-        const __bf16* vr = vbase + (size_t)(dt * 16 + g) * T_max + t0 + hq * 4;
-        v_a[dt] = *reinterpret_cast<const u16x4*>(vr);
-        v_b[dt] = *reinterpret_cast<const u16x4*>(vr + 16);
-      }
+      for (int dt = 0; dt < NDT; ++dt) v[dt] = *reinterpret_cast<const bf16x8*>(v0 + dt * 512);
     };
-    if (b0 + wave < b1) load_blk(b0 + wave, ka, kb, va, vb);
-    for (int blk = b0 + wave; blk < b1; blk += AW) {
+    auto process = [&](int blk, const bf16x8 (&ka)[NKS], const bf16x8 (&kb)[NKS], const bf16x8 (&va)[NDT]) {
       const int t0 = blk * 32;
-      bf16x8 nka[PREF ? NKS : 1], nkb[PREF ? NKS : 1];
-      u16x4 nva[PREF ? NDT : 1], nvb[PREF ? NDT : 1];
-      if constexpr (PREF) {
-        if (blk + AW < b1) load_blk(blk + AW, nka, nkb, nva, nvb);
-      }
       f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int i = 0; i < NKS; ++i) {
@@ -131,21 +128,31 @@ __global__ __launch_bounds__(AW * 64) void attn_decode_kernel(
 #pragma unroll
       for (int dt = 0; dt < NDT; ++dt) {
         o[dt] *= alpha;
-        u16x8 vv;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          vv[j] = va[dt][j];
-          vv[4 + j] = vb[dt][j];
-        }
-        o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, vv), pf, o[dt], 0, 0, 0);
+        o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va[dt], pf, o[dt], 0, 0, 0);
       }
-      if constexpr (PREF) {
-#pragma unroll
-        for (int i = 0; i < NKS; ++i) { ka[i] = nka[i]; kb[i] = nkb[i]; }
-#pragma unroll
-        for (int dt = 0; dt < NDT; ++dt) { va[dt] = nva[dt]; vb[dt] = nvb[dt]; }
-      } else {
-        if (blk + AW < b1) load_blk(blk + AW, ka, kb, va, vb);
+    };
+
+    const int first = b0 + wave;
+    bf16x8 ka[NKS], kb[NKS], va[NDT];
+    load_blk(first, ka, kb, va);
+    if constexpr (HD <= 128) {
+      // two register sets ping-pong, the next block's loads issued before the current block computes;
+      // no register copy of an in-flight load (that forces vmcnt(0)) and no load under a branch: a
+      // prefetch past the wave's last block is clamped to it (a cache hit, never used)
+      const int last = first + ((b1 - 1 - first) / AW) * AW;
+      bf16x8 kc2[NKS], kd2[NKS], vb2[NDT];
+      for (int blk = first; blk < b1; blk += 2 * AW) {
+        load_blk(min(blk + AW, last), kc2, kd2, vb2);
+        __builtin_amdgcn_sched_barrier(0);
+        process(blk, ka, kb, va);
+        load_blk(min(blk + 2 * AW, last), ka, kb, va);
+        __builtin_amdgcn_sched_barrier(0);
+        if (blk + AW < b1) process(blk + AW, kc2, kd2, vb2);
+      }
+    } else {  // hd 256: one register set (two would spill)
+      for (int blk = first; blk < b1; blk += AW) {
+        process(blk, ka, kb, va);
+        if (blk + AW < b1) load_blk(blk + AW, ka, kb, va);
       }
     }
   }

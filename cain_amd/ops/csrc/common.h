@@ -37,3 +37,13 @@ __device__ __forceinline__ float gelu_tanh_f(float g) {
 }
 
 static inline int cdiv(int a, int b) { return (a + b - 1) / b; }
+
+// Fragment-major KV cache (attention.hip header): element offset of (position t, head dim d) inside the
+// [T_max * hd] block of one (slot, kv head).
+__device__ __forceinline__ size_t kfrag_off(int t, int d, int hd) {
+  return ((size_t)(t >> 4) * (hd >> 5) + (d >> 5)) * 512 + (size_t)((t & 15) + 16 * ((d & 31) >> 3)) * 8 + (d & 7);
+}
+__device__ __forceinline__ size_t vfrag_off(int t, int d, int hd) {
+  return ((size_t)(t >> 5) * (hd >> 4) + (d >> 4)) * 512 + (size_t)((d & 15) + 16 * ((t & 15) >> 2)) * 8 +
+         4 * ((t >> 4) & 1) + (t & 3);
+}

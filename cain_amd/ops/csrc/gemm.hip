@@ -147,21 +147,25 @@ __device__ __forceinline__ void epi_store(const GemmArgs& a, int gt, int m, int 
           y1[i] = f2bf(v1 * e.c[i] - v2 * e.sn[i]);
           y2[i] = f2bf(v2 * e.c[i] + v1 * e.sn[i]);
         }
-        __bf16* dst;
-        if (head < a.H)
-          dst = reinterpret_cast<__bf16*>(a.Y) + (size_t)m * a.ldy + head * a.hd;
-        else
-          dst = a.kc + (((size_t)sl * a.Hkv + (head - a.H)) * a.T_max + e.p) * a.hd;
-        *reinterpret_cast<bf16x4*>(dst + j0) = y1;
-        *reinterpret_cast<bf16x4*>(dst + j0 + half) = y2;
+        if (head < a.H) {
+          __bf16* dst = reinterpret_cast<__bf16*>(a.Y) + (size_t)m * a.ldy + head * a.hd;
+          *reinterpret_cast<bf16x4*>(dst + j0) = y1;
+          *reinterpret_cast<bf16x4*>(dst + j0 + half) = y2;
+        } else {
+          // fragment-major K cache (attention.hip): 4 consecutive head dims of one position are contiguous
+          __bf16* kb = a.kc + ((size_t)sl * a.Hkv + (head - a.H)) * a.T_max * a.hd;
+          *reinterpret_cast<bf16x4*>(kb + kfrag_off(e.p, j0, a.hd)) = y1;
+          *reinterpret_cast<bf16x4*>(kb + kfrag_off(e.p, j0 + half, a.hd)) = y2;
+        }
       }
     } else if (sl >= 0) {
       const f32x4 v = get(0);
       const int vr = (gt - qt - kt) * 16 + nsub;  // row within the V block
       const int kh = vr / a.hd, d = vr - (vr / a.hd) * a.hd;
-      __bf16* dst = a.vtc + (((size_t)sl * a.Hkv + kh) * a.hd + d) * a.T_max + e.p;
+      // fragment-major V^T cache: head dims d..d+3 of position p sit in consecutive lanes (16 B apart)
+      __bf16* dst = a.vtc + ((size_t)sl * a.Hkv + kh) * a.hd * a.T_max + vfrag_off(e.p, d, a.hd);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) dst[(size_t)i * a.T_max] = f2bf(v[i] + e.b1[i]);
+      for (int i = 0; i < 4; ++i) dst[i * 8] = f2bf(v[i] + e.b1[i]);
     }
   } else {
     const f32x4 v = get(0);
@@ -508,8 +512,10 @@ __device__ __forceinline__ f32x4 ld_wt(const float* p) {
   return v;
 }
 
-template <int NB, int NTW, int W, int CK, int U, int D, int XS, int EPI, bool NORM>
-__global__ __launch_bounds__(W * 64, (W == 8 && NTW == 1 && CK * NB <= 32) ? 4 : 2) void bgemm_kernel(const GemmArgs a, const BgArgs bg) {
+// LB: minimum waves per SIMD the register allocation must allow (4 -> 128 VGPRs, 2 -> 256, 1 -> 512)
+// AR: activation register ring (see the AR branch of the chunk loop)
+template <int NB, int NTW, int W, int CK, int U, int D, int XS, int LB, bool AR, int EPI, bool NORM>
+__global__ __launch_bounds__(W * 64, LB) void bgemm_kernel(const GemmArgs a, const BgArgs bg) {
   constexpr int BG_CK = CK;
   constexpr int FR = BG_CK * NB;        // B fragments per chunk
   constexpr int FPW = FR / W;           // staged per wave per chunk
@@ -670,6 +676,40 @@ __global__ __launch_bounds__(W * 64, (W == 8 && NTW == 1 && CK * NB <= 32) ? 4 :
   static_assert(XS == 2 || NGRP == 1, "three activation stages need one group per chunk");
   if constexpr (NGRP % 2 == 0) {
     for (int c = 0; c < nch; ++c) run_chunk(c, true, wa, wb_, 1, xa_, xb_);
+  } else if constexpr (AR) {
+    // D-deep register rings for BOTH operands.  vmcnt retires loads in issue order, so with only the
+    // weights ring-buffered the per-chunk wait for the next chunk's activations (issued one chunk ahead)
+    // also drained every older weight prefetch and the effective prefetch depth fell back to ~1 chunk:
+    // one HBM round trip per chunk.  Here chunk c issues chunk c+D-1's activations and then its weights,
+    // computes chunk c and waits only for chunk c+1's activations, which are older than every weight
+    // load still in flight; the LDS stage stays double-buffered (XS = 2).
+    static_assert(XS == 2 && NGRP == 1, "activation ring: two LDS stages, one weight group per chunk");
+    bf16x8 ring[D][U][NTW];
+    bf16x8 xring[D][FPW];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int t = 0; t < NTW; ++t) ring[0][u][t] = wa[u][t];
+#pragma unroll
+    for (int j = 1; j < D - 1; ++j) {  // chunks 1 .. D-2, activations before weights (issue = wait order)
+      stage_load(min(j, nch - 1), xring[j]);
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int t = 0; t < NTW; ++t) ring[j][u][t] = load_w(min(s_beg + j * U + u, s_last), t);
+    }
+    for (int c = 0; c < nch; c += D) {
+#pragma unroll
+      for (int j = 0; j < D; ++j) {
+        const int cc = c + j;
+        const bool valid = cc < nch;
+        stage_load(min(cc + D - 1, nch - 1), xring[(j + D - 1) % D]);
+        __builtin_amdgcn_sched_barrier(0);
+        run_group(cc, 0, valid, ring[j], ring[(j + D - 1) % D], D - 1);
+        stage_store((cc + 1) % XS, xring[(j + 1) % D], (valid && cc + 1 < nch) ? 1.f : 0.f);
+        __syncthreads();
+      }
+    }
   } else if constexpr (D == 2) {
     for (int c = 0; c < nch; c += 2) {
       run_chunk(c, true, wa, wb_, 1, xa_, xb_);
@@ -826,6 +866,7 @@ __global__ __launch_bounds__(W * 64, (W == 8 && NTW == 1 && CK * NB <= 32) ? 4 :
 
 struct BgPlan {
   int nb, ntw, w, ck, nblk, ksplit, kspl;
+  int d;  // 128-row bodies: weight register-ring depth (0 = the default ping-pong / 4-deep ring)
   size_t part_floats, ss_floats;
 };
 
@@ -846,6 +887,7 @@ static BgPlan bgemm_plan(int N, int K, int M, int ntw_req) {
   static const int ksmax = env_int("CAIN_BGEMM_KSMAX", 8);
   static const int w_env = env_int("CAIN_BGEMM_W", 0);
   static const int ck_env = env_int("CAIN_BGEMM_CK", 0);
+  static const int d_env = env_int("CAIN_BGEMM_D", 0);
   BgPlan p{};
   p.nb = M <= 32 ? 2 : (M <= 64 ? 4 : 8);
   const int rows1 = 16 * BG_WAVES;
@@ -858,6 +900,7 @@ static BgPlan bgemm_plan(int N, int K, int M, int ntw_req) {
   if (p.nb == 8) {
     // 128 rows: 4-slice chunks keep the double-buffered stage at 64 KiB (2 workgroups per CU)
     p.ck = p.w == 8 && ck_env == 8 ? 8 : 4;
+    if (p.ck == 4 && (d_env == 4 || d_env == 6 || d_env == 8)) p.d = d_env;
   }
   else
   {
@@ -890,29 +933,33 @@ static size_t bgemm_ws_bytes(const BgPlan& p) {
   return BG_COUNTER_BYTES + (p.part_floats + p.ss_floats) * sizeof(float);
 }
 
-template <int NB, int NTW, int W, int CK, int EPI, bool NORM>
+template <int NB, int NTW, int W, int CK, int EPI, bool NORM, int DD>
 static hipError_t bg_launch(const GemmArgs& a, const BgArgs& b, int nblk, hipStream_t st) {
   constexpr int U = 4;  // slices per weight prefetch group
   // register sets of weight prefetch: 4-wave workgroups (narrow outputs, 2 waves per SIMD, 256-VGPR
   // budget) keep 3 groups in flight, the rest ping-pong between 2 (so do the fused-norm 4-wave bodies,
-  // whose 8 staged fragments per wave leave no room for the deeper ring)
-  constexpr int D = (W == 4 && CK == U && !NORM) ? 4 : 2;
+  // whose 8 staged fragments per wave leave no room for the deeper ring).  DD > 0 (128-row bodies): a
+  // DD-deep ring with the register budget of one workgroup per CU (4 waves: 512 VGPRs, 8 waves: 256),
+  // so DD-1 chunks of weights stay in flight per wave across the per-chunk barrier.
+  constexpr int D = DD > 0 ? DD : ((W == 4 && CK == U && !NORM) ? 4 : 2);
   // three activation stages for the 4-wave bodies (one workgroup per CU on the narrow grids anyway)
   constexpr int XS = (W == 4 && CK == U) ? 3 : 2;
-  hipLaunchKernelGGL((bgemm_kernel<NB, NTW, W, CK, U, D, XS, EPI, NORM>), dim3(nblk * b.ksplit), dim3(W * 64), 0, st,
-                     a, b);
+  constexpr int LB = DD > 0 ? (W == 4 ? 1 : 2) : ((W == 8 && NTW == 1 && CK * NB <= 32) ? 4 : 2);
+  constexpr bool AR = DD > 0;  // explicit depth: the activation + weight register rings
+  hipLaunchKernelGGL((bgemm_kernel<NB, NTW, W, CK, U, D, AR ? 2 : XS, LB, AR, EPI, NORM>), dim3(nblk * b.ksplit),
+                     dim3(W * 64), 0, st, a, b);
   return hipGetLastError();
 }
 
-template <int NB, int NTW, int W, int CK, bool NORM>
+template <int NB, int NTW, int W, int CK, bool NORM, int DD = 0>
 static hipError_t bg_launch_e(int epi, const GemmArgs& a, const BgArgs& b, int nblk, hipStream_t st) {
   switch (epi) {
-    case EPI_BF16: return bg_launch<NB, NTW, W, CK, EPI_BF16, NORM>(a, b, nblk, st);
-    case EPI_RESID: return bg_launch<NB, NTW, W, CK, EPI_RESID, NORM>(a, b, nblk, st);
-    case EPI_F32: return bg_launch<NB, NTW, W, CK, EPI_F32, NORM>(a, b, nblk, st);
-    case EPI_SILU: return bg_launch<NB, NTW, W, CK, EPI_SILU, NORM>(a, b, nblk, st);
-    case EPI_GELU: return bg_launch<NB, NTW, W, CK, EPI_GELU, NORM>(a, b, nblk, st);
-    case EPI_QKV_ROPE: return bg_launch<NB, NTW, W, CK, EPI_QKV_ROPE, NORM>(a, b, nblk, st);
+    case EPI_BF16: return bg_launch<NB, NTW, W, CK, EPI_BF16, NORM, DD>(a, b, nblk, st);
+    case EPI_RESID: return bg_launch<NB, NTW, W, CK, EPI_RESID, NORM, DD>(a, b, nblk, st);
+    case EPI_F32: return bg_launch<NB, NTW, W, CK, EPI_F32, NORM, DD>(a, b, nblk, st);
+    case EPI_SILU: return bg_launch<NB, NTW, W, CK, EPI_SILU, NORM, DD>(a, b, nblk, st);
+    case EPI_GELU: return bg_launch<NB, NTW, W, CK, EPI_GELU, NORM, DD>(a, b, nblk, st);
+    case EPI_QKV_ROPE: return bg_launch<NB, NTW, W, CK, EPI_QKV_ROPE, NORM, DD>(a, b, nblk, st);
     default: return hipErrorInvalidValue;
   }
 }
@@ -920,6 +967,13 @@ static hipError_t bg_launch_e(int epi, const GemmArgs& a, const BgArgs& b, int n
 template <int NB, bool NORM>
 static hipError_t bg_launch_shape(int epi, const BgPlan& p, const GemmArgs& a, const BgArgs& b, hipStream_t st) {
   if constexpr (NB == 8) {
+    // register rings (activations + weights) of depth p.d; the 8-wave bodies (256-VGPR budget) only at 4
+    if (p.d == 8 && p.w == 4) return bg_launch_e<8, 1, 4, 4, NORM, 8>(epi, a, b, p.nblk, st);
+    if (p.d == 6 && p.w == 4) return bg_launch_e<8, 1, 4, 4, NORM, 6>(epi, a, b, p.nblk, st);
+    if (p.d >= 4) {
+      if (p.w == 4) return bg_launch_e<8, 1, 4, 4, NORM, 4>(epi, a, b, p.nblk, st);
+      return bg_launch_e<8, 1, 8, 4, NORM, 4>(epi, a, b, p.nblk, st);
+    }
     if (p.w == 4) return bg_launch_e<8, 1, 4, 4, NORM>(epi, a, b, p.nblk, st);
     if (p.ck == 8) return bg_launch_e<8, 1, 8, 8, NORM>(epi, a, b, p.nblk, st);
     return bg_launch_e<8, 1, 8, 4, NORM>(epi, a, b, p.nblk, st);

@@ -19,6 +19,10 @@ are decoded together as one batch (up to the engine's ``max_batch``) — trial
 batching on the server side.  One worker thread per model owns
 the GPU work; HTTP handler threads only enqueue and stream results back.
 
+Tracing: started with ``--trace-dir DIR``, the engine backend records every decode batch
+with ``torch.profiler`` (host ops + GPU kernels) and writes a Chrome trace to DIR; the response JSON
+names it in ``cain_trace`` so the client can file it with its run (the study moves it into run_dir).
+
 Length policy: random weights rarely emit EOS, so when a request does not set
 ``options.num_predict`` the server derives it from the prompt: "In N words ..."
 (the study's prompt template, experiment/RunnerConfig.py:120) maps to
@@ -65,6 +69,7 @@ class Job:
     result: Any = None
     error: Optional[BaseException] = None
     t_submit: float = field(default_factory=time.perf_counter)
+    trace_file: Optional[str] = None  # Chrome trace of the batch that decoded this job (--trace-dir)
 
 
 class Backend:
@@ -87,8 +92,11 @@ class EngineBackend(Backend):
     """Backed by one DecodeEngine per model on ``device`` (created on first use, then resident)."""
 
     def __init__(self, models: List[str], device: str = "cuda:0", max_batch: int = 16, max_context: int = 2048,
-                 backend: Optional[str] = None, seed: int = 0, preload: bool = False, steps_per_graph: int = 8):
+                 backend: Optional[str] = None, seed: int = 0, preload: bool = False, steps_per_graph: int = 8,
+                 trace_dir: Optional[str] = None):
         self._models = list(models)
+        self.trace_dir = trace_dir
+        self._trace_seq = 0
         self.device = device
         self._max_batch = max_batch
         self.max_context = max_context
@@ -139,12 +147,41 @@ class EngineBackend(Backend):
                 if j.stream is not None and ids:
                     j.stream("".join(tok.piece(t) for t in ids))
 
-        res = eng.generate([j.prompt for j in jobs], [j.num_predict for j in jobs], [j.options for j in jobs],
-                           on_tokens=on_tokens if any(streams) else None)
+        def gen():
+            return eng.generate([j.prompt for j in jobs], [j.num_predict for j in jobs], [j.options for j in jobs],
+                                on_tokens=on_tokens if any(streams) else None)
+
+        if self.trace_dir:
+            res, path = self._traced(model, gen)
+            for j in jobs:
+                j.trace_file = path
+        else:
+            res = gen()
         ttft = getattr(eng, "last_ttft_ns", 0)
         for j, r in zip(jobs, res):
             j.result = r
             j.ttft_ns = ttft
+
+
+    def _traced(self, model: str, fn):
+        """Run ``fn`` under torch.profiler (CPU + GPU activity) and export a Chrome trace."""
+        import os
+        from pathlib import Path
+
+        import torch
+        from torch.profiler import ProfilerActivity, profile
+
+        acts = [ProfilerActivity.CPU]
+        if torch.cuda.is_available():
+            acts.append(ProfilerActivity.CUDA)
+        with profile(activities=acts) as prof:
+            res = fn()
+        self._trace_seq += 1
+        out = Path(self.trace_dir)
+        out.mkdir(parents=True, exist_ok=True)
+        path = out / f"trace_{os.getpid()}_{self._trace_seq:05d}_{model.replace(':', '_').replace('/', '_')}.json"
+        prof.export_chrome_trace(str(path))
+        return res, str(path)
 
 
 class FakeBackend(Backend):
@@ -244,6 +281,8 @@ def _result_json(job: Job, created: Optional[str] = None) -> Dict[str, Any]:
     r = job.result
     d = r.ollama_json(created or _now())
     d["cain_ttft_ns"] = int(getattr(job, "ttft_ns", 0))
+    if job.trace_file:
+        d["cain_trace"] = job.trace_file
     return d
 
 
@@ -426,6 +465,7 @@ def main(argv: Optional[List[str]] = None) -> None:
     ap.add_argument("--preload", action="store_true", help="load every model at startup (all stay resident)")
     ap.add_argument("--fake-tok-s", type=float, default=2000.0, help="fake backend: modelled decode rate")
     ap.add_argument("--fake-prefill-s", type=float, default=0.0, help="fake backend: modelled time to first token")
+    ap.add_argument("--trace-dir", default=None, help="write a torch.profiler Chrome trace of every decode batch here")
     ap.add_argument("-v", "--verbose", action="store_true")
     ns = ap.parse_args(argv)
     models = [m for m in ns.models.split(",") if m]
@@ -436,7 +476,7 @@ def main(argv: Optional[List[str]] = None) -> None:
         be: Backend = FakeBackend(models, tokens_per_s=ns.fake_tok_s, prefill_s=ns.fake_prefill_s)
     else:
         be = EngineBackend(models, device=ns.device, max_batch=ns.max_batch, max_context=ns.max_context,
-                           backend=ns.backend, preload=ns.preload)
+                           backend=ns.backend, preload=ns.preload, trace_dir=ns.trace_dir)
     srv = make_server(be, ns.host, ns.port, ns.batch_window_ms, ns.verbose)
     print(f"[serve] Ollama-compatible API on http://{ns.host}:{srv.server_address[1]} models={models}", flush=True)
     try:

@@ -181,6 +181,7 @@ def test_fused_qkv_rope_kv_append(H, Hkv, hd, M, norm):
     if norm:
         xr = xr * torch.rsqrt(xr.pow(2).mean(-1, keepdim=True) + 1e-6) * g.float()
     ref = (xr @ W.float().t() + bias).bfloat16().float()
+    kn, vn = ops.unpack_kcache(kc), ops.unpack_vcache(vt)  # fragment-major caches -> [S, Hkv, T, hd]
     for m in range(M):
         p, sl = int(pos[m]), int(slot[m])
         c, s_ = cos_t[p], sin_t[p]
@@ -188,8 +189,10 @@ def test_fused_qkv_rope_kv_append(H, Hkv, hd, M, norm):
         kh = ref[m, H * hd:(H + Hkv) * hd].view(Hkv, hd)
         vh = ref[m, (H + Hkv) * hd:].view(Hkv, hd)
         assert rel_err(q[m].view(H, hd), _rot(qh, c, s_)) < 1e-2
-        assert rel_err(kc[sl, :, p], _rot(kh, c, s_)) < 1e-2
-        assert rel_err(vt[sl, :, :, p], vh) < 1e-2
+        assert rel_err(kn[sl, :, p], _rot(kh, c, s_)) < 1e-2
+        assert rel_err(vn[sl, :, p], vh) < 1e-2
+    # nothing but the M appended positions was written
+    assert int((kn != 0).any(-1).sum()) == M * Hkv and int((vn != 0).any(-1).sum()) == M * Hkv
 
 
 def _attn_ref(q, K, V, L, G):
@@ -215,8 +218,9 @@ def test_attention_split_combine(H, Hkv, hd, lengths):
     slot = torch.arange(M, device=DEV, dtype=torch.int32)
     pos = torch.tensor([L - 1 for L in lengths], device=DEV, dtype=torch.int32)
     counters = torch.zeros(M * Hkv, device=DEV, dtype=torch.int32)
+    kp, vp = ops.pack_kcache(kc), ops.pack_vcache(vt.transpose(-1, -2))  # the kernel's cache layouts
     for nsplit in (1, 3, 16, 64, 16):  # repeated nsplit: the in-kernel counters must reset
-        out = ops.attention(q, kc, vt, slot, pos, H, Hkv, hd, nsplit, 1.0 / math.sqrt(hd), counters=counters)
+        out = ops.attention(q, kp, vp, slot, pos, H, Hkv, hd, nsplit, 1.0 / math.sqrt(hd), counters=counters)
         for m, L in enumerate(lengths):
             ref = _attn_ref(q[m].view(H, hd), kc[m].float(), vt[m].float().transpose(-1, -2), L, H // Hkv)
             assert rel_err(out[m].view(H, hd), ref) < 2e-2, (nsplit, m, L)

@@ -73,3 +73,16 @@ def test_engine_backend_torch_cpu_end_to_end():
         assert r2.text == r.text  # greedy is deterministic
         st = c.generate("tiny-qwen2:1.5b", "hello", stream=True, options={"num_predict": 5})
         assert st.eval_count == 5
+
+
+def test_engine_backend_trace_dir_writes_chrome_trace(tmp_path):
+    """--trace-dir: each decode batch is profiled and the response names its trace."""
+    import json
+
+    be = EngineBackend(["tiny-qwen2:1.5b"], device="cpu", max_batch=2, trace_dir=str(tmp_path / "traces"))
+    with ServerThread(be) as s:
+        r = OllamaClient(s.url).generate("tiny-qwen2:1.5b", "hello", options={"num_predict": 3})
+    path = r.stats()["trace_file"]
+    assert path.startswith(str(tmp_path)) and r.eval_count == 3
+    events = json.load(open(path))["traceEvents"]
+    assert any("aten::" in e.get("name", "") for e in events)

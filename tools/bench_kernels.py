@@ -44,6 +44,11 @@ def main():
     ap.add_argument("--gemm-only", action="store_true")
     ap.add_argument("--norm", action="store_true", help="fused RMSNorm on qkv/gateup/lm_head (as in the model)")
     ap.add_argument("--roles", default="qkv,o,gateup,down,lm_head")
+    ap.add_argument("--attn-only", action="store_true")
+    ap.add_argument("--attn", default="1:128,1:1400,16:700,64:1400,128:700,128:1400",
+                    help="attention cases M:L (rows : context length)")
+    ap.add_argument("--attn-splits", default="auto", help="comma list of split counts ('auto' = the engine's)")
+    ap.add_argument("--attn-tmax", type=int, default=1536)
     ns = ap.parse_args()
     cfg = get_config(ns.model)
     dev = torch.device("cuda")
@@ -65,7 +70,10 @@ def main():
     roles = {r: v for r, v in roles.items() if r in ns.roles.split(",")}
     W = {r: W[r] for r in roles}
     res = []
-    for M in [int(x) for x in ns.rows.split(",")]:
+    if ns.attn_only:
+        ns.rows = ""
+        ns.gemm_only = False
+    for M in [int(x) for x in ns.rows.split(",") if x]:
         for role, (n, k, epi) in roles.items():
             x = torch.randn(M, k, device=dev).bfloat16()
             out = torch.zeros(M, n // 2 if epi == ops.EPI_SILU else n, device=dev,
@@ -90,27 +98,33 @@ def main():
                 print(json.dumps(r), flush=True)
     if ns.gemm_only:
         return
-    # attention
-    T_max = 2048
-    for M, L in [(1, 128), (1, 1400), (16, 700), (64, 1400)]:
+    # attention (random bytes in the fragment-major cache layout: timing only)
+    T_max = ns.attn_tmax
+    from cain_amd.engine.engine import attention_splits
+    for case in ns.attn.split(","):
+        M, L = (int(x) for x in case.split(":"))
         kc = torch.randn(M, cfg.n_kv_heads, T_max, cfg.head_dim, device=dev).bfloat16()
         vt = torch.randn(M, cfg.n_kv_heads, cfg.head_dim, T_max, device=dev).bfloat16()
         q = torch.randn(M, cfg.q_dim, device=dev).bfloat16()
         slot = torch.arange(M, device=dev, dtype=torch.int32)
         pos = torch.full((M,), L - 1, device=dev, dtype=torch.int32)
         cnt = torch.zeros(M * cfg.n_kv_heads, device=dev, dtype=torch.int32)
-        from cain_amd.engine.engine import attention_splits
-        ns_ = attention_splits(M, cfg.n_kv_heads, T_max)
-        po = torch.empty(M * cfg.n_heads * ns_ * cfg.head_dim, device=dev)
-        pm = torch.empty(ops.attention_ml_floats(M, cfg.n_heads, cfg.n_kv_heads, ns_), device=dev)
         out = torch.empty(M, cfg.q_dim, device=dev).bfloat16()
-        us = timeit(lambda: ops.attention(q, kc, vt, slot, pos, cfg.n_heads, cfg.n_kv_heads, cfg.head_dim, ns_,
-                                          1 / math.sqrt(cfg.head_dim), out=out, part_o=po, part_ml=pm, counters=cnt))
-        kv_bytes = 2 * M * cfg.n_kv_heads * L * cfg.head_dim * 2
-        r = dict(kind="attention", model=cfg.name, M=M, L=L, nsplit=ns_, us=round(us, 2),
-                 TBps=round(kv_bytes / us / 1e6, 3))
-        res.append(r)
-        print(json.dumps(r), flush=True)
+        for sp in ns.attn_splits.split(","):
+            ns_ = attention_splits(M, cfg.n_kv_heads, T_max) if sp == "auto" else int(sp)
+            po = torch.empty(M * cfg.n_heads * ns_ * cfg.head_dim, device=dev)
+            pm = torch.empty(ops.attention_ml_floats(M, cfg.n_heads, cfg.n_kv_heads, ns_), device=dev)
+            us = timeit(lambda: ops.attention(q, kc, vt, slot, pos, cfg.n_heads, cfg.n_kv_heads, cfg.head_dim, ns_,
+                                              1 / math.sqrt(cfg.head_dim), out=out, part_o=po, part_ml=pm,
+                                              counters=cnt))
+            kv_bytes = 2 * M * cfg.n_kv_heads * L * cfg.head_dim * 2
+            r = dict(kind="attention", model=cfg.name, M=M, L=L, T_max=T_max, nsplit=ns_, split_arg=sp,
+                     us=round(us, 2), TBps=round(kv_bytes / us / 1e6, 3))
+            res.append(r)
+            print(json.dumps(r), flush=True)
+        del kc, vt
+    if ns.attn_only:
+        return
     # sampler
     for M in (1, 16, 64):
         lg = torch.randn(M, V, device=dev)
