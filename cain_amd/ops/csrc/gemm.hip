@@ -630,21 +630,29 @@ __global__ __launch_bounds__(W * 64, LB) void bgemm_kernel(const GemmArgs a, con
       for (int t = 0; t < NTW; ++t) nxt[u][t] = load_w(min(sn + u, s_last), t);
     __builtin_amdgcn_sched_barrier(0);  // issue the prefetch before this group's MFMAs, not after
     const uint32_t keep = valid ? 0xffffffffu : 0u;
+    // LDS fragments double-buffered across slices: slice u+1's NB ds_reads are issued before slice u's
+    // MFMAs, so every MFMA finds its operand landed.  Left to itself the scheduler minimised registers
+    // and paired each MFMA with its own ds_read (2 reads in flight, an LDS round trip exposed every
+    // second MFMA at one wave per SIMD).
+    bf16x8 xf[2][NB];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) xf[0][b] = xs[buf][(h * U) * NB + b][lane];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      bf16x8 xb[NB];
+      if (u + 1 < U) {
 #pragma unroll
-      for (int b = 0; b < NB; ++b) xb[b] = xs[buf][(h * U + u) * NB + b][lane];
+        for (int b = 0; b < NB; ++b) xf[(u + 1) & 1][b] = xs[buf][(h * U + u + 1) * NB + b][lane];
+      }
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int t = 0; t < NTW; ++t) {
         typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
         const bf16x8 w = __builtin_bit_cast(bf16x8, __builtin_bit_cast(u32x4, cur[u][t]) & keep);
 #pragma unroll
-        for (int b = 0; b < NB; ++b) acc[t][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w, xb[b], acc[t][b], 0, 0, 0);
+        for (int b = 0; b < NB; ++b)
+          acc[t][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w, xf[u & 1][b], acc[t][b], 0, 0, 0);
       }
-      // keep the scheduler from hoisting the next slices' LDS fragments above these MFMAs: with
-      // NB = 8 that would hold 4 x 8 fragments live and spill under the 128-VGPR budget
-      if constexpr (NB >= 8) __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_sched_barrier(0);
     }
   };
   // xa_/xb_: activation staging registers.  XS = 2: chunk c loads chunk c+1 into xa_ and stores it at
@@ -944,7 +952,8 @@ static hipError_t bg_launch(const GemmArgs& a, const BgArgs& b, int nblk, hipStr
   constexpr int D = DD > 0 ? DD : ((W == 4 && CK == U && !NORM) ? 4 : 2);
   // three activation stages for the 4-wave bodies (one workgroup per CU on the narrow grids anyway)
   constexpr int XS = (W == 4 && CK == U) ? 3 : 2;
-  constexpr int LB = DD > 0 ? (W == 4 ? 1 : 2) : ((W == 8 && NTW == 1 && CK * NB <= 32) ? 4 : 2);
+  // (the 128-row 8-wave body needs 256 VGPRs for its double-buffered LDS fragments: 1 workgroup per CU)
+  constexpr int LB = DD > 0 ? (W == 4 ? 1 : 2) : ((W == 8 && NTW == 1 && NB < 8 && CK * NB <= 32) ? 4 : 2);
   constexpr bool AR = DD > 0;  // explicit depth: the activation + weight register rings
   hipLaunchKernelGGL((bgemm_kernel<NB, NTW, W, CK, U, D, AR ? 2 : XS, LB, AR, EPI, NORM>), dim3(nblk * b.ksplit),
                      dim3(W * 64), 0, st, a, b);
