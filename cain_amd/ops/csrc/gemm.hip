@@ -545,7 +545,7 @@ __global__ __launch_bounds__(W * 64, LB) void bgemm_kernel(const GemmArgs a, con
   // XS activation stages: chunk c is read from xs[c % XS]; with XS = 3 the loads of chunk c+2 are in
   // flight while c computes (two chunk-times to land instead of one)
   __shared__ __attribute__((aligned(16))) bf16x8 xs[XS][FR][64];
-  __shared__ float ss_red[NORM ? W : 1][NORM ? NB * 16 : 1];
+  __shared__ float s_ss[NORM ? NB * 16 : 1];  // NORM: per-row sum of squares of this k-range
   __shared__ float s_inv[NB * 16];
   __shared__ unsigned s_ticket;
 
@@ -558,17 +558,37 @@ __global__ __launch_bounds__(W * 64, LB) void bgemm_kernel(const GemmArgs a, con
   }
   auto load_w = [&](int s, int t) -> bf16x8 { return __builtin_nontemporal_load(wb[t] + (size_t)s * 64); };
 
-  // staging: fragment f = wave + W*i of a chunk is (slice f / NB, row block f % NB); lane reads
-  // X[16*rb + (lane & 15)][32*slice + 8*(lane >> 4) .. +8]  (rows past M re-read row M-1)
+  // Activation staging in FULL 128-B lines: a chunk is rows [0, 16*NB) x CK slices = PPR 16-byte pieces per
+  // row; wave instruction i of wave w covers rows RPI*(w + W*i) .. +RPI, lane l -> row RPI*(w + W*i) + l / PPR,
+  // piece l % PPR (rows past M re-read row M-1).  A fragment-shaped load (16 rows x 64 B per instruction)
+  // touches twice the cache lines per byte and made the vector-memory path, not HBM, the limit
+  // (cdna_hip_programming.md §5, 'Projection GEMM at M = 256').  In LDS a row keeps its pieces in order
+  // up to an XOR swizzle, piece p at p ^ (row & 15): the 8-lane groups of ds_write_b128 and the 16-lane
+  // groups of the fragment reads (lane = row & 15 + 16 * k-group) are both bank-conflict free.
+  constexpr int PPR = 4 * BG_CK;   // 16-byte pieces per row and chunk
+  constexpr int RPI = 64 / PPR;    // rows per wave instruction
+  constexpr int STAGE = FR * 1024;
+  static_assert(BG_CK >= 4 && 16 * NB == RPI * FR, "full-line staging tiling");
+  char* const xsb = reinterpret_cast<char*>(&xs[0][0][0]);
   const __bf16* xrow[FPW];
-  float ssq[FPW];  // NORM: partial sum of x^2 of the row of staged fragment i (its k-groups)
+  int xoff[FPW];   // LDS byte offset of this lane's piece inside a stage
+  float ssq[FPW];  // NORM: this lane's partial sum of x^2 of its row (its pieces)
 #pragma unroll
   for (int i = 0; i < FPW; ++i) {
-    const int f = wave + W * i, rb = f % NB, sl = f / NB;
-    const int m = min(rb * 16 + (lane & 15), a.M - 1);
-    xrow[i] = a.X + (size_t)m * a.ldx + sl * 32 + ((lane >> 4) << 3);
+    const int r = RPI * (wave + W * i) + lane / PPR, pc = lane % PPR;
+    xrow[i] = a.X + (size_t)min(r, a.M - 1) * a.ldx + pc * 8;
+    xoff[i] = r * (PPR * 16) + ((pc ^ (r & 15)) << 4);
     ssq[i] = 0.f;
   }
+  // fragment of slice sl (0..CK-1) and row block b: lane (m = lane & 15, k-group g = lane >> 4) reads piece
+  // 4*sl + g of row 16b + m at (4*sl + g) ^ m = 4*((sl & ~3) | ((sl & 3) ^ (m >> 2))) + (g ^ (m & 3))
+  int fo[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    fo[j] = (lane & 15) * (PPR * 16) + ((((j ^ ((lane & 15) >> 2)) << 2) | ((lane >> 4) ^ (lane & 3))) << 4);
+  auto frag = [&](int buf, int sl, int b) -> bf16x8 {
+    return *reinterpret_cast<const bf16x8*>(xsb + buf * STAGE + b * 16 * (PPR * 16) + (sl & ~3) * 64 + fo[sl & 3]);
+  };
   auto stage_load = [&](int c, bf16x8 (&xr)[FPW]) {
     const int k0 = (s_beg + c * BG_CK) * 32;
 #pragma unroll
@@ -586,7 +606,7 @@ __global__ __launch_bounds__(W * 64, LB) void bgemm_kernel(const GemmArgs a, con
         }
         ssq[i] += wgt * q;
       }
-      xs[buf][wave + W * i][lane] = xr[i];
+      *reinterpret_cast<bf16x8*>(xsb + buf * STAGE + xoff[i]) = xr[i];
     }
   };
 
@@ -602,6 +622,9 @@ __global__ __launch_bounds__(W * 64, LB) void bgemm_kernel(const GemmArgs a, con
   for (int u = 0; u < U; ++u)
 #pragma unroll
     for (int t = 0; t < NTW; ++t) wa[u][t] = load_w(s_beg + u, t);
+  if constexpr (NORM) {
+    if (threadIdx.x < NB * 16) s_ss[threadIdx.x] = 0.f;  // ordered before the epilogue atomics by the barrier below
+  }
   {
     bf16x8 xr[FPW];
     stage_load(0, xr);
@@ -636,12 +659,12 @@ __global__ __launch_bounds__(W * 64, LB) void bgemm_kernel(const GemmArgs a, con
     // second MFMA at one wave per SIMD).
     bf16x8 xf[2][NB];
 #pragma unroll
-    for (int b = 0; b < NB; ++b) xf[0][b] = xs[buf][(h * U) * NB + b][lane];
+    for (int b = 0; b < NB; ++b) xf[0][b] = frag(buf, h * U, b);
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       if (u + 1 < U) {
 #pragma unroll
-        for (int b = 0; b < NB; ++b) xf[(u + 1) & 1][b] = xs[buf][(h * U + u + 1) * NB + b][lane];
+        for (int b = 0; b < NB; ++b) xf[(u + 1) & 1][b] = frag(buf, h * U + u + 1, b);
       }
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -748,24 +771,14 @@ __global__ __launch_bounds__(W * 64, LB) void bgemm_kernel(const GemmArgs a, con
     }
   }
 
-  // ---- per-row sum of squares of this workgroup's k-range (NORM)
+  // ---- per-row sum of squares of this workgroup's k-range (NORM): the PPR lanes of a row, then LDS atomics
   if constexpr (NORM) {
-    float v[NB];
-#pragma unroll
-    for (int b = 0; b < NB; ++b) v[b] = 0.f;
 #pragma unroll
     for (int i = 0; i < FPW; ++i) {
-      const int rb = (wave + W * i) % NB;
+      float x = ssq[i];
 #pragma unroll
-      for (int b = 0; b < NB; ++b)
-        if (b == rb) v[b] += ssq[i];
-    }
-#pragma unroll
-    for (int b = 0; b < NB; ++b) {
-      float x = v[b];
-      x += __shfl_xor(x, 16, 64);
-      x += __shfl_xor(x, 32, 64);
-      if (lane < 16) ss_red[wave][b * 16 + lane] = x;
+      for (int o = 1; o < PPR; o <<= 1) x += __shfl_xor(x, o, 64);
+      if (lane % PPR == 0) atomicAdd(&s_ss[RPI * (wave + W * i) + lane / PPR], x);
     }
   }
   // the staging buffer becomes the epilogue buffer: red[unit][lane], unit = (wave*NTW + t)*NB + b
@@ -777,12 +790,7 @@ __global__ __launch_bounds__(W * 64, LB) void bgemm_kernel(const GemmArgs a, con
       for (int b = 0; b < NB; ++b) red[((wave * NTW + t) * NB + b) * 64 + lane] = acc[t][b];
     __syncthreads();
     if constexpr (NORM) {
-      if (threadIdx.x < NB * 16) {
-        float x = 0.f;
-#pragma unroll
-        for (int w = 0; w < W; ++w) x += ss_red[w][threadIdx.x];
-        s_inv[threadIdx.x] = rsqrtf(x / float(a.K) + a.eps);
-      }
+      if (threadIdx.x < NB * 16) s_inv[threadIdx.x] = rsqrtf(s_ss[threadIdx.x] / float(a.K) + a.eps);
       __syncthreads();
     }
   } else {
@@ -793,14 +801,10 @@ __global__ __launch_bounds__(W * 64, LB) void bgemm_kernel(const GemmArgs a, con
 #pragma unroll
       for (int b = 0; b < NB; ++b) st_wt(mine + ((size_t)((wave * NTW + t) * NB + b) * 64 + lane) * 4, acc[t][b]);
     if constexpr (NORM) {
-      __syncthreads();  // ss_red complete
-      if (threadIdx.x < NB * 16) {
-        float x = 0.f;
-#pragma unroll
-        for (int w = 0; w < W; ++w) x += ss_red[w][threadIdx.x];
-        __hip_atomic_store(bg.part_ss + (pb + kc) * (NB * 16) + threadIdx.x, x, __ATOMIC_RELAXED,
+      __syncthreads();  // s_ss complete
+      if (threadIdx.x < NB * 16)
+        __hip_atomic_store(bg.part_ss + (pb + kc) * (NB * 16) + threadIdx.x, s_ss[threadIdx.x], __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
-      }
     }
     // every storing wave drains, one lane takes a ticket; the last arriver of the row block reduces
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
