@@ -501,15 +501,20 @@ struct BgArgs {
   unsigned* counters;  // [nblk], zero between launches (the reducer resets its own)
 };
 
-__device__ __forceinline__ void st_wt(float* p, const f32x4& v) {
-#pragma unroll
-  for (int i = 0; i < 4; ++i) __hip_atomic_store(p + i, v[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+// Split-K partial slabs: 16-byte write-through (sc1) buffer stores, read back by the last arriver with
+// 16-byte sc1 buffer loads (L2-served, never a stale L1 line): the hand-off needs no release/acquire fence
+// (cdna_hip_programming.md Guideline 16 R1; MI355X_MICROARCH.md 'Valid forms', first row).  Dword atomics did
+// the same job with four instructions per 16 B.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t slab_rsrc(const float* p) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), 0, 0x7fffffff, 0x00020000);
 }
-__device__ __forceinline__ f32x4 ld_wt(const float* p) {
-  f32x4 v;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) v[i] = __hip_atomic_load(p + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  return v;
+__device__ __forceinline__ void st_wt(__amdgpu_buffer_rsrc_t r, int byte_off, const f32x4& v) {
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, byte_off, 0, 16 /* sc1 */);
+}
+__device__ __forceinline__ f32x4 ld_wt(__amdgpu_buffer_rsrc_t r, int byte_off) {
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 16 /* sc1 */));
 }
 
 // LB: minimum waves per SIMD the register allocation must allow (4 -> 128 VGPRs, 2 -> 256, 1 -> 512)
@@ -795,11 +800,11 @@ __global__ __launch_bounds__(W * 64, LB) void bgemm_kernel(const GemmArgs a, con
     }
   } else {
     const size_t pb = (size_t)blk * bg.ksplit;
-    float* mine = bg.part + (pb + kc) * (size_t)UNITS * 256;
+    const __amdgpu_buffer_rsrc_t mine_r = slab_rsrc(bg.part + (pb + kc) * (size_t)UNITS * 256);
 #pragma unroll
     for (int t = 0; t < NTW; ++t)
 #pragma unroll
-      for (int b = 0; b < NB; ++b) st_wt(mine + ((size_t)((wave * NTW + t) * NB + b) * 64 + lane) * 4, acc[t][b]);
+      for (int b = 0; b < NB; ++b) st_wt(mine_r, (((wave * NTW + t) * NB + b) * 64 + lane) * 16, acc[t][b]);
     if constexpr (NORM) {
       __syncthreads();  // s_ss complete
       if (threadIdx.x < NB * 16)
@@ -816,30 +821,32 @@ __global__ __launch_bounds__(W * 64, LB) void bgemm_kernel(const GemmArgs a, con
     // sum the k-range partials, RB ranges x NTW*NB units of loads in flight per round trip (RB x NTW*NB
     // f32x4 registers: 2 ranges at 8 units keeps the 128-row variants inside 128 VGPRs)
     constexpr int RB = NTW * NB >= 8 ? 2 : 4;
-    const float* base = bg.part + pb * (size_t)UNITS * 256;
+    const __amdgpu_buffer_rsrc_t base_r = slab_rsrc(bg.part + pb * (size_t)UNITS * 256);
     f32x4 sum[NTW][NB];
 #pragma unroll
     for (int t = 0; t < NTW; ++t)
 #pragma unroll
       for (int b = 0; b < NB; ++b) sum[t][b] = f32x4{0.f, 0.f, 0.f, 0.f};
     for (int k0 = 0; k0 < bg.ksplit; k0 += RB) {
+      // every load issued unconditionally (a clamped range index; the surplus weighted 0): a select between a
+      // load and a constant made hipcc branch around each load and wait for it alone
       f32x4 l[RB][NTW][NB];
 #pragma unroll
       for (int j = 0; j < RB; ++j)
 #pragma unroll
         for (int t = 0; t < NTW; ++t)
 #pragma unroll
-          for (int b = 0; b < NB; ++b) {
-            const size_t off = ((size_t)((wave * NTW + t) * NB + b) * 64 + lane) * 4;
-            l[j][t][b] = (k0 + j < bg.ksplit) ? ld_wt(base + (size_t)(k0 + j) * UNITS * 256 + off)
-                                              : f32x4{0.f, 0.f, 0.f, 0.f};
-          }
+          for (int b = 0; b < NB; ++b)
+            l[j][t][b] = ld_wt(base_r, min(k0 + j, bg.ksplit - 1) * (UNITS * 1024) +
+                                           (((wave * NTW + t) * NB + b) * 64 + lane) * 16);
 #pragma unroll
-      for (int j = 0; j < RB; ++j)
+      for (int j = 0; j < RB; ++j) {
+        const float wj = (k0 + j < bg.ksplit) ? 1.f : 0.f;
 #pragma unroll
         for (int t = 0; t < NTW; ++t)
 #pragma unroll
-          for (int b = 0; b < NB; ++b) sum[t][b] += l[j][t][b];
+          for (int b = 0; b < NB; ++b) sum[t][b] += wj * l[j][t][b];
+      }
     }
 #pragma unroll
     for (int t = 0; t < NTW; ++t)
