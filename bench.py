@@ -17,7 +17,7 @@ generated token from the amd-smi counters (``J_per_token``; idle-subtracted
 variant too).  Baseline: the reference's llama3.1:8b on-device 1000-word cell,
 est. 19.2 tok/s and 0.574 J/token on a MacBook Pro M2.
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--model M] [--words W] [--batch B]
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--model M] [--words W] [--batch B (default 256)]
        (multi-GPU: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...)
 """
 from __future__ import annotations
@@ -58,7 +58,7 @@ def main() -> int:
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--model", default="llama3.1:8b")
     ap.add_argument("--words", type=int, default=1000)
-    ap.add_argument("--batch", type=int, default=128, help="concurrent trials per GPU (trial batching, <= 128)")
+    ap.add_argument("--batch", type=int, default=256, help="concurrent trials per GPU (trial batching, <= 256)")
     ap.add_argument("--context", type=int, default=1536)
     ap.add_argument("--steps-per-graph", type=int, default=16)
     ap.add_argument("--no-energy", action="store_true")

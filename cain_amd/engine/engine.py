@@ -15,7 +15,7 @@ Backends
            device, one host sync per generation.
 ``torch``  torch-eager oracle (``models/reference.py``): CPU tests / debugging.
 
-Batching: up to ``max_batch`` (≤ 128) sequences decode together ("trial
+Batching: up to ``max_batch`` (≤ 256) sequences decode together ("trial
 batching") — each row has its own cache slot, position, budget
 and sampling options; rows that finish early idle until the batch ends.
 Prefill: every prompt token but the last goes through the same forward as
@@ -42,7 +42,8 @@ from ..models.weights import ModelWeights, pack_for_engine, random_weights
 #: Ollama's default sampling options (SURVEY §2.4 "Sampling" row)
 OLLAMA_DEFAULTS = dict(temperature=0.8, top_k=40, top_p=0.9, repeat_penalty=1.1, repeat_last_n=64, seed=None)
 
-MAX_ROWS = 128  # rows per forward: decode batch / prefill chunk (runtime.hip CAIN_MAX_ROWS)
+MAX_ROWS = 256  # rows per forward: decode batch (runtime.hip CAIN_MAX_ROWS)
+PREFILL_ROWS = 128  # prompt tokens per prefill forward
 
 
 @dataclass
@@ -188,7 +189,7 @@ class DecodeEngine:
         ang = np.arange(T, dtype=np.float64)[:, None] * inv[None, :]
         self.cos_t = torch.tensor(np.cos(ang), dtype=torch.float32, device=dev).contiguous()
         self.sin_t = torch.tensor(np.sin(ang), dtype=torch.float32, device=dev).contiguous()
-        R = MAX_ROWS
+        R = max(self.max_batch, PREFILL_ROWS)  # rows any forward of this engine can have
         z = lambda *s, dt=bf: torch.zeros(*s, device=dev, dtype=dt)  # noqa: E731
         self.buf = dict(x=z(R, cfg.d_model), q=z(R, cfg.q_dim), attn=z(R, cfg.q_dim), act=z(R, cfg.ffn),
                         logits=z(R, cfg.vocab, dt=torch.float32), counters=z(R * cfg.n_kv_heads, dt=torch.int32))
@@ -350,7 +351,7 @@ class DecodeEngine:
         dev = self.device
         B = len(ids)
         with torch.cuda.stream(self.stream):
-            # ---- prefill: all prompt tokens except the last, in <=MAX_ROWS-row chunks
+            # ---- prefill: all prompt tokens except the last, in <=PREFILL_ROWS-row chunks
             t0 = time.perf_counter_ns()
             self._prefill(ids)
             # ---- decode rows
@@ -445,8 +446,8 @@ class DecodeEngine:
                 flat_pos.append(j)
                 flat_slot.append(b)
         pr = self.prefill_rows
-        for c in range(0, len(flat_tok), MAX_ROWS):
-            n = min(MAX_ROWS, len(flat_tok) - c)
+        for c in range(0, len(flat_tok), PREFILL_ROWS):
+            n = min(PREFILL_ROWS, len(flat_tok) - c)
             pr["tok"][:n].copy_(torch.tensor(flat_tok[c:c + n], dtype=torch.int32))
             pr["pos"][:n].copy_(torch.tensor(flat_pos[c:c + n], dtype=torch.int32))
             pr["slot"][:n].copy_(torch.tensor(flat_slot[c:c + n], dtype=torch.int32))

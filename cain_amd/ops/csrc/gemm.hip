@@ -473,7 +473,7 @@ static int gemm_dispatch(GemmArgs a, int epi, int norm, int waves, hipStream_t s
 }
 
 // =====================================================================================================
-// Batched weight-streaming GEMM, 16 < M <= 128 (batched decode, prefill chunks).
+// Batched weight-streaming GEMM, 16 < M <= 256 (batched decode, prefill chunks).
 //
 // The skinny kernel's waves split K and each wave reads its own activation fragments straight from L2:
 // at M = 64 that is 4 B of activation traffic per weight byte and the CU's vector-memory path, not HBM,
@@ -662,25 +662,47 @@ __global__ __launch_bounds__(W * 64, LB) void bgemm_kernel(const GemmArgs a, con
     // MFMAs, so every MFMA finds its operand landed.  Left to itself the scheduler minimised registers
     // and paired each MFMA with its own ds_read (2 reads in flight, an LDS round trip exposed every
     // second MFMA at one wave per SIMD).
-    bf16x8 xf[2][NB];
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    if constexpr (NB >= 16) {
+      // 256 rows: a P-deep ring over the group's (slice, row block) fragment sequence instead of a whole
+      // second slice of fragments (2 x 16 fragments do not fit beside the 256-row accumulators)
+      constexpr int NF = U * NB, P = 4;
+      bf16x8 q[P];
 #pragma unroll
-    for (int b = 0; b < NB; ++b) xf[0][b] = frag(buf, h * U, b);
+      for (int i = 0; i < P; ++i) q[i] = frag(buf, h * U + i / NB, i % NB);
+      bf16x8 w[NTW];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      if (u + 1 < U) {
+      for (int i = 0; i < NF; ++i) {
+        const int u = i / NB, b = i % NB;
+        if (b == 0) {
 #pragma unroll
-        for (int b = 0; b < NB; ++b) xf[(u + 1) & 1][b] = frag(buf, h * U + u + 1, b);
+          for (int t = 0; t < NTW; ++t) w[t] = __builtin_bit_cast(bf16x8, __builtin_bit_cast(u32x4, cur[u][t]) & keep);
+        }
+        const bf16x8 x = q[i % P];
+        if (i + P < NF) q[i % P] = frag(buf, h * U + (i + P) / NB, (i + P) % NB);
+#pragma unroll
+        for (int t = 0; t < NTW; ++t) acc[t][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[t], x, acc[t][b], 0, 0, 0);
       }
-      __builtin_amdgcn_sched_barrier(0);
+    } else {
+      bf16x8 xf[2][NB];
 #pragma unroll
-      for (int t = 0; t < NTW; ++t) {
-        typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-        const bf16x8 w = __builtin_bit_cast(bf16x8, __builtin_bit_cast(u32x4, cur[u][t]) & keep);
+      for (int b = 0; b < NB; ++b) xf[0][b] = frag(buf, h * U, b);
 #pragma unroll
-        for (int b = 0; b < NB; ++b)
-          acc[t][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w, xf[u & 1][b], acc[t][b], 0, 0, 0);
+      for (int u = 0; u < U; ++u) {
+        if (u + 1 < U) {
+#pragma unroll
+          for (int b = 0; b < NB; ++b) xf[(u + 1) & 1][b] = frag(buf, h * U + u + 1, b);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int t = 0; t < NTW; ++t) {
+          const bf16x8 w = __builtin_bit_cast(bf16x8, __builtin_bit_cast(u32x4, cur[u][t]) & keep);
+#pragma unroll
+          for (int b = 0; b < NB; ++b)
+            acc[t][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w, xf[u & 1][b], acc[t][b], 0, 0, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
       }
-      __builtin_amdgcn_sched_barrier(0);
     }
   };
   // xa_/xb_: activation staging registers.  XS = 2: chunk c loads chunk c+1 into xa_ and stores it at
@@ -820,7 +842,7 @@ __global__ __launch_bounds__(W * 64, LB) void bgemm_kernel(const GemmArgs a, con
     if (s_ticket != unsigned(bg.ksplit - 1)) return;
     // sum the k-range partials, RB ranges x NTW*NB units of loads in flight per round trip (RB x NTW*NB
     // f32x4 registers: 2 ranges at 8 units keeps the 128-row variants inside 128 VGPRs)
-    constexpr int RB = NTW * NB >= 8 ? 2 : 4;
+    constexpr int RB = NTW * NB >= 16 ? 1 : (NTW * NB >= 8 ? 2 : 4);
     const __amdgpu_buffer_rsrc_t base_r = slab_rsrc(bg.part + pb * (size_t)UNITS * 256);
     f32x4 sum[NTW][NB];
 #pragma unroll
@@ -906,20 +928,25 @@ static BgPlan bgemm_plan(int N, int K, int M, int ntw_req) {
   static const int ksmax = env_int("CAIN_BGEMM_KSMAX", 8);
   static const int w_env = env_int("CAIN_BGEMM_W", 0);
   static const int ck_env = env_int("CAIN_BGEMM_CK", 0);
-  static const int d_env = env_int("CAIN_BGEMM_D", 0);
+  static const int d_env = env_int("CAIN_BGEMM_D", -1);
   BgPlan p{};
-  p.nb = M <= 32 ? 2 : (M <= 64 ? 4 : 8);
+  p.nb = M <= 32 ? 2 : (M <= 64 ? 4 : (M <= 128 ? 8 : 16));
   const int rows1 = 16 * BG_WAVES;
-  p.ntw = p.nb == 8 ? 1 : (ntw_req > 0 ? ntw_req : ((N + rows1 - 1) / rows1 >= 512 ? 2 : 1));
+  p.ntw = p.nb >= 8 ? 1 : (ntw_req > 0 ? ntw_req : ((N + rows1 - 1) / rows1 >= 512 ? 2 : 1));
   // the 4-wave and 16-slice-chunk variants exist for NTW = 1 only; 4-wave workgroups (64-row blocks)
   // measured faster on N <= 6144 (O / QKV / down projections at M = 64: 23.1 vs 25.6, 27.0 vs 30.0,
   // 41.1 vs 46.5 us; profiles/bgemm_sweep.md)
   const bool narrow = N <= 6144 && p.ntw == 1;
   p.w = (w_env == 4 || (w_env == 0 && narrow)) && p.ntw == 1 ? 4 : BG_WAVES;
-  if (p.nb == 8) {
+  if (p.nb == 16) {
+    // 256 rows: 8 waves (a 4-wave body would stage 16 fragments per wave), 4-slice chunks, 128 KiB of stages
+    p.w = 8;
+    p.ck = 4;
+  } else if (p.nb == 8) {
     // 128 rows: 4-slice chunks keep the double-buffered stage at 64 KiB (2 workgroups per CU)
     p.ck = p.w == 8 && ck_env == 8 ? 8 : 4;
-    if (p.ck == 4 && (d_env == 4 || d_env == 6 || d_env == 8)) p.d = d_env;
+    // ring depth: CAIN_BGEMM_D = 4 / 6 / 8 (anything else: off); default 4 on the 4-wave (narrow-output) bodies
+    if (p.ck == 4) p.d = (d_env == 4 || d_env == 6 || d_env == 8) ? d_env : (d_env < 0 && p.w == 4 ? 4 : 0);
   }
   else
   {
@@ -986,13 +1013,18 @@ static hipError_t bg_launch_e(int epi, const GemmArgs& a, const BgArgs& b, int n
 
 template <int NB, bool NORM>
 static hipError_t bg_launch_shape(int epi, const BgPlan& p, const GemmArgs& a, const BgArgs& b, hipStream_t st) {
-  if constexpr (NB == 8) {
-    // register rings (activations + weights) of depth p.d; the 8-wave bodies (256-VGPR budget) only at 4
-    if (p.d == 8 && p.w == 4) return bg_launch_e<8, 1, 4, 4, NORM, 8>(epi, a, b, p.nblk, st);
-    if (p.d == 6 && p.w == 4) return bg_launch_e<8, 1, 4, 4, NORM, 6>(epi, a, b, p.nblk, st);
-    if (p.d >= 4) {
-      if (p.w == 4) return bg_launch_e<8, 1, 4, 4, NORM, 4>(epi, a, b, p.nblk, st);
-      return bg_launch_e<8, 1, 8, 4, NORM, 4>(epi, a, b, p.nblk, st);
+  if constexpr (NB == 16) {
+    return bg_launch_e<16, 1, 8, 4, NORM>(epi, a, b, p.nblk, st);
+  } else if constexpr (NB == 8) {
+    // register rings for activations AND weights (AR) of depth p.d; not for the fused-norm bodies, whose
+    // staging sums of squares make the rings spill (profiles/bgemm_r1.md)
+    if constexpr (!NORM) {
+      if (p.d == 8 && p.w == 4) return bg_launch_e<8, 1, 4, 4, NORM, 8>(epi, a, b, p.nblk, st);
+      if (p.d == 6 && p.w == 4) return bg_launch_e<8, 1, 4, 4, NORM, 6>(epi, a, b, p.nblk, st);
+      if (p.d == 4) {
+        if (p.w == 4) return bg_launch_e<8, 1, 4, 4, NORM, 4>(epi, a, b, p.nblk, st);
+        return bg_launch_e<8, 1, 8, 4, NORM, 4>(epi, a, b, p.nblk, st);
+      }
     }
     if (p.w == 4) return bg_launch_e<8, 1, 4, 4, NORM>(epi, a, b, p.nblk, st);
     if (p.ck == 8) return bg_launch_e<8, 1, 8, 8, NORM>(epi, a, b, p.nblk, st);
@@ -1016,7 +1048,8 @@ static int bgemm_dispatch(const GemmArgs& a, int epi, bool norm, const BgPlan& p
   hipError_t e;
   if (p.nb == 2) e = norm ? bg_launch_shape<2, true>(epi, p, a, b, st) : bg_launch_shape<2, false>(epi, p, a, b, st);
   else if (p.nb == 4) e = norm ? bg_launch_shape<4, true>(epi, p, a, b, st) : bg_launch_shape<4, false>(epi, p, a, b, st);
-  else e = norm ? bg_launch_shape<8, true>(epi, p, a, b, st) : bg_launch_shape<8, false>(epi, p, a, b, st);
+  else if (p.nb == 8) e = norm ? bg_launch_shape<8, true>(epi, p, a, b, st) : bg_launch_shape<8, false>(epi, p, a, b, st);
+  else e = norm ? bg_launch_shape<16, true>(epi, p, a, b, st) : bg_launch_shape<16, false>(epi, p, a, b, st);
   return int(e);
 }
 
@@ -1033,7 +1066,7 @@ static int bgemm_ntw() {
 // M <= 32 on narrow outputs with short K (N < 8192, K <= 4096: O / QKV projections) stays on the skinny
 // kernel, which measured faster there (its whole grid streams from the first cycle; no staging, no combine).
 static bool bgemm_eligible(int N, int K, int M) {
-  return M > bgemm_min_m() && M <= 128 && K % (32 * BG_CK) == 0 && (M > 32 || N >= 8192 || K > 4096);
+  return M > bgemm_min_m() && M <= 256 && K % (32 * BG_CK) == 0 && (M > 32 || N >= 8192 || K > 4096);
 }
 
 // Workspace the batched path needs for a GEMM of this shape (0 when the skinny kernel runs it).
@@ -1059,7 +1092,7 @@ CAIN_API int cain_skinny_gemm_ex(const void* Wp, const void* X, int ldx, int K, 
   return gemm_dispatch(a, epi, norm != 0, waves, st);
 }
 
-// Full entry: batched path for 16 < M <= 128 when a workspace of cain_gemm_ws_bytes() (zeroed once) is
+// Full entry: batched path for 16 < M <= 256 when a workspace of cain_gemm_ws_bytes() (zeroed once) is
 // given, the skinny kernel otherwise.
 CAIN_API int cain_gemm(const void* Wp, const void* X, int ldx, int K, int N, int M, void* Y, int ldy,
                        const float* bias, int norm, float eps, const int* slot, const int* pos,

@@ -20,7 +20,7 @@
 
 #include "common.h"
 
-constexpr int CAIN_MAX_ROWS = 128;  // rows per forward (decode batch / prefill chunk)
+constexpr int CAIN_MAX_ROWS = 256;  // rows per forward (decode batch / prefill chunk)
 
 CAIN_API int cain_gemm(const void* Wp, const void* X, int ldx, int K, int N, int M, void* Y, int ldy,
                        const float* bias, int norm, float eps, const int* slot, const int* pos,

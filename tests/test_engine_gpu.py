@@ -74,18 +74,18 @@ def test_flagship_llama_smoke():
     eng.close()
 
 
-@pytest.mark.parametrize("name", ["tiny-llama3.1:8b", "tiny-gemma:7b"])
-def test_wide_batch_and_long_prefill_match_oracle(name):
-    """100 rows: decode GEMMs on the batched (LDS-staged, NB = 8) path and prefill in 128-row chunks."""
-    eng = DecodeEngine(name, device="cuda", max_batch=128, max_context=512, keep_natural=True, seed=4)
+@pytest.mark.parametrize("name,rows", [("tiny-llama3.1:8b", 100), ("tiny-gemma:7b", 100), ("tiny-llama3.1:8b", 200)])
+def test_wide_batch_and_long_prefill_match_oracle(name, rows):
+    """100 / 200 rows: decode GEMMs on the batched (LDS-staged, NB = 8 / 16) path, prefill in 128-row chunks."""
+    eng = DecodeEngine(name, device="cuda", max_batch=rows, max_context=512, keep_natural=True, seed=4)
     long = " ".join(f"word{i}" for i in range(160))  # > 128 prompt tokens: several prefill chunks
-    prompts = [f"In {i} words, please give me information about topic {i}" for i in range(99)] + [long]
+    prompts = [f"In {i} words, please give me information about topic {i}" for i in range(rows - 1)] + [long]
     got = eng.last_logits(prompts)
     ref = ReferenceModel(eng.weights)
-    for i in (0, 37, 98, 99):
+    for i in (0, 37, rows - 2, rows - 1):
         want = ref.forward(torch.tensor([eng.encode(prompts[i])], device="cuda"))[0, -1]
         cos = torch.nn.functional.cosine_similarity(got[i].float(), want.float(), dim=0)
         assert cos > 0.995, (name, i, float(cos))
-    r = eng.generate(prompts, 4, [dict(temperature=0.8, seed=i, eos_id=-1) for i in range(100)])
+    r = eng.generate(prompts, 4, [dict(temperature=0.8, seed=i, eos_id=-1) for i in range(rows)])
     assert all(x.eval_count == 4 for x in r)
     eng.close()

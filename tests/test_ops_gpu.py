@@ -1,7 +1,7 @@
 """Numerics of every HIP kernel against a plain PyTorch fp32 reference.
 
 Shapes cover the study's variants: head_dim 96/128/256, GQA groups 1/4/6/7/8,
-M = 1..64 rows, gate/up SiLU and GeLU-tanh epilogues, QKV bias, residual add.
+M = 1..256 rows, gate/up SiLU and GeLU-tanh epilogues, QKV bias, residual add.
 """
 import math
 
@@ -102,11 +102,11 @@ def test_skinny_gemm_gateup(act, M):
     assert rel_err(y, a * u) < 1.5e-2
 
 
-@pytest.mark.parametrize("M", [17, 32, 48, 64, 65, 100, 128])
+@pytest.mark.parametrize("M", [17, 32, 48, 64, 65, 100, 128, 129, 200, 256])
 @pytest.mark.parametrize("N,K,norm", [(32064, 3072, True), (256, 14336, False), (4096, 4096, True),
                                       (1920, 8960, False)])
 def test_batched_gemm_matches_skinny_and_reference(M, N, K, norm):
-    """The LDS-staged split-K path (16 < M <= 64): N not a multiple of the 128-row block, deep k-splits
+    """The LDS-staged split-K path (16 < M <= 256): N not a multiple of the 128-row block, deep k-splits
     (N=256, K=14336 -> 56 partial ranges), fused norm; repeated launches check the self-resetting tickets."""
     torch.manual_seed(11)
     W = (torch.randn(N, K, device=DEV) * 0.02).bfloat16()
@@ -157,7 +157,7 @@ def _rot(x, c, s_):
 
 
 @pytest.mark.parametrize("H,Hkv,hd", [(32, 8, 128), (12, 2, 128), (8, 1, 256), (32, 32, 96), (28, 4, 128)])
-@pytest.mark.parametrize("M", [1, 5, 40, 128])
+@pytest.mark.parametrize("M", [1, 5, 40, 128, 256])
 @pytest.mark.parametrize("norm", [False, True])
 def test_fused_qkv_rope_kv_append(H, Hkv, hd, M, norm):
     torch.manual_seed(8)
