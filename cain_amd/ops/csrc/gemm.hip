@@ -939,7 +939,8 @@ static BgPlan bgemm_plan(int N, int K, int M, int ntw_req) {
   const bool narrow = N <= 6144 && p.ntw == 1;
   p.w = (w_env == 4 || (w_env == 0 && narrow)) && p.ntw == 1 ? 4 : BG_WAVES;
   if (p.nb == 16) {
-    // 256 rows: 8 waves (a 4-wave body would stage 16 fragments per wave), 4-slice chunks, 128 KiB of stages
+    // 256 rows: 8 waves x 1 tile, 4-slice chunks, 128 KiB of stages (4 waves x 2 tiles at one wave per SIMD
+    // measured 10-20 % slower on every shape, profiles/bgemm_r1.md)
     p.w = 8;
     p.ck = 4;
   } else if (p.nb == 8) {
@@ -987,11 +988,11 @@ static hipError_t bg_launch(const GemmArgs& a, const BgArgs& b, int nblk, hipStr
   // whose 8 staged fragments per wave leave no room for the deeper ring).  DD > 0 (128-row bodies): a
   // DD-deep ring with the register budget of one workgroup per CU (4 waves: 512 VGPRs, 8 waves: 256),
   // so DD-1 chunks of weights stay in flight per wave across the per-chunk barrier.
-  constexpr int D = DD > 0 ? DD : ((W == 4 && CK == U && !NORM) ? 4 : 2);
+  constexpr int D = DD > 0 ? DD : ((W == 4 && CK == U && !NORM && NB < 16) ? 4 : 2);
   // three activation stages for the 4-wave bodies (one workgroup per CU on the narrow grids anyway)
-  constexpr int XS = (W == 4 && CK == U) ? 3 : 2;
+  constexpr int XS = (W == 4 && CK == U && NB < 16) ? 3 : 2;  // 256-row stages are 64 KiB each
   // (the 128-row 8-wave body needs 256 VGPRs for its double-buffered LDS fragments: 1 workgroup per CU)
-  constexpr int LB = DD > 0 ? (W == 4 ? 1 : 2) : ((W == 8 && NTW == 1 && NB < 8 && CK * NB <= 32) ? 4 : 2);
+  constexpr int LB = (DD > 0 || NB >= 16) ? (W == 4 ? 1 : 2) : ((W == 8 && NTW == 1 && NB < 8 && CK * NB <= 32) ? 4 : 2);
   constexpr bool AR = DD > 0;  // explicit depth: the activation + weight register rings
   hipLaunchKernelGGL((bgemm_kernel<NB, NTW, W, CK, U, D, AR ? 2 : XS, LB, AR, EPI, NORM>), dim3(nblk * b.ksplit),
                      dim3(W * 64), 0, st, a, b);
