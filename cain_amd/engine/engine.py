@@ -128,7 +128,16 @@ def attention_splits(M: int, Hkv: int, T_max: int) -> int:
     """Position splits per (row, kv head): ~256 workgroups in flight, >= 4 blocks of 32 per split at
     full context, <= 64 splits (measured: 1024-WG targets lose more to the split combine than they
     gain in parallelism, profiles/kernels.md).  ``CAIN_ATTN_SPLIT_BLOCKS`` = b > 0 additionally caps a
-    split at b blocks of 32 positions (bounds one workgroup's serial work at wide batches)."""
+    split at b blocks of 32 positions (bounds one workgroup's serial work at wide batches); ``CAIN_ATTN_NSPLIT``
+    forces the count (tuning)."""
+    forced = int(os.environ.get("CAIN_ATTN_NSPLIT", "0") or 0)
+    if forced > 0:
+        return min(64, forced)
+    if M * Hkv <= 64:
+        # few (row, kv head) pairs run 8-wave workgroups (attention.hip): one split up to 64 blocks of 32
+        # positions (8 per wave) -- the split combine costs ~4 us of dependent memory round trips, more than
+        # it saves below that (profiles/single_stream_r1.md)
+        return int(max(1, min(64, math.ceil((T_max // 32) / 64))))
     ns = max(1, min(T_max // 128, math.ceil(256 / (M * Hkv))))
     per = int(os.environ.get("CAIN_ATTN_SPLIT_BLOCKS", "0") or 0)
     if per > 0:

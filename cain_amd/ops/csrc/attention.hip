@@ -13,9 +13,9 @@
 // every load instruction of a wave reads one contiguous 1 KiB (full 128-B lines; a row-major cache
 // made each K load touch 16 rows x 64 B and each V^T load 16 rows x 8 B).
 //
-// Workgroup = 4 waves = (row m, kv head kh, split sp).  The G = H/Hkv query
+// Workgroup = AW (4 or 8) waves = (row m, kv head kh, split sp).  The G = H/Hkv query
 // heads of the group are the 16 MFMA columns (G <= 16 covers MHA, GQA 4/6/7/8
-// and MQA).  The split's 32-position blocks are dealt to the 4 waves.  Per block:
+// and MQA).  The split's 32-position blocks are dealt to the AW waves.  Per block:
 //   S^T[t][g] = K[t][:] . Q[g][:]     2 tiles of v_mfma_f32_16x16x32_bf16 x hd/32
 //       A = K fragments straight from HBM, B = Q^T (lane: col g) held in registers
 //       for the whole wave;
@@ -26,7 +26,7 @@
 //       permuted k order (cdna_hip_programming.md §3 'An accumulator tile as the
 //       next MFMA's operand');
 //       A = V^T fragments stored in that same k order — nothing is staged through LDS.
-// The 4 waves merge their (m, l, O) in LDS.  With one split the workgroup
+// The AW waves merge their (m, l, O) in LDS.  With one split the workgroup
 // normalises and stores bf16 directly; otherwise each workgroup publishes an
 // unnormalised partial with write-through (sc1) stores and the LAST arriving
 // workgroup of (m, kh) merges all splits with sc1 loads (per-wave vmcnt drain ->
@@ -36,9 +36,9 @@
 #include "common.h"
 
 constexpr float LOG2E = 1.4426950408889634f;
-constexpr int AW = 4;  // waves per workgroup
-
-template <int HD>
+// AW: waves per workgroup (4; 8 for few (row, kv head) pairs: single-stream decode, where one workgroup per
+// pair with more waves beats a position split and its in-kernel combine)
+template <int HD, int AW>
 __global__ __launch_bounds__(AW * 64) void attn_decode_kernel(
     const __bf16* __restrict__ q, const __bf16* __restrict__ kc, const __bf16* __restrict__ vtc,
     const int* __restrict__ slot, const int* __restrict__ pos, float* __restrict__ part_o,
@@ -252,13 +252,13 @@ __global__ __launch_bounds__(AW * 64) void attn_decode_kernel(
   }
 }
 
-template <int HD>
+template <int HD, int AW>
 static hipError_t launch_attn(const void* q, const void* kc, const void* vtc, const int* slot, const int* pos,
                               float* part_o, float* part_ml, unsigned* counters, void* out, int ldo, int M, int H,
                               int Hkv, int T_max, int nsplit, float scale, hipStream_t st) {
-  hipLaunchKernelGGL(attn_decode_kernel<HD>, dim3(M * Hkv, nsplit), dim3(AW * 64), 0, st, (const __bf16*)q,
-                     (const __bf16*)kc, (const __bf16*)vtc, slot, pos, part_o, part_ml, counters, (__bf16*)out, ldo, M,
-                     H, Hkv, T_max, nsplit, scale);
+  hipLaunchKernelGGL((attn_decode_kernel<HD, AW>), dim3(M * Hkv, nsplit), dim3(AW * 64), 0, st, (const __bf16*)q,
+                     (const __bf16*)kc, (const __bf16*)vtc, slot, pos, part_o, part_ml, counters, (__bf16*)out, ldo,
+                     M, H, Hkv, T_max, nsplit, scale);
   return hipGetLastError();
 }
 
@@ -268,11 +268,20 @@ CAIN_API int cain_attention(const void* q, const void* kc, const void* vtc, cons
                             float* part_o, float* part_ml, unsigned* counters, void* out, int ldo, int M, int H,
                             int Hkv, int hd, int T_max, int nsplit, float scale, hipStream_t st) {
   if (H % Hkv || H / Hkv > 16 || T_max % 32 || nsplit < 1 || nsplit > 64 || M > 256) return -1;
+  // 8-wave workgroups for few (row, kv head) pairs (hd <= 128: the hd-256 body needs one wave per SIMD)
+  const bool wide = M * Hkv <= 64;
+#define CAIN_ATTN_CASE(HDV)                                                                                        \
+  case HDV:                                                                                                      \
+    return wide ? int(launch_attn<HDV, 8>(q, kc, vtc, slot, pos, part_o, part_ml, counters, out, ldo, M, H, Hkv,  \
+                                          T_max, nsplit, scale, st))                                             \
+                : int(launch_attn<HDV, 4>(q, kc, vtc, slot, pos, part_o, part_ml, counters, out, ldo, M, H, Hkv,  \
+                                          T_max, nsplit, scale, st));
   switch (hd) {
-    case 64: return int(launch_attn<64>(q, kc, vtc, slot, pos, part_o, part_ml, counters, out, ldo, M, H, Hkv, T_max, nsplit, scale, st));
-    case 96: return int(launch_attn<96>(q, kc, vtc, slot, pos, part_o, part_ml, counters, out, ldo, M, H, Hkv, T_max, nsplit, scale, st));
-    case 128: return int(launch_attn<128>(q, kc, vtc, slot, pos, part_o, part_ml, counters, out, ldo, M, H, Hkv, T_max, nsplit, scale, st));
-    case 256: return int(launch_attn<256>(q, kc, vtc, slot, pos, part_o, part_ml, counters, out, ldo, M, H, Hkv, T_max, nsplit, scale, st));
+    CAIN_ATTN_CASE(64)
+    CAIN_ATTN_CASE(96)
+    CAIN_ATTN_CASE(128)
+    case 256: return int(launch_attn<256, 4>(q, kc, vtc, slot, pos, part_o, part_ml, counters, out, ldo, M, H, Hkv, T_max, nsplit, scale, st));
     default: return -1;
   }
+#undef CAIN_ATTN_CASE
 }
