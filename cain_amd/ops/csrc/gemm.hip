@@ -946,8 +946,9 @@ static BgPlan bgemm_plan(int N, int K, int M, int ntw_req) {
   } else if (p.nb == 8) {
     // 128 rows: 4-slice chunks keep the double-buffered stage at 64 KiB (2 workgroups per CU)
     p.ck = p.w == 8 && ck_env == 8 ? 8 : 4;
-    // ring depth: CAIN_BGEMM_D = 4 / 6 / 8 (anything else: off); default 4 on the 4-wave (narrow-output) bodies
-    if (p.ck == 4) p.d = (d_env == 4 || d_env == 6 || d_env == 8) ? d_env : (d_env < 0 && p.w == 4 ? 4 : 0);
+    // activation + weight register rings, depth 4, on the 4-wave (narrow-output) bodies; CAIN_BGEMM_D = 4 also on
+    // the 8-wave ones, any other value: off (depths 6 and 8 measured slower, profiles/bgemm_r1.md)
+    if (p.ck == 4) p.d = d_env == 4 ? 4 : (d_env < 0 && p.w == 4 ? 4 : 0);
   }
   else
   {
@@ -1020,8 +1021,6 @@ static hipError_t bg_launch_shape(int epi, const BgPlan& p, const GemmArgs& a, c
     // register rings for activations AND weights (AR) of depth p.d; not for the fused-norm bodies, whose
     // staging sums of squares make the rings spill (profiles/bgemm_r1.md)
     if constexpr (!NORM) {
-      if (p.d == 8 && p.w == 4) return bg_launch_e<8, 1, 4, 4, NORM, 8>(epi, a, b, p.nblk, st);
-      if (p.d == 6 && p.w == 4) return bg_launch_e<8, 1, 4, 4, NORM, 6>(epi, a, b, p.nblk, st);
       if (p.d == 4) {
         if (p.w == 4) return bg_launch_e<8, 1, 4, 4, NORM, 4>(epi, a, b, p.nblk, st);
         return bg_launch_e<8, 1, 8, 4, NORM, 4>(epi, a, b, p.nblk, st);
