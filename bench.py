@@ -62,6 +62,8 @@ def main() -> int:
     ap.add_argument("--context", type=int, default=1536)
     ap.add_argument("--steps-per-graph", type=int, default=16)
     ap.add_argument("--no-energy", action="store_true")
+    ap.add_argument("--weights", choices=("bf16", "fp8"), default="bf16",
+                    help="GEMM weight storage: bf16 (headline) or fp8 e4m3 per-row scaled (W8A16, batch <= 64)")
     ns = ap.parse_args()
 
     import torch
@@ -81,7 +83,9 @@ def main() -> int:
 
     n_tok = tokens_for_words(ns.words)
     eng = DecodeEngine(ns.model, device=dev, max_batch=ns.batch, max_context=ns.context, seed=1234 + rank,
-                       steps_per_graph=ns.steps_per_graph)
+                       steps_per_graph=ns.steps_per_graph, weight_dtype=ns.weights)
+    if eng.max_batch < ns.batch:
+        raise SystemExit(f"--batch {ns.batch} exceeds the engine's row limit {eng.max_batch} for --weights {ns.weights}")
     tps = topics()
     opts = {"eos_id": -1}  # forced length: random weights never emit a meaningful EOS
 
@@ -148,7 +152,7 @@ def main() -> int:
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": round(value / base_tps, 2) if base_tps else None,
-            "dtype": "bf16",
+            "dtype": "bf16" if ns.weights == "bf16" else "bf16 activations, fp8-e4m3 weights",
             "data": "synthetic (reference topics.csv prompts, random-init weights)",
             "config": {"model": ns.model, "global_batch": ns.batch * world, "seq_len": n_tok,
                        "parallelism": f"dp{world}", "words": ns.words, "trials_per_gpu": ns.batch,

@@ -44,6 +44,7 @@ OLLAMA_DEFAULTS = dict(temperature=0.8, top_k=40, top_p=0.9, repeat_penalty=1.1,
 
 MAX_ROWS = 256  # rows per forward: decode batch (runtime.hip CAIN_MAX_ROWS)
 PREFILL_ROWS = 128  # prompt tokens per prefill forward
+W8_MAX_ROWS = 64  # fp8-weight kernels (gemm_w8.hip): rows per forward, decode and prefill
 
 
 @dataclass
@@ -101,7 +102,7 @@ def _row_options(opts: Optional[Dict], cfg: ModelConfig, index: int, base_seed: 
 
 # ============================================================== ctypes structs
 class _CainLayer(ctypes.Structure):
-    _fields_ = [(n, ctypes.c_void_p) for n in ("wqkv", "bqkv", "wo", "wgu", "wdown")]
+    _fields_ = [(n, ctypes.c_void_p) for n in ("wqkv", "bqkv", "wo", "wgu", "wdown", "sqkv", "so", "sgu", "sdown")]
 
 
 class _CainPlanDesc(ctypes.Structure):
@@ -112,7 +113,7 @@ class _CainPlanDesc(ctypes.Structure):
                 + [("kv_layer_elems", ctypes.c_longlong)]
                 + [(n, ctypes.c_void_p) for n in ("cos_t", "sin_t", "x", "q", "attn", "act", "logits",
                                                  "part_o", "part_ml", "counters", "gemm_ws")]
-                + [("gemm_ws_bytes", ctypes.c_longlong)])
+                + [("gemm_ws_bytes", ctypes.c_longlong), ("w8", ctypes.c_int), ("lm_head_scale", ctypes.c_void_p)])
 
 
 class _CainRows(ctypes.Structure):
@@ -149,13 +150,20 @@ class DecodeEngine:
     def __init__(self, model: Union[str, ModelConfig], device: Union[str, torch.device] = "cuda",
                  max_batch: int = 16, max_context: int = 2048, seed: int = 0, backend: Optional[str] = None,
                  steps_per_graph: int = 8, weights: Optional[ModelWeights] = None, tokenizer=None,
-                 keep_natural: bool = False):
+                 keep_natural: bool = False, weight_dtype: str = "bf16"):
+        """``weight_dtype="fp8"``: GEMM weights quantised per row to e4m3 (W8A16, half the weight bytes
+        per decode step -- the single-stream / small-batch option); limits rows per forward to 64."""
         self.cfg = get_config(model) if isinstance(model, str) else model
+        if weight_dtype not in ("bf16", "fp8"):
+            raise ValueError(f"weight_dtype must be 'bf16' or 'fp8', got {weight_dtype!r}")
+        self.weight_dtype = weight_dtype
+        row_cap = W8_MAX_ROWS if weight_dtype == "fp8" else MAX_ROWS
         self.device = torch.device(device)
         if backend is None:
             backend = "hip" if self.device.type == "cuda" else "torch"
         self.backend = backend
-        self.max_batch = int(min(max_batch, MAX_ROWS))
+        self.max_batch = int(min(max_batch, row_cap))
+        self.prefill_chunk = min(PREFILL_ROWS, row_cap)
         self.T_max = int(math.ceil(min(max_context, self.cfg.max_context) / 32) * 32)
         self.seed = seed
         self.steps_per_graph = max(1, int(steps_per_graph))
@@ -186,7 +194,7 @@ class DecodeEngine:
         cfg, dev = self.cfg, self.device
         if self.device.type != "cuda":
             raise ValueError("hip backend needs a GPU device")
-        packed = pack_for_engine(self.weights, free_natural=not self.keep_natural)
+        packed = pack_for_engine(self.weights, free_natural=not self.keep_natural, weight_dtype=self.weight_dtype)
         torch.cuda.synchronize(dev)
         S, T, L = self.max_batch, self.T_max, cfg.n_layers
         bf = torch.bfloat16
@@ -198,7 +206,7 @@ class DecodeEngine:
         ang = np.arange(T, dtype=np.float64)[:, None] * inv[None, :]
         self.cos_t = torch.tensor(np.cos(ang), dtype=torch.float32, device=dev).contiguous()
         self.sin_t = torch.tensor(np.sin(ang), dtype=torch.float32, device=dev).contiguous()
-        R = max(self.max_batch, PREFILL_ROWS)  # rows any forward of this engine can have
+        R = max(self.max_batch, self.prefill_chunk)  # rows any forward of this engine can have
         z = lambda *s, dt=bf: torch.zeros(*s, device=dev, dtype=dt)  # noqa: E731
         self.buf = dict(x=z(R, cfg.d_model), q=z(R, cfg.q_dim), attn=z(R, cfg.q_dim), act=z(R, cfg.ffn),
                         logits=z(R, cfg.vocab, dt=torch.float32), counters=z(R * cfg.n_kv_heads, dt=torch.int32))
@@ -218,8 +226,8 @@ class DecodeEngine:
             dev)
         self._layers = (_CainLayer * L)()
         for i, lp in enumerate(packed["layers"]):
-            self._layers[i] = _CainLayer(_ptr(lp["wqkv"]), _ptr(lp["bqkv"]), _ptr(lp["wo"]), _ptr(lp["wgu"]),
-                                         _ptr(lp["wdown"]))
+            self._layers[i] = _CainLayer(*(_ptr(lp.get(k)) for k in ("wqkv", "bqkv", "wo", "wgu", "wdown",
+                                                                     "sqkv", "so", "sgu", "sdown")))
         self._packed = packed
         d = _CainPlanDesc()
         d.n_layers, d.d, d.H, d.Hkv, d.hd = L, cfg.d_model, cfg.n_heads, cfg.n_kv_heads, cfg.head_dim
@@ -241,6 +249,7 @@ class DecodeEngine:
         ws = max([ops.gemm_ws_bytes(n, k, m) for n, k in shapes for m in range(17, R + 1)] + [0])
         self.gemm_ws = torch.zeros(max(ws, 16) // 4 + 1, device=dev, dtype=torch.int32)
         d.gemm_ws, d.gemm_ws_bytes = _ptr(self.gemm_ws), ws
+        d.w8, d.lm_head_scale = int(self.weight_dtype == "fp8"), _ptr(packed.get("lm_head_scale"))
         self._desc = d
         self._plans: Dict[int, int] = {}
         self._graphs: Dict[tuple, int] = {}
@@ -360,7 +369,7 @@ class DecodeEngine:
         dev = self.device
         B = len(ids)
         with torch.cuda.stream(self.stream):
-            # ---- prefill: all prompt tokens except the last, in <=PREFILL_ROWS-row chunks
+            # ---- prefill: all prompt tokens except the last, in <=prefill_chunk-row chunks
             t0 = time.perf_counter_ns()
             self._prefill(ids)
             # ---- decode rows
@@ -455,8 +464,8 @@ class DecodeEngine:
                 flat_pos.append(j)
                 flat_slot.append(b)
         pr = self.prefill_rows
-        for c in range(0, len(flat_tok), PREFILL_ROWS):
-            n = min(PREFILL_ROWS, len(flat_tok) - c)
+        for c in range(0, len(flat_tok), self.prefill_chunk):
+            n = min(self.prefill_chunk, len(flat_tok) - c)
             pr["tok"][:n].copy_(torch.tensor(flat_tok[c:c + n], dtype=torch.int32))
             pr["pos"][:n].copy_(torch.tensor(flat_pos[c:c + n], dtype=torch.int32))
             pr["slot"][:n].copy_(torch.tensor(flat_slot[c:c + n], dtype=torch.int32))

@@ -18,6 +18,12 @@ Two layouts:
   the activation in its epilogue.  Gemma's ``(1 + w)`` norm gain is folded into the stored gain.  Q/K rows
   are permuted per head (``rope_pair_order``) so every 16-row tile holds 8
   complete RoPE pairs and the QKV GEMM can rotate in its epilogue.
+* **packed fp8** (``weight_dtype="fp8"``, the W8A16 decode option) — the same
+  row orders, each row quantised to OCP e4m3 with one fp32 scale
+  (``quantize_fp8_rows``), bytes laid out ``[N/16][K/64][64 lanes][16]`` for
+  ``ops/csrc/gemm_w8.hip`` (``pack_mfma_a_fp8``).  The reference's models are
+  4-bit GGUF quantisations served by Ollama; fp8 is the gfx950
+  native narrow weight type.
 """
 from __future__ import annotations
 
@@ -45,6 +51,43 @@ def unpack_mfma_a(p: torch.Tensor) -> torch.Tensor:
     nt, ns = p.shape[0], p.shape[1]
     t = p.reshape(nt, ns, 4, 16, 8).permute(0, 3, 1, 2, 4)  # [t, r, s, g, j]
     return t.contiguous().reshape(nt * 16, ns * 32)
+
+
+FP8_MAX = 448.0  # largest finite OCP e4m3 value
+
+
+def quantize_fp8_rows(w: torch.Tensor):
+    """Per-output-row symmetric e4m3 quantisation: (q [N, K] float8_e4m3fn, scale [N] fp32), W ~= q * scale.
+
+    Scales are powers of two (the row's amax lands in e4m3's top binade): relative precision is e4m3's
+    either way, and q * scale is then exact in bf16, so ``fp8_roundtrip_weights`` gives the torch oracle
+    exactly the weights the fp8 kernels multiply by."""
+    wf = w.float()
+    amax = wf.abs().amax(dim=1).clamp_min(1e-30)
+    scale = torch.exp2(torch.ceil(torch.log2(amax / FP8_MAX)))
+    q = (wf / scale[:, None]).clamp(-FP8_MAX, FP8_MAX).to(torch.float8_e4m3fn)
+    return q, scale.contiguous()
+
+
+def dequantize_fp8_rows(q: torch.Tensor, scale: torch.Tensor) -> torch.Tensor:
+    return q.float() * scale.float()[:, None]
+
+
+def pack_mfma_a_fp8(q: torch.Tensor) -> torch.Tensor:
+    """e4m3 [N, K] -> uint8 [N/16, K/64, 64, 16]: lane = g*16 + r holds bytes h*8 + j = element
+    (16t + r, 64p + 32h + 8g + j) -- the two k-slices of one ``v_mfma_f32_16x16x32_bf16`` A fragment pair."""
+    n, k = q.shape
+    if n % 16 or k % 64:
+        raise ValueError(f"pack_mfma_a_fp8 needs N%16==0 and K%64==0, got {tuple(q.shape)}")
+    t = q.view(torch.uint8).reshape(n // 16, 16, k // 64, 2, 4, 8)  # [t, r, p, h, g, j]
+    t = t.permute(0, 2, 4, 1, 3, 5)                                   # [t, p, g, r, h, j]
+    return t.contiguous().reshape(n // 16, k // 64, 64, 16)
+
+
+def unpack_mfma_a_fp8(p: torch.Tensor) -> torch.Tensor:
+    nt, kp = p.shape[0], p.shape[1]
+    t = p.reshape(nt, kp, 4, 16, 2, 8).permute(0, 3, 1, 4, 2, 5)   # [t, r, p, h, g, j]
+    return t.contiguous().reshape(nt * 16, kp * 64).view(torch.float8_e4m3fn)
 
 
 def rope_pair_order(hd: int) -> torch.Tensor:
@@ -140,28 +183,53 @@ def fold_gain(w: torch.Tensor, g: torch.Tensor) -> torch.Tensor:
     return (w.float() * g.float()[None, :]).to(w.dtype)
 
 
-def pack_for_engine(mw: ModelWeights, free_natural: bool = False) -> Dict[str, object]:
+def fp8_roundtrip_weights(mw: ModelWeights) -> ModelWeights:
+    """Copy of ``mw`` whose GEMM weights are dequant(quant_fp8(W)) in bf16 (LM head untied from the
+    embedding table, which the engine keeps in bf16): the torch oracle of a ``weight_dtype="fp8"`` engine."""
+    def rt(w):
+        return dequantize_fp8_rows(*quantize_fp8_rows(w)).to(w.dtype)
+
+    layers = [LayerWeights(attn_norm=lw.attn_norm, wqkv=rt(lw.wqkv), bqkv=lw.bqkv, wo=rt(lw.wo), mlp_norm=lw.mlp_norm,
+                           w_gate=rt(lw.w_gate), w_up=rt(lw.w_up), w_down=rt(lw.w_down)) for lw in mw.layers]
+    return ModelWeights(mw.cfg, mw.embed, mw.final_norm, rt(mw.lm_head), layers)
+
+
+def pack_for_engine(mw: ModelWeights, free_natural: bool = False, weight_dtype: str = "bf16") -> Dict[str, object]:
     """Build the decode engine's packed tensors (see module doc); norm gains are folded into the GEMM
-    weights they feed (attn_norm -> wqkv, mlp_norm -> gate/up, final_norm -> lm_head)."""
+    weights they feed (attn_norm -> wqkv, mlp_norm -> gate/up, final_norm -> lm_head).
+
+    ``weight_dtype="fp8"``: every GEMM weight (LM head included) is quantised per row after the gain
+    fold; each matrix entry becomes the fp8 packing and its scales are stored under ``s<name>``."""
+    if weight_dtype not in ("bf16", "fp8"):
+        raise ValueError(f"weight_dtype must be 'bf16' or 'fp8', got {weight_dtype!r}")
     cfg = mw.cfg
+    fp8 = weight_dtype == "fp8"
     perm = qkv_row_permutation(cfg).to(mw.device)
+
+    def put(dst: Dict[str, object], name: str, w: torch.Tensor) -> None:
+        if fp8:
+            q, sc = quantize_fp8_rows(w)
+            dst[name], dst["s" + name[1:]] = pack_mfma_a_fp8(q), sc
+        else:
+            dst[name] = pack_mfma_a(w)
+
     layers = []
     for lw in mw.layers:
         ga = effective_gain(cfg, lw.attn_norm)
         gm = effective_gain(cfg, lw.mlp_norm)
-        layers.append({
-            "wqkv": pack_mfma_a(fold_gain(lw.wqkv[perm], ga)),
-            "bqkv": None if lw.bqkv is None else lw.bqkv.float()[perm].contiguous(),
-            "wo": pack_mfma_a(lw.wo),
-            "wgu": pack_mfma_a(interleave_tiles(fold_gain(lw.w_gate, gm), fold_gain(lw.w_up, gm), tile=8)),
-            "wdown": pack_mfma_a(lw.w_down),
-        })
+        lp: Dict[str, object] = {"bqkv": None if lw.bqkv is None else lw.bqkv.float()[perm].contiguous()}
+        put(lp, "wqkv", fold_gain(lw.wqkv[perm], ga))
+        put(lp, "wo", lw.wo)
+        put(lp, "wgu", interleave_tiles(fold_gain(lw.w_gate, gm), fold_gain(lw.w_up, gm), tile=8))
+        put(lp, "wdown", lw.w_down)
+        layers.append(lp)
         if free_natural:
             lw.wqkv = lw.wo = lw.w_gate = lw.w_up = lw.w_down = None
-    packed = {
-        "layers": layers,
-        "lm_head": pack_mfma_a(fold_gain(mw.lm_head, effective_gain(cfg, mw.final_norm))),
-    }
+    packed: Dict[str, object] = {"layers": layers, "weight_dtype": weight_dtype}
+    put(packed, "wlm_head", fold_gain(mw.lm_head, effective_gain(cfg, mw.final_norm)))
+    packed["lm_head"] = packed.pop("wlm_head")
+    if fp8:
+        packed["lm_head_scale"] = packed.pop("slm_head")
     if free_natural and not cfg.tie_embeddings:
         mw.lm_head = None
     mw.packed = packed

@@ -67,6 +67,8 @@ def load() -> ctypes.CDLL:
                                             + [ci] * 6 + [vp])
         lib.cain_gemm.argtypes = ([vp, vp, ci, ci, ci, ci, vp, ci, vp, ci, cf, vp, vp, vp, vp, vp, vp]
                                   + [ci] * 4 + [vp, ctypes.c_longlong, ci, ci, vp])
+        lib.cain_gemm_w8.argtypes = ([vp, vp, vp, ci, ci, ci, ci, vp, ci, vp, ci, cf, vp, vp, vp, vp, vp, vp]
+                                     + [ci] * 5 + [vp])
         lib.cain_gemm_ws_bytes.restype = ctypes.c_longlong
         lib.cain_gemm_ws_bytes.argtypes = [ci, ci, ci]
         lib.cain_rmsnorm.argtypes = [vp, ci, vp, vp, ci, ci, ci, cf, vp]
@@ -177,6 +179,35 @@ def qkv_rope(wp, x, n, q_out, kc, vtc, slot, pos, cos_t, sin_t, H, Hkv, hd, bias
     rc = _gemm_call(lib, wp, x, K, n, M, q_out, bias, norm, eps, slot, pos, cos_t, sin_t, kc, vtc, H, Hkv, hd,
                     T_max, EPI_QKV_ROPE, waves, batched)
     _check(rc, "qkv_rope")
+
+
+def gemm_w8(wq: torch.Tensor, scale: torch.Tensor, x: torch.Tensor, n: int, epi: int = EPI_BF16, bias=None,
+            out: Optional[torch.Tensor] = None, norm: bool = False, eps: float = 1e-6, rope=None) -> torch.Tensor:
+    """fp8-weight GEMM (``csrc/gemm_w8.hip``, M <= 64): y = epi(B(x) @ (q * scale)^T) with q packed by
+    ``models.weights.pack_mfma_a_fp8`` and ``scale`` the per-row fp32 scales.  Same epilogues and RMSNorm
+    fusion as ``skinny_gemm``; ``rope`` = dict(kc, vtc, slot, pos, cos_t, sin_t, H, Hkv, hd) for
+    ``EPI_QKV_ROPE`` (``out`` is then the Q buffer)."""
+    lib = load()
+    _gpu(wq, scale, x)
+    M, K = x.shape
+    assert x.dtype == torch.bfloat16 and x.stride(1) == 1 and 1 <= M <= 64
+    assert wq.dtype == torch.uint8 and wq.shape[0] * 16 == n and wq.shape[1] * 64 == K, (tuple(wq.shape), K, n)
+    assert scale.dtype == torch.float32 and scale.numel() == n
+    n_out = n // 2 if epi in (EPI_SILU, EPI_GELU) else n
+    if epi == EPI_RESID:
+        assert out is not None and out.shape == (M, n_out), "EPI_RESID updates `out` (the residual) in place"
+    if out is None:
+        out = torch.empty(M, n_out, device=x.device, dtype=torch.float32 if epi == EPI_F32 else torch.bfloat16)
+    r = rope or {}
+    if epi == EPI_QKV_ROPE:
+        assert rope is not None, "EPI_QKV_ROPE needs the rope/cache arguments"
+    T_max = r["kc"].shape[-2] if rope else 0
+    rc = lib.cain_gemm_w8(_p(wq), _p(scale), _p(x), x.stride(0), K, n, M, _p(out), out.stride(0), _p(bias),
+                          int(bool(norm)), eps, _p(r.get("slot")), _p(r.get("pos")), _p(r.get("cos_t")),
+                          _p(r.get("sin_t")), _p(r.get("kc")), _p(r.get("vtc")), r.get("H", 0), r.get("Hkv", 0),
+                          r.get("hd", 0), T_max, epi, _stream())
+    _check(rc, "gemm_w8")
+    return out
 
 
 def rmsnorm(x: torch.Tensor, g: torch.Tensor, eps: float, out: Optional[torch.Tensor] = None) -> torch.Tensor:

@@ -1,0 +1,154 @@
+// GEMM arguments and the fused epilogues shared by the bf16 kernels (gemm.hip) and the fp8-weight kernel
+// (gemm_w8.hip): see gemm.hip's header for what each epilogue does.
+#pragma once
+#include "common.h"
+
+enum { EPI_BF16 = 0, EPI_RESID = 1, EPI_F32 = 2, EPI_SILU = 3, EPI_GELU = 4, EPI_QKV_ROPE = 5 };
+
+struct GemmArgs {
+  const bf16x8* Wp;
+  const __bf16* X;
+  int ldx, K, N, M;
+  int msplit;  // workgroups per row tile, each owning 16*NB of the M rows
+  void* Y;
+  int ldy;
+  const float* bias;
+  // NORM (fused RMSNorm, gain folded into W): acc *= rsqrt(mean(x^2) + eps)
+  float eps;
+  // QKV_ROPE
+  const int* slot;
+  const int* pos;
+  const float* cos_t;
+  const float* sin_t;
+  __bf16* kc;
+  __bf16* vtc;
+  int H, Hkv, hd, T_max;
+};
+
+// Epilogue inputs of one (tile, column-tile, lane) unit, loaded BEFORE the main loop
+// so their latency hides under the weight stream (the residual row, bias, RoPE
+// position / tables).
+struct EpiIn {
+  bf16x4 r;      // EPI_RESID: residual values
+  f32x4 b1, b2;  // bias (QKV: rows n1.. and n2..)
+  f32x4 c, sn;   // QKV: cos / sin of the 4 rotation pairs
+  int p, sl;     // QKV: position, cache slot
+};
+
+// gt = global 16-row tile of N, m = output row of this lane
+template <int EPI>
+__device__ __forceinline__ EpiIn epi_load_at(const GemmArgs& a, int gt, int m, int lane) {
+  EpiIn e{};
+  const int nsub = (lane >> 4) * 4;
+  if (m >= a.M) return e;
+  if constexpr (EPI == EPI_RESID) {
+    e.r = *reinterpret_cast<const bf16x4*>(reinterpret_cast<const __bf16*>(a.Y) + (size_t)m * a.ldy + gt * 16 + nsub);
+  } else if constexpr (EPI == EPI_BF16) {
+    if (a.bias) e.b1 = *reinterpret_cast<const f32x4*>(a.bias + gt * 16 + nsub);
+  } else if constexpr (EPI == EPI_QKV_ROPE) {
+    e.sl = a.slot[m];
+    e.p = a.pos[m];
+    if (a.bias) {
+      e.b1 = *reinterpret_cast<const f32x4*>(a.bias + gt * 16 + nsub);
+      e.b2 = *reinterpret_cast<const f32x4*>(a.bias + gt * 16 + ((nsub + 8) & 15));
+    }
+    const int tph = a.hd >> 4;
+    if (gt < (a.H + a.Hkv) * tph && (lane >> 4) < 2 && e.sl >= 0) {
+      const int half = a.hd >> 1;
+      const int j0 = (gt - (gt / tph) * tph) * 8 + nsub;
+      e.c = *reinterpret_cast<const f32x4*>(a.cos_t + (size_t)e.p * half + j0);
+      e.sn = *reinterpret_cast<const f32x4*>(a.sin_t + (size_t)e.p * half + j0);
+    }
+  }
+  return e;
+}
+
+template <int NT, int NB, int EPI>
+__device__ __forceinline__ EpiIn epi_load(const GemmArgs& a, int tile0, int mo, int u) {
+  const int lane = u & 63, tb = u >> 6, b = tb % NB, t = tb / NB;
+  return epi_load_at<EPI>(a, tile0 + t, mo + b * 16 + (lane & 15), lane);
+}
+
+// Finish and store one 64-unit chunk (one 16x16 output block: n in tile gt, 16 rows m).
+// get(off) returns the final fp32 accumulator of the unit held by lane (lane + off) of the
+// chunk; the pair epilogues read their partner rows (+8 of the tile) at off = 32.
+template <int EPI, class Get>
+__device__ __forceinline__ void epi_store(const GemmArgs& a, int gt, int m, int lane, const EpiIn& e, Get get) {
+  const int nsub = (lane >> 4) * 4;
+  const bool mvalid = m < a.M;
+  if constexpr (EPI == EPI_SILU || EPI == EPI_GELU) {
+    // 8-row interleave: rows 0..7 of a tile are gate rows, rows 8..15 the matching up rows
+    if ((lane >> 4) < 2) {
+      const f32x4 g = get(0);
+      const f32x4 up = get(32);
+      const int n = gt * 8 + nsub;
+      bf16x4 o;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float av = (EPI == EPI_SILU) ? silu_f(g[i]) : gelu_tanh_f(g[i]);
+        o[i] = f2bf(av * up[i]);
+      }
+      if (mvalid) *reinterpret_cast<bf16x4*>(reinterpret_cast<__bf16*>(a.Y) + (size_t)m * a.ldy + n) = o;
+    }
+  } else if constexpr (EPI == EPI_QKV_ROPE) {
+    const int tph = a.hd >> 4;  // tiles per head
+    const int qt = a.H * tph, kt = a.Hkv * tph;
+    const int sl = mvalid ? e.sl : -1;
+    if (gt < qt + kt) {
+      // rows 0..7 of the tile = pair elements j (first half), rows 8..15 = j + hd/2
+      if ((lane >> 4) < 2 && sl >= 0) {
+        const f32x4 x1 = get(0);
+        const f32x4 x2 = get(32);  // partner rows +8 live in lane + 32
+        const int head = gt / tph, it = gt - (gt / tph) * tph;
+        const int half = a.hd >> 1;
+        const int j0 = it * 8 + nsub;  // first pair element of this thread
+        bf16x4 y1, y2;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          // round to bf16 first: the unfused path stores the projection in bf16 before RoPE
+          const float v1 = bf2f(f2bf(x1[i] + e.b1[i]));
+          const float v2 = bf2f(f2bf(x2[i] + e.b2[i]));
+          y1[i] = f2bf(v1 * e.c[i] - v2 * e.sn[i]);
+          y2[i] = f2bf(v2 * e.c[i] + v1 * e.sn[i]);
+        }
+        if (head < a.H) {
+          __bf16* dst = reinterpret_cast<__bf16*>(a.Y) + (size_t)m * a.ldy + head * a.hd;
+          *reinterpret_cast<bf16x4*>(dst + j0) = y1;
+          *reinterpret_cast<bf16x4*>(dst + j0 + half) = y2;
+        } else {
+          // fragment-major K cache (attention.hip): 4 consecutive head dims of one position are contiguous
+          __bf16* kb = a.kc + ((size_t)sl * a.Hkv + (head - a.H)) * a.T_max * a.hd;
+          *reinterpret_cast<bf16x4*>(kb + kfrag_off(e.p, j0, a.hd)) = y1;
+          *reinterpret_cast<bf16x4*>(kb + kfrag_off(e.p, j0 + half, a.hd)) = y2;
+        }
+      }
+    } else if (sl >= 0) {
+      const f32x4 v = get(0);
+      const int vr = (gt - qt - kt) * 16 + nsub;  // row within the V block
+      const int kh = vr / a.hd, d = vr - (vr / a.hd) * a.hd;
+      // fragment-major V^T cache: head dims d..d+3 of position p sit in consecutive lanes (16 B apart)
+      __bf16* dst = a.vtc + ((size_t)sl * a.Hkv + kh) * a.hd * a.T_max + vfrag_off(e.p, d, a.hd);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) dst[i * 8] = f2bf(v[i] + e.b1[i]);
+    }
+  } else {
+    const f32x4 v = get(0);
+    const int n = gt * 16 + nsub;
+    if constexpr (EPI == EPI_F32) {
+      if (mvalid) *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(a.Y) + (size_t)m * a.ldy + n) = v;
+    } else if constexpr (EPI == EPI_BF16) {
+      bf16x4 o;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) o[i] = f2bf(v[i] + e.b1[i]);
+      if (mvalid) *reinterpret_cast<bf16x4*>(reinterpret_cast<__bf16*>(a.Y) + (size_t)m * a.ldy + n) = o;
+    } else {  // EPI_RESID: in-place residual update
+      if (mvalid) {
+        bf16x4 o;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) o[i] = f2bf(v[i] + bf2f(e.r[i]));
+        *reinterpret_cast<bf16x4*>(reinterpret_cast<__bf16*>(a.Y) + (size_t)m * a.ldy + n) = o;
+      }
+    }
+  }
+}
+

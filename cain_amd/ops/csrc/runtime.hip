@@ -26,6 +26,10 @@ CAIN_API int cain_gemm(const void* Wp, const void* X, int ldx, int K, int N, int
                        const float* bias, int norm, float eps, const int* slot, const int* pos,
                        const float* cos_t, const float* sin_t, void* kc, void* vtc, int H, int Hkv, int hd, int T_max,
                        void* ws, long long ws_bytes, int epi, int waves, hipStream_t st);
+CAIN_API int cain_gemm_w8(const void* Wp, const float* wscale, const void* X, int ldx, int K, int N, int M, void* Y,
+                          int ldy, const float* bias, int norm, float eps, const int* slot, const int* pos,
+                          const float* cos_t, const float* sin_t, void* kc, void* vtc, int H, int Hkv, int hd,
+                          int T_max, int epi, hipStream_t st);
 CAIN_API int cain_embed(const int* tok, const void* E, void* out, int ldo, int M, int d, float scale, hipStream_t st);
 CAIN_API int cain_attention(const void* q, const void* kc, const void* vtc, const int* slot, const int* pos,
                             float* part_o, float* part_ml, unsigned* counters, void* out, int ldo, int M, int H,
@@ -44,6 +48,11 @@ struct CainLayer {
   const void* wo;
   const void* wgu;
   const void* wdown;
+  // fp8 weights (CainPlanDesc::w8): per-output-row scales of each packed matrix (null for bf16)
+  const float* sqkv;
+  const float* so;
+  const float* sgu;
+  const float* sdown;
 };
 
 struct CainPlanDesc {
@@ -67,6 +76,8 @@ struct CainPlanDesc {
   unsigned* counters;
   void* gemm_ws;  // batched-GEMM workspace (counters zeroed once + split-K partials), see gemm.hip
   long long gemm_ws_bytes;
+  int w8;                      // 1: fp8 (e4m3) weights with per-row scales, W8A16 kernels (gemm_w8.hip), M <= 64
+  const float* lm_head_scale;  // w8: scales of the packed LM head
 };
 
 struct CainRows {
@@ -105,25 +116,31 @@ int forward(const Plan& p, int M, const CainRows& r, int want_logits, int want_s
   const int qkv_dim = (d.H + 2 * d.Hkv) * d.hd;
   const int q_dim = d.H * d.hd;
   const int epi_act = d.act_kind == 1 ? 4 : 3;
+  // one GEMM of the schedule: the bf16 kernels (gemm.hip) or the fp8-weight ones (gemm_w8.hip)
+  auto gemm = [&](const void* W, const float* ws, const void* X, int ldx, int K, int N, void* Y, int ldy,
+                  const float* bias, int norm, const void* kc, const void* vc, int epi) -> int {
+    if (d.w8)
+      return cain_gemm_w8(W, ws, X, ldx, K, N, M, Y, ldy, bias, norm, d.eps, r.slot, r.pos, d.cos_t, d.sin_t,
+                          const_cast<void*>(kc), const_cast<void*>(vc), d.H, d.Hkv, d.hd, d.T_max, epi, st);
+    return cain_gemm(W, X, ldx, K, N, M, Y, ldy, bias, norm, d.eps, r.slot, r.pos, d.cos_t, d.sin_t,
+                     const_cast<void*>(kc), const_cast<void*>(vc), d.H, d.Hkv, d.hd, d.T_max, d.gemm_ws,
+                     d.gemm_ws_bytes, epi, d.waves, st);
+  };
   CK(cain_embed(r.tok, d.embed, d.x, d.d, M, d.d, d.embed_scale, st));
   for (int l = 0; l < d.n_layers; ++l) {
     const CainLayer& L = p.layers[l];
     __bf16* kc = reinterpret_cast<__bf16*>(d.kcache) + (size_t)l * d.kv_layer_elems;
     __bf16* vc = reinterpret_cast<__bf16*>(d.vtcache) + (size_t)l * d.kv_layer_elems;
-    CK(cain_gemm(L.wqkv, d.x, d.d, d.d, qkv_dim, M, d.q, q_dim, L.bqkv, 1, d.eps, r.slot, r.pos,
-                           d.cos_t, d.sin_t, kc, vc, d.H, d.Hkv, d.hd, d.T_max, d.gemm_ws, d.gemm_ws_bytes, /*EPI_QKV_ROPE*/ 5, d.waves, st));
+    CK(gemm(L.wqkv, L.sqkv, d.x, d.d, d.d, qkv_dim, d.q, q_dim, L.bqkv, 1, kc, vc, /*EPI_QKV_ROPE*/ 5));
     CK(cain_attention(d.q, kc, vc, r.slot, r.pos, d.part_o, d.part_ml, d.counters, d.attn, q_dim, M, d.H, d.Hkv,
                       d.hd, d.T_max, d.nsplit, d.attn_scale, st));
-    CK(cain_gemm(L.wo, d.attn, q_dim, q_dim, d.d, M, d.x, d.d, nullptr, 0, 0.f, nullptr, nullptr,
-                           nullptr, nullptr, nullptr, nullptr, 0, 0, 0, 0, d.gemm_ws, d.gemm_ws_bytes, /*EPI_RESID*/ 1, d.waves, st));
-    CK(cain_gemm(L.wgu, d.x, d.d, d.d, 2 * d.ffn, M, d.act, d.ffn, nullptr, 1, d.eps, nullptr,
-                           nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0, 0, 0, d.gemm_ws, d.gemm_ws_bytes, epi_act, d.waves, st));
-    CK(cain_gemm(L.wdown, d.act, d.ffn, d.ffn, d.d, M, d.x, d.d, nullptr, 0, 0.f, nullptr, nullptr,
-                           nullptr, nullptr, nullptr, nullptr, 0, 0, 0, 0, d.gemm_ws, d.gemm_ws_bytes, /*EPI_RESID*/ 1, d.waves, st));
+    CK(gemm(L.wo, L.so, d.attn, q_dim, q_dim, d.d, d.x, d.d, nullptr, 0, nullptr, nullptr, /*EPI_RESID*/ 1));
+    CK(gemm(L.wgu, L.sgu, d.x, d.d, d.d, 2 * d.ffn, d.act, d.ffn, nullptr, 1, nullptr, nullptr, epi_act));
+    CK(gemm(L.wdown, L.sdown, d.act, d.ffn, d.ffn, d.d, d.x, d.d, nullptr, 0, nullptr, nullptr, /*EPI_RESID*/ 1));
   }
   if (want_logits) {
-    CK(cain_gemm(d.lm_head, d.x, d.d, d.d, d.V, M, d.logits, d.V, nullptr, 1, d.eps, nullptr,
-                           nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0, 0, 0, d.gemm_ws, d.gemm_ws_bytes, /*EPI_F32*/ 2, d.waves, st));
+    CK(gemm(d.lm_head, d.lm_head_scale, d.x, d.d, d.d, d.V, d.logits, d.V, nullptr, 1, nullptr, nullptr,
+            /*EPI_F32*/ 2));
   }
   if (want_sample) {
     CK(cain_sample(d.logits, d.V, d.V, r.tok, r.pos, r.gen, r.ldg, r.n_gen, r.max_new, r.done, r.hist, r.slot,
@@ -149,7 +166,7 @@ CAIN_API void cain_plan_destroy(void* plan) { delete static_cast<Plan*>(plan); }
 CAIN_API int cain_plan_forward(void* plan, int M, const CainRows* rows, int want_logits, int want_sample,
                                hipStream_t st) {
   auto* p = static_cast<Plan*>(plan);
-  if (M < 1 || M > CAIN_MAX_ROWS || M > p->d.Mpad) return -1;
+  if (M < 1 || M > CAIN_MAX_ROWS || M > p->d.Mpad || (p->d.w8 && M > 64)) return -1;
   return forward(*p, M, *rows, want_logits, want_sample, st);
 }
 
@@ -157,7 +174,7 @@ CAIN_API int cain_plan_forward(void* plan, int M, const CainRows* rows, int want
 CAIN_API void* cain_plan_capture(void* plan, int M, const CainRows* rows, int steps, hipStream_t st, int* err) {
   auto* p = static_cast<Plan*>(plan);
   *err = 0;
-  if (M < 1 || M > CAIN_MAX_ROWS || M > p->d.Mpad || steps < 1) {
+  if (M < 1 || M > CAIN_MAX_ROWS || M > p->d.Mpad || (p->d.w8 && M > 64) || steps < 1) {
     *err = -1;
     return nullptr;
   }
