@@ -37,7 +37,7 @@ import torch
 
 from ..models.config import ModelConfig, get_config, rope_inv_freq
 from ..models.tokenizer import SyntheticTokenizer, get_tokenizer
-from ..models.weights import ModelWeights, pack_for_engine, random_weights
+from ..models.weights import ModelWeights, fp8_roundtrip_weights, pack_for_engine, random_weights
 
 #: Ollama's default sampling options (SURVEY §2.4 "Sampling" row)
 OLLAMA_DEFAULTS = dict(temperature=0.8, top_k=40, top_p=0.9, repeat_penalty=1.1, repeat_last_n=64, seed=None)
@@ -177,7 +177,9 @@ class DecodeEngine:
             self._init_hip()
         elif backend == "torch":
             from ..models.reference import ReferenceModel
-            self.ref = ReferenceModel(weights, memo_weights=self.device.type == "cpu")
+            # fp8: the oracle runs on the dequantised weights the fp8 kernels multiply by
+            ref_w = fp8_roundtrip_weights(weights) if weight_dtype == "fp8" else weights
+            self.ref = ReferenceModel(ref_w, memo_weights=self.device.type == "cpu")
         else:
             raise ValueError(f"unknown backend {backend!r}")
         if self.device.type == "cuda":

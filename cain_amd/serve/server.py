@@ -93,8 +93,9 @@ class EngineBackend(Backend):
 
     def __init__(self, models: List[str], device: str = "cuda:0", max_batch: int = 16, max_context: int = 2048,
                  backend: Optional[str] = None, seed: int = 0, preload: bool = False, steps_per_graph: int = 8,
-                 trace_dir: Optional[str] = None):
+                 trace_dir: Optional[str] = None, weight_dtype: str = "bf16"):
         self._models = list(models)
+        self.weight_dtype = weight_dtype
         self.trace_dir = trace_dir
         self._trace_seq = 0
         self.device = device
@@ -125,7 +126,7 @@ class EngineBackend(Backend):
                     raise KeyError(f"model '{model}' not found, try pulling it first")
                 eng = DecodeEngine(model, device=self.device, max_batch=self._max_batch,
                                    max_context=self.max_context, backend=self.backend, seed=self.seed,
-                                   steps_per_graph=self.steps_per_graph)
+                                   steps_per_graph=self.steps_per_graph, weight_dtype=self.weight_dtype)
                 self.engines[model] = eng
             return eng
 
@@ -466,6 +467,8 @@ def main(argv: Optional[List[str]] = None) -> None:
     ap.add_argument("--fake-tok-s", type=float, default=2000.0, help="fake backend: modelled decode rate")
     ap.add_argument("--fake-prefill-s", type=float, default=0.0, help="fake backend: modelled time to first token")
     ap.add_argument("--trace-dir", default=None, help="write a torch.profiler Chrome trace of every decode batch here")
+    ap.add_argument("--weights", choices=["bf16", "fp8"], default="bf16",
+                    help="GEMM weight storage (fp8: e4m3 per-row scaled, W8A16 kernels, batch <= 64)")
     ap.add_argument("-v", "--verbose", action="store_true")
     ns = ap.parse_args(argv)
     models = [m for m in ns.models.split(",") if m]
@@ -476,7 +479,7 @@ def main(argv: Optional[List[str]] = None) -> None:
         be: Backend = FakeBackend(models, tokens_per_s=ns.fake_tok_s, prefill_s=ns.fake_prefill_s)
     else:
         be = EngineBackend(models, device=ns.device, max_batch=ns.max_batch, max_context=ns.max_context,
-                           backend=ns.backend, preload=ns.preload, trace_dir=ns.trace_dir)
+                           backend=ns.backend, preload=ns.preload, trace_dir=ns.trace_dir, weight_dtype=ns.weights)
     srv = make_server(be, ns.host, ns.port, ns.batch_window_ms, ns.verbose)
     print(f"[serve] Ollama-compatible API on http://{ns.host}:{srv.server_address[1]} models={models}", flush=True)
     try:

@@ -59,3 +59,20 @@ def test_tiny_models_fit_w8_kernel_constraints():
     for name in TINY:
         cfg = get_config(name)
         assert cfg.d_model % 64 == 0 and cfg.q_dim % 64 == 0 and cfg.ffn % 64 == 0
+
+
+def test_torch_backend_fp8_uses_dequantised_oracle():
+    from cain_amd.engine import DecodeEngine
+    from cain_amd.models.reference import ReferenceModel
+
+    eng = DecodeEngine("tiny-llama3.1:8b", device="cpu", max_batch=2, max_context=128, seed=2, weight_dtype="fp8")
+    assert eng.backend == "torch" and eng.max_batch == 2 and eng.prefill_chunk == 64
+    got = eng.last_logits(["hello world"])[0]
+    want = ReferenceModel(fp8_roundtrip_weights(eng.weights)).forward(torch.tensor([eng.encode("hello world")]))[0, -1]
+    assert torch.allclose(got.float(), want.float())
+    bf = ReferenceModel(eng.weights).forward(torch.tensor([eng.encode("hello world")]))[0, -1]
+    assert not torch.equal(got.float(), bf.float())  # the fp8 engine is not silently the bf16 model
+    with pytest.raises(ValueError):
+        DecodeEngine("tiny-llama3.1:8b", device="cpu", weight_dtype="int4")
+    big = DecodeEngine("tiny-llama3.1:8b", device="cpu", max_batch=200, max_context=64, weight_dtype="fp8")
+    assert big.max_batch == 64
