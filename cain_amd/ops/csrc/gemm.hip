@@ -372,17 +372,25 @@ __device__ __forceinline__ f32x4 ld_wt(__amdgpu_buffer_rsrc_t r, int byte_off) {
 
 // LB: minimum waves per SIMD the register allocation must allow (4 -> 128 VGPRs, 2 -> 256, 1 -> 512)
 // AR: activation register ring (see the AR branch of the chunk loop)
-template <int NB, int NTW, int W, int CK, int U, int D, int XS, int LB, bool AR, int EPI, bool NORM>
+// WM: wave groups along M.  The W waves form WN = W/WM columns (each owns NTW 16-row tiles of N) times WM
+// rows (each owns NB/WM of the 16-row blocks of M): with WM = 2 and NTW = 2 a wave issues the same MFMAs per
+// slice as WM = 1, NTW = 1 but reads half as many activation fragments from LDS (each feeds 2 tiles); the
+// two wave rows of a tile column load the same weight fragments (the second from L2).
+template <int NB, int NTW, int W, int CK, int U, int D, int XS, int LB, bool AR, int EPI, bool NORM, int WM = 1>
 __global__ __launch_bounds__(W * 64, LB) void bgemm_kernel(const GemmArgs a, const BgArgs bg) {
   constexpr int BG_CK = CK;
   constexpr int FR = BG_CK * NB;        // B fragments per chunk
   constexpr int FPW = FR / W;           // staged per wave per chunk
   constexpr int NGRP = BG_CK / U;       // weight prefetch groups per chunk
-  constexpr int UNITS = W * NTW * NB;   // 64-lane output blocks per workgroup
+  constexpr int WN = W / WM;            // wave columns (N)
+  constexpr int NBW = NB / WM;          // row blocks of M per wave
+  constexpr int UNITS = WN * NTW * NB;  // 64-lane output blocks per workgroup
   static_assert(FR % W == 0 && BG_CK % U == 0, "tiling");
+  static_assert(W % WM == 0 && NB % WM == 0, "wave grid");
   static_assert(UNITS * 1024 <= XS * FR * 1024, "epilogue buffer must fit in the staging buffer");
   static_assert(XS == 2 || XS == 3, "activation stage depth");
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wn = wave % WN, b0 = (wave / WN) * NBW;  // wave column, first row block
   const int KS = a.K >> 5, ntiles = a.N >> 4;
   int blk, kc;
   {
@@ -411,7 +419,7 @@ __global__ __launch_bounds__(W * 64, LB) void bgemm_kernel(const GemmArgs a, con
   const bf16x8* wb[NTW];
 #pragma unroll
   for (int t = 0; t < NTW; ++t) {
-    gt[t] = (blk * W + wave) * NTW + t;
+    gt[t] = (blk * WN + wn) * NTW + t;
     wb[t] = a.Wp + (size_t)min(gt[t], ntiles - 1) * KS * 64 + lane;  // idle tiles re-read a valid one
   }
   auto load_w = [&](int s, int t) -> bf16x8 { return __builtin_nontemporal_load(wb[t] + (size_t)s * 64); };
@@ -468,11 +476,11 @@ __global__ __launch_bounds__(W * 64, LB) void bgemm_kernel(const GemmArgs a, con
     }
   };
 
-  f32x4 acc[NTW][NB];
+  f32x4 acc[NTW][NBW];
 #pragma unroll
   for (int t = 0; t < NTW; ++t)
 #pragma unroll
-    for (int b = 0; b < NB; ++b) acc[t][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int b = 0; b < NBW; ++b) acc[t][b] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   bf16x8 wa[U][NTW];
   bf16x8 xa_[FPW], xb_[FPW];  // activation staging registers (see run_chunk)
@@ -519,39 +527,39 @@ __global__ __launch_bounds__(W * 64, LB) void bgemm_kernel(const GemmArgs a, con
     if constexpr (NB >= 16) {
       // 256 rows: a P-deep ring over the group's (slice, row block) fragment sequence instead of a whole
       // second slice of fragments (2 x 16 fragments do not fit beside the 256-row accumulators)
-      constexpr int NF = U * NB, P = 4;
+      constexpr int NF = U * NBW, P = 4;
       bf16x8 q[P];
 #pragma unroll
-      for (int i = 0; i < P; ++i) q[i] = frag(buf, h * U + i / NB, i % NB);
+      for (int i = 0; i < P; ++i) q[i] = frag(buf, h * U + i / NBW, b0 + i % NBW);
       bf16x8 w[NTW];
 #pragma unroll
       for (int i = 0; i < NF; ++i) {
-        const int u = i / NB, b = i % NB;
+        const int u = i / NBW, b = i % NBW;
         if (b == 0) {
 #pragma unroll
           for (int t = 0; t < NTW; ++t) w[t] = __builtin_bit_cast(bf16x8, __builtin_bit_cast(u32x4, cur[u][t]) & keep);
         }
         const bf16x8 x = q[i % P];
-        if (i + P < NF) q[i % P] = frag(buf, h * U + (i + P) / NB, (i + P) % NB);
+        if (i + P < NF) q[i % P] = frag(buf, h * U + (i + P) / NBW, b0 + (i + P) % NBW);
 #pragma unroll
         for (int t = 0; t < NTW; ++t) acc[t][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[t], x, acc[t][b], 0, 0, 0);
       }
     } else {
-      bf16x8 xf[2][NB];
+      bf16x8 xf[2][NBW];
 #pragma unroll
-      for (int b = 0; b < NB; ++b) xf[0][b] = frag(buf, h * U, b);
+      for (int b = 0; b < NBW; ++b) xf[0][b] = frag(buf, h * U, b0 + b);
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         if (u + 1 < U) {
 #pragma unroll
-          for (int b = 0; b < NB; ++b) xf[(u + 1) & 1][b] = frag(buf, h * U + u + 1, b);
+          for (int b = 0; b < NBW; ++b) xf[(u + 1) & 1][b] = frag(buf, h * U + u + 1, b0 + b);
         }
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int t = 0; t < NTW; ++t) {
           const bf16x8 w = __builtin_bit_cast(bf16x8, __builtin_bit_cast(u32x4, cur[u][t]) & keep);
 #pragma unroll
-          for (int b = 0; b < NB; ++b)
+          for (int b = 0; b < NBW; ++b)
             acc[t][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w, xf[u & 1][b], acc[t][b], 0, 0, 0);
         }
         __builtin_amdgcn_sched_barrier(0);
@@ -661,13 +669,14 @@ __global__ __launch_bounds__(W * 64, LB) void bgemm_kernel(const GemmArgs a, con
       if (lane % PPR == 0) atomicAdd(&s_ss[RPI * (wave + W * i) + lane / PPR], x);
     }
   }
-  // the staging buffer becomes the epilogue buffer: red[unit][lane], unit = (wave*NTW + t)*NB + b
+  // the staging buffer becomes the epilogue buffer: red[unit][lane], unit = (wn*NTW + t)*NB + b0 + b
   f32x4* red = reinterpret_cast<f32x4*>(&xs[0][0][0]);
+  auto unit = [&](int t, int b) { return (wn * NTW + t) * NB + b0 + b; };
   if (bg.ksplit == 1) {
 #pragma unroll
     for (int t = 0; t < NTW; ++t)
 #pragma unroll
-      for (int b = 0; b < NB; ++b) red[((wave * NTW + t) * NB + b) * 64 + lane] = acc[t][b];
+      for (int b = 0; b < NBW; ++b) red[unit(t, b) * 64 + lane] = acc[t][b];
     __syncthreads();
     if constexpr (NORM) {
       if (threadIdx.x < NB * 16) s_inv[threadIdx.x] = rsqrtf(s_ss[threadIdx.x] / float(a.K) + a.eps);
@@ -679,7 +688,7 @@ __global__ __launch_bounds__(W * 64, LB) void bgemm_kernel(const GemmArgs a, con
 #pragma unroll
     for (int t = 0; t < NTW; ++t)
 #pragma unroll
-      for (int b = 0; b < NB; ++b) st_wt(mine_r, (((wave * NTW + t) * NB + b) * 64 + lane) * 16, acc[t][b]);
+      for (int b = 0; b < NBW; ++b) st_wt(mine_r, (unit(t, b) * 64 + lane) * 16, acc[t][b]);
     if constexpr (NORM) {
       __syncthreads();  // s_ss complete
       if (threadIdx.x < NB * 16)
@@ -695,38 +704,37 @@ __global__ __launch_bounds__(W * 64, LB) void bgemm_kernel(const GemmArgs a, con
     if (s_ticket != unsigned(bg.ksplit - 1)) return;
     // sum the k-range partials, RB ranges x NTW*NB units of loads in flight per round trip (RB x NTW*NB
     // f32x4 registers: 2 ranges at 8 units keeps the 128-row variants inside 128 VGPRs)
-    constexpr int RB = NTW * NB >= 16 ? 1 : (NTW * NB >= 8 ? 2 : 4);
+    constexpr int RB = NTW * NBW >= 16 ? 1 : (NTW * NBW >= 8 ? 2 : 4);
     const __amdgpu_buffer_rsrc_t base_r = slab_rsrc(bg.part + pb * (size_t)UNITS * 256);
-    f32x4 sum[NTW][NB];
+    f32x4 sum[NTW][NBW];
 #pragma unroll
     for (int t = 0; t < NTW; ++t)
 #pragma unroll
-      for (int b = 0; b < NB; ++b) sum[t][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int b = 0; b < NBW; ++b) sum[t][b] = f32x4{0.f, 0.f, 0.f, 0.f};
     for (int k0 = 0; k0 < bg.ksplit; k0 += RB) {
       // every load issued unconditionally (a clamped range index; the surplus weighted 0): a select between a
       // load and a constant made hipcc branch around each load and wait for it alone
-      f32x4 l[RB][NTW][NB];
+      f32x4 l[RB][NTW][NBW];
 #pragma unroll
       for (int j = 0; j < RB; ++j)
 #pragma unroll
         for (int t = 0; t < NTW; ++t)
 #pragma unroll
-          for (int b = 0; b < NB; ++b)
-            l[j][t][b] = ld_wt(base_r, min(k0 + j, bg.ksplit - 1) * (UNITS * 1024) +
-                                           (((wave * NTW + t) * NB + b) * 64 + lane) * 16);
+          for (int b = 0; b < NBW; ++b)
+            l[j][t][b] = ld_wt(base_r, min(k0 + j, bg.ksplit - 1) * (UNITS * 1024) + (unit(t, b) * 64 + lane) * 16);
 #pragma unroll
       for (int j = 0; j < RB; ++j) {
         const float wj = (k0 + j < bg.ksplit) ? 1.f : 0.f;
 #pragma unroll
         for (int t = 0; t < NTW; ++t)
 #pragma unroll
-          for (int b = 0; b < NB; ++b) sum[t][b] += wj * l[j][t][b];
+          for (int b = 0; b < NBW; ++b) sum[t][b] += wj * l[j][t][b];
       }
     }
 #pragma unroll
     for (int t = 0; t < NTW; ++t)
 #pragma unroll
-      for (int b = 0; b < NB; ++b) red[((wave * NTW + t) * NB + b) * 64 + lane] = sum[t][b];
+      for (int b = 0; b < NBW; ++b) red[unit(t, b) * 64 + lane] = sum[t][b];
     if constexpr (NORM) {
       if (threadIdx.x < NB * 16) {
         float x = 0.f;
@@ -745,13 +753,13 @@ __global__ __launch_bounds__(W * 64, LB) void bgemm_kernel(const GemmArgs a, con
   for (int t = 0; t < NTW; ++t) {
     if (gt[t] >= ntiles) continue;
 #pragma unroll
-    for (int b = 0; b < NB; ++b) {
-      const int ub = ((wave * NTW + t) * NB + b) * 64;
-      const int m = b * 16 + (lane & 15);
+    for (int b = 0; b < NBW; ++b) {
+      const int ub = unit(t, b) * 64;
+      const int m = (b0 + b) * 16 + (lane & 15);
       const EpiIn e = epi_load_at<EPI>(a, gt[t], m, lane);
       epi_store<EPI>(a, gt[t], m, lane, e, [&](int off) {
         f32x4 v = red[ub + lane + off];
-        if constexpr (NORM) v *= s_inv[b * 16 + ((lane + off) & 15)];
+        if constexpr (NORM) v *= s_inv[(b0 + b) * 16 + ((lane + off) & 15)];
         return v;
       });
     }
@@ -760,6 +768,7 @@ __global__ __launch_bounds__(W * 64, LB) void bgemm_kernel(const GemmArgs a, con
 
 struct BgPlan {
   int nb, ntw, w, ck, nblk, ksplit, kspl;
+  int wm;  // wave rows along M (1, or 2 with NTW = 2: half the LDS fragment reads per MFMA)
   int d;  // 128-row bodies: weight register-ring depth (0 = the default ping-pong / 4-deep ring)
   size_t part_floats, ss_floats;
 };
@@ -782,7 +791,9 @@ static BgPlan bgemm_plan(int N, int K, int M, int ntw_req) {
   static const int w_env = env_int("CAIN_BGEMM_W", 0);
   static const int ck_env = env_int("CAIN_BGEMM_CK", 0);
   static const int d_env = env_int("CAIN_BGEMM_D", -1);
+  static const int wm_env = env_int("CAIN_BGEMM_WM", 1);
   BgPlan p{};
+  p.wm = 1;
   p.nb = M <= 32 ? 2 : (M <= 64 ? 4 : (M <= 128 ? 8 : 16));
   const int rows1 = 16 * BG_WAVES;
   p.ntw = p.nb >= 8 ? 1 : (ntw_req > 0 ? ntw_req : ((N + rows1 - 1) / rows1 >= 512 ? 2 : 1));
@@ -796,12 +807,14 @@ static BgPlan bgemm_plan(int N, int K, int M, int ntw_req) {
     // measured 10-20 % slower on every shape, profiles/bgemm_r1.md)
     p.w = 8;
     p.ck = 4;
+    if (wm_env == 2) p.wm = 2, p.ntw = 2;
   } else if (p.nb == 8) {
     // 128 rows: 4-slice chunks keep the double-buffered stage at 64 KiB (2 workgroups per CU)
     p.ck = p.w == 8 && ck_env == 8 ? 8 : 4;
     // activation + weight register rings, depth 4, on the 4-wave (narrow-output) bodies; CAIN_BGEMM_D = 4 also on
     // the 8-wave ones, any other value: off (depths 6 and 8 measured slower, profiles/bgemm_r1.md)
     if (p.ck == 4) p.d = d_env == 4 ? 4 : (d_env < 0 && p.w == 4 ? 4 : 0);
+    if (wm_env == 2 && p.w == 8 && p.ck == 4) p.wm = 2, p.ntw = 2, p.d = 0;
   }
   else
   {
@@ -812,7 +825,7 @@ static BgPlan bgemm_plan(int N, int K, int M, int ntw_req) {
            : (ck_env == 16 && p.ntw == 1 && (K / 32) % 16 == 0) ? 16
            : (p.ntw == 1 && (ck_env == 4 || (ck_env == 0 && mid))) ? 4 : BG_CK;
   }
-  const int rows = 16 * p.w * p.ntw;
+  const int rows = 16 * (p.w / p.wm) * p.ntw;
   p.nblk = (N + rows - 1) / rows;
   const int nchunk = (K / 32) / p.ck;
   const int target = target_env > 0 ? target_env : (K > 4096 ? 256 : 128);
@@ -822,7 +835,7 @@ static BgPlan bgemm_plan(int N, int K, int M, int ntw_req) {
   p.ksplit = ks;
   p.kspl = cpw * p.ck;
   if (ks > 1) {
-    p.part_floats = (size_t)p.nblk * ks * p.w * p.ntw * p.nb * 64 * 4;
+    p.part_floats = (size_t)p.nblk * ks * (p.w / p.wm) * p.ntw * p.nb * 64 * 4;
     p.ss_floats = (size_t)p.nblk * ks * p.nb * 16;
   }
   return p;
@@ -834,9 +847,11 @@ static size_t bgemm_ws_bytes(const BgPlan& p) {
   return BG_COUNTER_BYTES + (p.part_floats + p.ss_floats) * sizeof(float);
 }
 
-template <int NB, int NTW, int W, int CK, int EPI, bool NORM, int DD>
+template <int NB, int NTW, int W, int CK, int EPI, bool NORM, int DD, int WM>
 static hipError_t bg_launch(const GemmArgs& a, const BgArgs& b, int nblk, hipStream_t st) {
-  constexpr int U = 4;  // slices per weight prefetch group
+  // slices per weight prefetch group (2 on the 256-row fused-norm bodies: with 4 they spill; two groups
+  // per chunk also let one activation staging register set serve every chunk)
+  constexpr int U = (NB == 16 && NORM) ? 2 : 4;
   // register sets of weight prefetch: 4-wave workgroups (narrow outputs, 2 waves per SIMD, 256-VGPR
   // budget) keep 3 groups in flight, the rest ping-pong between 2 (so do the fused-norm 4-wave bodies,
   // whose 8 staged fragments per wave leave no room for the deeper ring).  DD > 0 (128-row bodies): a
@@ -848,20 +863,20 @@ static hipError_t bg_launch(const GemmArgs& a, const BgArgs& b, int nblk, hipStr
   // (the 128-row 8-wave body needs 256 VGPRs for its double-buffered LDS fragments: 1 workgroup per CU)
   constexpr int LB = (DD > 0 || NB >= 16) ? (W == 4 ? 1 : 2) : ((W == 8 && NTW == 1 && NB < 8 && CK * NB <= 32) ? 4 : 2);
   constexpr bool AR = DD > 0;  // explicit depth: the activation + weight register rings
-  hipLaunchKernelGGL((bgemm_kernel<NB, NTW, W, CK, U, D, AR ? 2 : XS, LB, AR, EPI, NORM>), dim3(nblk * b.ksplit),
+  hipLaunchKernelGGL((bgemm_kernel<NB, NTW, W, CK, U, D, AR ? 2 : XS, LB, AR, EPI, NORM, WM>), dim3(nblk * b.ksplit),
                      dim3(W * 64), 0, st, a, b);
   return hipGetLastError();
 }
 
-template <int NB, int NTW, int W, int CK, bool NORM, int DD = 0>
+template <int NB, int NTW, int W, int CK, bool NORM, int DD = 0, int WM = 1>
 static hipError_t bg_launch_e(int epi, const GemmArgs& a, const BgArgs& b, int nblk, hipStream_t st) {
   switch (epi) {
-    case EPI_BF16: return bg_launch<NB, NTW, W, CK, EPI_BF16, NORM, DD>(a, b, nblk, st);
-    case EPI_RESID: return bg_launch<NB, NTW, W, CK, EPI_RESID, NORM, DD>(a, b, nblk, st);
-    case EPI_F32: return bg_launch<NB, NTW, W, CK, EPI_F32, NORM, DD>(a, b, nblk, st);
-    case EPI_SILU: return bg_launch<NB, NTW, W, CK, EPI_SILU, NORM, DD>(a, b, nblk, st);
-    case EPI_GELU: return bg_launch<NB, NTW, W, CK, EPI_GELU, NORM, DD>(a, b, nblk, st);
-    case EPI_QKV_ROPE: return bg_launch<NB, NTW, W, CK, EPI_QKV_ROPE, NORM, DD>(a, b, nblk, st);
+    case EPI_BF16: return bg_launch<NB, NTW, W, CK, EPI_BF16, NORM, DD, WM>(a, b, nblk, st);
+    case EPI_RESID: return bg_launch<NB, NTW, W, CK, EPI_RESID, NORM, DD, WM>(a, b, nblk, st);
+    case EPI_F32: return bg_launch<NB, NTW, W, CK, EPI_F32, NORM, DD, WM>(a, b, nblk, st);
+    case EPI_SILU: return bg_launch<NB, NTW, W, CK, EPI_SILU, NORM, DD, WM>(a, b, nblk, st);
+    case EPI_GELU: return bg_launch<NB, NTW, W, CK, EPI_GELU, NORM, DD, WM>(a, b, nblk, st);
+    case EPI_QKV_ROPE: return bg_launch<NB, NTW, W, CK, EPI_QKV_ROPE, NORM, DD, WM>(a, b, nblk, st);
     default: return hipErrorInvalidValue;
   }
 }
@@ -869,8 +884,10 @@ static hipError_t bg_launch_e(int epi, const GemmArgs& a, const BgArgs& b, int n
 template <int NB, bool NORM>
 static hipError_t bg_launch_shape(int epi, const BgPlan& p, const GemmArgs& a, const BgArgs& b, hipStream_t st) {
   if constexpr (NB == 16) {
+    if (p.wm == 2) return bg_launch_e<16, 2, 8, 4, NORM, 0, 2>(epi, a, b, p.nblk, st);
     return bg_launch_e<16, 1, 8, 4, NORM>(epi, a, b, p.nblk, st);
   } else if constexpr (NB == 8) {
+    if (p.wm == 2) return bg_launch_e<8, 2, 8, 4, NORM, 0, 2>(epi, a, b, p.nblk, st);
     // register rings for activations AND weights (AR) of depth p.d; not for the fused-norm bodies, whose
     // staging sums of squares make the rings spill (profiles/bgemm_r1.md)
     if constexpr (!NORM) {
