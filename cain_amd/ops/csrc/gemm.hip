@@ -527,7 +527,7 @@ __global__ __launch_bounds__(W * 64, LB) void bgemm_kernel(const GemmArgs a, con
     if constexpr (NB >= 16) {
       // 256 rows: a P-deep ring over the group's (slice, row block) fragment sequence instead of a whole
       // second slice of fragments (2 x 16 fragments do not fit beside the 256-row accumulators)
-      constexpr int NF = U * NBW, P = 4;
+      constexpr int NF = U * NBW, P = W == 16 ? 2 : 4;
       bf16x8 q[P];
 #pragma unroll
       for (int i = 0; i < P; ++i) q[i] = frag(buf, h * U + i / NBW, b0 + i % NBW);
@@ -704,7 +704,7 @@ __global__ __launch_bounds__(W * 64, LB) void bgemm_kernel(const GemmArgs a, con
     if (s_ticket != unsigned(bg.ksplit - 1)) return;
     // sum the k-range partials, RB ranges x NTW*NB units of loads in flight per round trip (RB x NTW*NB
     // f32x4 registers: 2 ranges at 8 units keeps the 128-row variants inside 128 VGPRs)
-    constexpr int RB = NTW * NBW >= 16 ? 1 : (NTW * NBW >= 8 ? 2 : 4);
+    constexpr int RB = (NTW * NBW >= 16 || W == 16) ? 1 : (NTW * NBW >= 8 ? 2 : 4);
     const __amdgpu_buffer_rsrc_t base_r = slab_rsrc(bg.part + pb * (size_t)UNITS * 256);
     f32x4 sum[NTW][NBW];
 #pragma unroll
@@ -808,6 +808,8 @@ static BgPlan bgemm_plan(int N, int K, int M, int ntw_req) {
     p.w = 8;
     p.ck = 4;
     if (wm_env == 2) p.wm = 2, p.ntw = 2;
+    // 16 waves as 8 columns x 2 rows, one tile each: 4 waves per SIMD (128 VGPRs) to hide the weight latency
+    if (wm_env == 3) p.wm = 2, p.ntw = 1, p.w = 16;
   } else if (p.nb == 8) {
     // 128 rows: 4-slice chunks keep the double-buffered stage at 64 KiB (2 workgroups per CU)
     p.ck = p.w == 8 && ck_env == 8 ? 8 : 4;
@@ -851,7 +853,7 @@ template <int NB, int NTW, int W, int CK, int EPI, bool NORM, int DD, int WM>
 static hipError_t bg_launch(const GemmArgs& a, const BgArgs& b, int nblk, hipStream_t st) {
   // slices per weight prefetch group (2 on the 256-row fused-norm bodies: with 4 they spill; two groups
   // per chunk also let one activation staging register set serve every chunk)
-  constexpr int U = (NB == 16 && NORM) ? 2 : 4;
+  constexpr int U = (NB == 16 && (NORM || W == 16)) ? 2 : 4;
   // register sets of weight prefetch: 4-wave workgroups (narrow outputs, 2 waves per SIMD, 256-VGPR
   // budget) keep 3 groups in flight, the rest ping-pong between 2 (so do the fused-norm 4-wave bodies,
   // whose 8 staged fragments per wave leave no room for the deeper ring).  DD > 0 (128-row bodies): a
@@ -861,7 +863,9 @@ static hipError_t bg_launch(const GemmArgs& a, const BgArgs& b, int nblk, hipStr
   // three activation stages for the 4-wave bodies (one workgroup per CU on the narrow grids anyway)
   constexpr int XS = (W == 4 && CK == U && NB < 16) ? 3 : 2;  // 256-row stages are 64 KiB each
   // (the 128-row 8-wave body needs 256 VGPRs for its double-buffered LDS fragments: 1 workgroup per CU)
-  constexpr int LB = (DD > 0 || NB >= 16) ? (W == 4 ? 1 : 2) : ((W == 8 && NTW == 1 && NB < 8 && CK * NB <= 32) ? 4 : 2);
+  constexpr int LB = W == 16 ? 4
+                     : (DD > 0 || NB >= 16) ? (W == 4 ? 1 : 2)
+                     : ((W == 8 && NTW == 1 && NB < 8 && CK * NB <= 32) ? 4 : 2);
   constexpr bool AR = DD > 0;  // explicit depth: the activation + weight register rings
   hipLaunchKernelGGL((bgemm_kernel<NB, NTW, W, CK, U, D, AR ? 2 : XS, LB, AR, EPI, NORM, WM>), dim3(nblk * b.ksplit),
                      dim3(W * 64), 0, st, a, b);
@@ -884,6 +888,7 @@ static hipError_t bg_launch_e(int epi, const GemmArgs& a, const BgArgs& b, int n
 template <int NB, bool NORM>
 static hipError_t bg_launch_shape(int epi, const BgPlan& p, const GemmArgs& a, const BgArgs& b, hipStream_t st) {
   if constexpr (NB == 16) {
+    if (p.wm == 2 && p.w == 16) return bg_launch_e<16, 1, 16, 4, NORM, 0, 2>(epi, a, b, p.nblk, st);
     if (p.wm == 2) return bg_launch_e<16, 2, 8, 4, NORM, 0, 2>(epi, a, b, p.nblk, st);
     return bg_launch_e<16, 1, 8, 4, NORM>(epi, a, b, p.nblk, st);
   } else if constexpr (NB == 8) {
