@@ -76,7 +76,8 @@ def build_kernels(force: bool = False, verbose: bool = False, jobs: int = 0) -> 
         objs = list(ex.map(compile_one, srcs))
     if force or _stale(KLIB, objs):
         tmp = str(KLIB) + ".tmp"
-        cmd = [cc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + [str(o) for o in objs]
+        cmd = ([cc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + [str(o) for o in objs]
+               + [f"-L{ROCM}/lib", f"-Wl,-rpath,{ROCM}/lib", "-lhipblaslt"])  # blas.hip: the M >= 128 library path
         if verbose:
             print(" ".join(cmd), flush=True)
         subprocess.run(cmd, check=True)

@@ -100,9 +100,25 @@ def _row_options(opts: Optional[Dict], cfg: ModelConfig, index: int, base_seed: 
                 seed=int(seed) & 0xFFFFFFFFFFFFFFFF)
 
 
+LT_WS_BYTES = 64 << 20  # hipBLASLt workspace of the wide-batch path
+
+
+def lt_min_rows(max_batch: int, weight_dtype: str = "bf16") -> int:
+    """Row count from which a forward runs its O and gate/up projections on hipBLASLt (0: never).
+
+    128 by default: hipBLASLt wins both projections from 128 rows up and loses gate/up at 64
+    (profiles/bgemm_sweep.md, profiles/lt_gemm.md).  ``CAIN_LT_MIN_ROWS`` overrides (0 disables); the fp8
+    weight path has no library equivalent."""
+    v = int(os.environ.get("CAIN_LT_MIN_ROWS", "128"))
+    if v <= 0 or weight_dtype != "bf16" or max_batch < v:
+        return 0
+    return v
+
+
 # ============================================================== ctypes structs
 class _CainLayer(ctypes.Structure):
-    _fields_ = [(n, ctypes.c_void_p) for n in ("wqkv", "bqkv", "wo", "wgu", "wdown", "sqkv", "so", "sgu", "sdown")]
+    _fields_ = [(n, ctypes.c_void_p) for n in ("wqkv", "bqkv", "wo", "wgu", "wdown", "sqkv", "so", "sgu", "sdown",
+                                                  "wo_lt", "wgu_lt")]
 
 
 class _CainPlanDesc(ctypes.Structure):
@@ -113,7 +129,9 @@ class _CainPlanDesc(ctypes.Structure):
                 + [("kv_layer_elems", ctypes.c_longlong)]
                 + [(n, ctypes.c_void_p) for n in ("cos_t", "sin_t", "x", "q", "attn", "act", "logits",
                                                  "part_o", "part_ml", "counters", "gemm_ws")]
-                + [("gemm_ws_bytes", ctypes.c_longlong), ("w8", ctypes.c_int), ("lm_head_scale", ctypes.c_void_p)])
+                + [("gemm_ws_bytes", ctypes.c_longlong), ("w8", ctypes.c_int), ("lm_head_scale", ctypes.c_void_p)]
+                + [("lt_min_rows", ctypes.c_int), ("gu", ctypes.c_void_p), ("lt_ws", ctypes.c_void_p),
+                   ("lt_ws_bytes", ctypes.c_longlong)])
 
 
 class _CainRows(ctypes.Structure):
@@ -196,7 +214,12 @@ class DecodeEngine:
         cfg, dev = self.cfg, self.device
         if self.device.type != "cuda":
             raise ValueError("hip backend needs a GPU device")
-        packed = pack_for_engine(self.weights, free_natural=not self.keep_natural, weight_dtype=self.weight_dtype)
+        # O and gate/up projections of forwards with >= lt_rows rows go through hipBLASLt (ops/csrc/blas.hip:
+        # 23 vs 39 us and 66 vs 103 us at 256 rows on llama3.1:8b, profiles/lt_gemm.md); it needs plain
+        # row-major copies of those two weights beside the MFMA packing
+        lt_rows = lt_min_rows(self.max_batch, self.weight_dtype)
+        packed = pack_for_engine(self.weights, free_natural=not self.keep_natural, weight_dtype=self.weight_dtype,
+                                 plain_lt=lt_rows > 0)
         torch.cuda.synchronize(dev)
         S, T, L = self.max_batch, self.T_max, cfg.n_layers
         bf = torch.bfloat16
@@ -229,7 +252,8 @@ class DecodeEngine:
         self._layers = (_CainLayer * L)()
         for i, lp in enumerate(packed["layers"]):
             self._layers[i] = _CainLayer(*(_ptr(lp.get(k)) for k in ("wqkv", "bqkv", "wo", "wgu", "wdown",
-                                                                     "sqkv", "so", "sgu", "sdown")))
+                                                                     "sqkv", "so", "sgu", "sdown", "wo_lt",
+                                                                     "wgu_lt")))
         self._packed = packed
         d = _CainPlanDesc()
         d.n_layers, d.d, d.H, d.Hkv, d.hd = L, cfg.d_model, cfg.n_heads, cfg.n_kv_heads, cfg.head_dim
@@ -252,6 +276,11 @@ class DecodeEngine:
         self.gemm_ws = torch.zeros(max(ws, 16) // 4 + 1, device=dev, dtype=torch.int32)
         d.gemm_ws, d.gemm_ws_bytes = _ptr(self.gemm_ws), ws
         d.w8, d.lm_head_scale = int(self.weight_dtype == "fp8"), _ptr(packed.get("lm_head_scale"))
+        d.lt_min_rows = lt_rows
+        if lt_rows > 0:
+            self.gu = z(R, 2 * cfg.ffn)
+            self.lt_ws = torch.zeros(LT_WS_BYTES // 4, device=dev, dtype=torch.int32)
+            d.gu, d.lt_ws, d.lt_ws_bytes = _ptr(self.gu), _ptr(self.lt_ws), LT_WS_BYTES
         self._desc = d
         self._plans: Dict[int, int] = {}
         self._graphs: Dict[tuple, int] = {}

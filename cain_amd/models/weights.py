@@ -194,7 +194,8 @@ def fp8_roundtrip_weights(mw: ModelWeights) -> ModelWeights:
     return ModelWeights(mw.cfg, mw.embed, mw.final_norm, rt(mw.lm_head), layers)
 
 
-def pack_for_engine(mw: ModelWeights, free_natural: bool = False, weight_dtype: str = "bf16") -> Dict[str, object]:
+def pack_for_engine(mw: ModelWeights, free_natural: bool = False, weight_dtype: str = "bf16",
+                    plain_lt: bool = False) -> Dict[str, object]:
     """Build the decode engine's packed tensors (see module doc); norm gains are folded into the GEMM
     weights they feed (attn_norm -> wqkv, mlp_norm -> gate/up, final_norm -> lm_head).
 
@@ -220,7 +221,10 @@ def pack_for_engine(mw: ModelWeights, free_natural: bool = False, weight_dtype: 
         lp: Dict[str, object] = {"bqkv": None if lw.bqkv is None else lw.bqkv.float()[perm].contiguous()}
         put(lp, "wqkv", fold_gain(lw.wqkv[perm], ga))
         put(lp, "wo", lw.wo)
-        put(lp, "wgu", interleave_tiles(fold_gain(lw.w_gate, gm), fold_gain(lw.w_up, gm), tile=8))
+        wgu = interleave_tiles(fold_gain(lw.w_gate, gm), fold_gain(lw.w_up, gm), tile=8)
+        put(lp, "wgu", wgu)
+        if plain_lt and not fp8:
+            lp["wo_lt"], lp["wgu_lt"] = lw.wo.contiguous(), wgu.contiguous()
         put(lp, "wdown", lw.w_down)
         layers.append(lp)
         if free_natural:

@@ -13,6 +13,8 @@ op                     source                      replaces (Ollama/llama.cpp)
 ``skinny_gemm``        csrc/gemm.hip               O / gate-up(+act) / down / LM head GEMV,
                                                    fused RMSNorm, residual epilogue
 ``qkv_rope``           csrc/gemm.hip               QKV GEMV + bias + RoPE + KV-cache append
+``lt_gemm``            csrc/blas.hip               O / gate-up GEMM at >= 128 rows (hipBLASLt)
+``rownorm_act``        csrc/blas.hip               RMSNorm scale + SiLU/GeLU*up after lt_gemm
 ``rmsnorm``            csrc/norm.hip               RMSNorm (standalone; the engine fuses it)
 ``embed``              csrc/norm.hip               embedding gather (+Gemma scale)
 ``attention``          csrc/attention.hip          decode / prefill attention (split-K, in-kernel combine)
@@ -71,6 +73,9 @@ def load() -> ctypes.CDLL:
                                      + [ci] * 5 + [vp])
         lib.cain_gemm_ws_bytes.restype = ctypes.c_longlong
         lib.cain_gemm_ws_bytes.argtypes = [ci, ci, ci]
+        lib.cain_lt_gemm.argtypes = [vp, vp, ci, ci, ci, ci, vp, ci, ci, vp, ctypes.c_longlong, vp]
+        lib.cain_lt_prepare.argtypes = [ci, ci, ci, ci, ci, ci, ctypes.c_longlong]
+        lib.cain_rownorm_act.argtypes = [vp, ci, ci, cf, ci, vp, ci, vp, ci, ci, ci, ci, vp]
         lib.cain_rmsnorm.argtypes = [vp, ci, vp, vp, ci, ci, ci, cf, vp]
         lib.cain_embed.argtypes = [vp, vp, vp, ci, ci, ci, cf, vp]
         lib.cain_attention.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp, ci, ci, ci, ci, ci, ci, ci, cf, vp]
@@ -321,3 +326,39 @@ def sample(logits, tok, pos, gen, n_gen, max_new, done, hist, slot, params, T_ma
     M, V = logits.shape[0], logits.shape[1]
     _check(lib.cain_sample(_p(logits), logits.stride(0), V, _p(tok), _p(pos), _p(gen), gen.stride(0), _p(n_gen),
                            _p(max_new), _p(done), _p(hist), _p(slot), T_max, M, _p(params), _stream()), "sample")
+
+
+_LT_WS: dict = {}
+
+
+def lt_gemm(w: torch.Tensor, x: torch.Tensor, out: Optional[torch.Tensor] = None,
+            accumulate: bool = False) -> torch.Tensor:
+    """``out = x @ w.T`` (``out += x @ w.T`` with ``accumulate``) on hipBLASLt: w [N, K], x [M, K] bf16
+    row-major; the engine's wide-batch O and gate/up projections (csrc/blas.hip)."""
+    _gpu(w, x, out)
+    N, K = w.shape
+    M = x.shape[0]
+    if out is None:
+        out = torch.empty(M, N, device=x.device, dtype=torch.bfloat16)
+    assert w.is_contiguous() and x.stride(1) == 1 and out.stride(1) == 1 and x.shape[1] == K
+    ws = _LT_WS.get(x.device)
+    if ws is None:
+        ws = _LT_WS[x.device] = torch.zeros((64 << 20) // 4, device=x.device, dtype=torch.int32)
+    _check(load().cain_lt_gemm(_p(w), _p(x), x.stride(0), K, N, M, _p(out), out.stride(0), int(accumulate), _p(ws),
+                               ws.numel() * 4, _stream()), "cain_lt_gemm")
+    return out
+
+
+def rownorm_act(x: torch.Tensor, gu: torch.Tensor, eps: float, kind: int = 0, norm: bool = True,
+                out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``act = f(s*gate) * (s*up)`` from an 8-row-interleaved gate/up GEMM output ``gu`` [M, 2 ffn]
+    (s = rsqrt(mean(x^2) + eps) per row when ``norm``; kind 0 SiLU, 1 tanh-GeLU)."""
+    _gpu(x, gu, out)
+    M, d = x.shape
+    ffn = gu.shape[1] // 2
+    if out is None:
+        out = torch.empty(M, ffn, device=x.device, dtype=torch.bfloat16)
+    assert x.stride(1) == 1 and gu.stride(1) == 1 and out.stride(1) == 1 and gu.shape[0] == M
+    _check(load().cain_rownorm_act(_p(x), x.stride(0), d, eps, int(norm), _p(gu), gu.stride(0), _p(out),
+                                   out.stride(0), M, ffn, kind, _stream()), "cain_rownorm_act")
+    return out

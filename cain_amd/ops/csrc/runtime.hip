@@ -30,6 +30,11 @@ CAIN_API int cain_gemm_w8(const void* Wp, const float* wscale, const void* X, in
                           int ldy, const float* bias, int norm, float eps, const int* slot, const int* pos,
                           const float* cos_t, const float* sin_t, void* kc, void* vtc, int H, int Hkv, int hd,
                           int T_max, int epi, hipStream_t st);
+CAIN_API int cain_lt_gemm(const void* W, const void* X, int ldx, int K, int N, int M, void* Y, int ldy, int accumulate,
+                          void* ws, long long ws_bytes, hipStream_t st);
+CAIN_API int cain_lt_prepare(int N, int K, int M, int ldx, int ldy, int accumulate, long long ws_bytes);
+CAIN_API int cain_rownorm_act(const void* x, int ldx, int d, float eps, int norm, const void* gu, int ldgu, void* act,
+                              int ldact, int M, int ffn, int kind, hipStream_t st);
 CAIN_API int cain_embed(const int* tok, const void* E, void* out, int ldo, int M, int d, float scale, hipStream_t st);
 CAIN_API int cain_attention(const void* q, const void* kc, const void* vtc, const int* slot, const int* pos,
                             float* part_o, float* part_ml, unsigned* counters, void* out, int ldo, int M, int H,
@@ -53,6 +58,10 @@ struct CainLayer {
   const float* so;
   const float* sgu;
   const float* sdown;
+  // plain row-major bf16 copies for the hipBLASLt path (blas.hip; null: fused kernels only): Wo [d, q_dim] and
+  // the 8-row-interleaved gate/up [2 ffn, d]
+  const void* wo_lt;
+  const void* wgu_lt;
 };
 
 struct CainPlanDesc {
@@ -78,6 +87,12 @@ struct CainPlanDesc {
   long long gemm_ws_bytes;
   int w8;                      // 1: fp8 (e4m3) weights with per-row scales, W8A16 kernels (gemm_w8.hip), M <= 64
   const float* lm_head_scale;  // w8: scales of the packed LM head
+  // forwards with >= lt_min_rows rows (0: never) run the O and gate/up projections through hipBLASLt
+  // (blas.hip); gu: [Mpad, 2 ffn] bf16 gate/up output, lt_ws: the library's workspace
+  int lt_min_rows;
+  void* gu;
+  void* lt_ws;
+  long long lt_ws_bytes;
 };
 
 struct CainRows {
@@ -109,6 +124,18 @@ struct Plan {
     if (_e != 0) return _e;       \
   } while (0)
 
+bool lt_rows(const CainPlanDesc& d, int M) { return d.lt_min_rows > 0 && M >= d.lt_min_rows && !d.w8 && d.gu; }
+
+// hipBLASLt heuristics allocate and synchronise: resolve them before a stream capture
+int lt_prepare(const Plan& p, int M) {
+  const CainPlanDesc& d = p.d;
+  if (!lt_rows(d, M) || p.layers.empty()) return 0;
+  const int q_dim = d.H * d.hd;
+  if (p.layers[0].wo_lt) CK(cain_lt_prepare(d.d, q_dim, M, q_dim, d.d, 1, d.lt_ws_bytes));
+  if (p.layers[0].wgu_lt) CK(cain_lt_prepare(2 * d.ffn, d.d, M, d.d, 2 * d.ffn, 0, d.lt_ws_bytes));
+  return 0;
+}
+
 // 5 launches per layer: QKV(+RMSNorm, bias, RoPE, KV append) -> attention(+combine) ->
 // O(+residual) -> gate/up(+RMSNorm, act*mul) -> down(+residual).
 int forward(const Plan& p, int M, const CainRows& r, int want_logits, int want_sample, hipStream_t st) {
@@ -126,6 +153,7 @@ int forward(const Plan& p, int M, const CainRows& r, int want_logits, int want_s
                      const_cast<void*>(kc), const_cast<void*>(vc), d.H, d.Hkv, d.hd, d.T_max, d.gemm_ws,
                      d.gemm_ws_bytes, epi, d.waves, st);
   };
+  const bool lt = lt_rows(d, M);
   CK(cain_embed(r.tok, d.embed, d.x, d.d, M, d.d, d.embed_scale, st));
   for (int l = 0; l < d.n_layers; ++l) {
     const CainLayer& L = p.layers[l];
@@ -134,8 +162,16 @@ int forward(const Plan& p, int M, const CainRows& r, int want_logits, int want_s
     CK(gemm(L.wqkv, L.sqkv, d.x, d.d, d.d, qkv_dim, d.q, q_dim, L.bqkv, 1, kc, vc, /*EPI_QKV_ROPE*/ 5));
     CK(cain_attention(d.q, kc, vc, r.slot, r.pos, d.part_o, d.part_ml, d.counters, d.attn, q_dim, M, d.H, d.Hkv,
                       d.hd, d.T_max, d.nsplit, d.attn_scale, st));
-    CK(gemm(L.wo, L.so, d.attn, q_dim, q_dim, d.d, d.x, d.d, nullptr, 0, nullptr, nullptr, /*EPI_RESID*/ 1));
-    CK(gemm(L.wgu, L.sgu, d.x, d.d, d.d, 2 * d.ffn, d.act, d.ffn, nullptr, 1, nullptr, nullptr, epi_act));
+    if (lt && L.wo_lt)
+      CK(cain_lt_gemm(L.wo_lt, d.attn, q_dim, q_dim, d.d, M, d.x, d.d, 1, d.lt_ws, d.lt_ws_bytes, st));
+    else
+      CK(gemm(L.wo, L.so, d.attn, q_dim, q_dim, d.d, d.x, d.d, nullptr, 0, nullptr, nullptr, /*EPI_RESID*/ 1));
+    if (lt && L.wgu_lt) {
+      CK(cain_lt_gemm(L.wgu_lt, d.x, d.d, d.d, 2 * d.ffn, M, d.gu, 2 * d.ffn, 0, d.lt_ws, d.lt_ws_bytes, st));
+      CK(cain_rownorm_act(d.x, d.d, d.d, d.eps, 1, d.gu, 2 * d.ffn, d.act, d.ffn, M, d.ffn, d.act_kind, st));
+    } else {
+      CK(gemm(L.wgu, L.sgu, d.x, d.d, d.d, 2 * d.ffn, d.act, d.ffn, nullptr, 1, nullptr, nullptr, epi_act));
+    }
     CK(gemm(L.wdown, L.sdown, d.act, d.ffn, d.ffn, d.d, d.x, d.d, nullptr, 0, nullptr, nullptr, /*EPI_RESID*/ 1));
   }
   if (want_logits) {
@@ -178,6 +214,7 @@ CAIN_API void* cain_plan_capture(void* plan, int M, const CainRows* rows, int st
     *err = -1;
     return nullptr;
   }
+  if ((*err = lt_prepare(*p, M)) != 0) return nullptr;
   hipGraph_t g = nullptr;
   hipError_t e = hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal);
   if (e != hipSuccess) {
