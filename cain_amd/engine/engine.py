@@ -131,7 +131,7 @@ class _CainPlanDesc(ctypes.Structure):
                                                  "part_o", "part_ml", "counters", "gemm_ws")]
                 + [("gemm_ws_bytes", ctypes.c_longlong), ("w8", ctypes.c_int), ("lm_head_scale", ctypes.c_void_p)]
                 + [("lt_min_rows", ctypes.c_int), ("gu", ctypes.c_void_p), ("lt_ws", ctypes.c_void_p),
-                   ("lt_ws_bytes", ctypes.c_longlong)])
+                   ("lt_ws_bytes", ctypes.c_longlong), ("lm_head_lt", ctypes.c_void_p), ("xn", ctypes.c_void_p)])
 
 
 class _CainRows(ctypes.Structure):
@@ -219,7 +219,8 @@ class DecodeEngine:
         # row-major copies of those two weights beside the MFMA packing
         lt_rows = lt_min_rows(self.max_batch, self.weight_dtype)
         packed = pack_for_engine(self.weights, free_natural=not self.keep_natural, weight_dtype=self.weight_dtype,
-                                 plain_lt=lt_rows > 0)
+                                 plain_lt=lt_rows > 0,
+                                 plain_lm_head=lt_rows > 0 and os.environ.get("CAIN_LT_LM_HEAD", "1") != "0")
         torch.cuda.synchronize(dev)
         S, T, L = self.max_batch, self.T_max, cfg.n_layers
         bf = torch.bfloat16
@@ -281,6 +282,10 @@ class DecodeEngine:
             self.gu = z(R, 2 * cfg.ffn)
             self.lt_ws = torch.zeros(LT_WS_BYTES // 4, device=dev, dtype=torch.int32)
             d.gu, d.lt_ws, d.lt_ws_bytes = _ptr(self.gu), _ptr(self.lt_ws), LT_WS_BYTES
+            if packed.get("lm_head_lt") is not None:
+                # LM head on hipBLASLt too (~300 vs ~400 us at 256 rows on llama3.1:8b, profiles/lt_gemm.md)
+                self.xn = z(R, cfg.d_model)
+                d.lm_head_lt, d.xn = _ptr(packed["lm_head_lt"]), _ptr(self.xn)
         self._desc = d
         self._plans: Dict[int, int] = {}
         self._graphs: Dict[tuple, int] = {}

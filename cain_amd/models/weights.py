@@ -195,7 +195,7 @@ def fp8_roundtrip_weights(mw: ModelWeights) -> ModelWeights:
 
 
 def pack_for_engine(mw: ModelWeights, free_natural: bool = False, weight_dtype: str = "bf16",
-                    plain_lt: bool = False) -> Dict[str, object]:
+                    plain_lt: bool = False, plain_lm_head: bool = False) -> Dict[str, object]:
     """Build the decode engine's packed tensors (see module doc); norm gains are folded into the GEMM
     weights they feed (attn_norm -> wqkv, mlp_norm -> gate/up, final_norm -> lm_head).
 
@@ -230,7 +230,11 @@ def pack_for_engine(mw: ModelWeights, free_natural: bool = False, weight_dtype: 
         if free_natural:
             lw.wqkv = lw.wo = lw.w_gate = lw.w_up = lw.w_down = None
     packed: Dict[str, object] = {"layers": layers, "weight_dtype": weight_dtype}
-    put(packed, "wlm_head", fold_gain(mw.lm_head, effective_gain(cfg, mw.final_norm)))
+    lm = fold_gain(mw.lm_head, effective_gain(cfg, mw.final_norm))
+    put(packed, "wlm_head", lm)
+    if plain_lm_head and not fp8:
+        packed["lm_head_lt"] = lm.contiguous()  # plain row-major copy for the hipBLASLt LM head (blas.hip)
+    del lm
     packed["lm_head"] = packed.pop("wlm_head")
     if fp8:
         packed["lm_head_scale"] = packed.pop("slm_head")

@@ -36,12 +36,14 @@ struct LtPlan {
 
 std::mutex g_mu;
 hipblasLtHandle_t g_handle = nullptr;
-std::map<std::tuple<int, int, int, int, int, int, long long, int>, LtPlan> g_plans;
+std::map<std::tuple<int, int, int, int, int, int, long long, int, int>, LtPlan> g_plans;
 
-// Y[M, N] (+)= X[M, K] . W[N, K]^T, all row-major bf16 = column-major D[N x M] = op_T(W[K x N]) . X[K x M].
-const LtPlan* lt_plan(int N, int K, int M, int ldx, int ldy, bool accumulate, long long ws_bytes, int dev) {
+// Y[M, N] (+)= X[M, K] . W[N, K]^T, all row-major = column-major D[N x M] = op_T(W[K x N]) . X[K x M]; X and W
+// bf16, Y bf16 or (f32out: the LM head's logits) fp32.
+const LtPlan* lt_plan(int N, int K, int M, int ldx, int ldy, bool accumulate, long long ws_bytes, int dev,
+                      bool f32out = false) {
   std::lock_guard<std::mutex> lk(g_mu);
-  auto key = std::make_tuple(N, K, M, ldx, ldy, int(accumulate), ws_bytes, dev);
+  auto key = std::make_tuple(N, K, M, ldx, ldy, int(accumulate), ws_bytes, dev, int(f32out));
   auto it = g_plans.find(key);
   if (it != g_plans.end()) return it->second.ok ? &it->second : nullptr;
   LtPlan& p = g_plans[key];
@@ -52,7 +54,7 @@ const LtPlan* lt_plan(int N, int K, int M, int ldx, int ldy, bool accumulate, lo
   hipblasLtMatmulDescSetAttribute(p.md, HIPBLASLT_MATMUL_DESC_TRANSB, &tb, sizeof(tb));
   if (hipblasLtMatrixLayoutCreate(&p.la, HIP_R_16BF, K, N, K) != HIPBLAS_STATUS_SUCCESS ||
       hipblasLtMatrixLayoutCreate(&p.lb, HIP_R_16BF, K, M, ldx) != HIPBLAS_STATUS_SUCCESS ||
-      hipblasLtMatrixLayoutCreate(&p.lc, HIP_R_16BF, N, M, ldy) != HIPBLAS_STATUS_SUCCESS)
+      hipblasLtMatrixLayoutCreate(&p.lc, f32out ? HIP_R_32F : HIP_R_16BF, N, M, ldy) != HIPBLAS_STATUS_SUCCESS)
     return nullptr;
   hipblasLtMatmulPreference_t pref = nullptr;
   if (hipblasLtMatmulPreferenceCreate(&pref) != HIPBLAS_STATUS_SUCCESS) return nullptr;
@@ -113,6 +115,36 @@ __global__ __launch_bounds__(ACT_THREADS) void rownorm_act_kernel(const __bf16* 
   }
 }
 
+// xn[m, :] = x[m, :] * rsqrt(mean(x[m]^2) + eps): the final RMSNorm ahead of the library LM head (its gain is
+// folded into the LM head's columns, as for every fused-norm GEMM).  One workgroup per row.
+__global__ __launch_bounds__(ACT_THREADS) void rownorm_kernel(const __bf16* __restrict__ x, int ldx, int d, float eps,
+                                                              __bf16* __restrict__ xn, int ldxn) {
+  __shared__ float red[ACT_THREADS / 64];
+  const int m = blockIdx.x, tid = threadIdx.x;
+  const __bf16* xr = x + (size_t)m * ldx;
+  float ss = 0.f;
+  for (int i = tid * 8; i < d; i += ACT_THREADS * 8) {
+    const bf16x8 v = *reinterpret_cast<const bf16x8*>(xr + i);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) ss += bf2f(v[j]) * bf2f(v[j]);
+  }
+  ss = wave_sum(ss);
+  if ((tid & 63) == 0) red[tid >> 6] = ss;
+  __syncthreads();
+  float t = 0.f;
+#pragma unroll
+  for (int w = 0; w < ACT_THREADS / 64; ++w) t += red[w];
+  const float s = rsqrtf(t / d + eps);
+  __bf16* o = xn + (size_t)m * ldxn;
+  for (int i = tid * 8; i < d; i += ACT_THREADS * 8) {
+    const bf16x8 v = *reinterpret_cast<const bf16x8*>(xr + i);
+    bf16x8 r;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] = f2bf(s * bf2f(v[j]));
+    *reinterpret_cast<bf16x8*>(o + i) = r;
+  }
+}
+
 }  // namespace
 
 // Y = X . W^T (+ Y when accumulate): W plain row-major [N, K] bf16, X [M, ldx], Y [M, ldy].  The heuristic
@@ -137,6 +169,36 @@ CAIN_API int cain_lt_prepare(int N, int K, int M, int ldx, int ldy, int accumula
   (void)hipGetDevice(&dev);
   const LtPlan* p = lt_plan(N, K, M, ldx, ldy, accumulate != 0, ws_bytes, dev);
   return !p ? -2 : (p->ws > (size_t)ws_bytes ? -3 : 0);
+}
+
+// fp32 Y[M, N] = X . W^T (LM head logits; W plain row-major [N, K] bf16).
+CAIN_API int cain_lt_gemm_f32(const void* W, const void* X, int ldx, int K, int N, int M, float* Y, int ldy, void* ws,
+                              long long ws_bytes, hipStream_t st) {
+  if (M < 1 || N < 1 || K < 1 || ldx < K || ldy < N || (ldx % 8) || (ldy % 4) || (K % 8)) return -1;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  const LtPlan* p = lt_plan(N, K, M, ldx, ldy, false, ws ? ws_bytes : 0, dev, true);
+  if (!p) return -2;
+  if (p->ws > (size_t)(ws ? ws_bytes : 0)) return -3;
+  const float alpha = 1.0f, beta = 0.0f;
+  hipblasStatus_t s = hipblasLtMatmul(g_handle, p->md, &alpha, W, p->la, X, p->lb, &beta, Y, p->lc, Y, p->lc,
+                                      &p->algo, ws, p->ws, st);
+  return s == HIPBLAS_STATUS_SUCCESS ? 0 : 1000 + int(s);
+}
+
+CAIN_API int cain_lt_prepare_f32(int N, int K, int M, int ldx, int ldy, long long ws_bytes) {
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  const LtPlan* p = lt_plan(N, K, M, ldx, ldy, false, ws_bytes, dev, true);
+  return !p ? -2 : (p->ws > (size_t)ws_bytes ? -3 : 0);
+}
+
+// xn[m, :d] = x[m, :d] * rsqrt(mean(x[m]^2) + eps), M rows.
+CAIN_API int cain_rownorm(const void* x, int ldx, int d, float eps, void* xn, int ldxn, int M, hipStream_t st) {
+  if (M < 1 || (d % 8) || (ldx % 8) || (ldxn % 8) || ldx < d || ldxn < d) return -1;
+  hipLaunchKernelGGL(rownorm_kernel, dim3(M), dim3(ACT_THREADS), 0, st, reinterpret_cast<const __bf16*>(x), ldx, d,
+                     eps, reinterpret_cast<__bf16*>(xn), ldxn);
+  return int(hipGetLastError());
 }
 
 // act[m, :ffn] = f(s_m * gate) * (s_m * up) from the interleaved gate/up GEMM output gu[m, :2 ffn];

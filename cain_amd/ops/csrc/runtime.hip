@@ -33,6 +33,10 @@ CAIN_API int cain_gemm_w8(const void* Wp, const float* wscale, const void* X, in
 CAIN_API int cain_lt_gemm(const void* W, const void* X, int ldx, int K, int N, int M, void* Y, int ldy, int accumulate,
                           void* ws, long long ws_bytes, hipStream_t st);
 CAIN_API int cain_lt_prepare(int N, int K, int M, int ldx, int ldy, int accumulate, long long ws_bytes);
+CAIN_API int cain_lt_gemm_f32(const void* W, const void* X, int ldx, int K, int N, int M, float* Y, int ldy, void* ws,
+                              long long ws_bytes, hipStream_t st);
+CAIN_API int cain_lt_prepare_f32(int N, int K, int M, int ldx, int ldy, long long ws_bytes);
+CAIN_API int cain_rownorm(const void* x, int ldx, int d, float eps, void* xn, int ldxn, int M, hipStream_t st);
 CAIN_API int cain_rownorm_act(const void* x, int ldx, int d, float eps, int norm, const void* gu, int ldgu, void* act,
                               int ldact, int M, int ffn, int kind, hipStream_t st);
 CAIN_API int cain_embed(const int* tok, const void* E, void* out, int ldo, int M, int d, float scale, hipStream_t st);
@@ -93,6 +97,10 @@ struct CainPlanDesc {
   void* gu;
   void* lt_ws;
   long long lt_ws_bytes;
+  // wide forwards with lm_head_lt set run the final RMSNorm (rownorm into xn [Mpad, d] bf16) and the LM head
+  // (plain row-major [V, d] bf16, gain folded, fp32 logits) through hipBLASLt; the hand GEMM is the fallback
+  const void* lm_head_lt;
+  void* xn;
 };
 
 struct CainRows {
@@ -133,6 +141,8 @@ int lt_prepare(const Plan& p, int M) {
   const int q_dim = d.H * d.hd;
   if (p.layers[0].wo_lt) CK(cain_lt_prepare(d.d, q_dim, M, q_dim, d.d, 1, d.lt_ws_bytes));
   if (p.layers[0].wgu_lt) CK(cain_lt_prepare(2 * d.ffn, d.d, M, d.d, 2 * d.ffn, 0, d.lt_ws_bytes));
+  // no library algorithm for the fp32-output LM head is not an error: forward() falls back to the hand GEMM
+  if (d.lm_head_lt && d.xn) (void)cain_lt_prepare_f32(d.V, d.d, M, d.d, d.V, d.lt_ws_bytes);
   return 0;
 }
 
@@ -175,7 +185,13 @@ int forward(const Plan& p, int M, const CainRows& r, int want_logits, int want_s
     CK(gemm(L.wdown, L.sdown, d.act, d.ffn, d.ffn, d.d, d.x, d.d, nullptr, 0, nullptr, nullptr, /*EPI_RESID*/ 1));
   }
   if (want_logits) {
-    CK(gemm(d.lm_head, d.lm_head_scale, d.x, d.d, d.d, d.V, d.logits, d.V, nullptr, 1, nullptr, nullptr,
+    int e = -2;
+    if (lt && d.lm_head_lt && d.xn) {
+      CK(cain_rownorm(d.x, d.d, d.d, d.eps, d.xn, d.d, M, st));
+      e = cain_lt_gemm_f32(d.lm_head_lt, d.xn, d.d, d.d, d.V, M, d.logits, d.V, d.lt_ws, d.lt_ws_bytes, st);
+      if (e > 0) CK(e);  // a library failure; no plan / unsupported shape (< 0) falls back
+    }
+    if (e != 0) CK(gemm(d.lm_head, d.lm_head_scale, d.x, d.d, d.d, d.V, d.logits, d.V, nullptr, 1, nullptr, nullptr,
             /*EPI_F32*/ 2));
   }
   if (want_sample) {

@@ -62,11 +62,13 @@ def test_rownorm_act_matches_fp32(kind, M, d, ffn):
 
 @pytest.mark.parametrize("name", sorted(TINY))
 def test_engine_lt_path_matches_oracle(name, monkeypatch):
-    """Every family with the O and gate/up projections on hipBLASLt from 2 rows up (decode and prefill)."""
+    """Every family with the O, gate/up and LM head projections on hipBLASLt from 2 rows up (decode and
+    prefill); the LM head runs rownorm + an fp32-output library GEMM."""
     monkeypatch.setenv("CAIN_LT_MIN_ROWS", "2")
+    monkeypatch.delenv("CAIN_LT_LM_HEAD", raising=False)
     prompts = ["In 100 words, please give me information about India", "hi", "Elizabeth II, Queen"]
     eng = DecodeEngine(name, device="cuda", max_batch=4, max_context=256, keep_natural=True, seed=3)
-    assert eng._desc.lt_min_rows == 2 and eng._layers[0].wo_lt
+    assert eng._desc.lt_min_rows == 2 and eng._layers[0].wo_lt and eng._desc.lm_head_lt and eng._desc.xn
     got = eng.last_logits(prompts)
     ref = ReferenceModel(eng.weights)
     for i, p in enumerate(prompts):
@@ -82,3 +84,17 @@ def test_engine_lt_default_threshold(monkeypatch):
     monkeypatch.delenv("CAIN_LT_MIN_ROWS", raising=False)
     from cain_amd.engine.engine import lt_min_rows
     assert lt_min_rows(256) == 128 and lt_min_rows(64) == 0 and lt_min_rows(256, "fp8") == 0
+
+
+def test_engine_lt_lm_head_matches_hand_gemm(monkeypatch):
+    """The library LM head (rownorm + fp32-output hipBLASLt) against the fused hand GEMM on the same weights."""
+    monkeypatch.setenv("CAIN_LT_MIN_ROWS", "2")
+    prompts = ["In 100 words, please give me information about India", "hi"]
+    out = {}
+    for flag in ("1", "0"):
+        monkeypatch.setenv("CAIN_LT_LM_HEAD", flag)
+        eng = DecodeEngine("tiny-llama3.1:8b", device="cuda", max_batch=2, max_context=128, seed=5)
+        assert bool(eng._desc.lm_head_lt) == (flag == "1")
+        out[flag] = eng.last_logits(prompts).float()
+        eng.close()
+    assert _rel(out["1"], out["0"]) < 1e-2
