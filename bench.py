@@ -18,7 +18,12 @@ variant too).  Baseline: the reference's llama3.1:8b on-device 1000-word cell,
 est. 19.2 tok/s and 0.574 J/token on a MacBook Pro M2.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--model M] [--words W] [--batch B (default 256)]
-       (multi-GPU: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...)
+       (multi-GPU: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ..., or plain
+       ``python bench.py --gpus N``, which spawns the N ranks itself before anything touches a GPU)
+
+After the timed steps every rank also runs ONE trial alone (batch 1, the reference's one-request-at-a-time
+protocol) and the JSON reports it beside the batched number: ``single_stream_tok_per_s`` and
+``single_stream_J_per_token``.
 """
 from __future__ import annotations
 
@@ -27,6 +32,8 @@ import csv
 import json
 import math
 import os
+import socket
+import subprocess
 import sys
 import time
 from pathlib import Path
@@ -51,6 +58,29 @@ def topics():
         return ["United States", "India", "Elizabeth II", "World War II"]
 
 
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_ranks(n: int, argv) -> int:
+    """``--gpus N`` without a launcher: start N ranks of this script (one per GPU, LOCAL_RANK = GPU) as child
+    processes -- this process never initialises HIP -- and return the worst exit code."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+    rcs = [p.wait() for p in procs]
+    bad = [rc for rc in rcs if rc != 0]
+    return bad[0] if bad else 0
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -64,19 +94,37 @@ def main() -> int:
     ap.add_argument("--no-energy", action="store_true")
     ap.add_argument("--weights", choices=("bf16", "fp8"), default="bf16",
                     help="GEMM weight storage: bf16 (headline) or fp8 e4m3 per-row scaled (W8A16, batch <= 64)")
+    ap.add_argument("--device", choices=("cuda", "cpu"), default="cuda",
+                    help="cpu: the torch oracle backend over gloo (tests of the multi-rank plumbing; tiny models)")
+    ap.add_argument("--settle", type=float, default=8.0, help="seconds of rest before the idle-power baseline")
+    ap.add_argument("--no-single", action="store_true", help="skip the batch-1 (single-stream) measurement")
     ns = ap.parse_args()
+
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is None and ns.gpus > 1:
+        return spawn_ranks(ns.gpus, sys.argv[1:])
+    world = int(world_env or "1")
+    if world != ns.gpus:
+        raise SystemExit(f"bench.py: --gpus {ns.gpus} but the launcher started WORLD_SIZE={world} ranks")
 
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    cpu = ns.device == "cpu"
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
-    torch.cuda.set_device(dev)
+        if cpu:
+            dist.init_process_group("gloo")
+        else:
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        assert dist.get_world_size() == world
+    if cpu:
+        dev = torch.device("cpu")
+    else:
+        dev = torch.device("cuda", local)
+        torch.cuda.set_device(dev)
 
     from cain_amd.engine import DecodeEngine
     from cain_amd.models.tokenizer import tokens_for_words
@@ -97,23 +145,33 @@ def main() -> int:
         res = eng.generate(prompts(step), n_tok, [dict(opts, seed=step * 100003 + i + 1) for i in range(ns.batch)])
         return sum(r.eval_count for r in res)
 
+    def sync():
+        if not cpu:
+            torch.cuda.synchronize(dev)
+
     for w in range(ns.warmup):
         one_step(-1 - w)
 
     meter = None
-    if not ns.no_energy:
+    if not ns.no_energy and not cpu:
         try:
             from cain_amd.energy import EnergyMeter
-            meter = EnergyMeter(devices=[local], period_ms=100.0, keep_samples=False)
-            meter.measure_idle(1.0)
+            # host CPU + RAM energy is shared by every rank of the node: each rank is charged its share
+            meter = EnergyMeter(devices=[local], period_ms=100.0, keep_samples=False, sources=("gpu", "cpu", "ram"),
+                                host_share=1.0 / int(os.environ.get("LOCAL_WORLD_SIZE", world)))
+            # the board stays ~15 % above its idle floor for seconds after a burst: settle first
+            sync()
+            time.sleep(max(0.0, ns.settle))
+            meter.measure_idle(2.0)
         except Exception as exc:  # energy is auxiliary to the throughput metric
             print(f"[bench] energy meter unavailable: {exc}", file=sys.stderr)
             meter = None
+        one_step(-100)  # back to a warm steady state before the timed region
 
     def barrier():
         if world > 1:
             dist.barrier()
-        torch.cuda.synchronize(dev)
+        sync()
 
     barrier()
     if meter:
@@ -126,8 +184,26 @@ def main() -> int:
     dt = time.perf_counter() - t0
     reading = meter.stop() if meter else None
 
+    # batch-1 trial (outside the timed region): the reference's one-request-at-a-time protocol
+    ss_tps, ss_j = float("nan"), float("nan")
+    if not ns.no_single:
+        eng.generate(prompts(-7)[:1], min(n_tok, 32), [dict(opts, seed=7)])  # warm the batch-1 graphs
+        barrier()
+        if meter:
+            meter.start()
+        t1 = time.perf_counter()
+        r1 = eng.generate(prompts(-8)[:1], n_tok, [dict(opts, seed=8)])[0]
+        sync()
+        dt1 = time.perf_counter() - t1
+        rd1 = meter.stop() if meter else None
+        ss_tps = r1.eval_count / dt1
+        if rd1 is not None:
+            ss_j = rd1.gpu_energy_j / max(1, r1.eval_count)
+
     vals = torch.tensor([dt, float(toks), reading.gpu_energy_j if reading else float("nan"),
-                         reading.idle_subtracted_j if reading else float("nan")], dtype=torch.float64, device=dev)
+                         reading.idle_subtracted_j if reading else float("nan"),
+                         reading.total_energy_j if reading else float("nan"), ss_tps, ss_j],
+                        dtype=torch.float64, device=dev)
     if world > 1:
         allv = [torch.zeros_like(vals) for _ in range(world)]
         dist.all_gather(allv, vals)
@@ -138,6 +214,9 @@ def main() -> int:
     tokens = float(allv[:, 1].sum())
     energy = float(allv[:, 2].sum())
     energy_idle_sub = float(allv[:, 3].sum())
+    energy_total = float(allv[:, 4].sum())
+    ss_tps_mean = float(allv[:, 5].mean())
+    ss_j_mean = float(allv[:, 6].mean())
     value = tokens / t_max
     base_tps, base_jpt = BASELINE.get((ns.model, ns.words), (None, None))
     if rank == 0:
@@ -153,6 +232,7 @@ def main() -> int:
             "scaling": "weak",
             "vs_baseline": round(value / base_tps, 2) if base_tps else None,
             "dtype": "bf16" if ns.weights == "bf16" else "bf16 activations, fp8-e4m3 weights",
+            "device": "cpu (torch oracle)" if cpu else "MI355X",
             "data": "synthetic (reference topics.csv prompts, random-init weights)",
             "config": {"model": ns.model, "global_batch": ns.batch * world, "seq_len": n_tok,
                        "parallelism": f"dp{world}", "words": ns.words, "trials_per_gpu": ns.batch,
@@ -161,10 +241,16 @@ def main() -> int:
             "J_per_token": round(energy / tokens, 5) if not math.isnan(energy) else None,
             "J_per_token_idle_subtracted": (round(energy_idle_sub / tokens, 5)
                                             if not math.isnan(energy_idle_sub) else None),
+            "J_per_token_incl_host": (round(energy_total / tokens, 5) if not math.isnan(energy_total) else None),
+            "host_energy_source": reading.cpu_energy_source if reading else None,
             "avg_gpu_power_W": round(energy / t_max / world, 1) if not math.isnan(energy) else None,
+            "single_stream_tok_per_s": round(ss_tps_mean, 2) if not math.isnan(ss_tps_mean) else None,
+            "single_stream_J_per_token": round(ss_j_mean, 4) if not math.isnan(ss_j_mean) else None,
             "baseline": {"tok_per_s": base_tps, "J_per_token": base_jpt, "hardware": "MacBook Pro M2 (est.)"},
             "vs_baseline_J_per_token": (round(base_jpt / (energy / tokens), 2)
                                         if base_jpt and not math.isnan(energy) and energy > 0 else None),
+            "single_stream_vs_baseline_J_per_token": (round(base_jpt / ss_j_mean, 3)
+                                                      if base_jpt and not math.isnan(ss_j_mean) else None),
         }
         print(json.dumps(out), flush=True)
     if meter:

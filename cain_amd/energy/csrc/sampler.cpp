@@ -16,9 +16,11 @@
 // energies sit on a ~6.8 J lattice).  Every `period_us` (default
 // 100 ms, powermetrics' cadence) it also takes a slow sample: board power,
 // gfx/umc activity, VRAM %, host CPU % (/proc/stat deltas), host memory %
-// (/proc/meminfo, psutil's formula) and, when the kernel exposes it, RAPL
-// package energy.  libamd_smi is dlopen'ed so the library loads (and the
-// CPU-side metrics work) on hosts without a GPU.
+// (/proc/meminfo, psutil's formula) and the host CPU energy counter when one
+// is readable (HostEnergy below: amd-smi CPU sockets via HSMP, else RAPL
+// powercap package zones, else hwmon `amd_energy` socket sensors), accumulated
+// per counter with modular wrap handling.  libamd_smi is dlopen'ed so the
+// library loads (and the CPU-side metrics work) on hosts without a GPU.
 //
 // Exposed as a plain C ABI consumed through ctypes (cain_amd/energy/native.py).
 
@@ -54,6 +56,8 @@ using fn_activity_t = amdsmi_status_t (*)(amdsmi_processor_handle, amdsmi_engine
 using fn_vram_t = amdsmi_status_t (*)(amdsmi_processor_handle, amdsmi_vram_usage_t*);
 using fn_bdf_t = amdsmi_status_t (*)(amdsmi_processor_handle, amdsmi_bdf_t*);
 using fn_type_t = amdsmi_status_t (*)(amdsmi_processor_handle, processor_type_t*);
+using fn_cpu_handles_t = amdsmi_status_t (*)(uint32_t*, amdsmi_processor_handle*);
+using fn_cpu_energy_t = amdsmi_status_t (*)(amdsmi_processor_handle, uint64_t*);
 
 struct Smi {
   void* lib = nullptr;
@@ -67,7 +71,10 @@ struct Smi {
   fn_vram_t vram = nullptr;
   fn_bdf_t bdf = nullptr;
   fn_type_t ptype = nullptr;
+  fn_cpu_handles_t cpu_handles = nullptr;
+  fn_cpu_energy_t cpu_energy = nullptr;
   std::vector<amdsmi_processor_handle> gpus;
+  std::vector<amdsmi_processor_handle> cpus;  // CPU sockets (only when the HSMP driver is usable)
   bool ok = false;
   std::string error;
 };
@@ -114,9 +121,30 @@ int smi_open() {
     g_smi.error = "libamd_smi.so lacks required symbols";
     return -1;
   }
-  if (g_smi.init(AMDSMI_INIT_AMD_GPUS) != AMDSMI_STATUS_SUCCESS) {
+  sym(g_smi.lib, "amdsmi_get_cpu_handles", g_smi.cpu_handles);
+  sym(g_smi.lib, "amdsmi_get_cpu_socket_energy", g_smi.cpu_energy);
+  // CPU sockets need the HSMP driver (usually root-only on a shared host): try GPUs + CPUs, then GPUs alone
+  bool cpus_ok = false;
+  if (g_smi.cpu_handles && g_smi.cpu_energy &&
+      g_smi.init(AMDSMI_INIT_AMD_GPUS | AMDSMI_INIT_AMD_CPUS) == AMDSMI_STATUS_SUCCESS) {
+    cpus_ok = true;
+  } else if (g_smi.init(AMDSMI_INIT_AMD_GPUS) != AMDSMI_STATUS_SUCCESS) {
     g_smi.error = "amdsmi_init failed";
     return -1;
+  }
+  if (cpus_ok) {
+    uint32_t nc = 0;
+    if (g_smi.cpu_handles(&nc, nullptr) == AMDSMI_STATUS_SUCCESS && nc > 0) {
+      g_smi.cpus.resize(nc);
+      if (g_smi.cpu_handles(&nc, g_smi.cpus.data()) != AMDSMI_STATUS_SUCCESS) nc = 0;
+      g_smi.cpus.resize(nc);
+      uint64_t e = 0;
+      for (auto h : g_smi.cpus)
+        if (g_smi.cpu_energy(h, &e) != AMDSMI_STATUS_SUCCESS) {
+          g_smi.cpus.clear();
+          break;
+        }
+    }
   }
   uint32_t ns = 0;
   if (g_smi.sockets(&ns, nullptr) != AMDSMI_STATUS_SUCCESS) {
@@ -134,6 +162,8 @@ int smi_open() {
       if (g_smi.ptype) {
         processor_type_t t;
         if (g_smi.ptype(h, &t) == AMDSMI_STATUS_SUCCESS && t != AMDSMI_PROCESSOR_TYPE_AMD_GPU) continue;
+      } else if (!g_smi.cpus.empty()) {
+        continue;  // cannot tell GPUs from CPU sockets: keep the CPU path off rather than mix them
       }
       g_smi.gpus.push_back(h);
     }
@@ -188,35 +218,121 @@ double read_mem_percent() {
   return 100.0 * double(total - avail) / double(total);
 }
 
-std::vector<std::string> rapl_files() {
-  std::vector<std::string> out;
-  const char* base = "/sys/class/powercap";
-  DIR* d = opendir(base);
-  if (!d) return out;
-  while (dirent* e = readdir(d)) {
-    std::string n = e->d_name;
-    // top-level package zones only: intel-rapl:0, amd-rapl:0 … (not sub-zones "x:y:z")
-    if (n.find("rapl:") == std::string::npos) continue;
-    if (std::count(n.begin(), n.end(), ':') != 1) continue;
-    std::string p = std::string(base) + "/" + n + "/energy_uj";
-    if (access(p.c_str(), R_OK) == 0) out.push_back(p);
-  }
-  closedir(d);
-  return out;
+bool read_u64_file(const std::string& path, uint64_t* out) {
+  FILE* f = fopen(path.c_str(), "r");
+  if (!f) return false;
+  unsigned long long v = 0;
+  const bool ok = fscanf(f, "%llu", &v) == 1;
+  fclose(f);
+  if (ok) *out = uint64_t(v);
+  return ok;
 }
 
-double read_rapl_uj(const std::vector<std::string>& files) {
-  double s = 0;
-  for (auto& p : files) {
-    FILE* f = fopen(p.c_str(), "r");
-    if (!f) return NAN;
-    unsigned long long v = 0;
-    if (fscanf(f, "%llu", &v) != 1) v = 0;
-    fclose(f);
-    s += double(v);
-  }
+std::string read_line_file(const std::string& path) {
+  char buf[128] = {0};
+  FILE* f = fopen(path.c_str(), "r");
+  if (!f) return "";
+  if (!fgets(buf, sizeof(buf), f)) buf[0] = 0;
+  fclose(f);
+  std::string s(buf);
+  while (!s.empty() && (s.back() == '\n' || s.back() == ' ')) s.pop_back();
   return s;
 }
+
+// Increment of a cumulative counter from `last` to `v` with wrap modulus `range` (0: unknown, a backwards step is
+// dropped rather than turned into a huge positive one).
+uint64_t wrap_delta(uint64_t v, uint64_t last, uint64_t range) {
+  if (v >= last) return v - last;
+  if (range > last) return (range - last) + v;  // wrapped once
+  return 0;
+}
+
+// Host CPU energy: a set of cumulative microjoule counters of one kind, summed.  Each counter is accumulated from
+// its own deltas with modular wrap handling (RAPL energy_uj wraps at max_energy_range_uj, every few minutes to
+// tens of minutes at server package power), so a window that crosses a wrap still integrates correctly.
+struct HostCounter {
+  std::string path;                    // sysfs file (rapl / hwmon)
+  amdsmi_processor_handle h = nullptr;  // amd-smi CPU socket
+  uint64_t range = 0;                  // wrap modulus (0: 64-bit, treated as monotone)
+  uint64_t last = 0;
+  bool have = false;
+};
+
+struct HostEnergy {
+  std::string source;  // "amdsmi-cpu" | "rapl" | "hwmon" | "" (none: the Python side models it)
+  std::vector<HostCounter> ctr;
+  double acc_uj = 0;
+
+  bool raw(HostCounter& c, uint64_t* v) {
+    if (c.h) {
+      std::lock_guard<std::mutex> g(g_smi_mu);
+      return g_smi.cpu_energy && g_smi.cpu_energy(c.h, v) == AMDSMI_STATUS_SUCCESS;
+    }
+    return read_u64_file(c.path, v);
+  }
+
+  void open() {
+    ctr.clear();
+    source.clear();
+    if (!g_smi.cpus.empty()) {
+      for (auto h : g_smi.cpus) {
+        HostCounter c;
+        c.h = h;
+        ctr.push_back(c);
+      }
+      source = "amdsmi-cpu";
+      return;
+    }
+    if (DIR* d = opendir("/sys/class/powercap")) {
+      while (dirent* e = readdir(d)) {
+        std::string n = e->d_name;
+        // top-level package zones only: intel-rapl:0, amd-rapl:0 ... (not sub-zones "x:y:z")
+        if (n.find("rapl:") == std::string::npos || std::count(n.begin(), n.end(), ':') != 1) continue;
+        HostCounter c;
+        c.path = "/sys/class/powercap/" + n + "/energy_uj";
+        uint64_t v;
+        if (access(c.path.c_str(), R_OK) != 0 || !read_u64_file(c.path, &v)) continue;
+        read_u64_file("/sys/class/powercap/" + n + "/max_energy_range_uj", &c.range);
+        ctr.push_back(c);
+      }
+      closedir(d);
+    }
+    if (!ctr.empty()) {
+      source = "rapl";
+      return;
+    }
+    if (DIR* d = opendir("/sys/class/hwmon")) {
+      while (dirent* e = readdir(d)) {
+        std::string base = std::string("/sys/class/hwmon/") + e->d_name;
+        if (read_line_file(base + "/name") != "amd_energy") continue;
+        for (int i = 1; i < 1024; ++i) {
+          std::string lbl = read_line_file(base + "/energy" + std::to_string(i) + "_label");
+          if (lbl.empty()) break;
+          if (lbl.rfind("Esocket", 0) != 0) continue;
+          HostCounter c;
+          c.path = base + "/energy" + std::to_string(i) + "_input";
+          uint64_t v;
+          if (read_u64_file(c.path, &v)) ctr.push_back(c);
+        }
+      }
+      closedir(d);
+    }
+    if (!ctr.empty()) source = "hwmon";
+  }
+
+  // poll every counter; returns the cumulative joules since the first poll (NaN without a source)
+  double poll() {
+    if (ctr.empty()) return NAN;
+    for (auto& c : ctr) {
+      uint64_t v = 0;
+      if (!raw(c, &v)) continue;
+      if (c.have) acc_uj += double(wrap_delta(v, c.last, c.range));
+      c.last = v;
+      c.have = true;
+    }
+    return acc_uj * 1e-6;
+  }
+};
 
 }  // namespace
 
@@ -270,8 +386,7 @@ struct Sampler {
   std::atomic<uint64_t> dropped{0};  // written under mu by the sampler, read lock-free by es_dropped
   uint64_t t_start = 0;
   CpuTimes last_cpu;
-  std::vector<std::string> rapl;
-  double rapl_start_uj = NAN;
+  HostEnergy host;
   std::string error;
 
   void push(const es_sample_t& s) {
@@ -315,11 +430,7 @@ struct Sampler {
       last_cpu = c;
     }
     double mem = read_mem_percent();
-    double cpu_j = NAN;
-    if (!rapl.empty()) {
-      double uj = read_rapl_uj(rapl);
-      if (!std::isnan(uj) && !std::isnan(rapl_start_uj)) cpu_j = (uj - rapl_start_uj) * 1e-6;
-    }
+    const double cpu_j = host.poll();
     if (gpus.empty()) {
       es_sample_t s{};
       s.t_ns = t;
@@ -484,7 +595,7 @@ void* es_create(const int* gpu_idx, int n, int period_us, int fast_period_us, in
   s->fast_us = std::max(200, fast_period_us);
   s->core = cpu_core;
   if (ring_cap > 0) s->ring_cap = size_t(ring_cap);
-  s->rapl = rapl_files();
+  s->host.open();
   return s;
 }
 
@@ -495,7 +606,7 @@ int es_start(void* h) {
   if (!s || s->running.load()) return -1;
   s->t_start = now_ns();
   read_cpu_times(&s->last_cpu);
-  if (!s->rapl.empty()) s->rapl_start_uj = read_rapl_uj(s->rapl);
+  s->host.poll();  // first reading: the zero of the cumulative host joules
   for (auto& g : s->gpus) s->poll_energy(g, s->t_start);
   s->running.store(true, std::memory_order_release);
   s->th = std::thread([s] { s->loop(); });
@@ -581,5 +692,20 @@ int es_drain(void* h, es_sample_t* out, int max) {
 uint64_t es_dropped(void* h) { return h ? static_cast<Sampler*>(h)->dropped.load(std::memory_order_relaxed) : 0; }
 
 int es_sample_size(void) { return int(sizeof(es_sample_t)); }
+
+// Host CPU energy source of a sampler: "amdsmi-cpu", "rapl", "hwmon" or "" (none readable).
+const char* es_host_energy_source(void* h) { return h ? static_cast<Sampler*>(h)->host.source.c_str() : ""; }
+
+// Test hook: feed raw readings of one counter with modulus `range` through the wrap-aware accumulator; returns
+// the accumulated joules (tests/test_energy.py).
+double es_test_wrap_accumulate(const uint64_t* raw, int n, uint64_t range) {
+  double acc = 0;
+  uint64_t last = 0;
+  for (int i = 0; i < n; ++i) {
+    if (i) acc += double(wrap_delta(raw[i], last, range));
+    last = raw[i];
+  }
+  return acc * 1e-6;
+}
 
 }  // extern "C"

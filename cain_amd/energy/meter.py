@@ -10,11 +10,20 @@ Energy sources, per window:
 * ``gpu``  — amd-smi energy accumulator of the tracked GPUs, integrated on the
   native sampler's piecewise-linear trace (exact counter deltas, interpolated
   at the window edges);
-* ``cpu``  — RAPL package energy when ``/sys/class/powercap`` exposes it,
-  otherwise a model ``cpu_tdp_w × mean CPU utilisation × duration``
-  (codecarbon's fallback strategy; labelled ``cpu_energy_source = model``);
-* ``ram``  — optional model ``ram_w_per_gb × GB × duration`` (codecarbon's
-  3 W / 8 GB rule), off by default.
+* ``cpu``  — the host CPU energy counter the native sampler can read (amd-smi
+  CPU sockets through HSMP, RAPL package zones, hwmon ``amd_energy``; wrap-aware),
+  otherwise codecarbon's CPU-load model ``TDP × mean CPU utilisation × duration``
+  with the TDP of this host's CPU model × sockets (``cpu_tdp_w`` / ``CAIN_CPU_TDP_W``
+  override; labelled ``cpu_energy_source = model(...)``).  On by default;
+* ``ram``  — codecarbon's 3 W per 8 GB rule applied to this process's resident
+  memory (the client's share of the DIMMs, not the whole 3 TB host).
+
+The host is shared by every rank of a node: ``host_share`` (1 / ranks per node)
+scales the host-wide CPU energy charged to one window.  Idle subtraction is per
+source: a window charged with GPU and CPU energy subtracts the idle GPU and the
+idle CPU power measured by ``measure_idle`` (never the GPU's idle power from a
+CPU-only window).  Reference: codecarbon measured CPU + GPU + RAM of the client
+(experiment-runner/Plugins/Profilers/CodecarbonWrapper.py:43-68).
 
 The window also reports the reference's utilisation columns: mean CPU %
 (``cpu_usage``), mean GPU gfx activity % (``gpu_usage``, mean like the
@@ -40,6 +49,32 @@ def _env_float(name: str, default: float) -> float:
         return default
 
 
+#: TDP (W per socket) by CPU model substring, codecarbon-style (its cpu_power.csv); first match wins
+CPU_TDP_TABLE = [("EPYC 9965", 500.0), ("EPYC 9755", 500.0), ("EPYC 9575F", 400.0), ("EPYC 9655", 400.0),
+                 ("EPYC 9555", 360.0), ("EPYC 9654", 360.0), ("EPYC 9754", 360.0), ("EPYC 9474F", 360.0),
+                 ("EPYC 9534", 280.0), ("EPYC 7763", 280.0), ("EPYC 7713", 225.0), ("Xeon(R) Platinum 8592", 350.0),
+                 ("Xeon(R) Platinum 8480", 350.0), ("Xeon(R) Platinum 8380", 270.0), ("Apple M2", 20.0)]
+DEFAULT_TDP_PER_SOCKET_W = 250.0
+RAM_W_PER_GB = 3.0 / 8.0  # codecarbon's RAM rule
+
+
+def host_cpu_tdp_w() -> tuple:
+    """(total TDP in W, description) of this host's CPU sockets from /proc/cpuinfo."""
+    model, sockets = "", set()
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name") and not model:
+                    model = line.split(":", 1)[1].strip()
+                elif line.startswith("physical id"):
+                    sockets.add(line.split(":", 1)[1].strip())
+    except OSError:
+        pass
+    n = max(1, len(sockets))
+    per = next((w for key, w in CPU_TDP_TABLE if key in model), DEFAULT_TDP_PER_SOCKET_W)
+    return per * n, f"{n}x {model or 'unknown CPU'} @ {per:.0f} W"
+
+
 @dataclass
 class EnergyReading:
     t_start_ns: int
@@ -59,6 +94,8 @@ class EnergyReading:
     idle_subtracted_j: float = float("nan")
     gpu_counter_updates: int = 0
     per_gpu_energy_j: List[float] = field(default_factory=list)
+    host_share: float = 1.0
+    idle_cpu_power_w: float = float("nan")
     samples: List[dict] = field(default_factory=list)
 
     @property
@@ -118,18 +155,28 @@ class EnergyMeter:
 
     def __init__(self, devices: Optional[Sequence[int]] = None, smi_indices: Optional[Sequence[int]] = None,
                  period_ms: float = 100.0, fast_period_ms: float = 1.0, cpu_core: int = -1,
-                 cpu_tdp_w: Optional[float] = None, ram_w_per_gb: float = 0.0,
-                 sources: Sequence[str] = ("gpu", "cpu"), keep_samples: bool = True):
+                 cpu_tdp_w: Optional[float] = None, ram_w_per_gb: float = RAM_W_PER_GB,
+                 sources: Sequence[str] = ("gpu", "cpu", "ram"), keep_samples: bool = True,
+                 host_share: float = 1.0):
         self.smi = list(smi_indices) if smi_indices is not None else resolve_smi_indices(devices)
         self.sources = tuple(sources)
-        self.cpu_tdp_w = cpu_tdp_w if cpu_tdp_w is not None else _env_float("CAIN_CPU_TDP_W", 0.0)
+        tdp, desc = host_cpu_tdp_w()
+        env_tdp = _env_float("CAIN_CPU_TDP_W", 0.0)
+        if cpu_tdp_w is not None or env_tdp > 0:
+            tdp = float(cpu_tdp_w if cpu_tdp_w is not None else env_tdp)
+            desc = f"configured {tdp:.0f} W"
+        self.cpu_tdp_w, self.cpu_tdp_desc = tdp, desc
         self.ram_w_per_gb = ram_w_per_gb
+        self.host_share = float(host_share)
         self.keep_samples = keep_samples
         self.sampler = native.NativeSampler(self.smi, period_ms=period_ms, fast_period_ms=fast_period_ms,
                                             cpu_core=cpu_core)
         self.sampler.start()
+        self.host_source = self.sampler.host_energy_source
         self._t0: Optional[int] = None
-        self.idle_power_w: float = float("nan")
+        self._rss0 = 0.0
+        self.idle_power_w: float = float("nan")      # idle GPU board power (W, summed over tracked GPUs)
+        self.idle_cpu_power_w: float = float("nan")  # idle host CPU power charged to this meter (W, shared)
         self._lock = threading.Lock()
         self._pending: List[dict] = []
 
@@ -154,16 +201,14 @@ class EnergyMeter:
 
     # -- idle baseline ----------------------------------------------------
     def measure_idle(self, seconds: float = 2.0) -> float:
-        """Mean board power of the tracked GPUs while idle (W, summed over GPUs)."""
-        if self.n_gpus == 0:
-            self.idle_power_w = 0.0
-            return 0.0
-        t0 = native.now_ns()
+        """Idle baselines over one quiet window: GPU board power of the tracked GPUs (W, summed; the return value)
+        and host CPU power as charged by ``_cpu_energy`` (W, this meter's share), each subtracted from its own
+        source only."""
+        self.start()
         time.sleep(seconds)
-        t1 = native.now_ns()
-        time.sleep(0.05)  # let the counter tick past t1
-        e = sum(self.sampler.energy_between(i, t0, t1) for i in range(self.n_gpus))
-        self.idle_power_w = e / ((t1 - t0) * 1e-9)
+        r = self.stop(settle_ms=50.0)
+        self.idle_power_w = r.gpu_energy_j / r.duration_s if self.n_gpus else 0.0
+        self.idle_cpu_power_w = r.cpu_energy_j / r.duration_s
         return self.idle_power_w
 
     # -- windows ----------------------------------------------------------
@@ -172,6 +217,10 @@ class EnergyMeter:
             self._pending = []
         self.sampler.drain()  # discard samples before the window
         self._t0 = native.now_ns()
+        # bound the counter trace of a long-lived meter (a study keeps one for ~1,260 runs): keep 2 s of history
+        # before the window for the interpolation at its left edge
+        self.sampler.trim(max(0, self._t0 - 2_000_000_000))
+        self._rss0 = _rss_gb()
         return self._t0
 
     def stop(self, settle_ms: float = 25.0) -> EnergyReading:
@@ -210,20 +259,21 @@ class EnergyMeter:
         vram = mean("vram_pct", True)
         cpu_j, cpu_src = 0.0, "none"
         if "cpu" in self.sources:
-            rapl = [s["cpu_energy_j"] for s in samples if not math.isnan(s["cpu_energy_j"])]
-            if len(rapl) >= 2:
-                cpu_j = (rapl[-1] - rapl[0]) * dur / max(1e-9, (samples[-1]["t_ns"] - samples[0]["t_ns"]) * 1e-9)
-                cpu_src = "rapl"
-            elif self.cpu_tdp_w > 0:
-                cpu_j = self.cpu_tdp_w * (cpu_pct / 100.0 if not math.isnan(cpu_pct) else 0.0) * dur
-                cpu_src = "model"
+            cpu_j, cpu_src = self._cpu_energy(samples, dur, cpu_pct)
         ram_j = 0.0
         if "ram" in self.sources and self.ram_w_per_gb > 0:
-            ram_j = self.ram_w_per_gb * _total_mem_gb() * dur
+            ram_j = self.ram_w_per_gb * 0.5 * (self._rss0 + _rss_gb()) * dur
         total = gpu_j + cpu_j + ram_j
+        # idle subtraction per source: GPU idle only from GPU energy, CPU idle only from CPU energy; the RAM model
+        # is the client's working set, charged as is
         idle_sub = float("nan")
-        if not math.isnan(self.idle_power_w):
-            idle_sub = total - self.idle_power_w * dur
+        parts = []
+        if "gpu" in self.sources and self.n_gpus:
+            parts.append(gpu_j - self.idle_power_w * dur)
+        if "cpu" in self.sources:
+            parts.append(cpu_j - self.idle_cpu_power_w * dur)
+        if parts and not any(math.isnan(x) for x in parts):
+            idle_sub = float(sum(parts)) + ram_j
         updates = 0
         if self.n_gpus:
             updates = self.sampler.trace_points(0)
@@ -232,7 +282,25 @@ class EnergyMeter:
             total_energy_j=total, cpu_energy_source=cpu_src, gpu_usage=gfx, cpu_usage=cpu_pct, memory_usage=mem_pct,
             gpu_power_w=gpu_j / dur if self.n_gpus else float("nan"), vram_usage=vram,
             idle_power_w=self.idle_power_w, idle_subtracted_j=idle_sub, gpu_counter_updates=updates,
-            per_gpu_energy_j=per_gpu, samples=samples if self.keep_samples else [])
+            per_gpu_energy_j=per_gpu, host_share=self.host_share, idle_cpu_power_w=self.idle_cpu_power_w,
+            samples=samples if self.keep_samples else [])
+
+    def _cpu_energy(self, samples: List[dict], dur: float, cpu_pct: float):
+        """(joules, source) of host CPU energy charged to a window of ``dur`` s: the readable counter's increase
+        (rescaled from the sample span to the window), else the CPU-load model; times ``host_share``."""
+        ctr = [s for s in samples if not math.isnan(s["cpu_energy_j"])]
+        # one host sample per slow period (the per-GPU rows repeat it)
+        seen, pts = set(), []
+        for s in ctr:
+            if s["t_ns"] not in seen:
+                seen.add(s["t_ns"])
+                pts.append((s["t_ns"], s["cpu_energy_j"]))
+        if self.host_source and len(pts) >= 2 and pts[-1][0] > pts[0][0]:
+            span = (pts[-1][0] - pts[0][0]) * 1e-9
+            return (pts[-1][1] - pts[0][1]) * dur / span * self.host_share, self.host_source
+        util = (cpu_pct / 100.0) if not math.isnan(cpu_pct) else 0.0
+        return (self.cpu_tdp_w * util * dur * self.host_share,
+                f"model(tdp {self.cpu_tdp_w:.0f} W x util; {self.cpu_tdp_desc})")
 
 
 def _instant_cpu_pct() -> float:
@@ -251,11 +319,12 @@ def _instant_mem_pct() -> float:
         return float("nan")
 
 
-def _total_mem_gb() -> float:
+def _rss_gb() -> float:
+    """Resident memory of this process (GB): the RAM model's working set."""
     try:
-        import psutil
-        return psutil.virtual_memory().total / 2**30
-    except Exception:  # pragma: no cover
+        with open("/proc/self/statm") as fh:
+            return int(fh.read().split()[1]) * os.sysconf("SC_PAGE_SIZE") / 1e9
+    except (OSError, ValueError, IndexError):  # pragma: no cover
         return 0.0
 
 

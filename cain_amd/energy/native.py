@@ -85,6 +85,10 @@ def load() -> ctypes.CDLL:
         lib.es_drain.argtypes = [ctypes.c_void_p, ctypes.POINTER(ESample), ctypes.c_int]
         lib.es_dropped.argtypes = [ctypes.c_void_p]
         lib.es_dropped.restype = ctypes.c_uint64
+        lib.es_host_energy_source.argtypes = [ctypes.c_void_p]
+        lib.es_host_energy_source.restype = ctypes.c_char_p
+        lib.es_test_wrap_accumulate.argtypes = [ctypes.POINTER(ctypes.c_uint64), ctypes.c_int, ctypes.c_uint64]
+        lib.es_test_wrap_accumulate.restype = ctypes.c_double
         if lib.es_sample_size() != ctypes.sizeof(ESample):
             raise RuntimeError("libcain_energy.so ABI mismatch (rebuild with python -m cain_amd.build)")
         _lib = lib
@@ -154,6 +158,11 @@ class NativeSampler:
     def trim(self, before_ns: int) -> None:
         self.lib.es_trim(self.h, ctypes.c_uint64(before_ns))
 
+    @property
+    def host_energy_source(self) -> str:
+        """Readable host CPU energy counter: "amdsmi-cpu", "rapl", "hwmon" or "" (none)."""
+        return self.lib.es_host_energy_source(self.h).decode()
+
     def drain(self, max_samples: int = 65536) -> List[dict]:
         buf = (ESample * max_samples)()
         n = self.lib.es_drain(self.h, buf, max_samples)
@@ -170,3 +179,9 @@ class NativeSampler:
             self.close()
         except Exception:
             pass
+
+
+def wrap_accumulate(raw: List[int], modulus: int) -> float:
+    """Joules the native wrap-aware accumulator makes of a raw microjoule counter sequence (tests)."""
+    arr = (ctypes.c_uint64 * len(raw))(*raw)
+    return float(load().es_test_wrap_accumulate(arr, len(raw), ctypes.c_uint64(modulus)))

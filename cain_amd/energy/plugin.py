@@ -96,7 +96,7 @@ def emission_tracker(online: bool = False, *decargs, **deckwargs):
     """Class decorator (reference signature ``emission_tracker(online=False, *args, **kwargs)``)."""
     data_columns = list(deckwargs.pop("data_columns", [DataColumns.EMISSIONS]))
     meter_kwargs = {k: deckwargs.pop(k) for k in ("devices", "smi_indices", "period_ms", "fast_period_ms",
-                                                    "cpu_core", "cpu_tdp_w", "ram_w_per_gb", "sources")
+                                                    "cpu_core", "cpu_tdp_w", "ram_w_per_gb", "sources", "host_share")
                     if k in deckwargs}
     country = deckwargs.pop("country_iso_code", "WORLD")
     carbon = deckwargs.pop("carbon_intensity", None)
@@ -136,12 +136,16 @@ def _meter_for(self, meter_kwargs, idle_s) -> EnergyMeter:
     if meter is None:
         kw = dict(getattr(self, "__energy_meter_kwargs__", None) or meter_kwargs)
         kw.setdefault("devices", getattr(self, "energy_devices", None))
+        # the host's CPU energy is shared by the data-parallel ranks of the node
+        kw.setdefault("host_share", 1.0 / max(1, int(getattr(self, "dp_world", 1) or 1)))
         meter = EnergyMeter(**kw)
         if getattr(self, "idle_power_w", None) is not None:
             meter.idle_power_w = float(self.idle_power_w)
+            meter.idle_cpu_power_w = float(getattr(self, "idle_cpu_power_w", float("nan")))
         elif idle_s:
             meter.measure_idle(idle_s)
             self.idle_power_w = meter.idle_power_w
+            self.idle_cpu_power_w = meter.idle_cpu_power_w
         self.__energy_meter__ = meter
     return meter
 
@@ -152,13 +156,16 @@ def ensure_meter(config) -> EnergyMeter:
 
 
 def measure_idle_baseline(config, seconds: float = 2.0) -> float:
-    """Idle board power of the config's measured GPUs (W), measured with a short-lived meter and stored
-    as ``config.idle_power_w`` — call it from BEFORE_EXPERIMENT, before any run and without leaving a
-    sampler thread behind (forked run children could not use it)."""
+    """Idle board power of the config's measured GPUs (W) and idle host CPU power (W, this rank's share),
+    measured with a short-lived meter and stored as ``config.idle_power_w`` / ``config.idle_cpu_power_w`` —
+    call it from BEFORE_EXPERIMENT, before any run and without leaving a sampler thread behind (forked run
+    children could not use it)."""
     kw = dict(getattr(config, "__energy_meter_kwargs__", None) or {})
     kw.setdefault("devices", getattr(config, "energy_devices", None))
+    kw.setdefault("host_share", 1.0 / max(1, int(getattr(config, "dp_world", 1) or 1)))
     with EnergyMeter(**kw) as m:
         config.idle_power_w = m.measure_idle(seconds)
+        config.idle_cpu_power_w = m.idle_cpu_power_w
     return config.idle_power_w
 
 

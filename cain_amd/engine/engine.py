@@ -104,12 +104,12 @@ LT_WS_BYTES = 64 << 20  # hipBLASLt workspace of the wide-batch path
 
 
 def lt_min_rows(max_batch: int, weight_dtype: str = "bf16") -> int:
-    """Row count from which a forward runs its O and gate/up projections on hipBLASLt (0: never).
+    """Row count from which a forward runs its O and gate/up projections on hipBLASLt (0: never, the default).
 
-    128 by default: hipBLASLt wins both projections from 128 rows up and loses gate/up at 64
-    (profiles/bgemm_sweep.md, profiles/lt_gemm.md).  ``CAIN_LT_MIN_ROWS`` overrides (0 disables); the fp8
-    weight path has no library equivalent."""
-    v = int(os.environ.get("CAIN_LT_MIN_ROWS", "128"))
+    Off by default since the hand-written wide-batch kernel (csrc/wgemm.hip) took over 64 < M <= 256
+    (profiles/wgemm_r2.md); ``CAIN_LT_MIN_ROWS=128`` brings the library path back for A/B runs.  The fp8 weight
+    path has no library equivalent."""
+    v = int(os.environ.get("CAIN_LT_MIN_ROWS", "0"))
     if v <= 0 or weight_dtype != "bf16" or max_batch < v:
         return 0
     return v

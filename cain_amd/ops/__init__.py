@@ -11,7 +11,8 @@ Kernel inventory:
 op                     source                      replaces (Ollama/llama.cpp)
 =====================  ==========================  =============================
 ``skinny_gemm``        csrc/gemm.hip               O / gate-up(+act) / down / LM head GEMV,
-                                                   fused RMSNorm, residual epilogue
+                       csrc/wgemm.hip              fused RMSNorm, residual epilogue (wgemm: the
+                                                   LDS-DMA ring kernel for 64 < M <= 256 rows)
 ``qkv_rope``           csrc/gemm.hip               QKV GEMV + bias + RoPE + KV-cache append
 ``lt_gemm``            csrc/blas.hip               O / gate-up GEMM at >= 128 rows (hipBLASLt)
 ``rownorm_act``        csrc/blas.hip               RMSNorm scale + SiLU/GeLU*up after lt_gemm
@@ -73,6 +74,8 @@ def load() -> ctypes.CDLL:
                                      + [ci] * 5 + [vp])
         lib.cain_gemm_ws_bytes.restype = ctypes.c_longlong
         lib.cain_gemm_ws_bytes.argtypes = [ci, ci, ci]
+        lib.cain_wgemm_set_min_m.argtypes = [ci]
+        lib.cain_wgemm_eligible.argtypes = [ci, ci, ci]
         lib.cain_lt_gemm.argtypes = [vp, vp, ci, ci, ci, ci, vp, ci, ci, vp, ctypes.c_longlong, vp]
         lib.cain_lt_prepare.argtypes = [ci, ci, ci, ci, ci, ci, ctypes.c_longlong]
         lib.cain_rownorm_act.argtypes = [vp, ci, ci, cf, ci, vp, ci, vp, ci, ci, ci, ci, vp]
@@ -126,6 +129,16 @@ _ws_cache: dict = {}
 def gemm_ws_bytes(n: int, k: int, m: int) -> int:
     """Workspace the batched GEMM path needs for this shape (0: the skinny kernel runs it)."""
     return int(load().cain_gemm_ws_bytes(n, k, m))
+
+
+def set_wide_gemm_min_m(m: int) -> None:
+    """Rows from which GEMMs run on the wide-batch kernel (csrc/wgemm.hip; default 64, 0 disables): A/B switch
+    for tests and tuning, read at every launch and graph capture."""
+    load().cain_wgemm_set_min_m(int(m))
+
+
+def wide_gemm_eligible(n: int, k: int, m: int) -> bool:
+    return bool(load().cain_wgemm_eligible(n, k, m))
 
 
 def _workspace(device, nbytes: int) -> Optional[torch.Tensor]:

@@ -944,8 +944,14 @@ static bool bgemm_eligible(int N, int K, int M) {
   return M > bgemm_min_m() && M <= 256 && K % (32 * BG_CK) == 0 && (M > 32 || N >= 8192 || K > 4096);
 }
 
-// Workspace the batched path needs for a GEMM of this shape (0 when the skinny kernel runs it).
+// wgemm.hip: the wide-batch (64 < M <= 256) kernel; its split-K slabs live after the batched path's counters
+CAIN_API int cain_wgemm_eligible(int N, int K, int M);
+CAIN_API long long cain_wgemm_ws_bytes(int N, int K, int M);
+int wgemm_dispatch(const GemmArgs& a, int epi, bool norm, void* ws, long long ws_bytes, hipStream_t st);
+
+// Workspace the batched paths need for a GEMM of this shape (0 when the skinny kernel runs it).
 CAIN_API long long cain_gemm_ws_bytes(int N, int K, int M) {
+  if (cain_wgemm_eligible(N, K, M)) return (long long)BG_COUNTER_BYTES + cain_wgemm_ws_bytes(N, K, M);
   if (!bgemm_eligible(N, K, M)) return 0;
   return (long long)bgemm_ws_bytes(bgemm_plan(N, K, M, bgemm_ntw()));
 }
@@ -967,12 +973,27 @@ CAIN_API int cain_skinny_gemm_ex(const void* Wp, const void* X, int ldx, int K, 
   return gemm_dispatch(a, epi, norm != 0, waves, st);
 }
 
-// Full entry: batched path for 16 < M <= 256 when a workspace of cain_gemm_ws_bytes() (zeroed once) is
-// given, the skinny kernel otherwise.
+// Full entry: the wide kernel (wgemm.hip) for 64 < M <= 256, the batched path for 16 < M <= 64, when a
+// workspace of cain_gemm_ws_bytes() (zeroed once) is given; the skinny kernel otherwise.
 CAIN_API int cain_gemm(const void* Wp, const void* X, int ldx, int K, int N, int M, void* Y, int ldy,
                        const float* bias, int norm, float eps, const int* slot, const int* pos,
                        const float* cos_t, const float* sin_t, void* kc, void* vtc, int H, int Hkv, int hd, int T_max,
                        void* ws, long long ws_bytes, int epi, int waves, hipStream_t st) {
+  if (ws && cain_wgemm_eligible(N, K, M) && ws_bytes >= (long long)BG_COUNTER_BYTES) {
+    if (epi == EPI_QKV_ROPE && (hd % 16 || (hd / 2) % 8)) return -1;
+    GemmArgs a{};
+    a.Wp = reinterpret_cast<const bf16x8*>(Wp);
+    a.X = reinterpret_cast<const __bf16*>(X);
+    a.ldx = ldx, a.K = K, a.N = N, a.M = M, a.Y = Y, a.ldy = ldy, a.bias = bias;
+    a.eps = eps;
+    a.slot = slot, a.pos = pos, a.cos_t = cos_t, a.sin_t = sin_t;
+    a.kc = reinterpret_cast<__bf16*>(kc), a.vtc = reinterpret_cast<__bf16*>(vtc);
+    a.H = H, a.Hkv = Hkv, a.hd = hd, a.T_max = T_max;
+    // the batched path's counters (first BG_COUNTER_BYTES) must stay zero: the slabs go after them
+    const int rc = wgemm_dispatch(a, epi, norm != 0, static_cast<char*>(ws) + BG_COUNTER_BYTES,
+                                  ws_bytes - (long long)BG_COUNTER_BYTES, st);
+    if (rc >= 0) return rc;
+  }
   if (ws && bgemm_eligible(N, K, M) && K % 32 == 0 && N % 16 == 0) {
     const BgPlan p = bgemm_plan(N, K, M, bgemm_ntw());
     if ((long long)bgemm_ws_bytes(p) <= ws_bytes && p.nblk * 4 <= (int)BG_COUNTER_BYTES) {

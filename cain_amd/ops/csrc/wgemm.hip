@@ -1,0 +1,512 @@
+// Wide-batch projection GEMM for 64 < M <= 256 rows (the batched decode step and prefill chunks), gfx950.
+//
+//   Y[m][n] = epilogue( inv[m] * sum_k X[m][k] * W[n][k] )
+//
+// Replaces, at the trial-batched decode shapes, the per-token GEMVs llama.cpp runs inside Ollama for the
+// reference's workload (reference experiment/RunnerConfig.py:128-131; SURVEY §2.4 rows QKV / O / gate-up / down /
+// LM head).  The M <= 64 shapes stay on the weight-streaming kernels of gemm.hip.
+//
+// Why a different kernel at these widths: at M = 256 every weight byte feeds 256 MFMA rows, so the GEMM is no
+// longer a pure weight stream -- per CU it has to ingest its weight slice AND the activation panel it multiplies,
+// and the per-CU load path (~60-70 GB/s per CU, MI355X_MICROARCH.md rows 'ldsdma-fill' / 'ring-gemm') becomes the
+// limit long before HBM.  A workgroup therefore owns the largest output tile the LDS ring allows, BM = all rows x
+// BN = 128 columns, so per weight byte it ingests (BM + BN) / BN = 3 bytes, and both operands move by LDS-DMA
+// (global_load_lds_dwordx4: no VGPR staging, no ds_write pass; cdna_hip_programming.md §5 'glds vs register
+// staging', rows 'M = 256 projection GEMM'):
+//
+//   * W tiles come straight from the engine's MFMA-fragment-major packing (models/weights.py pack_mfma_a): a
+//     16-row x 32-k fragment block is 1 KiB contiguous in HBM, so one LDS-DMA instruction moves one block and
+//     the LDS image is fragment-major too -- every A-fragment read is lane-linear ds_read_b128, conflict-free.
+//     Streamed once: non-temporal (aux = nt).
+//   * X (activations, [M][ldx] bf16 row-major, L2-resident) is staged in full 128-B lines: a stage holds BK = 64
+//     k, i.e. one line per row, and one LDS-DMA instruction covers 8 rows.  The lane-linear LDS image is
+//     XOR-swizzled by permuting the per-lane SOURCE piece (rule 21): LDS slot q of row r holds global piece
+//     q ^ ((r >> 1) & 7), which makes the 16-lane groups of the B-fragment ds_read_b128 conflict-free.
+//   * Two LDS rings, X (DX + 1 slots of 32 KiB at BM = 256) and W (DW + 1 slots of 16 KiB), the deeper one for
+//     the HBM stream; one raw s_barrier per 64-deep k-step; counted `s_waitcnt vmcnt` keeps the younger stages
+//     in flight across it (§5 'Pipelining across barriers').
+//   * Warp-specialised: 4 loader waves (one per SIMD) issue every LDS-DMA piece and wait for it; 8 MFMA waves
+//     only read fragments and compute.  Measured on the 256-row gate/up shape, DMA alone took 55-63 us and the
+//     MFMA body alone 60 us, but 85-92 us when the MFMA waves issued the DMA themselves; split roles: 68 us.
+//   * 8 waves as WM (M) x WN (N): each wave owns MB 16-row blocks x TN 16-column tiles (4 x 4 at BM = 256), so
+//     per 32-deep slice it reads TN + MB fragments for TN * MB v_mfma_f32_16x16x32_bf16 (LDS ~50 % busy at full
+//     MFMA rate).
+//   * Fused RMSNorm: the norm gain is folded into W (models/weights.py fold_gain), so only the per-row sum of
+//     squares of X is needed; it comes from the MFMA unit itself -- mfma(xfrag, xfrag) accumulates X X^T whose
+//     diagonal is the row's sum of squares (exact fp32 accumulation of bf16 products), one extra MFMA per
+//     fragment, split between the WN waves that read the same rows.
+//
+// Split-K: narrow outputs (QKV, O, down: 32-48 column tiles) split K over ks workgroups so ~256 workgroups
+// stream; each writes its fp32 tile to a workspace slab (plain stores) and `wgemm_reduce_kernel` -- the next
+// launch on the stream, so the kernel boundary orders the hand-off -- sums the slabs and runs the fused
+// epilogue.  With ks = 1 (gate/up, LM head) the GEMM kernel runs the epilogue itself.  The epilogues are
+// gemm_epi.h's (residual, bias, SiLU/GeLU x up, RoPE + KV-cache append, fp32 logits).
+#include <algorithm>
+#include <cstdlib>
+
+#include "common.h"
+#include "gemm_epi.h"
+
+namespace {
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) const void gbl_void_t;
+
+constexpr int WG_NT = 8;    // output columns per workgroup: 8 tiles of 16
+constexpr int WG_BK = 64;   // k per ring stage (2 slices of 32)
+
+template <int BM>
+struct WgGeo {
+  static constexpr int WM = BM == 256 ? 4 : 2;  // waves along M
+  static constexpr int WN = 8 / WM;             // waves along N
+  static constexpr int MB = BM / 16 / WM;       // 16-row blocks per wave
+  static constexpr int TN = WG_NT / WN;         // 16-column tiles per wave
+  static constexpr int W_BYTES = WG_NT * 2 * 1024;  // one W stage: 8 tiles x 2 slices of 1 KiB
+  static constexpr int X_BYTES = BM * WG_BK * 2;    // one X stage: BM rows x 128 B
+  static constexpr int XPW = BM / 8 / 8;        // X LDS-DMA instructions per wave per stage (8 rows each)
+  static constexpr int RB = BM / 16;            // row blocks per tile (split-K slab units)
+};
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+// wave-uniform runtime count (the pipeline tail issues fewer stages): one uniform branch per value
+template <int N = 0>
+__device__ __forceinline__ void wait_vmcnt_rt(int n) {
+  if constexpr (N >= 30) {
+    wait_vmcnt<N>();
+  } else {
+    if (n <= N) wait_vmcnt<N>();
+    else wait_vmcnt_rt<N + 1>(n);
+  }
+}
+
+// every wave's LDS-DMA of the stage being consumed has landed (its own counted wait before this), and every
+// wave has finished reading the slot about to be refilled
+__device__ __forceinline__ void ring_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+__device__ __forceinline__ void glds16(const void* src, char* lds_wave_base, int aux_nt) {
+  if (aux_nt)
+    __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)lds_wave_base, 16, 0, 2);
+  else
+    __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)lds_wave_base, 16, 0, 0);
+}
+
+}  // namespace
+
+struct WgArgs {
+  int ks;           // k-splits (workgroups per column block)
+  int kst;          // ring stages (64-deep k-steps) per split
+  float* part;      // [ks][n_units][64 lanes] f32x4 (ks > 1)
+  float* part_ss;   // [ks][BM] per-row partial sums of squares (ks > 1 && NORM)
+};
+
+// DX / DW: prefetch distance (stages in flight) of the X and the W ring; the rings have DX + 1 and DW + 1 slots.
+// W streams from HBM (latency ~2-3 us under load) and gets the deeper ring; X comes from L2.
+//
+// NDMA: waves dedicated to the LDS-DMA (0: the 8 MFMA waves issue their own shares).  Measured on the 256-row
+// gate/up shape (tools/wgemm_bench.py ablations): DMA alone 63 us, fragment reads + MFMAs alone 60 us, both in
+// the same waves 85-92 us -- a wave cannot issue MFMAs while it issues ~60-cycle DMA pieces, and the per-stage
+// barrier keeps the two waves of a SIMD in the same phase.  With NDMA = 4 one loader wave per SIMD issues every
+// piece and waits for it; the MFMA waves only compute.  Both roles pass the same one barrier per stage.
+//
+// Loop (compute waves): the barrier of stage t + 1 sits between stage t's two slices, so the next slice's
+// fragment reads are always in flight under 16 MFMAs and no wave restarts the matrix pipe behind a barrier.
+//
+// ABL (diagnostics only): 1 = DMA without the fragment reads and MFMAs, 2 = fragment reads and MFMAs without the
+// DMA.  Results are garbage in both.
+template <int BM, int DX, int DW, int EPI, bool NORM, int NDMA, int ABL = 0>
+__global__ __launch_bounds__(64 * (8 + NDMA), (8 + NDMA) / 4) void wgemm_kernel(const GemmArgs a, const WgArgs w) {
+  using G = WgGeo<BM>;
+  constexpr int NX = DX + 1, NW = DW + 1;
+  constexpr int NLOAD = NDMA ? NDMA : 8;            // waves issuing LDS-DMA
+  constexpr int WPW = 16 / NLOAD;                   // W blocks (1 KiB) per loader wave per stage
+  constexpr int XPW = (BM / 8) / NLOAD;             // X row octets per loader wave per stage
+  constexpr int NTHR = 64 * (8 + NDMA);
+  static_assert(DW >= DX && DX >= 1, "W is issued no later than X of the same stage");
+  static_assert(WPW * NLOAD == 16 && XPW * NLOAD == BM / 8, "loader split");
+  extern __shared__ __attribute__((aligned(16))) char smem[];  // the one LDS array: [NW W slots][NX X slots]
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const bool compute = wave < 8;
+  const bool loader = NDMA ? !compute : true;
+  const int lw = NDMA ? wave - 8 : wave;  // loader index
+  const int wm = wave % G::WM, wn = (wave / G::WM) % G::WN;
+  const int KS = a.K >> 5, ntiles = a.N >> 4;
+  const int nblk = (ntiles + WG_NT - 1) / WG_NT;
+
+  // block -> (column block, k-split); the k-split partners of one column block read disjoint X panels, the
+  // column blocks of one k-split read the SAME X panel: keep those on one XCD (blocks b and b + 8 share an XCD
+  // under round-robin dispatch; speed only, any placement is correct)
+  int blk, kc;
+  {
+    const int bid = blockIdx.x, ks = w.ks;
+    if (ks == 1) blk = bid, kc = 0;
+    else if ((8 % ks) == 0) kc = bid % ks, blk = bid / ks;
+    else kc = bid / nblk, blk = bid - kc * nblk;
+  }
+  const int tile0 = blk * WG_NT;
+  const int st0 = kc * w.kst;                    // first stage (64-deep k-step) of this split
+  const int nst = min(w.kst, (a.K >> 6) - st0);  // stages of this split
+
+  // ---- LDS-DMA sources of this loader (per stage: WPW W blocks + XPW X row-octets)
+  // W block j of loader lw: tile (lw * WPW + j) / 2, slice (lw * WPW + j) & 1 (a tile's two slices are 2 KiB
+  // contiguous in the packing); LDS W image: block (tile * 2 + slice) at 1 KiB each
+  const char* wsrc[WPW];
+#pragma unroll
+  for (int j = 0; j < WPW; ++j) {
+    const int q = lw * WPW + j, tn = q >> 1, sl = q & 1;
+    wsrc[j] = reinterpret_cast<const char*>(a.Wp) +
+              ((size_t)min(tile0 + tn, ntiles - 1) * KS + (size_t)st0 * 2 + sl) * 1024 + lane * 16;
+  }
+  // X: octet i covers rows 8i .. 8i + 7; lane -> row 8i + (lane >> 3), LDS slot lane & 7 holding global piece
+  // (lane & 7) ^ ((r >> 1) & 7) (the read side's XOR swizzle)
+  const char* xsrc[XPW];
+#pragma unroll
+  for (int j = 0; j < XPW; ++j) {
+    const int i = lw + NLOAD * j;
+    const int r = 8 * i + (lane >> 3);
+    const int p = (lane & 7) ^ ((r >> 1) & 7);
+    xsrc[j] = reinterpret_cast<const char*>(a.X) + ((size_t)min(r, a.M - 1) * a.ldx + (size_t)st0 * WG_BK + p * 8) * 2;
+  }
+  char* const xring = smem + NW * G::W_BYTES;
+  auto issue_w = [&](int t) {  // W stage t (relative to st0) into W slot t % NW
+    if constexpr (ABL == 2) return;
+    char* base = smem + (t % NW) * G::W_BYTES;
+#pragma unroll
+    for (int j = 0; j < WPW; ++j) glds16(wsrc[j] + (size_t)t * 2048, base + (lw * WPW + j) * 1024, 1);
+  };
+  auto issue_x = [&](int t) {  // X stage t into X slot t % NX
+    if constexpr (ABL == 2) return;
+    char* base = xring + (t % NX) * G::X_BYTES;
+#pragma unroll
+    for (int j = 0; j < XPW; ++j) glds16(xsrc[j] + (size_t)t * (WG_BK * 2), base + (lw + NLOAD * j) * 1024, 0);
+  };
+  // issue order: step u (u < 0: prologue) issues W(u + DW), then X(u + DX); so W(t) is always older than X(t) and
+  // waiting for X(t) covers both (vmcnt retires in issue order).  Loads younger than X(t): steps t-DX+1 .. t-1.
+  auto younger_than = [&](int t) {
+    int n = 0;
+#pragma unroll
+    for (int u = t - DX + 1; u < t; ++u) n += WPW * (u + DW < nst) + XPW * (u + DX < nst);
+    return n;
+  };
+  auto land = [&](int t) {  // this loader's pieces of stage t have landed (a loader's own counted wait)
+    if constexpr (ABL != 2) {
+      if (loader) wait_vmcnt_rt(younger_than(t));
+    }
+  };
+  auto issue_step = [&](int t) {
+    if (loader) {
+      if (t + DW < nst) issue_w(t + DW);
+      if (t + DX < nst) issue_x(t + DX);
+    }
+  };
+
+  // ---- fragment read offsets inside a stage (compute waves)
+  const int c = lane & 15, g = lane >> 4;
+  int woff[G::TN];
+#pragma unroll
+  for (int tn = 0; tn < G::TN; ++tn) woff[tn] = (wn * G::TN + tn) * 2048 + lane * 16;
+  int xoff[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) xoff[s] = c * 128 + (((4 * s + g) ^ (c >> 1)) << 4);
+  const int xrow0 = wm * G::MB * 16 * 128;  // byte offset of this wave's first row block in the X image
+
+  f32x4 acc[G::TN][G::MB];
+#pragma unroll
+  for (int tn = 0; tn < G::TN; ++tn)
+#pragma unroll
+    for (int mb = 0; mb < G::MB; ++mb) acc[tn][mb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  f32x4 ssq[G::MB];  // NORM: X X^T diagonal blocks of this wave's rows (slice wn of every stage)
+#pragma unroll
+  for (int mb = 0; mb < G::MB; ++mb) ssq[mb] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto read_slice = [&](int t, int s, bf16x8 (&af)[G::TN], bf16x8 (&bfr)[G::MB]) {
+    const char* wbase = smem + (t % NW) * G::W_BYTES + s * 1024;
+    const char* xbase = xring + (t % NX) * G::X_BYTES + xrow0 + xoff[s];
+#pragma unroll
+    for (int tn = 0; tn < G::TN; ++tn) af[tn] = *reinterpret_cast<const bf16x8*>(wbase + woff[tn]);
+#pragma unroll
+    for (int mb = 0; mb < G::MB; ++mb) bfr[mb] = *reinterpret_cast<const bf16x8*>(xbase + mb * 2048);
+  };
+  // MFMAs of one slice; `mid` runs after the first one (the next slice's reads go there, so only the first MFMA
+  // waits for this slice's reads and the reads in flight never hold an MFMA back)
+  auto mfma_slice = [&](int s, const bf16x8 (&af)[G::TN], const bf16x8 (&bfr)[G::MB], auto mid) {
+#pragma unroll
+    for (int tn = 0; tn < G::TN; ++tn)
+#pragma unroll
+      for (int mb = 0; mb < G::MB; ++mb) {
+        acc[tn][mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[tn], bfr[mb], acc[tn][mb], 0, 0, 0);
+        if (tn == 0 && mb == 0) {
+          __builtin_amdgcn_sched_barrier(0);
+          mid();
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+    if constexpr (NORM) {
+      if (wn == s) {
+#pragma unroll
+        for (int mb = 0; mb < G::MB; ++mb)
+          ssq[mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[mb], bfr[mb], ssq[mb], 0, 0, 0);
+      }
+    }
+  };
+
+  // ---- prologue: steps -DW .. -1
+  if (loader) {
+#pragma unroll
+    for (int u = -DW; u < 0; ++u) {
+      if (u + DW < nst) issue_w(u + DW);
+      if (u + DX >= 0 && u + DX < nst) issue_x(u + DX);
+    }
+  }
+
+  // ---- main loop: nst barriers for every wave; the barrier of stage t + 1 retires stage t's slots, which take
+  // the loads of step t + 1 (every wave's reads of stage t completed: lgkmcnt(0) in ring_barrier)
+  if (NDMA && !compute) {
+    for (int t = 0; t < nst; ++t) {
+      land(t);
+      ring_barrier();
+      issue_step(t);
+    }
+  } else if constexpr (ABL == 1) {
+    for (int t = 0; t < nst; ++t) {
+      land(t);
+      ring_barrier();
+      issue_step(t);
+    }
+  } else {
+    bf16x8 a0[G::TN], b0[G::MB], a1[G::TN], b1[G::MB];
+    land(0);
+    ring_barrier();
+    if constexpr (!NDMA) issue_step(0);
+    read_slice(0, 0, a0, b0);
+    for (int t = 0; t < nst; ++t) {
+      __builtin_amdgcn_sched_barrier(0);
+      mfma_slice(0, a0, b0, [&] { read_slice(t, 1, a1, b1); });
+      __builtin_amdgcn_sched_barrier(0);
+      if (t + 1 < nst) {
+        land(t + 1);
+        ring_barrier();
+        if constexpr (!NDMA) issue_step(t + 1);
+        read_slice(t + 1, 0, a0, b0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      mfma_slice(1, a1, b1, [] {});
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  ring_barrier();  // every wave is done with the ring: its LDS becomes epilogue scratch
+
+  // ---- per-row sums of squares: the diagonal of each X X^T block (lane (c, g) holds C[4g + i][c], so the
+  // diagonal element of row c sits in lane c + 16 * (c >> 2), register c & 3)
+  float* s_ss = reinterpret_cast<float*>(smem);  // [2][BM]
+  if constexpr (NORM) {
+    if (compute && wn < 2 && (c >> 2) == g) {
+#pragma unroll
+      for (int mb = 0; mb < G::MB; ++mb) s_ss[wn * BM + (wm * G::MB + mb) * 16 + c] = ssq[mb][c & 3];
+    }
+    __syncthreads();
+  }
+  if (!compute) return;
+
+  if (w.ks > 1) {
+    // fp32 slab of this split: unit (gt, rb) = 16 x 16 outputs, lane-major f32x4 (the reducer's layout)
+    const int n_units = nblk * WG_NT * G::RB;
+#pragma unroll
+    for (int tn = 0; tn < G::TN; ++tn)
+#pragma unroll
+      for (int mb = 0; mb < G::MB; ++mb) {
+        const int unit = (tile0 + wn * G::TN + tn) * G::RB + wm * G::MB + mb;
+        *reinterpret_cast<f32x4*>(w.part + (((size_t)kc * n_units + unit) * 64 + lane) * 4) = acc[tn][mb];
+      }
+    if constexpr (NORM) {
+      if (blk == 0)
+        for (int r = threadIdx.x; r < BM; r += 512) w.part_ss[(size_t)kc * BM + r] = s_ss[r] + s_ss[BM + r];
+    }
+    return;
+  }
+  (void)NTHR;
+
+  // ---- fused epilogue (ks = 1)
+#pragma unroll
+  for (int tn = 0; tn < G::TN; ++tn) {
+    const int gt = tile0 + wn * G::TN + tn;
+#pragma unroll
+    for (int mb = 0; mb < G::MB; ++mb) {
+      const int rb = wm * G::MB + mb;
+      const int m = rb * 16 + c;
+      f32x4 v = acc[tn][mb];
+      if constexpr (NORM) v *= rsqrtf((s_ss[m] + s_ss[BM + m]) / float(a.K) + a.eps);
+      // the pair epilogues read the partner rows (+8 of the tile) from lane + 32: exchanged by every lane
+      f32x4 pv;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) pv[i] = __shfl_xor(v[i], 32, 64);
+      if (gt < ntiles) {
+        const EpiIn e = epi_load_at<EPI>(a, gt, m, lane);
+        epi_store<EPI>(a, gt, m, lane, e, [&](int off) { return off ? pv : v; });
+      }
+    }
+  }
+}
+
+// Split-K combine + fused epilogue: one wave per 16 x 16 output unit.
+template <int BM, int EPI, bool NORM>
+__global__ __launch_bounds__(256) void wgemm_reduce_kernel(const GemmArgs a, const WgArgs w, int n_units) {
+  constexpr int RB = BM / 16;
+  const int lane = threadIdx.x & 63;
+  const int unit = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (unit >= n_units) return;
+  const int gt = unit / RB, rb = unit - gt * RB;
+  const int ntiles = a.N >> 4;
+  const int m = rb * 16 + (lane & 15);
+  f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int k = 0; k < w.ks; ++k) v += *reinterpret_cast<const f32x4*>(w.part + (((size_t)k * n_units + unit) * 64 + lane) * 4);
+  if constexpr (NORM) {
+    float ss = 0.f;
+    for (int k = 0; k < w.ks; ++k) ss += w.part_ss[(size_t)k * BM + m];
+    v *= rsqrtf(ss / float(a.K) + a.eps);
+  }
+  f32x4 pv;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) pv[i] = __shfl_xor(v[i], 32, 64);
+  if (gt >= ntiles) return;
+  const EpiIn e = epi_load_at<EPI>(a, gt, m, lane);
+  epi_store<EPI>(a, gt, m, lane, e, [&](int off) { return off ? pv : v; });
+}
+
+namespace {
+
+struct WgPlan {
+  int bm, nblk, ks, kst;
+  size_t part_floats, ss_floats;
+};
+
+int wg_env(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e ? atoi(e) : dflt;
+}
+
+// Split count: ~256 streaming workgroups (one per CU: the ring takes 128-144 KiB of LDS), at most 8 splits and
+// at least 4 stages per split.  Column-block counts >= 128 (gate/up, LM head) run unsplit.
+int g_wg_target = -1, g_wg_ksmax = -1;
+
+WgPlan wg_plan(int N, int K, int M) {
+  if (g_wg_target < 0) g_wg_target = wg_env("CAIN_WGEMM_TARGET", 256);
+  if (g_wg_ksmax < 0) g_wg_ksmax = wg_env("CAIN_WGEMM_KSMAX", 8);
+  const int target = g_wg_target, ksmax = g_wg_ksmax;
+  WgPlan p{};
+  p.bm = M > 128 ? 256 : 128;
+  p.nblk = ((N >> 4) + WG_NT - 1) / WG_NT;
+  const int stages = K / WG_BK;
+  int ks = p.nblk >= 128 ? 1 : std::max(1, std::min(ksmax, (target + p.nblk / 2) / p.nblk));
+  ks = std::min(ks, std::max(1, stages / 4));
+  p.kst = (stages + ks - 1) / ks;
+  p.ks = (stages + p.kst - 1) / p.kst;
+  if (p.ks > 1) {
+    p.part_floats = (size_t)p.ks * p.nblk * WG_NT * (p.bm / 16) * 256;
+    p.ss_floats = (size_t)p.ks * p.bm;
+  }
+  return p;
+}
+
+template <int BM, int DX, int DW, int EPI, bool NORM, int NDMA, int ABL = 0>
+hipError_t wg_launch(const GemmArgs& a, const WgArgs& w, const WgPlan& p, hipStream_t st) {
+  using G = WgGeo<BM>;
+  constexpr int lds = (DW + 1) * G::W_BYTES + (DX + 1) * G::X_BYTES;
+  static_assert(lds <= 160 * 1024, "LDS");
+  static bool attr = [] {
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(&wgemm_kernel<BM, DX, DW, EPI, NORM, NDMA, ABL>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, lds) == hipSuccess;
+  }();
+  if (!attr) return hipErrorInvalidConfiguration;
+  hipLaunchKernelGGL((wgemm_kernel<BM, DX, DW, EPI, NORM, NDMA, ABL>), dim3(p.nblk * p.ks), dim3(64 * (8 + NDMA)), lds,
+                     st, a, w);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess || p.ks == 1) return e;
+  const int n_units = p.nblk * WG_NT * G::RB;
+  hipLaunchKernelGGL((wgemm_reduce_kernel<BM, EPI, NORM>), dim3((n_units + 3) / 4), dim3(256), 0, st, a, w, n_units);
+  return hipGetLastError();
+}
+
+// ring / loader variants: 0 = default; the rest are tuning alternatives (cain_wgemm_set_variant,
+// CAIN_WGEMM_VARIANT) and the ablations of tools/wgemm_bench.py
+int g_wgemm_variant = -1;
+
+template <int BM, int EPI, bool NORM>
+hipError_t wg_launch_v(const GemmArgs& a, const WgArgs& w, const WgPlan& p, hipStream_t st) {
+  if (g_wgemm_variant < 0) g_wgemm_variant = wg_env("CAIN_WGEMM_VARIANT", 0);
+  if constexpr (BM == 256) {  // X stage 32 KiB, W stage 16 KiB
+    switch (g_wgemm_variant) {
+      case 1: return wg_launch<BM, 2, 3, EPI, NORM, 0>(a, w, p, st);     // MFMA waves load
+      case 2: return wg_launch<BM, 2, 2, EPI, NORM, 4>(a, w, p, st);     // 144 KiB
+      case 3: return wg_launch<BM, 1, 5, EPI, NORM, 4>(a, w, p, st);     // 160 KiB
+      case 8: return wg_launch<BM, 2, 3, EPI, NORM, 4, 1>(a, w, p, st);  // DMA only
+      case 9: return wg_launch<BM, 2, 3, EPI, NORM, 4, 2>(a, w, p, st);  // compute only
+      default: return wg_launch<BM, 2, 3, EPI, NORM, 4>(a, w, p, st);    // 160 KiB
+    }
+  } else {  // X stage 16 KiB, W stage 16 KiB
+    switch (g_wgemm_variant) {
+      case 1: return wg_launch<BM, 3, 5, EPI, NORM, 0>(a, w, p, st);
+      case 2: return wg_launch<BM, 3, 3, EPI, NORM, 4>(a, w, p, st);     // 128 KiB
+      case 3: return wg_launch<BM, 2, 6, EPI, NORM, 4>(a, w, p, st);     // 160 KiB
+      default: return wg_launch<BM, 3, 5, EPI, NORM, 4>(a, w, p, st);    // 160 KiB
+    }
+  }
+}
+
+template <int BM, bool NORM>
+hipError_t wg_launch_e(int epi, const GemmArgs& a, const WgArgs& w, const WgPlan& p, hipStream_t st) {
+  switch (epi) {
+    case EPI_BF16: return wg_launch_v<BM, EPI_BF16, NORM>(a, w, p, st);
+    case EPI_RESID: return wg_launch_v<BM, EPI_RESID, NORM>(a, w, p, st);
+    case EPI_F32: return wg_launch_v<BM, EPI_F32, NORM>(a, w, p, st);
+    case EPI_SILU: return wg_launch_v<BM, EPI_SILU, NORM>(a, w, p, st);
+    case EPI_GELU: return wg_launch_v<BM, EPI_GELU, NORM>(a, w, p, st);
+    case EPI_QKV_ROPE: return wg_launch_v<BM, EPI_QKV_ROPE, NORM>(a, w, p, st);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+}  // namespace
+
+// Rows from which the wide kernel takes a GEMM (CAIN_WGEMM_MIN_M; default 64: M in (64, 256]; 0 disables).
+static int g_wgemm_min_m = -1;
+CAIN_API int cain_wgemm_min_m() {
+  if (g_wgemm_min_m < 0) g_wgemm_min_m = wg_env("CAIN_WGEMM_MIN_M", 64);
+  return g_wgemm_min_m;
+}
+// A/B switches for tests and tuning tools (take effect for launches and graph captures after the call).
+CAIN_API void cain_wgemm_set_min_m(int m) { g_wgemm_min_m = m; }
+CAIN_API void cain_wgemm_set_variant(int v) { g_wgemm_variant = v; }
+CAIN_API void cain_wgemm_set_split(int target, int ksmax) { g_wg_target = target, g_wg_ksmax = ksmax; }
+
+CAIN_API int cain_wgemm_eligible(int N, int K, int M) {
+  const int mm = cain_wgemm_min_m();
+  return mm > 0 && M > mm && M <= 256 && K % WG_BK == 0 && N % 16 == 0 && K >= 4 * WG_BK;
+}
+
+CAIN_API long long cain_wgemm_ws_bytes(int N, int K, int M) {
+  if (!cain_wgemm_eligible(N, K, M)) return 0;
+  const WgPlan p = wg_plan(N, K, M);
+  return (long long)((p.part_floats + p.ss_floats) * sizeof(float));
+}
+
+// a: the GEMM (gemm_epi.h); ws: >= cain_wgemm_ws_bytes of scratch (no zeroing needed).
+int wgemm_dispatch(const GemmArgs& a, int epi, bool norm, void* ws, long long ws_bytes, hipStream_t st) {
+  if (!cain_wgemm_eligible(a.N, a.K, a.M)) return -1;
+  const WgPlan p = wg_plan(a.N, a.K, a.M);
+  if ((long long)((p.part_floats + p.ss_floats) * sizeof(float)) > ws_bytes) return -1;
+  WgArgs w{};
+  w.ks = p.ks;
+  w.kst = p.kst;
+  w.part = reinterpret_cast<float*>(ws);
+  w.part_ss = w.part + p.part_floats;
+  hipError_t e;
+  if (p.bm == 256) e = norm ? wg_launch_e<256, true>(epi, a, w, p, st) : wg_launch_e<256, false>(epi, a, w, p, st);
+  else e = norm ? wg_launch_e<128, true>(epi, a, w, p, st) : wg_launch_e<128, false>(epi, a, w, p, st);
+  return int(e);
+}

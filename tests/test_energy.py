@@ -36,9 +36,71 @@ def test_meter_window_cpu_model_without_gpu():
     r = m.stop(settle_ms=0)
     m.close()
     assert 0.19 < r.duration_s < 0.5
-    assert r.gpu_energy_j == 0.0 and r.cpu_energy_source in ("model", "rapl")
+    assert r.gpu_energy_j == 0.0 and r.cpu_energy_source.split("(")[0] in ("model", "rapl", "hwmon", "amdsmi-cpu")
     assert r.total_energy_j == pytest.approx(r.gpu_energy_j + r.cpu_energy_j + r.ram_energy_j)
     assert 0 < r.memory_usage < 100
+
+
+def test_cpu_energy_on_by_default_with_host_tdp(monkeypatch):
+    """No readable counter (this container): the CPU-load model with this host's TDP is ON by default, so the
+    client's CPU energy is never silently 0 (codecarbon's fallback)."""
+    monkeypatch.delenv("CAIN_CPU_TDP_W", raising=False)
+    m = EnergyMeter(smi_indices=[], period_ms=10)
+    assert m.cpu_tdp_w > 0 and "ram" in m.sources and "cpu" in m.sources
+    m.start()
+    x, t_end = 0, time.time() + 0.3
+    while time.time() < t_end:  # one busy core
+        x += 1
+    r = m.stop(settle_ms=0)
+    m.close()
+    if not m.host_source:
+        assert r.cpu_energy_source.startswith("model")
+    assert r.cpu_energy_j > 0 and r.ram_energy_j > 0
+    assert r.total_energy_j == pytest.approx(r.gpu_energy_j + r.cpu_energy_j + r.ram_energy_j)
+
+
+def test_host_share_scales_cpu_energy():
+    full = EnergyMeter(smi_indices=[], period_ms=10, cpu_tdp_w=400.0, sources=("cpu",))
+    half = EnergyMeter(smi_indices=[], period_ms=10, cpu_tdp_w=400.0, sources=("cpu",), host_share=0.5)
+    samples = [{"t_ns": 0, "cpu_energy_j": float("nan")}]
+    jf, _ = full._cpu_energy(samples, 2.0, 50.0)
+    jh, _ = half._cpu_energy(samples, 2.0, 50.0)
+    full.close(), half.close()
+    assert jf == pytest.approx(400.0) and jh == pytest.approx(200.0)
+
+
+def test_idle_subtraction_is_per_source():
+    """A CPU-only window (the remote arm's client) must not subtract the GPU's idle board power
+    (~300 W of GPU idle taken off CPU-only energy gave large negative idle_subtracted_J)."""
+    m = EnergyMeter(smi_indices=[], period_ms=10, cpu_tdp_w=100.0, sources=("cpu",))
+    m.idle_power_w = 300.0     # GPU idle board power of a GPU rank
+    m.idle_cpu_power_w = 1.0   # CPU idle share
+    m.start()
+    time.sleep(0.2)
+    r = m.stop(settle_ms=0)
+    m.close()
+    assert r.gpu_energy_j == 0.0
+    assert r.idle_subtracted_j == pytest.approx(r.cpu_energy_j - 1.0 * r.duration_s)
+    assert r.idle_subtracted_j > -1.0  # no GPU idle term
+
+
+def test_native_wrap_accumulation():
+    """RAPL energy_uj wraps at max_energy_range_uj: deltas accumulate modulo the range."""
+    rng = 262143328850  # a typical package zone max_energy_range_uj
+    raw = [rng - 3_000_000, rng - 1_000_000, 1_000_000, 4_000_000]
+    assert native.wrap_accumulate(raw, rng) == pytest.approx(7.0)
+    # unknown modulus: a backwards step is dropped, never turned into a huge positive delta
+    assert native.wrap_accumulate([5_000_000, 1_000_000, 2_000_000], 0) == pytest.approx(1.0)
+
+
+def test_meter_trims_the_counter_trace():
+    m = EnergyMeter(smi_indices=[], period_ms=10, sources=("cpu",))
+    calls = []
+    m.sampler.trim = lambda t: calls.append(t)
+    t0 = m.start()
+    m.stop(settle_ms=0)
+    m.close()
+    assert calls and calls[0] <= t0
 
 
 def test_column_values_units():

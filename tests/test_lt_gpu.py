@@ -80,9 +80,12 @@ def test_engine_lt_path_matches_oracle(name, monkeypatch):
     eng.close()
 
 
-def test_engine_lt_default_threshold(monkeypatch):
+def test_engine_lt_default_off(monkeypatch):
+    """The library path is opt-in: the hand-written wide-batch kernel (csrc/wgemm.hip) is the default."""
     monkeypatch.delenv("CAIN_LT_MIN_ROWS", raising=False)
     from cain_amd.engine.engine import lt_min_rows
+    assert lt_min_rows(256) == 0 and lt_min_rows(64) == 0
+    monkeypatch.setenv("CAIN_LT_MIN_ROWS", "128")
     assert lt_min_rows(256) == 128 and lt_min_rows(64) == 0 and lt_min_rows(256, "fp8") == 0
 
 
