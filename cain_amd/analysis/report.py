@@ -259,70 +259,82 @@ def per_model_markdown(rows) -> str:
 
 # ---------------------------------------------------------------------------------------------- plots
 def make_plots(df, subsets, out: Path) -> List[Path]:
-    """Density / violin / QQ / scatter PDFs (matplotlib; the notebook used ggplot2)."""
+    """The notebook's 75 PDFs in its directory tree (matplotlib; the notebook used ggplot2):
+
+    * ``density_plots/<metric>/density_plot_<length>.pdf`` + ``combined_density_plots_<metric>.pdf``
+      (analysis-visualization.ipynb:696, :720);
+    * ``violin_plots/<metric>/violin_plot_<length>.pdf`` + ``combined_violin_plots_<metric>.pdf`` (:710, :724)
+      + ``violin_plots/energy_usage_J/combined_violin_plots_llms_energy_usage_J.pdf`` (:919);
+    * ``qq_plots/<method>/<metric>/qq_plot_<length>.pdf`` (:964-1007);
+    * ``scatter_plots/<metric>_vs_energy_usage_J.pdf`` (:1484)."""
     import matplotlib
 
     matplotlib.use("Agg")
     import matplotlib.pyplot as plt
     from scipy import stats as st
 
-    written = []
-    for sub in ("density_plots", "violin_plots", "qq_plots", "scatter_plots"):
-        (out / sub).mkdir(parents=True, exist_ok=True)
+    written: List[Path] = []
     labels = list(LENGTH_MAP)
-    for k in METRICS:
-        fig, axes = plt.subplots(1, len(labels), figsize=(12, 3.5))
-        for ax, label in zip(axes, labels):
-            for m in METHODS:
-                d = subsets.get(f"{m}_{label}")
-                if d is None or len(d) < 2:
-                    continue
-                v = d[k].to_numpy(float)
-                if np.ptp(v) > 0:
-                    xs = np.linspace(v.min(), v.max(), 200)
-                    ax.fill_between(xs, st.gaussian_kde(v)(xs), alpha=0.5, color=COLOR_MAP[m], label=m)
-            ax.set_title(f"{_title(label)} ({LENGTH_MAP[label]})")
-            ax.set_xlabel(AXIS_LABELS[k])
-        axes[0].legend()
-        p = out / "density_plots" / f"combined_density_{k}.pdf"
+
+    def save(fig, p: Path) -> None:
+        p.parent.mkdir(parents=True, exist_ok=True)
         fig.tight_layout()
         fig.savefig(p)
         plt.close(fig)
         written.append(p)
 
-        fig, ax = plt.subplots(figsize=(8, 4))
-        data, ticks = [], []
-        for label in labels:
-            for m in METHODS:
-                d = subsets.get(f"{m}_{label}")
-                if d is not None and len(d):
-                    data.append(d[k].to_numpy(float))
-                    ticks.append(f"{label}\n{m}")
+    def density(ax, k, label):
+        for m in METHODS:
+            d = subsets.get(f"{m}_{label}")
+            if d is None or len(d) < 2:
+                continue
+            v = d[k].to_numpy(float)
+            if np.ptp(v) > 0:
+                xs = np.linspace(v.min(), v.max(), 200)
+                ax.fill_between(xs, st.gaussian_kde(v)(xs), alpha=0.5, color=COLOR_MAP[m], label=m)
+        ax.set_title(f"{_title(label)} ({LENGTH_MAP[label]})")
+        ax.set_xlabel(AXIS_LABELS[k])
+        ax.set_ylabel("Density")
+
+    def violin(ax, k, label):
+        data, ticks, cols = [], [], []
+        for m in METHODS:
+            d = subsets.get(f"{m}_{label}")
+            if d is not None and len(d):
+                data.append(d[k].to_numpy(float))
+                ticks.append(_title(m))
+                cols.append(COLOR_MAP[m])
         if data:
             parts = ax.violinplot(data, showmedians=True)
-            for i, b in enumerate(parts["bodies"]):
-                b.set_facecolor(COLOR_MAP[METHODS[i % 2]])
+            for b, c in zip(parts["bodies"], cols):
+                b.set_facecolor(c)
             ax.set_xticks(range(1, len(ticks) + 1), ticks)
+        ax.set_title(f"{_title(label)} ({LENGTH_MAP[label]})")
         ax.set_ylabel(AXIS_LABELS[k])
-        p = out / "violin_plots" / f"combined_violin_{k}.pdf"
-        fig.tight_layout()
-        fig.savefig(p)
-        plt.close(fig)
-        written.append(p)
 
+    for k in METRICS:
+        for kind, draw in (("density", density), ("violin", violin)):
+            d_dir = out / f"{kind}_plots" / k
+            for label in labels:
+                fig, ax = plt.subplots(figsize=(4, 3.5))
+                draw(ax, k, label)
+                if kind == "density":
+                    ax.legend()
+                save(fig, d_dir / f"{kind}_plot_{label}.pdf")
+            fig, axes = plt.subplots(1, len(labels), figsize=(4 * len(labels), 3.5))
+            for ax, label in zip(axes, labels):
+                draw(ax, k, label)
+            if kind == "density":
+                axes[0].legend()
+            save(fig, d_dir / f"combined_{kind}_plots_{k}.pdf")
         for m in METHODS:
             for label in labels:
                 d = subsets.get(f"{m}_{label}")
-                if d is None or len(d) < 3:
-                    continue
                 fig, ax = plt.subplots(figsize=(4, 4))
-                st.probplot(d[k].to_numpy(float), plot=ax)
-                ax.set_title(f"{m} {label}: {AXIS_LABELS[k]}")
-                p = out / "qq_plots" / f"qq_{m}_{label}_{k}.pdf"
-                fig.tight_layout()
-                fig.savefig(p)
-                plt.close(fig)
-                written.append(p)
+                if d is not None and len(d) >= 3:
+                    st.probplot(d[k].to_numpy(float), plot=ax)
+                ax.set_title(f"{_title(m)} {_title(label)}: {AXIS_LABELS[k]}")
+                save(fig, out / "qq_plots" / m / k / f"qq_plot_{label}.pdf")
 
     for k in (TIME, CPU, GPU, MEMORY):
         fig, axes = plt.subplots(2, 3, figsize=(12, 8))
@@ -340,30 +352,22 @@ def make_plots(df, subsets, out: Path) -> List[Path]:
                 ax.set_title(f"{_title(m)} - {_title(label)} ({LENGTH_MAP[label]})")
                 ax.set_xlabel(AXIS_LABELS[ENERGY] if m == REMOTE else "")
                 ax.set_ylabel(AXIS_LABELS[k] if label == "short" else "")
-        p = out / "scatter_plots" / f"{k}_vs_{ENERGY}.pdf"
-        fig.tight_layout()
-        fig.savefig(p)
-        plt.close(fig)
-        written.append(p)
+        save(fig, out / "scatter_plots" / f"{k}_vs_{ENERGY}.pdf")
 
+    fig, ax = plt.subplots(figsize=(12, 4))
+    data, ticks = [], []
     if "model" in df.columns:
-        fig, ax = plt.subplots(figsize=(12, 4))
-        data, ticks = [], []
         for nice, name in LLM_NAMES.items():
             for m in METHODS:
                 v = df[(df["model"] == name) & (df["method"] == m)][ENERGY].dropna().to_numpy(float)
                 if v.size:
                     data.append(v)
                     ticks.append(f"{nice}\n{m}")
-        if data:
-            ax.violinplot(data, showmedians=True)
-            ax.set_xticks(range(1, len(ticks) + 1), ticks, fontsize=6)
-            ax.set_ylabel(AXIS_LABELS[ENERGY])
-            p = out / "violin_plots" / f"combined_violin_plots_llms_{ENERGY}.pdf"
-            fig.tight_layout()
-            fig.savefig(p)
-            written.append(p)
-        plt.close(fig)
+    if data:
+        ax.violinplot(data, showmedians=True)
+        ax.set_xticks(range(1, len(ticks) + 1), ticks, fontsize=6)
+    ax.set_ylabel(AXIS_LABELS[ENERGY])
+    save(fig, out / "violin_plots" / ENERGY / f"combined_violin_plots_llms_{ENERGY}.pdf")
     return written
 
 

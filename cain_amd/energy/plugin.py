@@ -53,6 +53,8 @@ class DataColumns(Enum):
     ENERGY_USAGE_J = "energy_usage_J"
     GPU_ENERGY_J = "gpu_energy_J"
     CPU_ENERGY_J = "cpu_energy_J"
+    RAM_ENERGY_J = "ram_energy_J"
+    CPU_ENERGY_SOURCE = "cpu_energy_source"
     IDLE_SUBTRACTED_J = "idle_subtracted_J"
     AVG_GPU_POWER_W = "avg_gpu_power_W"
     WINDOW_S = "energy_window_s"
@@ -84,6 +86,8 @@ def column_values(reading: EnergyReading, cols: Iterable[DataColumns], country: 
         DataColumns.ENERGY_USAGE_J: round(reading.total_energy_j, 3),
         DataColumns.GPU_ENERGY_J: round(reading.gpu_energy_j, 3),
         DataColumns.CPU_ENERGY_J: round(reading.cpu_energy_j, 3),
+        DataColumns.RAM_ENERGY_J: round(reading.ram_energy_j, 3),
+        DataColumns.CPU_ENERGY_SOURCE: reading.cpu_energy_source,
         DataColumns.IDLE_SUBTRACTED_J: (round(reading.idle_subtracted_j, 3)
                                         if not math.isnan(reading.idle_subtracted_j) else ""),
         DataColumns.AVG_GPU_POWER_W: (round(reading.gpu_power_w, 3) if not math.isnan(reading.gpu_power_w) else ""),

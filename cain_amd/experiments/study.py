@@ -15,9 +15,10 @@ MI355X-native differences:
 
 * the on-device arm is this framework's own decode engine behind an Ollama-compatible server started per
   data-parallel rank on that rank's GPU (``python -m cain_amd serve``, port ``port_base + 1 + rank``);
-* energy is the amd-smi hardware accumulator of the measured GPU plus host CPU (RAPL or a TDP model), on a
-  native sampler thread (``cain_amd.energy``); the remote arm measures the client only (the rank's GPU
-  when the server lives on another device, otherwise host CPU only);
+* energy is the amd-smi hardware accumulator of the measured GPU plus host CPU (HSMP / RAPL counters or the
+  CPU-load TDP model, this rank's share of the host) and the client's RAM, on a native sampler thread
+  (``cain_amd.energy``); the remote arm measures the client only (the rank's GPU when the server lives on
+  another device, otherwise host CPU + RAM only);
 * the response JSON is captured (the reference's curl printed it and dropped it), so the run table gains
   ``tokens_generated``, ``J_per_token``, ``tok_per_s``, ``ttft_s`` ... after the reference's columns;
 * topics are drawn with a per-run seeded RNG (reproducible), prompts/lengths are the reference's.
@@ -60,8 +61,8 @@ REFERENCE_COLUMNS = ["topic", "execution_time", "cpu_usage", "gpu_usage", "memor
 EXTRA_COLUMNS = ["tokens_generated", "prompt_tokens", "J_per_token", "tok_per_s", "ttft_s", "gen_time_s",
                  "server_total_s", "server_eval_s", "client_wall_s", "device", "server"]
 ENERGY_COLUMNS = [DataColumns.ENERGY_CONSUMED, DataColumns.ENERGY_USAGE_J, DataColumns.GPU_ENERGY_J,
-                  DataColumns.CPU_ENERGY_J, DataColumns.IDLE_SUBTRACTED_J, DataColumns.AVG_GPU_POWER_W,
-                  DataColumns.WINDOW_S]
+                  DataColumns.CPU_ENERGY_J, DataColumns.RAM_ENERGY_J, DataColumns.IDLE_SUBTRACTED_J,
+                  DataColumns.AVG_GPU_POWER_W, DataColumns.WINDOW_S, DataColumns.CPU_ENERGY_SOURCE]
 
 
 @dataclass
@@ -413,9 +414,11 @@ class _StudyBase:
             self._lock_fh = None
 
     def energy_sources_for(self, context: RunnerContext):
+        """The client's energy, as codecarbon counted it: CPU + RAM, plus the client GPU -- except for the remote
+        arm when its server shares that GPU (then the board's energy is the server's, not the client's)."""
         if context.run_variation.get("method") == "remote" and self.remote_shares_gpu:
-            return ("cpu",)
-        return ("gpu", "cpu")
+            return ("cpu", "ram")
+        return ("gpu", "cpu", "ram")
 
     def start_measurement(self, context: RunnerContext) -> None:
         # the energy window (opened by the plugin just before this body) covers the request; with

@@ -122,4 +122,10 @@ def test_cli_analyze(tmp_path):
     assert r.returncode == 0, r.stderr[-2000:]
     assert "28370" in r.stdout
     assert (tmp_path / "scatter_plots" / "cpu_usage_vs_energy_usage_J.pdf").exists()
-    assert (tmp_path / "violin_plots" / "combined_violin_plots_llms_energy_usage_J.pdf").exists()
+    # the reference's 75 PDFs, same tree and file names (data-analysis/{violin,density,qq,scatter}_plots)
+    ref = Path("/root/reference/data-analysis")
+    ours = sorted(str(p.relative_to(tmp_path)) for p in tmp_path.rglob("*.pdf"))
+    assert len(ours) == 75
+    if ref.exists():
+        theirs = sorted(str(p.relative_to(ref)) for p in ref.rglob("*.pdf"))
+        assert ours == theirs

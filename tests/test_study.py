@@ -72,3 +72,32 @@ def test_study_on_device_arm_on_gpu_measures_energy(tmp_path):
         assert int(x["tokens_generated"]) == 134
         assert float(x["gpu_energy_J"]) > 0 and float(x["avg_gpu_power_W"]) > 50
         assert float(x["J_per_token"]) > 0 and x["idle_subtracted_J"] != ""
+
+
+@pytest.mark.gpu
+def test_study_both_arms_against_real_engine_servers(tmp_path):
+    """Both arms through curl against this framework's own engine: the on-device server and a remote server
+    (``CAIN_STUDY_REMOTE=local:0``: a separate engine process on the box's GPU).  The remote rows decode at the
+    engine's rate (not the 70 tok/s modelled server) and are charged client-side energy only: the GPU board
+    belongs to the server, so gpu_energy_J is 0 and the CPU + RAM energy is what remains."""
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    r = subprocess.run([sys.executable, "-m", "cain_amd", str(ROOT / "experiments" / "study.py")],
+                       capture_output=True, text=True, timeout=900, cwd=ROOT,
+                       env=_env(tmp_path, CAIN_STUDY_MODELS="qwen2:1.5b", CAIN_STUDY_LENGTHS="100",
+                                CAIN_STUDY_REPETITIONS="2", CAIN_STUDY_METHODS="on_device,remote",
+                                CAIN_STUDY_REMOTE="local:0", CAIN_STUDY_CLIENT="curl"))
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    rows = list(csv.DictReader(open(tmp_path / "full_factorial" / "run_table.csv")))
+    assert len(rows) == 4 and all(x["__done"] == "DONE" for x in rows)
+    for x in rows:
+        assert int(x["tokens_generated"]) == 134
+        assert float(x["cpu_energy_J"]) > 0
+    remote = [x for x in rows if x["method"] == "remote"]
+    local = [x for x in rows if x["method"] == "on_device"]
+    assert all(float(x["tok_per_s"]) > 150 for x in remote), [x["tok_per_s"] for x in remote]
+    assert all(float(x["gpu_energy_J"]) == 0.0 for x in remote)
+    assert all(float(x["gpu_energy_J"]) > 0 for x in local)
+    assert all(x["server"] != local[0]["server"] for x in remote)
