@@ -14,14 +14,19 @@ they are sharded over N worker processes, one per GPU:
 * BEFORE_EXPERIMENT runs on every rank (per-GPU setup such as starting that
   rank's local server); AFTER_EXPERIMENT — the reference's run-table
   post-processing — on the writer only, then ``config.teardown_rank()`` if defined;
-* work proceeds in waves: each rank runs one row (hooks see
+* work is a dynamic queue, not lock-step waves: a rank takes the next TODO row
+  with one atomic ``add`` on the process group's key-value store (the c10d
+  TCPStore the rendezvous already created), runs it (hooks see
   ``context.rank`` / ``context.device``; the energy plugin measures that
-  rank's GPU), then ``gather_object`` brings the finished rows to rank 0, which
-  commits them in ONE atomic rewrite (single writer), and the
-  cooldown overlaps across GPUs;
-* the collectives are a few hundred bytes (RCCL over xGMI when the process
-  group is ``nccl``; ``gloo`` on CPU), i.e. latency-bound: there is nothing to
-  tune for bandwidth here.
+  rank's GPU), publishes the finished row under its queue index and takes the
+  next -- a slow run (a 1,000-word on-device trial of a 7B model next to a
+  100-word one) no longer holds every other GPU at a wave boundary.  Rank 0
+  also runs rows; between its own runs it commits every published row to
+  ``run_table.csv`` in one atomic rewrite (single writer).  The
+  cooldown is per rank, so it overlaps across GPUs;
+* the control messages are a few hundred bytes (the store, plus RCCL over xGMI
+  for the broadcast / barrier when the process group is ``nccl``; ``gloo`` on
+  CPU), i.e. latency-bound: there is nothing to tune for bandwidth here.
 
 Failure handling: an exception in a run leaves that row TODO (reference
 semantics) and is logged to ``errors.jsonl``; ``retry_failed`` re-runs such rows
@@ -113,33 +118,10 @@ def run_rank(config_path: str, rank: int, world: int, isolation: Optional[str] =
         output.console_log_OK(f"{len(todo_ids)} TODO runs over {world} ranks")
         EventSubscriptionController.raise_event(RunnerEvents.BEFORE_EXPERIMENT)
         passes = 1 + max(0, int(retry_failed))
+        store = dist.distributed_c10d._get_default_store()
         for p in range(passes):
-            n_waves = (len(todo_ids) + world - 1) // world
-            failed: List[str] = []
-            for w in range(n_waves):
-                idx = w * world + rank
-                row: Optional[Dict[str, Any]] = None
-                if idx < len(todo_ids):
-                    rid = todo_ids[idx]
-                    row = ctrl.run_variation(by_id[rid], commit=lambda r: None)
-                    if row is None:
-                        failed.append(rid)
-                rows: List[Optional[Dict[str, Any]]] = [None] * world if writer else None
-                dist.gather_object(row, rows, dst=0)
-                if writer:
-                    done = [dict(r) for r in rows if r is not None]
-                    for r in done:
-                        r["__done"] = RunProgress.DONE
-                    if done:
-                        CSVOutputManager(ctrl.path).update_rows(done)
-                        output.console_log_WARNING(f"CSVManager: committed {len(done)} rows (wave {w + 1}/{n_waves})")
-                if w + 1 < n_waves:
-                    ctrl.cooldown()
-                if config.operation_type is OperationType.SEMI:
-                    EventSubscriptionController.raise_event(RunnerEvents.CONTINUE)
-            all_failed: List[List[str]] = [None] * world if writer else None
-            dist.gather_object(failed, all_failed, dst=0)
-            retry = [[rid for lst in all_failed for rid in lst] if writer else None]
+            failed = _work_queue(store, f"cain/{p}/", todo_ids, by_id, ctrl, config, writer, world)
+            retry = [failed if writer else None]
             dist.broadcast_object_list(retry, src=0)
             todo_ids = retry[0]
             if not todo_ids or p + 1 >= passes:
@@ -163,6 +145,64 @@ def run_rank(config_path: str, rank: int, world: int, isolation: Optional[str] =
             dist.destroy_process_group()
         except Exception:
             pass
+
+
+def _work_queue(store, prefix: str, todo_ids: List[str], by_id: Dict[str, Dict[str, Any]], ctrl, config,
+                writer: bool, world: int, poll_s: float = 0.2) -> List[str]:
+    """One pass over ``todo_ids`` as a shared queue.  Every rank claims indices with ``store.add`` and publishes
+    each finished row (pickled; None = the run failed) under ``<prefix>res/<index>``; the writer commits what is
+    published between its own runs and, after its last one, until every index is in.  Returns, on the writer,
+    the run ids that failed in this pass."""
+    import pickle
+    import time
+
+    from ..runner.events import EventSubscriptionController, RunnerEvents
+    from ..runner.models import OperationType, RunProgress
+    from ..runner.output import OutputProcedure as output
+    from ..runner.store import CSVOutputManager
+
+    n = len(todo_ids)
+    pending = set(range(n))  # writer: indices not committed yet
+    failed: List[str] = []
+
+    def commit_published() -> None:
+        keys = [i for i in sorted(pending) if store.check([f"{prefix}res/{i}"])]
+        done = []
+        for i in keys:
+            row = pickle.loads(store.get(f"{prefix}res/{i}"))
+            pending.discard(i)
+            if row is None:
+                failed.append(todo_ids[i])
+            else:
+                row = dict(row)
+                row["__done"] = RunProgress.DONE
+                done.append(row)
+        if done:
+            CSVOutputManager(ctrl.path).update_rows(done)
+            output.console_log_WARNING(f"CSVManager: committed {len(done)} rows ({n - len(pending)}/{n})")
+
+    ran = 0
+    while True:
+        i = int(store.add(f"{prefix}next", 1)) - 1
+        if i >= n:
+            break
+        if ran:
+            ctrl.cooldown()  # per rank: overlaps with the other ranks' runs
+        rid = todo_ids[i]
+        row = ctrl.run_variation(by_id[rid], commit=lambda r: None)
+        store.set(f"{prefix}res/{i}", pickle.dumps(row))
+        ran += 1
+        if writer:
+            commit_published()
+        if config.operation_type is OperationType.SEMI:
+            EventSubscriptionController.raise_event(RunnerEvents.CONTINUE)
+    if writer:
+        while pending:
+            commit_published()
+            if pending:
+                time.sleep(poll_s)
+    output.console_log(f"rank ran {ran} of {n} runs in this pass ({world} ranks)")
+    return failed
 
 
 def _spawn_entry(rank, world, port, config_path, isolation, timeout, assume_yes, retry_failed):

@@ -104,3 +104,38 @@ def test_dead_rank_is_detected_and_job_restarts(tmp_path):
     assert "died" in r.stdout and "elastic restart 1/1" in r.stdout
     rows = list(csv.DictReader(open(tmp_path / "dp" / "run_table.csv")))
     assert len(rows) == 12 and all(x["__done"] == "DONE" for x in rows)
+
+
+QUEUE_CFG = CFG.replace('repetitions=2, data_columns=["rank", "pid"], shuffle=True, seed=7)',
+                        'repetitions=4, data_columns=["rank", "pid"], shuffle=True, seed=7)')
+assert QUEUE_CFG != CFG
+
+
+def test_fanout_eight_ranks_work_queue_then_resume_on_three(tmp_path):
+    """8 gloo ranks pull rows from the shared queue (24 runs); the injected failure stays TODO; a resume on 3
+    ranks runs exactly that row (1/2/4/8 ranks, resume across world sizes)."""
+    cfg = tmp_path / "cfg.py"
+    cfg.write_text(QUEUE_CFG)
+    r = _run(cfg, 8, tmp_path)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    rows = list(csv.DictReader(open(tmp_path / "dp" / "run_table.csv")))
+    assert len(rows) == 24
+    done = [x for x in rows if x["__done"] == "DONE"]
+    assert len(done) == 23 and len({x["rank"] for x in done}) >= 4  # the queue spread the work
+    assert (tmp_path / "after_ran").read_text() == "0"
+    r = _run(cfg, 3, tmp_path)
+    assert r.returncode == 0, r.stdout[-3000:]
+    rows2 = list(csv.DictReader(open(tmp_path / "dp" / "run_table.csv")))
+    assert all(x["__done"] == "DONE" for x in rows2)
+    assert [x["__run_id"] for x in rows2] == [x["__run_id"] for x in rows]
+    assert r.stdout.count("NEW RUN") == 1
+
+
+def test_fanout_four_ranks(tmp_path):
+    cfg = tmp_path / "cfg.py"
+    cfg.write_text(CFG)
+    r = _run(cfg, 4, tmp_path)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    rows = list(csv.DictReader(open(tmp_path / "dp" / "run_table.csv")))
+    assert sum(x["__done"] == "DONE" for x in rows) == 11
+    assert "12 TODO runs over 4 ranks" in r.stdout
