@@ -199,6 +199,8 @@ def cliff_delta(x, y, conf_level: float = 0.95, use_normal: bool = False) -> Cli
     s = math.sqrt(s2)
     root = math.sqrt((1 - d * d) ** 2 + z * z * s2)
     den = 1 - d * d + z * z * s2
+    if den <= 0.0:  # complete separation (|δ| = 1, s² = 0): the interval degenerates to the point estimate
+        return CliffResult(d, d, d, s2, cliff_magnitude(d))
     lo = (d - d ** 3 - z * s * root) / den
     hi = (d - d ** 3 + z * s * root) / den
     return CliffResult(d, float(max(-1.0, lo)), float(min(1.0, hi)), s2, cliff_magnitude(d))

@@ -129,3 +129,10 @@ def test_cli_analyze(tmp_path):
     if ref.exists():
         theirs = sorted(str(p.relative_to(ref)) for p in ref.rglob("*.pdf"))
         assert ours == theirs
+
+
+def test_cliff_delta_complete_separation_has_a_point_interval():
+    """Every on-device run above every remote run (the MI355X study): δ = 1 with a degenerate [1, 1] interval,
+    not the [-1, 1] a 0/0 made of it."""
+    r = S.cliff_delta([10.0, 11.0, 12.0, 13.0], [1.0, 2.0, 3.0])
+    assert r.estimate == 1.0 and r.lower == 1.0 and r.upper == 1.0 and r.magnitude == "Large"
