@@ -47,3 +47,25 @@ __device__ __forceinline__ size_t vfrag_off(int t, int d, int hd) {
   return ((size_t)(t >> 5) * (hd >> 4) + (d >> 4)) * 512 + (size_t)((d & 15) + 16 * ((t & 15) >> 2)) * 8 +
          4 * ((t >> 4) & 1) + (t & 3);
 }
+
+// Split-K partial slabs: 16-byte write-through (sc1) buffer stores, read back by the last arriver with
+// 16-byte sc1 buffer loads (L2-served, never a stale L1 line): the hand-off needs no release/acquire fence
+// (cdna_hip_programming.md Guideline 16 R1; MI355X_MICROARCH.md 'Valid forms', first row).  Dword atomics did
+// the same job with four instructions per 16 B.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t slab_rsrc(const float* p) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), 0, 0x7fffffff, 0x00020000);
+}
+__device__ __forceinline__ void st_wt(__amdgpu_buffer_rsrc_t r, int byte_off, const f32x4& v) {
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, byte_off, 0, 16 /* sc1 */);
+}
+__device__ __forceinline__ f32x4 ld_wt(__amdgpu_buffer_rsrc_t r, int byte_off) {
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 16 /* sc1 */));
+}
+
+__device__ __forceinline__ void st_wt_f32(__amdgpu_buffer_rsrc_t r, int byte_off, float v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, byte_off, 0, 16 /* sc1 */);
+}
+__device__ __forceinline__ float ld_wt_f32(__amdgpu_buffer_rsrc_t r, int byte_off) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, byte_off, 0, 16 /* sc1 */));
+}

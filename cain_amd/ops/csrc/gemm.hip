@@ -354,21 +354,7 @@ struct BgArgs {
   unsigned* counters;  // [nblk], zero between launches (the reducer resets its own)
 };
 
-// Split-K partial slabs: 16-byte write-through (sc1) buffer stores, read back by the last arriver with
-// 16-byte sc1 buffer loads (L2-served, never a stale L1 line): the hand-off needs no release/acquire fence
-// (cdna_hip_programming.md Guideline 16 R1; MI355X_MICROARCH.md 'Valid forms', first row).  Dword atomics did
-// the same job with four instructions per 16 B.
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t slab_rsrc(const float* p) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), 0, 0x7fffffff, 0x00020000);
-}
-__device__ __forceinline__ void st_wt(__amdgpu_buffer_rsrc_t r, int byte_off, const f32x4& v) {
-  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, byte_off, 0, 16 /* sc1 */);
-}
-__device__ __forceinline__ f32x4 ld_wt(__amdgpu_buffer_rsrc_t r, int byte_off) {
-  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 16 /* sc1 */));
-}
+// Split-K partial slabs: the write-through (sc1) helpers of common.h (slab_rsrc, st_wt, ld_wt).
 
 // LB: minimum waves per SIMD the register allocation must allow (4 -> 128 VGPRs, 2 -> 256, 1 -> 512)
 // AR: activation register ring (see the AR branch of the chunk loop)
@@ -843,10 +829,14 @@ static BgPlan bgemm_plan(int N, int K, int M, int ntw_req) {
   return p;
 }
 
-constexpr size_t BG_COUNTER_BYTES = 64 * 1024;  // counters live at the start of the workspace
+// GEMM workspace layout: [batched-path tickets, 64 KiB][wide-path counters, 16 KiB][split-K slabs ...].  Both
+// counter regions must read zero at rest (each path resets its own); the slab area is shared scratch.
+constexpr size_t BG_COUNTER_BYTES = 64 * 1024;
+constexpr size_t WG_COUNTER_BYTES = 16 * 1024;
+constexpr size_t GEMM_SLAB_OFFSET = BG_COUNTER_BYTES + WG_COUNTER_BYTES;
 
 static size_t bgemm_ws_bytes(const BgPlan& p) {
-  return BG_COUNTER_BYTES + (p.part_floats + p.ss_floats) * sizeof(float);
+  return GEMM_SLAB_OFFSET + (p.part_floats + p.ss_floats) * sizeof(float);
 }
 
 template <int NB, int NTW, int W, int CK, int EPI, bool NORM, int DD, int WM>
@@ -918,7 +908,7 @@ static int bgemm_dispatch(const GemmArgs& a, int epi, bool norm, const BgPlan& p
   b.ksplit = p.ksplit;
   b.kspl = p.kspl;
   b.counters = reinterpret_cast<unsigned*>(ws);
-  b.part = reinterpret_cast<float*>(reinterpret_cast<char*>(ws) + BG_COUNTER_BYTES);
+  b.part = reinterpret_cast<float*>(reinterpret_cast<char*>(ws) + GEMM_SLAB_OFFSET);
   b.part_ss = b.part + p.part_floats;
   hipError_t e;
   if (p.nb == 2) e = norm ? bg_launch_shape<2, true>(epi, p, a, b, st) : bg_launch_shape<2, false>(epi, p, a, b, st);

@@ -101,8 +101,10 @@ struct WgArgs {
   int ks;           // k-splits (workgroups per column block)
   int kst;          // ring stages (64-deep k-steps) per split
   float* part;      // [ks][n_units][64 lanes] f32x4 (ks > 1)
-  float* part_ss;   // [ks][BM] per-row partial sums of squares (ks > 1 && NORM)
+  float* part_ss;   // [nblk][ks][BM] per-row partial sums of squares (ks > 1 && NORM)
 };
+
+constexpr int WG_CTR_BYTES = 16 * 1024;  // the workspace region before the slabs (gemm.hip WG_COUNTER_BYTES)
 
 // DX / DW: prefetch distance (stages in flight) of the X and the W ring; the rings have DX + 1 and DW + 1 slots.
 // W streams from HBM (latency ~2-3 us under load) and gets the deeper ring; X comes from L2.
@@ -311,25 +313,28 @@ __global__ __launch_bounds__(64 * (8 + NDMA), (8 + NDMA) / 4) void wgemm_kernel(
     }
     __syncthreads();
   }
-  if (!compute) return;
 
   if (w.ks > 1) {
-    // fp32 slab of this split: unit (gt, rb) = 16 x 16 outputs, lane-major f32x4 (the reducer's layout)
-    const int n_units = nblk * WG_NT * G::RB;
+    // fp32 slab of this split (unit (gt, rb) = 16 x 16 outputs, lane-major f32x4: the reducer's layout) and this
+    // split's per-row sums of squares; wgemm_reduce_kernel, the next launch on the stream, combines them.
+    // (Measured: a combine inside this launch -- write-through slabs, arrival tickets, row groups claimed by the
+    // block's workgroups -- took 2-8 us longer per GEMM than the separate launch on QKV / O / down at 256 rows.)
+    if (compute) {
+      const int n_units = nblk * WG_NT * G::RB;
 #pragma unroll
-    for (int tn = 0; tn < G::TN; ++tn)
+      for (int tn = 0; tn < G::TN; ++tn)
 #pragma unroll
-      for (int mb = 0; mb < G::MB; ++mb) {
-        const int unit = (tile0 + wn * G::TN + tn) * G::RB + wm * G::MB + mb;
-        *reinterpret_cast<f32x4*>(w.part + (((size_t)kc * n_units + unit) * 64 + lane) * 4) = acc[tn][mb];
-      }
+        for (int mb = 0; mb < G::MB; ++mb) {
+          const int unit = (tile0 + wn * G::TN + tn) * G::RB + wm * G::MB + mb;
+          *reinterpret_cast<f32x4*>(w.part + (((size_t)kc * n_units + unit) * 64 + lane) * 4) = acc[tn][mb];
+        }
+    }
     if constexpr (NORM) {
-      if (blk == 0)
-        for (int r = threadIdx.x; r < BM; r += 512) w.part_ss[(size_t)kc * BM + r] = s_ss[r] + s_ss[BM + r];
+      for (int r = threadIdx.x; r < BM; r += NTHR) w.part_ss[((size_t)blk * w.ks + kc) * BM + r] = s_ss[r] + s_ss[BM + r];
     }
     return;
   }
-  (void)NTHR;
+  if (!compute) return;
 
   // ---- fused epilogue (ks = 1)
 #pragma unroll
@@ -366,8 +371,9 @@ __global__ __launch_bounds__(256) void wgemm_reduce_kernel(const GemmArgs a, con
   f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
   for (int k = 0; k < w.ks; ++k) v += *reinterpret_cast<const f32x4*>(w.part + (((size_t)k * n_units + unit) * 64 + lane) * 4);
   if constexpr (NORM) {
+    const int blk = gt / WG_NT;
     float ss = 0.f;
-    for (int k = 0; k < w.ks; ++k) ss += w.part_ss[(size_t)k * BM + m];
+    for (int k = 0; k < w.ks; ++k) ss += w.part_ss[((size_t)blk * w.ks + k) * BM + m];
     v *= rsqrtf(ss / float(a.K) + a.eps);
   }
   f32x4 pv;
@@ -408,7 +414,7 @@ WgPlan wg_plan(int N, int K, int M) {
   p.ks = (stages + p.kst - 1) / p.kst;
   if (p.ks > 1) {
     p.part_floats = (size_t)p.ks * p.nblk * WG_NT * (p.bm / 16) * 256;
-    p.ss_floats = (size_t)p.ks * p.bm;
+    p.ss_floats = (size_t)p.nblk * p.ks * p.bm;
   }
   return p;
 }
@@ -492,18 +498,20 @@ CAIN_API int cain_wgemm_eligible(int N, int K, int M) {
 CAIN_API long long cain_wgemm_ws_bytes(int N, int K, int M) {
   if (!cain_wgemm_eligible(N, K, M)) return 0;
   const WgPlan p = wg_plan(N, K, M);
-  return (long long)((p.part_floats + p.ss_floats) * sizeof(float));
+  return (long long)(WG_CTR_BYTES + (p.part_floats + p.ss_floats) * sizeof(float));
 }
+
 
 // a: the GEMM (gemm_epi.h); ws: >= cain_wgemm_ws_bytes of scratch (no zeroing needed).
 int wgemm_dispatch(const GemmArgs& a, int epi, bool norm, void* ws, long long ws_bytes, hipStream_t st) {
   if (!cain_wgemm_eligible(a.N, a.K, a.M)) return -1;
   const WgPlan p = wg_plan(a.N, a.K, a.M);
-  if ((long long)((p.part_floats + p.ss_floats) * sizeof(float)) > ws_bytes) return -1;
+  if ((long long)(WG_CTR_BYTES + (p.part_floats + p.ss_floats) * sizeof(float)) > ws_bytes) return -1;
   WgArgs w{};
   w.ks = p.ks;
   w.kst = p.kst;
-  w.part = reinterpret_cast<float*>(ws);
+  // [reserved counter region][slabs][sums]
+  w.part = reinterpret_cast<float*>(static_cast<char*>(ws) + WG_CTR_BYTES);
   w.part_ss = w.part + p.part_floats;
   hipError_t e;
   if (p.bm == 256) e = norm ? wg_launch_e<256, true>(epi, a, w, p, st) : wg_launch_e<256, false>(epi, a, w, p, st);

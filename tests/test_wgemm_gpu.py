@@ -88,3 +88,29 @@ def test_wide_matches_previous_batched_kernel():
     ops.set_wide_gemm_min_m(0)
     y_old = ops.skinny_gemm(wp, x, N, ops.EPI_F32, norm=True)
     assert rel_err(y_new, y_old) < 1e-3
+
+
+@pytest.mark.parametrize("N,K,norm,epi", [(4096, 4096, False, "resid"), (6144, 4096, True, "f32"),
+                                          (4096, 14336, False, "f32"), (1920, 8960, True, "f32")])
+def test_wide_splitk_repeatable_after_batched_path(N, K, norm, epi):
+    """Split-K plans (narrow N) right after a batched-path (M <= 64) GEMM on the same workspace: the two paths'
+    counter regions must not overlap (their slabs do), and repeated launches give identical results."""
+    torch.manual_seed(N + K)
+    M = 256
+    W = (torch.randn(N, K, device=DEV) * 0.02).bfloat16()
+    x = (2 * torch.randn(M, K, device=DEV)).bfloat16()
+    wp = pack_mfma_a(W)
+    ops.skinny_gemm(wp, x[:48], N, ops.EPI_F32, norm=norm)  # the batched path's split-K slabs + tickets
+    ref = _normed(x, norm) @ W.float().t()
+    if epi == "resid":
+        r0 = torch.randn(M, N, device=DEV).bfloat16()
+        outs = []
+        for _ in range(3):
+            r = r0.clone()
+            ops.skinny_gemm(wp, x, N, ops.EPI_RESID, out=r, norm=norm)
+            outs.append(r)
+        assert rel_err(outs[0], ref + r0.float()) < 1e-2
+    else:
+        outs = [ops.skinny_gemm(wp, x, N, ops.EPI_F32, norm=norm, eps=1e-6) for _ in range(3)]
+        assert rel_err(outs[0], ref) < 2e-3
+    assert all(torch.equal(o, outs[0]) for o in outs)

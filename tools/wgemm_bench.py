@@ -49,6 +49,7 @@ def main() -> int:
     lib.cain_wgemm_set_min_m.argtypes = [ops.ci]
     lib.cain_wgemm_set_variant.argtypes = [ops.ci]
     lib.cain_wgemm_set_split.argtypes = [ops.ci, ops.ci]
+
     variants = [int(v) for v in ns.variants.split(",")]
     splits = [tuple(int(y) for y in x.split(":")) for x in ns.splits.split(",") if x] or [(256, 8)]
     rows = [int(r) for r in ns.rows.split(",")]
