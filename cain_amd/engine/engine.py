@@ -492,13 +492,14 @@ class DecodeEngine:
             self.stream.synchronize()
         return out
 
-    def _prefill(self, ids) -> None:
+    def _prefill(self, ids, slots: Optional[Sequence[int]] = None) -> None:
+        """All prompt tokens but the last through the forward, into KV-cache slot ``slots[b]`` (default b)."""
         flat_tok, flat_pos, flat_slot = [], [], []
         for b, p in enumerate(ids):
             for j, t in enumerate(p[:-1]):
                 flat_tok.append(t)
                 flat_pos.append(j)
-                flat_slot.append(b)
+                flat_slot.append(b if slots is None else int(slots[b]))
         pr = self.prefill_rows
         for c in range(0, len(flat_tok), self.prefill_chunk):
             n = min(self.prefill_chunk, len(flat_tok) - c)
@@ -506,6 +507,14 @@ class DecodeEngine:
             pr["pos"][:n].copy_(torch.tensor(flat_pos[c:c + n], dtype=torch.int32))
             pr["slot"][:n].copy_(torch.tensor(flat_slot[c:c + n], dtype=torch.int32))
             self._forward(n, pr, want_logits=False, want_sample=False)
+
+    # ------------------------------------------------------------ continuous batching
+    def continuous(self) -> "ContinuousBatch":
+        """A persistent decode batch that requests join and leave between graph chunks (the server's
+        continuous batching, serve/server.py); HIP backend only."""
+        if self.backend != "hip":
+            raise RuntimeError("continuous batching needs the hip backend")
+        return ContinuousBatch(self)
 
     def _generate_torch(self, ids, nps, row_opts):
         """Oracle backend with a KV cache (one token of compute per step), sampled on the host."""
@@ -547,3 +556,145 @@ def sample_host(logits: torch.Tensor, history: List[int], o: Dict, rng) -> int:
         p = p[:cut] / p[:cut].sum()
         idx = idx[:cut]
     return int(idx[int(rng.choice(len(p), p=p.numpy()))])
+
+
+class ContinuousBatch:
+    """Rows ``[0, n)`` of the engine's decode state are the live requests; each owns a KV-cache slot for its
+    lifetime (``slot`` column), so rows can be compacted when requests leave while their caches stay put.
+
+    * ``admit(prompts, num_predict, options)`` prefills new requests into free slots and appends them as rows
+      ``n .. n+k-1`` (between graph chunks only);
+    * ``step(steps)`` runs ``steps`` decode steps over the ``n`` live rows (hipGraphs per row count, cached);
+    * ``poll()`` returns, per live row, the tokens generated since the previous poll and whether it finished;
+    * ``retire(rows)`` drops finished rows, moving the last live rows into the holes (device-side copies of the
+      row state, generated ids and sampling parameters) and freeing their slots.
+
+    A request that arrives while others decode waits at most one chunk (``steps_per_graph`` steps) plus its own
+    prefill, instead of the whole earlier batch (static batching)."""
+
+    def __init__(self, eng: DecodeEngine):
+        self.eng = eng
+        self.n = 0
+        self.free_slots = list(range(eng.max_batch))[::-1]
+        self.row_slot: List[int] = []
+        self.emitted: List[int] = []
+        self.prompt_tokens: List[List[int]] = []
+        self.options: List[Dict] = []
+
+    @property
+    def capacity(self) -> int:
+        return len(self.free_slots)
+
+    def admit(self, prompts: Sequence[Union[str, Sequence[int]]], num_predict: Sequence[int],
+              options: Sequence[Optional[Dict]]) -> List[int]:
+        from .. import ops
+
+        eng = self.eng
+        k = len(prompts)
+        if k == 0:
+            return []
+        if k > len(self.free_slots):
+            raise ValueError(f"{k} requests but only {len(self.free_slots)} free rows")
+        ids = [eng.encode(p) or [eng.cfg.bos_id] for p in prompts]
+        nps, row_opts = [], []
+        for i, (p, n, o) in enumerate(zip(ids, num_predict, options)):
+            budget = eng.T_max - len(p)
+            if budget < 1:
+                raise ValueError(f"prompt of {len(p)} tokens exceeds the context ({eng.T_max})")
+            nps.append(max(1, min(int(n), budget)))
+            row_opts.append(_row_options(o, eng.cfg, self.n + i, eng.seed))
+        slots = [self.free_slots.pop() for _ in range(k)]
+        rows = list(range(self.n, self.n + k))
+        r = eng.rows
+        with torch.cuda.stream(eng.stream):
+            eng._prefill(ids, slots)
+            sl = slice(self.n, self.n + k)
+            r["tok"][sl].copy_(torch.tensor([p[-1] for p in ids], dtype=torch.int32))
+            r["pos"][sl].copy_(torch.tensor([len(p) - 1 for p in ids], dtype=torch.int32))
+            r["slot"][sl].copy_(torch.tensor(slots, dtype=torch.int32))
+            r["n_gen"][sl].zero_()
+            r["done"][sl].zero_()
+            r["max_new"][sl].copy_(torch.tensor(nps, dtype=torch.int32))
+            eng.sample_params[32 * self.n: 32 * (self.n + k)].copy_(ops.sample_params_tensor(row_opts, "cpu").to(eng.device))
+        self.n += k
+        self.row_slot += slots
+        self.emitted += [0] * k
+        self.prompt_tokens += ids
+        self.options += row_opts
+        return rows
+
+    def step(self, steps: Optional[int] = None) -> None:
+        eng = self.eng
+        if self.n == 0:
+            return
+        steps = steps or eng.steps_per_graph
+        stream_h = ctypes.c_void_p(eng.stream.cuda_stream)
+        with torch.cuda.stream(eng.stream):
+            k = eng.steps_per_graph
+            if steps >= k:
+                g = eng._graph(self.n, k)
+                for _ in range(steps // k):
+                    if eng.lib.cain_graph_launch(ctypes.c_void_p(g), stream_h) != 0:
+                        raise RuntimeError("hipGraphLaunch failed")
+            if steps % k:
+                g1 = eng._graph(self.n, 1)
+                for _ in range(steps % k):
+                    eng.lib.cain_graph_launch(ctypes.c_void_p(g1), stream_h)
+
+    def poll(self):
+        """([new token ids per live row], [finished flag per live row])."""
+        eng = self.eng
+        if self.n == 0:
+            return [], []
+        with torch.cuda.stream(eng.stream):
+            ng = eng.rows["n_gen"][: self.n].cpu().tolist()
+            done = eng.rows["done"][: self.n].cpu().tolist()
+            hi = max(ng)
+            gen = eng.gen[: self.n, :hi].cpu() if hi else None
+        new = []
+        for i in range(self.n):
+            new.append(gen[i, self.emitted[i]: ng[i]].tolist() if ng[i] > self.emitted[i] else [])
+            self.emitted[i] = ng[i]
+        return new, [bool(d) for d in done]
+
+    def tokens(self, row: int) -> List[int]:
+        ng = int(self.eng.rows["n_gen"][row])
+        return self.eng.gen[row, :ng].cpu().tolist()
+
+    def retire(self, rows: Sequence[int]) -> Dict[int, int]:
+        """Drop ``rows``; returns {old row index: new row index} for the rows that moved into the holes."""
+        eng = self.eng
+        dead = sorted(set(int(x) for x in rows))
+        if not dead:
+            return {}
+        keep = [i for i in range(self.n) if i not in set(dead)]
+        n_new = len(keep)
+        moves = {}
+        holes = [h for h in dead if h < n_new]
+        movers = [j for j in keep if j >= n_new]
+        for h, j in zip(holes, movers):
+            moves[j] = h
+        for h in dead:
+            self.free_slots.append(self.row_slot[h])
+        if moves:
+            src = torch.tensor(list(moves.keys()), device=eng.device, dtype=torch.long)
+            dst = torch.tensor(list(moves.values()), device=eng.device, dtype=torch.long)
+            r = eng.rows
+            with torch.cuda.stream(eng.stream):
+                for key in ("tok", "pos", "slot", "n_gen", "max_new", "done"):
+                    r[key][dst] = r[key][src]
+                h64 = r["hist"].view(-1, 64)
+                h64[dst] = h64[src]
+                eng.gen[dst] = eng.gen[src]
+                sp = eng.sample_params.view(-1, 32)
+                sp[dst] = sp[src]
+            for j, h in moves.items():
+                self.row_slot[h] = self.row_slot[j]
+                self.emitted[h] = self.emitted[j]
+                self.prompt_tokens[h] = self.prompt_tokens[j]
+                self.options[h] = self.options[j]
+        with torch.cuda.stream(eng.stream):
+            eng.rows["slot"][n_new: self.n].fill_(-1)  # vacated rows: skipped by the sampler
+        self.n = n_new
+        del self.row_slot[n_new:], self.emitted[n_new:], self.prompt_tokens[n_new:], self.options[n_new:]
+        return moves

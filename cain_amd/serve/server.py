@@ -14,10 +14,16 @@ Endpoints: ``POST /api/generate`` (stream NDJSON or one JSON), ``POST /api/chat`
 and units (ns): ``total_duration``, ``load_duration``, ``prompt_eval_count``,
 ``prompt_eval_duration``, ``eval_count``, ``eval_duration``.
 
-Concurrency: requests for the same model that arrive within ``batch_window_ms``
-are decoded together as one batch (up to the engine's ``max_batch``) — trial
-batching on the server side.  One worker thread per model owns
-the GPU work; HTTP handler threads only enqueue and stream results back.
+Concurrency: one worker thread per model owns the GPU work; HTTP handler
+threads only enqueue and stream results back.  On the HIP backend the worker
+runs **continuous batching** (``EngineBackend.serve_queue`` over
+``engine.ContinuousBatch``): a request joins the running decode batch at the
+next graph boundary (every ``steps_per_graph`` decode steps) and leaves it as
+soon as it finishes, so a late request waits one chunk plus its own prefill
+rather than the whole earlier batch.  Other backends (torch oracle, fake) and
+``--static-batching`` collect the requests that arrive within
+``batch_window_ms`` into one batch and run it to completion (trial batching on
+the server side).
 
 Tracing: started with ``--trace-dir DIR``, the engine backend records every decode batch
 with ``torch.profiler`` (host ops + GPU kernels) and writes a Chrome trace to DIR; the response JSON
@@ -93,8 +99,10 @@ class EngineBackend(Backend):
 
     def __init__(self, models: List[str], device: str = "cuda:0", max_batch: int = 16, max_context: int = 2048,
                  backend: Optional[str] = None, seed: int = 0, preload: bool = False, steps_per_graph: int = 8,
-                 trace_dir: Optional[str] = None, weight_dtype: str = "bf16"):
+                 trace_dir: Optional[str] = None, weight_dtype: str = "bf16", continuous: bool = True):
         self._models = list(models)
+        # continuous batching needs the HIP engine; tracing records whole static batches
+        self.continuous = continuous and not trace_dir
         self.weight_dtype = weight_dtype
         self.trace_dir = trace_dir
         self._trace_seq = 0
@@ -163,6 +171,74 @@ class EngineBackend(Backend):
             j.result = r
             j.ttft_ns = ttft
 
+
+    def serve_queue(self, model: str, q: "queue.Queue[Job]") -> bool:
+        """Continuous batching loop of one model (never returns on the HIP engine; False: not supported here,
+        the scheduler falls back to static batches)."""
+        from ..engine.engine import GenResult
+
+        eng = self.engine(model)
+        if eng.backend != "hip":
+            return False
+        cb = eng.continuous()
+        tok = eng.tokenizer
+        live: Dict[int, Dict[str, Any]] = {}  # row -> {job, prefill_ns, t_first}
+        while True:
+            pending: List[Job] = []
+            if cb.n == 0:
+                pending.append(q.get())  # idle: block for the next request
+            while len(pending) < cb.capacity:
+                try:
+                    pending.append(q.get_nowait())
+                except queue.Empty:
+                    break
+            if pending:
+                t0 = time.perf_counter_ns()
+                try:
+                    rows = cb.admit([j.prompt for j in pending], [j.num_predict for j in pending],
+                                    [j.options for j in pending])
+                    eng.stream.synchronize()
+                except BaseException as exc:  # noqa: BLE001 - reported per job
+                    for j in pending:
+                        j.error = exc
+                        j.done.set()
+                    continue
+                dt = time.perf_counter_ns() - t0
+                for r, j in zip(rows, pending):
+                    live[r] = {"job": j, "prefill_ns": dt, "t_first": None}
+            try:
+                cb.step()
+                new, fin = cb.poll()
+            except BaseException as exc:  # noqa: BLE001 - fail the live requests, start a fresh batch
+                for st in live.values():
+                    st["job"].error = exc
+                    st["job"].done.set()
+                live = {}
+                cb = eng.continuous()
+                continue
+            now = time.perf_counter_ns()
+            for r, ids in enumerate(new):
+                st = live[r]
+                if ids and st["t_first"] is None:
+                    st["t_first"] = now
+                if ids and st["job"].stream is not None:
+                    st["job"].stream("".join(tok.piece(t) for t in ids))
+            done_rows = [r for r, f in enumerate(fin) if f]
+            for r in done_rows:
+                st, j = live[r], live[r]["job"]
+                toks = cb.tokens(r)
+                eos = cb.options[r]["eos_id"]
+                reason = "stop" if (eos >= 0 and toks and toks[-1] == eos) else "length"
+                t_first = st["t_first"] or now
+                j.result = GenResult(model, list(cb.prompt_tokens[r]), toks, tok.decode(toks), reason,
+                                     load_duration_ns=0, prompt_eval_duration_ns=st["prefill_ns"],
+                                     eval_duration_ns=int(now - t_first),
+                                     total_duration_ns=int(now - j.t_submit * 1e9))
+                j.ttft_ns = int(t_first - j.t_submit * 1e9)
+                j.done.set()
+            if done_rows:
+                moves = cb.retire(done_rows)
+                live = {moves.get(r, r): st for r, st in live.items() if r not in set(done_rows)}
 
     def _traced(self, model: str, fn):
         """Run ``fn`` under torch.profiler (CPU + GPU activity) and export a Chrome trace."""
@@ -256,6 +332,15 @@ class Scheduler:
         return job
 
     def _worker(self, model: str, q: "queue.Queue[Job]") -> None:
+        if getattr(self.backend, "continuous", False):
+            try:
+                if self.backend.serve_queue(model, q) is not False:
+                    return
+            except BaseException as exc:  # noqa: BLE001 - e.g. the model failed to load
+                while True:  # fail every request of this model rather than hang it
+                    j = q.get()
+                    j.error = exc
+                    j.done.set()
         while True:
             first = q.get()
             batch = [first]
@@ -469,6 +554,9 @@ def main(argv: Optional[List[str]] = None) -> None:
     ap.add_argument("--trace-dir", default=None, help="write a torch.profiler Chrome trace of every decode batch here")
     ap.add_argument("--weights", choices=["bf16", "fp8"], default="bf16",
                     help="GEMM weight storage (fp8: e4m3 per-row scaled, W8A16 kernels, batch <= 64)")
+    ap.add_argument("--static-batching", action="store_true",
+                    help="batch requests that arrive within --batch-window-ms and run each batch to completion "
+                         "(default on the HIP engine: continuous batching)")
     ap.add_argument("-v", "--verbose", action="store_true")
     ns = ap.parse_args(argv)
     models = [m for m in ns.models.split(",") if m]
@@ -479,7 +567,8 @@ def main(argv: Optional[List[str]] = None) -> None:
         be: Backend = FakeBackend(models, tokens_per_s=ns.fake_tok_s, prefill_s=ns.fake_prefill_s)
     else:
         be = EngineBackend(models, device=ns.device, max_batch=ns.max_batch, max_context=ns.max_context,
-                           backend=ns.backend, preload=ns.preload, trace_dir=ns.trace_dir, weight_dtype=ns.weights)
+                           backend=ns.backend, preload=ns.preload, trace_dir=ns.trace_dir, weight_dtype=ns.weights,
+                           continuous=not ns.static_batching)
     srv = make_server(be, ns.host, ns.port, ns.batch_window_ms, ns.verbose)
     print(f"[serve] Ollama-compatible API on http://{ns.host}:{srv.server_address[1]} models={models}", flush=True)
     try:
