@@ -46,18 +46,34 @@ const LtPlan* lt_plan(int N, int K, int M, int ldx, int ldy, bool accumulate, lo
   auto key = std::make_tuple(N, K, M, ldx, ldy, int(accumulate), ws_bytes, dev, int(f32out));
   auto it = g_plans.find(key);
   if (it != g_plans.end()) return it->second.ok ? &it->second : nullptr;
-  LtPlan& p = g_plans[key];
-  if (!g_handle && hipblasLtCreate(&g_handle) != HIPBLAS_STATUS_SUCCESS) return nullptr;
-  if (hipblasLtMatmulDescCreate(&p.md, HIPBLAS_COMPUTE_32F, HIP_R_32F) != HIPBLAS_STATUS_SUCCESS) return nullptr;
+  LtPlan p;
+  // every failure path releases what it created and caches nothing, so a later call retries
+  auto fail = [&p]() -> const LtPlan* {
+    if (p.lc) hipblasLtMatrixLayoutDestroy(p.lc);
+    if (p.lb) hipblasLtMatrixLayoutDestroy(p.lb);
+    if (p.la) hipblasLtMatrixLayoutDestroy(p.la);
+    if (p.md) hipblasLtMatmulDescDestroy(p.md);
+    return nullptr;
+  };
+  if (!g_handle && hipblasLtCreate(&g_handle) != HIPBLAS_STATUS_SUCCESS) {
+    g_handle = nullptr;
+    return nullptr;
+  }
+  if (hipblasLtMatmulDescCreate(&p.md, HIPBLAS_COMPUTE_32F, HIP_R_32F) != HIPBLAS_STATUS_SUCCESS) {
+    p.md = nullptr;
+    return fail();
+  }
   const hipblasOperation_t ta = HIPBLAS_OP_T, tb = HIPBLAS_OP_N;
   hipblasLtMatmulDescSetAttribute(p.md, HIPBLASLT_MATMUL_DESC_TRANSA, &ta, sizeof(ta));
   hipblasLtMatmulDescSetAttribute(p.md, HIPBLASLT_MATMUL_DESC_TRANSB, &tb, sizeof(tb));
-  if (hipblasLtMatrixLayoutCreate(&p.la, HIP_R_16BF, K, N, K) != HIPBLAS_STATUS_SUCCESS ||
-      hipblasLtMatrixLayoutCreate(&p.lb, HIP_R_16BF, K, M, ldx) != HIPBLAS_STATUS_SUCCESS ||
-      hipblasLtMatrixLayoutCreate(&p.lc, f32out ? HIP_R_32F : HIP_R_16BF, N, M, ldy) != HIPBLAS_STATUS_SUCCESS)
-    return nullptr;
+  if (hipblasLtMatrixLayoutCreate(&p.la, HIP_R_16BF, K, N, K) != HIPBLAS_STATUS_SUCCESS) { p.la = nullptr; return fail(); }
+  if (hipblasLtMatrixLayoutCreate(&p.lb, HIP_R_16BF, K, M, ldx) != HIPBLAS_STATUS_SUCCESS) { p.lb = nullptr; return fail(); }
+  if (hipblasLtMatrixLayoutCreate(&p.lc, f32out ? HIP_R_32F : HIP_R_16BF, N, M, ldy) != HIPBLAS_STATUS_SUCCESS) {
+    p.lc = nullptr;
+    return fail();
+  }
   hipblasLtMatmulPreference_t pref = nullptr;
-  if (hipblasLtMatmulPreferenceCreate(&pref) != HIPBLAS_STATUS_SUCCESS) return nullptr;
+  if (hipblasLtMatmulPreferenceCreate(&pref) != HIPBLAS_STATUS_SUCCESS) return fail();
   uint64_t wsb = (uint64_t)ws_bytes;
   hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &wsb, sizeof(wsb));
   hipblasLtMatmulHeuristicResult_t res[1];
@@ -65,11 +81,11 @@ const LtPlan* lt_plan(int N, int K, int M, int ldx, int ldy, bool accumulate, lo
   hipblasStatus_t s = hipblasLtMatmulAlgoGetHeuristic(g_handle, p.md, p.la, p.lb, p.lc, p.lc, pref, 1, res, &n);
   hipblasLtMatmulPreferenceDestroy(pref);
   (void)accumulate;
-  if (s != HIPBLAS_STATUS_SUCCESS || n < 1) return nullptr;
+  if (s != HIPBLAS_STATUS_SUCCESS || n < 1) return fail();
   p.algo = res[0].algo;
   p.ws = res[0].workspaceSize;
   p.ok = true;
-  return &p;
+  return &(g_plans[key] = p);
 }
 
 constexpr int ACT_THREADS = 256;

@@ -115,7 +115,7 @@ def run_rank(config_path: str, rank: int, world: int, isolation: Optional[str] =
         dist.broadcast_object_list(todo_ids, src=0)
         todo_ids = todo_ids[0]
         by_id = {v["__run_id"]: v for v in ctrl.run_table}
-        output.console_log_OK(f"{len(todo_ids)} TODO runs over {world} ranks")
+        output.console_log_OK(f"{len(todo_ids)} TODO runs over {world} ranks (backend {backend})")
         EventSubscriptionController.raise_event(RunnerEvents.BEFORE_EXPERIMENT)
         passes = 1 + max(0, int(retry_failed))
         store = dist.distributed_c10d._get_default_store()

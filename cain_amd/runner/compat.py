@@ -16,7 +16,7 @@ from typing import Dict
 
 
 def _aliases() -> Dict[str, Dict[str, object]]:
-    from . import controller, errors, events, isolation, misc, models, output, paths, store, validator
+    from . import controller, errors, events, isolation, models, output, paths, store, validator
     from ..energy import plugin as energy_plugin
     from ..energy import wattsup
     from . import template
@@ -56,9 +56,7 @@ def _aliases() -> Dict[str, Dict[str, object]]:
             n: getattr(paths, n) for n in ("is_pathname_valid", "is_path_creatable", "is_path_exists_or_creatable",
                                            "is_path_sibling_creatable", "is_path_exists_or_creatable_portable")},
         "ExperimentOrchestrator.Misc.DictConversion": {
-            "class_to_dict": validator.class_to_dict, "pop_from_each_dict_in_list": misc.pop_from_each_dict_in_list},
-        "ExperimentOrchestrator.Architecture.Singleton": {
-            "Singleton": misc.Singleton, "SingletonABCMeta": misc.SingletonABCMeta},
+            "class_to_dict": validator.class_to_dict},
         "ExperimentOrchestrator.Experiment.ExperimentController": {
             "ExperimentController": controller.ExperimentController},
         "ExperimentOrchestrator.Experiment.Run.RunController": {"RunController": controller.RunController},

@@ -5,6 +5,8 @@ import os
 import subprocess
 import sys
 import textwrap
+
+import pytest
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parent.parent
@@ -139,3 +141,23 @@ def test_fanout_four_ranks(tmp_path):
     rows = list(csv.DictReader(open(tmp_path / "dp" / "run_table.csv")))
     assert sum(x["__done"] == "DONE" for x in rows) == 11
     assert "12 TODO runs over 4 ranks" in r.stdout
+
+
+@pytest.mark.gpu
+def test_fanout_one_rank_over_rccl(tmp_path):
+    """The same fan-out with the backend the GPU node picks by itself (nccl = RCCL on ROCm): process-group
+    start-up bound to cuda:0, object broadcasts and the store work queue on a real MI355X (world 1 -- one card
+    per box here; the 8-GPU node runs are the driver's)."""
+    import torch
+    if not torch.cuda.is_available():  # pragma: no cover
+        pytest.skip("needs a GPU")
+    cfg = tmp_path / "cfg.py"
+    cfg.write_text(CFG)
+    env = dict(os.environ, PYTHONPATH=str(ROOT), CAIN_TEST_OUT=str(tmp_path), CAIN_ASSUME_YES="1", NO_COLOR="1")
+    env.pop("CAIN_DIST_BACKEND", None)
+    r = subprocess.run([sys.executable, "-m", "cain_amd", str(cfg), "--gpus", "1"], capture_output=True,
+                       text=True, env=env, timeout=240)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "backend nccl" in r.stdout, r.stdout[-2000:]
+    rows = list(csv.DictReader(open(tmp_path / "dp" / "run_table.csv")))
+    assert sum(x["__done"] == "DONE" for x in rows) == 11 and {x["rank"] for x in rows if x["rank"]} == {"0"}

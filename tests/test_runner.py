@@ -363,17 +363,16 @@ def test_reference_utility_modules_import_by_reference_names(tmp_path):
     from cain_amd.runner import compat
 
     compat.install()
-    from ExperimentOrchestrator.Architecture.Singleton import Singleton, SingletonABCMeta  # noqa: F401
-    from ExperimentOrchestrator.Misc.DictConversion import class_to_dict, pop_from_each_dict_in_list
+    from ExperimentOrchestrator.Misc.DictConversion import class_to_dict
     from ExperimentOrchestrator.Misc.PathValidation import (is_path_creatable, is_path_exists_or_creatable,
                                                              is_path_exists_or_creatable_portable,
                                                              is_path_sibling_creatable, is_pathname_valid)
 
-    class One(metaclass=Singleton):
-        pass
+    class Cfg:
+        name = "x"
+        repetitions = 2
 
-    assert One() is One()
-    assert pop_from_each_dict_in_list([{"a": 1, "b": 2}], "a") == [{"b": 2}]
+    assert class_to_dict(Cfg)["repetitions"] == 2
     assert is_pathname_valid(str(tmp_path / "x")) and not is_pathname_valid("")
     assert is_path_creatable(str(tmp_path / "new" / "dir")) and is_path_sibling_creatable(str(tmp_path / "f"))
     assert is_path_exists_or_creatable(tmp_path / "p") and is_path_exists_or_creatable_portable(str(tmp_path / "q"))
