@@ -94,6 +94,8 @@ def main() -> int:
     ap.add_argument("--no-energy", action="store_true")
     ap.add_argument("--weights", choices=("bf16", "fp8"), default="bf16",
                     help="GEMM weight storage: bf16 (headline) or fp8 e4m3 per-row scaled (W8A16, batch <= 64)")
+    ap.add_argument("--kv", choices=("bf16", "fp8"), default="bf16",
+                    help="KV-cache storage: bf16 (headline) or fp8 e4m3 (half the attention bytes; separate config)")
     ap.add_argument("--device", choices=("cuda", "cpu"), default="cuda",
                     help="cpu: the torch oracle backend over gloo (tests of the multi-rank plumbing; tiny models)")
     ap.add_argument("--settle", type=float, default=8.0, help="seconds of rest before the idle-power baseline")
@@ -131,7 +133,7 @@ def main() -> int:
 
     n_tok = tokens_for_words(ns.words)
     eng = DecodeEngine(ns.model, device=dev, max_batch=ns.batch, max_context=ns.context, seed=1234 + rank,
-                       steps_per_graph=ns.steps_per_graph, weight_dtype=ns.weights)
+                       steps_per_graph=ns.steps_per_graph, weight_dtype=ns.weights, kv_dtype=ns.kv)
     if eng.max_batch < ns.batch:
         raise SystemExit(f"--batch {ns.batch} exceeds the engine's row limit {eng.max_batch} for --weights {ns.weights}")
     tps = topics()
@@ -231,7 +233,8 @@ def main() -> int:
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": round(value / base_tps, 2) if base_tps else None,
-            "dtype": "bf16" if ns.weights == "bf16" else "bf16 activations, fp8-e4m3 weights",
+            "dtype": ("bf16" if ns.weights == "bf16" else "bf16 activations, fp8-e4m3 weights")
+                     + (", fp8-e4m3 KV cache" if ns.kv == "fp8" else ""),
             "device": "cpu (torch oracle)" if cpu else "MI355X",
             "data": "synthetic (reference topics.csv prompts, random-init weights)",
             "config": {"model": ns.model, "global_batch": ns.batch * world, "seq_len": n_tok,
@@ -251,6 +254,9 @@ def main() -> int:
                                         if base_jpt and not math.isnan(energy) and energy > 0 else None),
             "single_stream_vs_baseline_J_per_token": (round(base_jpt / ss_j_mean, 3)
                                                       if base_jpt and not math.isnan(ss_j_mean) else None),
+            # start-up autotune of the wide-batch GEMM plans: N x K @ rows -> splits x ring variant (us)
+            "wgemm_plans": {f"{t['n']}x{t['k']}@{t['m']}": f"{t['ks']}x{t['variant']} ({t['us']} us)"
+                            for t in getattr(eng, "wgemm_tuning", [])},
         }
         print(json.dumps(out), flush=True)
     if meter:

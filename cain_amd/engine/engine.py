@@ -131,7 +131,8 @@ class _CainPlanDesc(ctypes.Structure):
                                                  "part_o", "part_ml", "counters", "gemm_ws")]
                 + [("gemm_ws_bytes", ctypes.c_longlong), ("w8", ctypes.c_int), ("lm_head_scale", ctypes.c_void_p)]
                 + [("lt_min_rows", ctypes.c_int), ("gu", ctypes.c_void_p), ("lt_ws", ctypes.c_void_p),
-                   ("lt_ws_bytes", ctypes.c_longlong), ("lm_head_lt", ctypes.c_void_p), ("xn", ctypes.c_void_p)])
+                   ("lt_ws_bytes", ctypes.c_longlong), ("lm_head_lt", ctypes.c_void_p), ("xn", ctypes.c_void_p)]
+                + [("kv8", ctypes.c_int)])
 
 
 class _CainRows(ctypes.Structure):
@@ -168,13 +169,18 @@ class DecodeEngine:
     def __init__(self, model: Union[str, ModelConfig], device: Union[str, torch.device] = "cuda",
                  max_batch: int = 16, max_context: int = 2048, seed: int = 0, backend: Optional[str] = None,
                  steps_per_graph: int = 8, weights: Optional[ModelWeights] = None, tokenizer=None,
-                 keep_natural: bool = False, weight_dtype: str = "bf16"):
+                 keep_natural: bool = False, weight_dtype: str = "bf16", kv_dtype: str = "bf16"):
         """``weight_dtype="fp8"``: GEMM weights quantised per row to e4m3 (W8A16, half the weight bytes
-        per decode step -- the single-stream / small-batch option); limits rows per forward to 64."""
+        per decode step -- the single-stream / small-batch option); limits rows per forward to 64.
+        ``kv_dtype="fp8"``: the KV cache holds e4m3 elements (half the attention bytes per decode step and half
+        the cache memory; csrc/attention.hip KV8)."""
         self.cfg = get_config(model) if isinstance(model, str) else model
         if weight_dtype not in ("bf16", "fp8"):
             raise ValueError(f"weight_dtype must be 'bf16' or 'fp8', got {weight_dtype!r}")
+        if kv_dtype not in ("bf16", "fp8"):
+            raise ValueError(f"kv_dtype must be 'bf16' or 'fp8', got {kv_dtype!r}")
         self.weight_dtype = weight_dtype
+        self.kv_dtype = kv_dtype
         row_cap = W8_MAX_ROWS if weight_dtype == "fp8" else MAX_ROWS
         self.device = torch.device(device)
         if backend is None:
@@ -197,7 +203,7 @@ class DecodeEngine:
             from ..models.reference import ReferenceModel
             # fp8: the oracle runs on the dequantised weights the fp8 kernels multiply by
             ref_w = fp8_roundtrip_weights(weights) if weight_dtype == "fp8" else weights
-            self.ref = ReferenceModel(ref_w, memo_weights=self.device.type == "cpu")
+            self.ref = ReferenceModel(ref_w, memo_weights=self.device.type == "cpu", kv_dtype=kv_dtype)
         else:
             raise ValueError(f"unknown backend {backend!r}")
         if self.device.type == "cuda":
@@ -226,8 +232,9 @@ class DecodeEngine:
         bf = torch.bfloat16
         kv_layer = S * cfg.n_kv_heads * T * cfg.head_dim
         # zero-init: positions past a row's length must hold finite values (masked P = 0 multiplies them)
-        self.kcache = torch.zeros(L * kv_layer, device=dev, dtype=bf)
-        self.vtcache = torch.zeros(L * kv_layer, device=dev, dtype=bf)
+        kv_t = torch.uint8 if self.kv_dtype == "fp8" else bf
+        self.kcache = torch.zeros(L * kv_layer, device=dev, dtype=kv_t)
+        self.vtcache = torch.zeros(L * kv_layer, device=dev, dtype=kv_t)
         inv = rope_inv_freq(cfg)
         ang = np.arange(T, dtype=np.float64)[:, None] * inv[None, :]
         self.cos_t = torch.tensor(np.cos(ang), dtype=torch.float32, device=dev).contiguous()
@@ -266,11 +273,14 @@ class DecodeEngine:
         d.embed, d.lm_head = _ptr(self.weights.embed), _ptr(packed["lm_head"])
         d.layers = ctypes.cast(self._layers, ctypes.c_void_p).value
         d.kcache, d.vtcache, d.kv_layer_elems = _ptr(self.kcache), _ptr(self.vtcache), kv_layer
+        d.kv8 = int(self.kv_dtype == "fp8")
         d.cos_t, d.sin_t = _ptr(self.cos_t), _ptr(self.sin_t)
         for k in ("x", "q", "attn", "act", "logits", "counters"):
             setattr(d, k, _ptr(self.buf[k]))
         d.part_o, d.part_ml = _ptr(self.part_o), _ptr(self.part_ml)
-        # batched GEMM (16 < M <= 128) split-K workspace: largest need over this model's GEMM shapes
+        self.wgemm_tuning = self._tune_wide_gemm(packed, R)
+        # batched GEMM (16 < M <= 128) split-K workspace: largest need over this model's GEMM shapes (after the
+        # autotune, which may pick larger split counts than the default rule)
         shapes = [(cfg.qkv_dim, cfg.d_model), (cfg.d_model, cfg.q_dim), (2 * cfg.ffn, cfg.d_model),
                   (cfg.d_model, cfg.ffn), (cfg.vocab, cfg.d_model)]
         ws = max([ops.gemm_ws_bytes(n, k, m) for n, k in shapes for m in range(17, R + 1)] + [0])
@@ -290,6 +300,29 @@ class DecodeEngine:
         self._plans: Dict[int, int] = {}
         self._graphs: Dict[tuple, int] = {}
         self.stream = torch.cuda.Stream(device=dev)
+
+    def _tune_wide_gemm(self, packed, R: int) -> list:
+        """Start-up autotune of the wide-batch GEMM plans (split count, ring variant) for this model's projection
+        shapes, timed on its own layer weights (ops.tune_wide_gemm) at the row tiles the engine will run: the
+        max batch (256-row tile when > 128) and the 128-row prefill chunk.  Opt-in (CAIN_WGEMM_TUNE=1): on the
+        headline bench the tuned plans (faster in isolation, e.g. O at 5 splits 25.5 us vs 30.5) measured 23.5k
+        vs 23.9k tok/s untuned on the same box -- the isolated winner is not the in-graph winner, so the default
+        rule stays.  Runs before any graph capture and before the GEMM workspace is sized."""
+        from .. import ops
+        if self.weight_dtype != "bf16" or os.environ.get("CAIN_WGEMM_TUNE", "0") != "1":
+            return []
+        cfg = self.cfg
+        layers = packed["layers"]
+        act = ops.EPI_GELU if cfg.act == "gelu_tanh" else ops.EPI_SILU
+        cases = [(cfg.qkv_dim, cfg.d_model, ops.EPI_BF16, True, [lp["wqkv"] for lp in layers]),
+                 (cfg.d_model, cfg.q_dim, ops.EPI_RESID, False, [lp["wo"] for lp in layers]),
+                 (2 * cfg.ffn, cfg.d_model, act, True, [lp["wgu"] for lp in layers]),
+                 (cfg.d_model, cfg.ffn, ops.EPI_RESID, False, [lp["wdown"] for lp in layers])]
+        if self.max_batch > 128:
+            cases.append((cfg.vocab, cfg.d_model, ops.EPI_F32, True, [packed["lm_head"]]))
+        rows = sorted({m for m in (self.max_batch, min(R, 128)) if m > 64})
+        with torch.cuda.device(self.device):
+            return [r for m in rows for r in ops.tune_wide_gemm(cases, m)]
 
     def _plan(self, M: int) -> int:
         """One native plan per attention split count (nsplit depends on the row count)."""

@@ -45,6 +45,11 @@ def activation(cfg: ModelConfig, g: torch.Tensor) -> torch.Tensor:
     return F.silu(g)
 
 
+def fp8_kv_roundtrip(t: torch.Tensor) -> torch.Tensor:
+    """A KV value as the fp8 cache holds it: rounded to bf16, then to e4m3 (saturating at +-448), widened."""
+    return t.to(torch.bfloat16).float().clamp(-448.0, 448.0).to(torch.float8_e4m3fn).float()
+
+
 class ReferenceModel:
     """Causal forward: tokens [B, T] → logits [B, T, V] (fp32).
 
@@ -52,10 +57,13 @@ class ReferenceModel:
     the CPU serving path of the engine uses it so a generation costs one token of compute per step.
     ``memo_weights`` keeps the compute-dtype copies of the weights (CPU serving: no per-call conversion)."""
 
-    def __init__(self, mw: ModelWeights, compute_dtype=torch.float32, memo_weights: bool = False):
+    def __init__(self, mw: ModelWeights, compute_dtype=torch.float32, memo_weights: bool = False,
+                 kv_dtype: str = "bf16"):
         self.mw = mw
         self.cfg = mw.cfg
         self.dt = compute_dtype
+        # "fp8": K (after RoPE) and V pass through bf16 -> e4m3 as the engine's fp8 KV cache stores them
+        self.kv_fp8 = kv_dtype == "fp8"
         self._memo = {} if memo_weights else None
 
     def _w(self, t: torch.Tensor) -> torch.Tensor:
@@ -88,6 +96,8 @@ class ReferenceModel:
         cos, sin = rope_cos_sin(cfg, positions)                     # [B, T, hd/2]
         q = apply_rope(q.float(), cos[:, :, None], sin[:, :, None]).to(self.dt)
         k = apply_rope(k.float(), cos[:, :, None], sin[:, :, None]).to(self.dt)
+        if self.kv_fp8:
+            k, v = fp8_kv_roundtrip(k).to(self.dt), fp8_kv_roundtrip(v).to(self.dt)
         past = 0
         if cache is not None:
             if len(cache) > li:

@@ -37,6 +37,7 @@ HERE = Path(__file__).resolve().parent
 LIB_PATH = HERE / "libcain_kernels.so"
 
 EPI_BF16, EPI_RESID, EPI_F32, EPI_SILU, EPI_GELU, EPI_QKV_ROPE = 0, 1, 2, 3, 4, 5
+EPI_KV_FP8 = 0x100  # or-ed into EPI_QKV_ROPE: the KV cache is fp8 e4m3 (csrc/gemm_epi.h)
 
 
 class NativeOpsUnavailable(RuntimeError):
@@ -76,12 +77,16 @@ def load() -> ctypes.CDLL:
         lib.cain_gemm_ws_bytes.argtypes = [ci, ci, ci]
         lib.cain_wgemm_set_min_m.argtypes = [ci]
         lib.cain_wgemm_eligible.argtypes = [ci, ci, ci]
+        lib.cain_wgemm_set_shape.argtypes = [ci, ci, ci, ci, ci]
+        lib.cain_wgemm_plan.argtypes = [ci, ci, ci]
         lib.cain_lt_gemm.argtypes = [vp, vp, ci, ci, ci, ci, vp, ci, ci, vp, ctypes.c_longlong, vp]
         lib.cain_lt_prepare.argtypes = [ci, ci, ci, ci, ci, ci, ctypes.c_longlong]
         lib.cain_rownorm_act.argtypes = [vp, ci, ci, cf, ci, vp, ci, vp, ci, ci, ci, ci, vp]
         lib.cain_rmsnorm.argtypes = [vp, ci, vp, vp, ci, ci, ci, cf, vp]
         lib.cain_embed.argtypes = [vp, vp, vp, ci, ci, ci, cf, vp]
         lib.cain_attention.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp, ci, ci, ci, ci, ci, ci, ci, cf, vp]
+        lib.cain_attention_ex.argtypes = ([vp, vp, vp, vp, vp, vp, vp, vp, vp, ci, ci, ci, ci, ci, ci, ci, cf, ci, cf, cf]
+                                          + [vp])
         lib.cain_sample.argtypes = [vp, ci, ci, vp, vp, vp, ci, vp, vp, vp, vp, vp, ci, ci, vp, vp]
         lib.cain_plan_create.restype = vp
         lib.cain_plan_create.argtypes = [vp]
@@ -141,6 +146,73 @@ def wide_gemm_eligible(n: int, k: int, m: int) -> bool:
     return bool(load().cain_wgemm_eligible(n, k, m))
 
 
+def set_wide_gemm_plan(n: int, k: int, bm: int, ks: int, variant: int = -1) -> None:
+    """Per-shape wide-GEMM plan (csrc/wgemm.hip): split count ``ks`` (<= 0: the default rule) and ring
+    ``variant`` (< 0: the global one) for N = n, K = k with the bm-row tile (128 or 256)."""
+    if load().cain_wgemm_set_shape(int(n), int(k), int(bm), int(ks), int(variant)) != 0:
+        raise RuntimeError("wide-GEMM plan table full")
+
+
+def clear_wide_gemm_plans() -> None:
+    load().cain_wgemm_clear_shapes()
+
+
+def wide_gemm_plan(n: int, k: int, m: int) -> Optional[tuple]:
+    """(split count, ring variant) the next wide-GEMM launch of this shape uses; None if not eligible."""
+    v = int(load().cain_wgemm_plan(n, k, m))
+    return None if v < 0 else (v // 16, v % 16)
+
+
+#: ring variants the autotune tries (csrc/wgemm.hip wg_launch_v): 0 = default ring, 2 = shallower W ring
+TUNE_VARIANTS = (0, 2)
+
+
+def tune_wide_gemm(cases, m: int, iters: int = 2, candidates=(2, 3, 4, 5, 6, 8, 10, 12, 16)) -> list:
+    """Pick each wide-GEMM shape's split count and ring variant by timing the candidates on real weights.
+
+    ``cases``: (n, k, epi, norm, [packed weights]) -- one packed matrix per layer; every candidate cycles through
+    all of them so, as in a decode step, each launch streams its weights from HBM rather than a warm cache.
+    ``m``: rows (the tile class 128 / 256 follows from it).  Unsplit shapes (>= 128 column blocks) only get the
+    ring variant tuned.  Returns one dict per shape (chosen plan, time per call of every candidate, in us) and
+    installs the winners with ``set_wide_gemm_plan``.
+    """
+    load()
+    bm = 256 if m > 128 else 128
+    out = []
+    for n, k, epi, norm, wps in cases:
+        if not wide_gemm_eligible(n, k, m) or not wps:
+            continue
+        dev = wps[0].device
+        g = torch.Generator(device=dev).manual_seed(n ^ k)
+        x = (torch.randn(m, k, device=dev, generator=g) * 2).bfloat16()
+        n_out = n // 2 if epi in (EPI_SILU, EPI_GELU) else n
+        y = torch.zeros(m, n_out, device=dev, dtype=torch.float32 if epi == EPI_F32 else torch.bfloat16)
+        nblk = (n // 16 + 7) // 8
+        splits = [1] if nblk >= 128 else [c for c in candidates if k // 64 // c >= 4]
+        times = {}
+        for ks in splits:
+            for v in TUNE_VARIANTS:
+                set_wide_gemm_plan(n, k, bm, ks, v)
+                if wide_gemm_plan(n, k, m) != (ks, v):
+                    continue  # clamped to a plan already timed
+                for wp in wps[:2]:
+                    skinny_gemm(wp, x, n, epi, out=y, norm=norm)
+                torch.cuda.synchronize(dev)
+                a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a.record()
+                for _ in range(iters):
+                    for wp in wps:
+                        skinny_gemm(wp, x, n, epi, out=y, norm=norm)
+                b.record()
+                torch.cuda.synchronize(dev)
+                times[(ks, v)] = a.elapsed_time(b) * 1000.0 / (iters * len(wps))
+        best = min(times, key=times.get)
+        set_wide_gemm_plan(n, k, bm, *best)
+        out.append(dict(n=n, k=k, m=m, ks=best[0], variant=best[1], us=round(times[best], 2),
+                        candidates={f"{a}x{b}": round(t, 2) for (a, b), t in sorted(times.items())}))
+    return out
+
+
 def _workspace(device, nbytes: int) -> Optional[torch.Tensor]:
     """Per-device zero-initialised GEMM workspace, grown on demand (its counters self-reset)."""
     if nbytes <= 0:
@@ -188,14 +260,21 @@ def skinny_gemm(wp: torch.Tensor, x: torch.Tensor, n: int, epi: int = EPI_BF16, 
     return out
 
 
+def is_fp8_cache(t: torch.Tensor) -> bool:
+    """An fp8 (e4m3) KV cache: uint8 storage (the engine's) or torch.float8_e4m3fn."""
+    return t.dtype in (torch.uint8, torch.float8_e4m3fn)
+
+
 def qkv_rope(wp, x, n, q_out, kc, vtc, slot, pos, cos_t, sin_t, H, Hkv, hd, bias=None, norm: bool = False,
              eps: float = 1e-6, waves: int = 0, batched: bool = True) -> None:
-    """Fused QKV projection (+RMSNorm, +bias) -> RoPE -> Q buffer / K cache / V^T cache."""
+    """Fused QKV projection (+RMSNorm, +bias) -> RoPE -> Q buffer / K cache / V^T cache.  8-bit caches
+    (``is_fp8_cache``) receive e4m3 elements (EPI_KV_FP8)."""
     lib = load()
     M, K = x.shape
     T_max = kc.shape[-2]
+    epi = EPI_QKV_ROPE | (EPI_KV_FP8 if is_fp8_cache(kc) else 0)
     rc = _gemm_call(lib, wp, x, K, n, M, q_out, bias, norm, eps, slot, pos, cos_t, sin_t, kc, vtc, H, Hkv, hd,
-                    T_max, EPI_QKV_ROPE, waves, batched)
+                    T_max, epi, waves, batched)
     _check(rc, "qkv_rope")
 
 
@@ -220,6 +299,8 @@ def gemm_w8(wq: torch.Tensor, scale: torch.Tensor, x: torch.Tensor, n: int, epi:
     if epi == EPI_QKV_ROPE:
         assert rope is not None, "EPI_QKV_ROPE needs the rope/cache arguments"
     T_max = r["kc"].shape[-2] if rope else 0
+    if rope and is_fp8_cache(r["kc"]):
+        epi |= EPI_KV_FP8
     rc = lib.cain_gemm_w8(_p(wq), _p(scale), _p(x), x.stride(0), K, n, M, _p(out), out.stride(0), _p(bias),
                           int(bool(norm)), eps, _p(r.get("slot")), _p(r.get("pos")), _p(r.get("cos_t")),
                           _p(r.get("sin_t")), _p(r.get("kc")), _p(r.get("vtc")), r.get("H", 0), r.get("Hkv", 0),
@@ -302,7 +383,9 @@ def attention_ml_floats(M: int, H: int, Hkv: int, nsplit: int) -> int:
 
 
 def attention(q, kc, vtc, slot, pos, H, Hkv, hd, nsplit, scale, out=None, part_o=None, part_ml=None,
-              counters=None):
+              counters=None, kscale: float = 1.0, vscale: float = 1.0):
+    """Decode attention over the fragment-major caches (csrc/attention.hip); 8-bit caches (``is_fp8_cache``)
+    hold e4m3 elements whose values are element * kscale / vscale."""
     lib = load()
     M = q.shape[0]
     T_max = kc.shape[-2]
@@ -312,8 +395,11 @@ def attention(q, kc, vtc, slot, pos, H, Hkv, hd, nsplit, scale, out=None, part_o
     if counters is None:
         counters = torch.zeros(M * Hkv, device=q.device, dtype=torch.int32)
     out = torch.empty(M, H * hd, device=q.device, dtype=torch.bfloat16) if out is None else out
-    _check(lib.cain_attention(_p(q), _p(kc), _p(vtc), _p(slot), _p(pos), _p(part_o), _p(part_ml), _p(counters),
-                              _p(out), out.stride(0), M, H, Hkv, hd, T_max, nsplit, scale, _stream()),
+    kv8 = is_fp8_cache(kc)
+    assert kv8 == is_fp8_cache(vtc)
+    _check(lib.cain_attention_ex(_p(q), _p(kc), _p(vtc), _p(slot), _p(pos), _p(part_o), _p(part_ml), _p(counters),
+                                 _p(out), out.stride(0), M, H, Hkv, hd, T_max, nsplit, scale, int(kv8), kscale,
+                                 vscale, _stream()),
            "attention")
     return out
 

@@ -26,6 +26,10 @@
 //       permuted k order (cdna_hip_programming.md §3 'An accumulator tile as the
 //       next MFMA's operand');
 //       A = V^T fragments stored in that same k order — nothing is staged through LDS.
+// fp8 KV cache (KV8): the same fragment-major layouts with e4m3 elements (the QKV epilogue writes them,
+// gemm_epi.h EPI_KV_FP8), so a lane's fragment is 8 contiguous bytes and a block moves half the bytes; each
+// fragment widens to bf16 in registers (v_cvt_scalef32_pk_bf16_fp8, 4 per fragment, the per-tensor scale
+// folded in) and both products stay on the bf16 MFMA.
 // The AW waves merge their (m, l, O) in LDS.  With one split the workgroup
 // normalises and stores bf16 directly; otherwise each workgroup publishes an
 // unnormalised partial with write-through (sc1) stores and the LAST arriving
@@ -33,17 +37,33 @@
 // barrier -> relaxed agent ticket; no release/acquire fences, counter reset by the
 // reducer: cdna_hip_programming.md §5 'In-launch split-K reduction'), so there
 // is no separate combine launch.
+#include <type_traits>
+
 #include "common.h"
 
 constexpr float LOG2E = 1.4426950408889634f;
 // AW: waves per workgroup (4; 8 for few (row, kv head) pairs: single-stream decode, where one workgroup per
 // pair with more waves beats a position split and its in-kernel combine)
-template <int HD, int AW>
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+// 8 e4m3 values (one lane's fragment) -> bf16x8, times `sc`
+__device__ __forceinline__ bf16x8 fp8x8_to_bf16(u32x2 v, float sc) {
+  bf16x8 r;
+#pragma unroll
+  for (int w = 0; w < 2; ++w) {
+    const bf16x2 lo = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(int(v[w]), sc, false);
+    const bf16x2 hi = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(int(v[w]), sc, true);
+    r[4 * w + 0] = lo[0], r[4 * w + 1] = lo[1], r[4 * w + 2] = hi[0], r[4 * w + 3] = hi[1];
+  }
+  return r;
+}
+
+template <int HD, int AW, bool KV8>
 __global__ __launch_bounds__(AW * 64) void attn_decode_kernel(
     const __bf16* __restrict__ q, const __bf16* __restrict__ kc, const __bf16* __restrict__ vtc,
     const int* __restrict__ slot, const int* __restrict__ pos, float* __restrict__ part_o,
     float* __restrict__ part_ml, unsigned* __restrict__ counters, __bf16* __restrict__ out, int ldo, int M, int H,
-    int Hkv, int T_max, int nsplit, float scale) {
+    int Hkv, int T_max, int nsplit, float scale, float kscale, float vscale) {
   constexpr int NKS = HD / 32;  // MFMAs per S tile
   constexpr int NDT = HD / 16;  // O^T d-tiles
   const int lane = threadIdx.x & 63;
@@ -81,26 +101,33 @@ __global__ __launch_bounds__(AW * 64) void attn_decode_kernel(
     const float sl2 = scale * LOG2E;
     // fragment-major caches (layout at the top of this file): a 32-position block of one (slot, kv head) is
     // 2*NKS contiguous 1-KiB K fragments and NDT contiguous 1-KiB V^T fragments; lane l's 16 B sit at 16*l
-    const __bf16* kbase = kc + ((size_t)s * Hkv + kh) * T_max * HD + lane * 8;
-    const __bf16* vbase = vtc + ((size_t)s * Hkv + kh) * HD * T_max + lane * 8;
-    auto load_blk = [&](int blk, bf16x8 (&k_a)[NKS], bf16x8 (&k_b)[NKS], bf16x8 (&v)[NDT]) {
-      const __bf16* k0 = kbase + (size_t)blk * (2 * NKS * 512);
+    // a fragment in registers: 16 B of bf16, or (KV8) 8 B of e4m3 widened right before its MFMA
+    using frag_t = std::conditional_t<KV8, u32x2, bf16x8>;
+    constexpr int ESZ = KV8 ? 1 : 2;  // bytes per cache element
+    const char* kbase = reinterpret_cast<const char*>(kc) + (((size_t)s * Hkv + kh) * T_max * HD + lane * 8) * ESZ;
+    const char* vbase = reinterpret_cast<const char*>(vtc) + (((size_t)s * Hkv + kh) * HD * T_max + lane * 8) * ESZ;
+    auto load_blk = [&](int blk, frag_t (&k_a)[NKS], frag_t (&k_b)[NKS], frag_t (&v)[NDT]) {
+      const char* k0 = kbase + (size_t)blk * (2 * NKS * 512 * ESZ);
 #pragma unroll
       for (int i = 0; i < NKS; ++i) {
-        k_a[i] = *reinterpret_cast<const bf16x8*>(k0 + i * 512);
-        k_b[i] = *reinterpret_cast<const bf16x8*>(k0 + (NKS + i) * 512);
+        k_a[i] = *reinterpret_cast<const frag_t*>(k0 + i * 512 * ESZ);
+        k_b[i] = *reinterpret_cast<const frag_t*>(k0 + (NKS + i) * 512 * ESZ);
       }
-      const __bf16* v0 = vbase + (size_t)blk * (NDT * 512);
+      const char* v0 = vbase + (size_t)blk * (NDT * 512 * ESZ);
 #pragma unroll
-      for (int dt = 0; dt < NDT; ++dt) v[dt] = *reinterpret_cast<const bf16x8*>(v0 + dt * 512);
+      for (int dt = 0; dt < NDT; ++dt) v[dt] = *reinterpret_cast<const frag_t*>(v0 + dt * 512 * ESZ);
     };
-    auto process = [&](int blk, const bf16x8 (&ka)[NKS], const bf16x8 (&kb)[NKS], const bf16x8 (&va)[NDT]) {
+    auto widen = [&](const frag_t& f, float sc) -> bf16x8 {
+      if constexpr (KV8) return fp8x8_to_bf16(f, sc);
+      else return f;
+    };
+    auto process = [&](int blk, const frag_t (&ka)[NKS], const frag_t (&kb)[NKS], const frag_t (&va)[NDT]) {
       const int t0 = blk * 32;
       f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int i = 0; i < NKS; ++i) {
-        s0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ka[i], qf[i], s0, 0, 0, 0);
-        s1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kb[i], qf[i], s1, 0, 0, 0);
+        s0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(widen(ka[i], kscale), qf[i], s0, 0, 0, 0);
+        s1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(widen(kb[i], kscale), qf[i], s1, 0, 0, 0);
       }
       float bmax = -INFINITY;
 #pragma unroll
@@ -128,19 +155,19 @@ __global__ __launch_bounds__(AW * 64) void attn_decode_kernel(
 #pragma unroll
       for (int dt = 0; dt < NDT; ++dt) {
         o[dt] *= alpha;
-        o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va[dt], pf, o[dt], 0, 0, 0);
+        o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(widen(va[dt], vscale), pf, o[dt], 0, 0, 0);
       }
     };
 
     const int first = b0 + wave;
-    bf16x8 ka[NKS], kb[NKS], va[NDT];
+    frag_t ka[NKS], kb[NKS], va[NDT];
     load_blk(first, ka, kb, va);
     if constexpr (HD <= 128) {
       // two register sets ping-pong, the next block's loads issued before the current block computes;
       // no register copy of an in-flight load (that forces vmcnt(0)) and no load under a branch: a
       // prefetch past the wave's last block is clamped to it (a cache hit, never used)
       const int last = first + ((b1 - 1 - first) / AW) * AW;
-      bf16x8 kc2[NKS], kd2[NKS], vb2[NDT];
+      frag_t kc2[NKS], kd2[NKS], vb2[NDT];
       for (int blk = first; blk < b1; blk += 2 * AW) {
         load_blk(min(blk + AW, last), kc2, kd2, vb2);
         __builtin_amdgcn_sched_barrier(0);
@@ -255,33 +282,49 @@ __global__ __launch_bounds__(AW * 64) void attn_decode_kernel(
 template <int HD, int AW>
 static hipError_t launch_attn(const void* q, const void* kc, const void* vtc, const int* slot, const int* pos,
                               float* part_o, float* part_ml, unsigned* counters, void* out, int ldo, int M, int H,
-                              int Hkv, int T_max, int nsplit, float scale, hipStream_t st) {
-  hipLaunchKernelGGL((attn_decode_kernel<HD, AW>), dim3(M * Hkv, nsplit), dim3(AW * 64), 0, st, (const __bf16*)q,
-                     (const __bf16*)kc, (const __bf16*)vtc, slot, pos, part_o, part_ml, counters, (__bf16*)out, ldo,
-                     M, H, Hkv, T_max, nsplit, scale);
+                              int Hkv, int T_max, int nsplit, float scale, int kv8, float kscale, float vscale,
+                              hipStream_t st) {
+  if (kv8)
+    hipLaunchKernelGGL((attn_decode_kernel<HD, AW, true>), dim3(M * Hkv, nsplit), dim3(AW * 64), 0, st,
+                       (const __bf16*)q, (const __bf16*)kc, (const __bf16*)vtc, slot, pos, part_o, part_ml, counters,
+                       (__bf16*)out, ldo, M, H, Hkv, T_max, nsplit, scale, kscale, vscale);
+  else
+    hipLaunchKernelGGL((attn_decode_kernel<HD, AW, false>), dim3(M * Hkv, nsplit), dim3(AW * 64), 0, st,
+                       (const __bf16*)q, (const __bf16*)kc, (const __bf16*)vtc, slot, pos, part_o, part_ml, counters,
+                       (__bf16*)out, ldo, M, H, Hkv, T_max, nsplit, scale, 1.f, 1.f);
   return hipGetLastError();
 }
 
 // Workspace: part_o M*H*nsplit*hd floats, part_ml M*Hkv*align32(G*nsplit*2) floats, counters M*Hkv uints
-// (zeroed once; the reducer resets them).
-CAIN_API int cain_attention(const void* q, const void* kc, const void* vtc, const int* slot, const int* pos,
-                            float* part_o, float* part_ml, unsigned* counters, void* out, int ldo, int M, int H,
-                            int Hkv, int hd, int T_max, int nsplit, float scale, hipStream_t st) {
+// (zeroed once; the reducer resets them).  kv8: the caches hold e4m3 elements (value = element * k/vscale).
+CAIN_API int cain_attention_ex(const void* q, const void* kc, const void* vtc, const int* slot, const int* pos,
+                               float* part_o, float* part_ml, unsigned* counters, void* out, int ldo, int M, int H,
+                               int Hkv, int hd, int T_max, int nsplit, float scale, int kv8, float kscale,
+                               float vscale, hipStream_t st) {
   if (H % Hkv || H / Hkv > 16 || T_max % 32 || nsplit < 1 || nsplit > 64 || M > 256) return -1;
   // 8-wave workgroups for few (row, kv head) pairs (hd <= 128: the hd-256 body needs one wave per SIMD)
   const bool wide = M * Hkv <= 64;
 #define CAIN_ATTN_CASE(HDV)                                                                                        \
   case HDV:                                                                                                      \
     return wide ? int(launch_attn<HDV, 8>(q, kc, vtc, slot, pos, part_o, part_ml, counters, out, ldo, M, H, Hkv,  \
-                                          T_max, nsplit, scale, st))                                             \
+                                          T_max, nsplit, scale, kv8, kscale, vscale, st))                        \
                 : int(launch_attn<HDV, 4>(q, kc, vtc, slot, pos, part_o, part_ml, counters, out, ldo, M, H, Hkv,  \
-                                          T_max, nsplit, scale, st));
+                                          T_max, nsplit, scale, kv8, kscale, vscale, st));
   switch (hd) {
     CAIN_ATTN_CASE(64)
     CAIN_ATTN_CASE(96)
     CAIN_ATTN_CASE(128)
-    case 256: return int(launch_attn<256, 4>(q, kc, vtc, slot, pos, part_o, part_ml, counters, out, ldo, M, H, Hkv, T_max, nsplit, scale, st));
+    case 256:
+      return int(launch_attn<256, 4>(q, kc, vtc, slot, pos, part_o, part_ml, counters, out, ldo, M, H, Hkv, T_max,
+                                     nsplit, scale, kv8, kscale, vscale, st));
     default: return -1;
   }
 #undef CAIN_ATTN_CASE
+}
+
+CAIN_API int cain_attention(const void* q, const void* kc, const void* vtc, const int* slot, const int* pos,
+                            float* part_o, float* part_ml, unsigned* counters, void* out, int ldo, int M, int H,
+                            int Hkv, int hd, int T_max, int nsplit, float scale, hipStream_t st) {
+  return cain_attention_ex(q, kc, vtc, slot, pos, part_o, part_ml, counters, out, ldo, M, H, Hkv, hd, T_max, nsplit,
+                           scale, 0, 1.f, 1.f, st);
 }

@@ -951,6 +951,8 @@ CAIN_API int cain_skinny_gemm_ex(const void* Wp, const void* X, int ldx, int K, 
                                  const float* bias, int norm, float eps, const int* slot, const int* pos,
                                  const float* cos_t, const float* sin_t, void* kc, void* vtc, int H, int Hkv, int hd,
                                  int T_max, int epi, int waves, hipStream_t st) {
+  const int kv8 = (epi & EPI_KV_FP8) ? 1 : 0;
+  epi &= EPI_MASK;
   GemmArgs a{};
   a.Wp = reinterpret_cast<const bf16x8*>(Wp);
   a.X = reinterpret_cast<const __bf16*>(X);
@@ -958,7 +960,7 @@ CAIN_API int cain_skinny_gemm_ex(const void* Wp, const void* X, int ldx, int K, 
   a.eps = eps;
   a.slot = slot, a.pos = pos, a.cos_t = cos_t, a.sin_t = sin_t;
   a.kc = reinterpret_cast<__bf16*>(kc), a.vtc = reinterpret_cast<__bf16*>(vtc);
-  a.H = H, a.Hkv = Hkv, a.hd = hd, a.T_max = T_max;
+  a.H = H, a.Hkv = Hkv, a.hd = hd, a.T_max = T_max, a.kv8 = kv8;
   if (epi == EPI_QKV_ROPE && (hd % 16 || (hd / 2) % 8)) return -1;
   return gemm_dispatch(a, epi, norm != 0, waves, st);
 }
@@ -968,7 +970,8 @@ CAIN_API int cain_skinny_gemm_ex(const void* Wp, const void* X, int ldx, int K, 
 CAIN_API int cain_gemm(const void* Wp, const void* X, int ldx, int K, int N, int M, void* Y, int ldy,
                        const float* bias, int norm, float eps, const int* slot, const int* pos,
                        const float* cos_t, const float* sin_t, void* kc, void* vtc, int H, int Hkv, int hd, int T_max,
-                       void* ws, long long ws_bytes, int epi, int waves, hipStream_t st) {
+                       void* ws, long long ws_bytes, int epi_flags, int waves, hipStream_t st) {
+  const int epi = epi_flags & EPI_MASK, kv8 = (epi_flags & EPI_KV_FP8) ? 1 : 0;
   if (ws && cain_wgemm_eligible(N, K, M) && ws_bytes >= (long long)BG_COUNTER_BYTES) {
     if (epi == EPI_QKV_ROPE && (hd % 16 || (hd / 2) % 8)) return -1;
     GemmArgs a{};
@@ -978,7 +981,7 @@ CAIN_API int cain_gemm(const void* Wp, const void* X, int ldx, int K, int N, int
     a.eps = eps;
     a.slot = slot, a.pos = pos, a.cos_t = cos_t, a.sin_t = sin_t;
     a.kc = reinterpret_cast<__bf16*>(kc), a.vtc = reinterpret_cast<__bf16*>(vtc);
-    a.H = H, a.Hkv = Hkv, a.hd = hd, a.T_max = T_max;
+    a.H = H, a.Hkv = Hkv, a.hd = hd, a.T_max = T_max, a.kv8 = kv8;
     // the batched path's counters (first BG_COUNTER_BYTES) must stay zero: the slabs go after them
     const int rc = wgemm_dispatch(a, epi, norm != 0, static_cast<char*>(ws) + BG_COUNTER_BYTES,
                                   ws_bytes - (long long)BG_COUNTER_BYTES, st);
@@ -994,12 +997,12 @@ CAIN_API int cain_gemm(const void* Wp, const void* X, int ldx, int K, int N, int
       a.eps = eps;
       a.slot = slot, a.pos = pos, a.cos_t = cos_t, a.sin_t = sin_t;
       a.kc = reinterpret_cast<__bf16*>(kc), a.vtc = reinterpret_cast<__bf16*>(vtc);
-      a.H = H, a.Hkv = Hkv, a.hd = hd, a.T_max = T_max;
+      a.H = H, a.Hkv = Hkv, a.hd = hd, a.T_max = T_max, a.kv8 = kv8;
       if (epi == EPI_QKV_ROPE && (hd % 16 || (hd / 2) % 8)) return -1;
       return bgemm_dispatch(a, epi, norm != 0, p, ws, st);
     }
   }
   return cain_skinny_gemm_ex(Wp, X, ldx, K, N, M, Y, ldy, bias, norm, eps, slot, pos, cos_t, sin_t, kc, vtc, H, Hkv,
-                             hd, T_max, epi, waves, st);
+                             hd, T_max, epi_flags, waves, st);
 }
 

@@ -4,6 +4,17 @@
 #include "common.h"
 
 enum { EPI_BF16 = 0, EPI_RESID = 1, EPI_F32 = 2, EPI_SILU = 3, EPI_GELU = 4, EPI_QKV_ROPE = 5 };
+// flag or-ed into the epilogue id at the C entries: EPI_QKV_ROPE writes an fp8 (e4m3) KV cache
+constexpr int EPI_KV_FP8 = 0x100;
+constexpr int EPI_MASK = 0xff;
+
+// fp8 e4m3 (OCP, gfx950) KV-cache elements: saturate to +-448, then v_cvt_pk_fp8_f32 (RNE)
+__device__ __forceinline__ float fp8_sat(float v) { return fminf(fmaxf(v, -448.f), 448.f); }
+__device__ __forceinline__ uint32_t fp8x4(float a, float b, float c, float d) {
+  int p = __builtin_amdgcn_cvt_pk_fp8_f32(fp8_sat(a), fp8_sat(b), 0, false);
+  p = __builtin_amdgcn_cvt_pk_fp8_f32(fp8_sat(c), fp8_sat(d), p, true);
+  return uint32_t(p);
+}
 
 struct GemmArgs {
   const bf16x8* Wp;
@@ -20,9 +31,10 @@ struct GemmArgs {
   const int* pos;
   const float* cos_t;
   const float* sin_t;
-  __bf16* kc;
+  __bf16* kc;   // bf16 caches; with kv8, the same element offsets in bytes (fp8 e4m3)
   __bf16* vtc;
   int H, Hkv, hd, T_max;
+  int kv8;
 };
 
 // Epilogue inputs of one (tile, column-tile, lane) unit, loaded BEFORE the main loop
@@ -117,19 +129,38 @@ __device__ __forceinline__ void epi_store(const GemmArgs& a, int gt, int m, int 
           *reinterpret_cast<bf16x4*>(dst + j0 + half) = y2;
         } else {
           // fragment-major K cache (attention.hip): 4 consecutive head dims of one position are contiguous
-          __bf16* kb = a.kc + ((size_t)sl * a.Hkv + (head - a.H)) * a.T_max * a.hd;
-          *reinterpret_cast<bf16x4*>(kb + kfrag_off(e.p, j0, a.hd)) = y1;
-          *reinterpret_cast<bf16x4*>(kb + kfrag_off(e.p, j0 + half, a.hd)) = y2;
+          const size_t base = ((size_t)sl * a.Hkv + (head - a.H)) * a.T_max * a.hd;
+          if (a.kv8) {  // the bf16-rounded values, as e4m3: one dword per 4 head dims
+            uint8_t* kb = reinterpret_cast<uint8_t*>(a.kc) + base;
+            *reinterpret_cast<uint32_t*>(kb + kfrag_off(e.p, j0, a.hd)) =
+                fp8x4(bf2f(y1[0]), bf2f(y1[1]), bf2f(y1[2]), bf2f(y1[3]));
+            *reinterpret_cast<uint32_t*>(kb + kfrag_off(e.p, j0 + half, a.hd)) =
+                fp8x4(bf2f(y2[0]), bf2f(y2[1]), bf2f(y2[2]), bf2f(y2[3]));
+          } else {
+            __bf16* kb = a.kc + base;
+            *reinterpret_cast<bf16x4*>(kb + kfrag_off(e.p, j0, a.hd)) = y1;
+            *reinterpret_cast<bf16x4*>(kb + kfrag_off(e.p, j0 + half, a.hd)) = y2;
+          }
         }
       }
     } else if (sl >= 0) {
       const f32x4 v = get(0);
       const int vr = (gt - qt - kt) * 16 + nsub;  // row within the V block
       const int kh = vr / a.hd, d = vr - (vr / a.hd) * a.hd;
-      // fragment-major V^T cache: head dims d..d+3 of position p sit in consecutive lanes (16 B apart)
-      __bf16* dst = a.vtc + ((size_t)sl * a.Hkv + kh) * a.hd * a.T_max + vfrag_off(e.p, d, a.hd);
+      // fragment-major V^T cache: head dims d..d+3 of position p sit in consecutive lanes (8 elements apart)
+      const size_t off = ((size_t)sl * a.Hkv + kh) * a.hd * a.T_max + vfrag_off(e.p, d, a.hd);
+      if (a.kv8) {
+        uint8_t* dst = reinterpret_cast<uint8_t*>(a.vtc) + off;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) dst[i * 8] = f2bf(v[i] + e.b1[i]);
+        for (int i = 0; i < 4; ++i) {
+          const int p8 = __builtin_amdgcn_cvt_pk_fp8_f32(fp8_sat(bf2f(f2bf(v[i] + e.b1[i]))), 0.f, 0, false);
+          dst[i * 8] = uint8_t(p8 & 0xff);
+        }
+      } else {
+        __bf16* dst = a.vtc + off;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) dst[i * 8] = f2bf(v[i] + e.b1[i]);
+      }
     }
   } else {
     const f32x4 v = get(0);

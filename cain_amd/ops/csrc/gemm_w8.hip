@@ -230,7 +230,8 @@ static int env_int(const char* name, int dflt) {
 CAIN_API int cain_gemm_w8(const void* Wp, const float* wscale, const void* X, int ldx, int K, int N, int M, void* Y,
                           int ldy, const float* bias, int norm, float eps, const int* slot, const int* pos,
                           const float* cos_t, const float* sin_t, void* kc, void* vtc, int H, int Hkv, int hd,
-                          int T_max, int epi, hipStream_t st) {
+                          int T_max, int epi_flags, hipStream_t st) {
+  const int epi = epi_flags & EPI_MASK;
   if (K % 64 || N % 16 || M < 1 || M > 64) return -1;
   if (epi == EPI_QKV_ROPE && (hd % 16 || (hd / 2) % 8)) return -1;
   GemmArgs a{};
@@ -240,8 +241,8 @@ CAIN_API int cain_gemm_w8(const void* Wp, const float* wscale, const void* X, in
   a.eps = eps;
   a.slot = slot, a.pos = pos, a.cos_t = cos_t, a.sin_t = sin_t;
   a.kc = reinterpret_cast<__bf16*>(kc), a.vtc = reinterpret_cast<__bf16*>(vtc);
-  a.H = H, a.Hkv = Hkv, a.hd = hd, a.T_max = T_max;
-  // tuning overrides (tools/sweep_r1*.sh): CAIN_W8_WAVES, CAIN_W8_U, CAIN_W8_NT, CAIN_W8_NB
+  a.H = H, a.Hkv = Hkv, a.hd = hd, a.T_max = T_max, a.kv8 = (epi_flags & EPI_KV_FP8) ? 1 : 0;
+  // tuning overrides (tools/sweep.py --env): CAIN_W8_WAVES, CAIN_W8_U, CAIN_W8_NT, CAIN_W8_NB
   static const int f_w = env_int("CAIN_W8_WAVES", 0), f_u = env_int("CAIN_W8_U", 0), f_nt = env_int("CAIN_W8_NT", 0),
                    f_nb = env_int("CAIN_W8_NB", 0);
   const int nb = f_nb ? (f_nb >= 2 ? 2 : 1) : (M > 16 ? 2 : 1);

@@ -40,6 +40,10 @@ CAIN_API int cain_rownorm(const void* x, int ldx, int d, float eps, void* xn, in
 CAIN_API int cain_rownorm_act(const void* x, int ldx, int d, float eps, int norm, const void* gu, int ldgu, void* act,
                               int ldact, int M, int ffn, int kind, hipStream_t st);
 CAIN_API int cain_embed(const int* tok, const void* E, void* out, int ldo, int M, int d, float scale, hipStream_t st);
+CAIN_API int cain_attention_ex(const void* q, const void* kc, const void* vtc, const int* slot, const int* pos,
+                               float* part_o, float* part_ml, unsigned* counters, void* out, int ldo, int M, int H,
+                               int Hkv, int hd, int T_max, int nsplit, float scale, int kv8, float kscale,
+                               float vscale, hipStream_t st);
 CAIN_API int cain_attention(const void* q, const void* kc, const void* vtc, const int* slot, const int* pos,
                             float* part_o, float* part_ml, unsigned* counters, void* out, int ldo, int M, int H,
                             int Hkv, int hd, int T_max, int nsplit, float scale, hipStream_t st);
@@ -74,7 +78,7 @@ struct CainPlanDesc {
   const void* embed;
   const void* lm_head;
   const CainLayer* layers;
-  void* kcache;  // [L][S][Hkv][T_max][hd]
+  void* kcache;  // [L][S][Hkv][T_max][hd] fragment-major, bf16 (kv8: e4m3)
   void* vtcache; // [L][S][Hkv][hd][T_max]
   long long kv_layer_elems;
   const float* cos_t;
@@ -101,6 +105,9 @@ struct CainPlanDesc {
   // (plain row-major [V, d] bf16, gain folded, fp32 logits) through hipBLASLt; the hand GEMM is the fallback
   const void* lm_head_lt;
   void* xn;
+  // 1: the KV caches hold fp8 e4m3 elements (same fragment-major offsets, one byte each, unscaled and
+  // saturated at +-448): the QKV epilogue writes them (gemm_epi.h EPI_KV_FP8), attention widens them
+  int kv8;
 };
 
 struct CainRows {
@@ -167,11 +174,13 @@ int forward(const Plan& p, int M, const CainRows& r, int want_logits, int want_s
   CK(cain_embed(r.tok, d.embed, d.x, d.d, M, d.d, d.embed_scale, st));
   for (int l = 0; l < d.n_layers; ++l) {
     const CainLayer& L = p.layers[l];
-    __bf16* kc = reinterpret_cast<__bf16*>(d.kcache) + (size_t)l * d.kv_layer_elems;
-    __bf16* vc = reinterpret_cast<__bf16*>(d.vtcache) + (size_t)l * d.kv_layer_elems;
-    CK(gemm(L.wqkv, L.sqkv, d.x, d.d, d.d, qkv_dim, d.q, q_dim, L.bqkv, 1, kc, vc, /*EPI_QKV_ROPE*/ 5));
-    CK(cain_attention(d.q, kc, vc, r.slot, r.pos, d.part_o, d.part_ml, d.counters, d.attn, q_dim, M, d.H, d.Hkv,
-                      d.hd, d.T_max, d.nsplit, d.attn_scale, st));
+    const size_t kv_off = (size_t)l * d.kv_layer_elems * (d.kv8 ? 1 : 2);  // bytes
+    char* kc = static_cast<char*>(d.kcache) + kv_off;
+    char* vc = static_cast<char*>(d.vtcache) + kv_off;
+    CK(gemm(L.wqkv, L.sqkv, d.x, d.d, d.d, qkv_dim, d.q, q_dim, L.bqkv, 1, kc, vc,
+            /*EPI_QKV_ROPE*/ 5 | (d.kv8 ? /*EPI_KV_FP8*/ 0x100 : 0)));
+    CK(cain_attention_ex(d.q, kc, vc, r.slot, r.pos, d.part_o, d.part_ml, d.counters, d.attn, q_dim, M, d.H, d.Hkv,
+                         d.hd, d.T_max, d.nsplit, d.attn_scale, d.kv8, 1.f, 1.f, st));
     if (lt && L.wo_lt)
       CK(cain_lt_gemm(L.wo_lt, d.attn, q_dim, q_dim, d.d, M, d.x, d.d, 1, d.lt_ws, d.lt_ws_bytes, st));
     else

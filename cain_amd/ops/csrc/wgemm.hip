@@ -400,6 +400,25 @@ int wg_env(const char* name, int dflt) {
 // at least 4 stages per split.  Column-block counts >= 128 (gate/up, LM head) run unsplit.
 int g_wg_target = -1, g_wg_ksmax = -1;
 
+// Per-shape plan overrides (split count, ring variant) keyed by (N, K, row tile): written by the engine's start-up
+// autotune (ops.tune_wide_gemm times the candidates on the model's own weights) before any graph is captured.
+// The default split rule is a heuristic; measured on one box at 256 rows, the O projection (N = K = 4096) ran
+// 24.7 us at 6 splits against 29.4 at 8 and 29.5 at 4, and the best split and ring differ per shape.
+struct WgShape {
+  int N, K, bm, ks, variant;
+};
+constexpr int WG_MAX_SHAPES = 64;
+WgShape g_wg_shapes[WG_MAX_SHAPES];
+int g_wg_nshapes = 0;
+
+const WgShape* wg_shape(int N, int K, int bm) {
+  for (int i = 0; i < g_wg_nshapes; ++i) {
+    const WgShape& s = g_wg_shapes[i];
+    if (s.N == N && s.K == K && s.bm == bm) return &s;
+  }
+  return nullptr;
+}
+
 WgPlan wg_plan(int N, int K, int M) {
   if (g_wg_target < 0) g_wg_target = wg_env("CAIN_WGEMM_TARGET", 256);
   if (g_wg_ksmax < 0) g_wg_ksmax = wg_env("CAIN_WGEMM_KSMAX", 8);
@@ -409,6 +428,9 @@ WgPlan wg_plan(int N, int K, int M) {
   p.nblk = ((N >> 4) + WG_NT - 1) / WG_NT;
   const int stages = K / WG_BK;
   int ks = p.nblk >= 128 ? 1 : std::max(1, std::min(ksmax, (target + p.nblk / 2) / p.nblk));
+  if (const WgShape* o = wg_shape(N, K, p.bm)) {
+    if (o->ks > 0) ks = o->ks;
+  }
   ks = std::min(ks, std::max(1, stages / 4));
   p.kst = (stages + ks - 1) / ks;
   p.ks = (stages + p.kst - 1) / p.kst;
@@ -445,8 +467,12 @@ int g_wgemm_variant = -1;
 template <int BM, int EPI, bool NORM>
 hipError_t wg_launch_v(const GemmArgs& a, const WgArgs& w, const WgPlan& p, hipStream_t st) {
   if (g_wgemm_variant < 0) g_wgemm_variant = wg_env("CAIN_WGEMM_VARIANT", 0);
+  int variant = g_wgemm_variant;
+  if (const WgShape* o = wg_shape(a.N, a.K, BM)) {
+    if (o->variant >= 0) variant = o->variant;
+  }
   if constexpr (BM == 256) {  // X stage 32 KiB, W stage 16 KiB
-    switch (g_wgemm_variant) {
+    switch (variant) {
       case 1: return wg_launch<BM, 2, 3, EPI, NORM, 0>(a, w, p, st);     // MFMA waves load
       case 2: return wg_launch<BM, 2, 2, EPI, NORM, 4>(a, w, p, st);     // 144 KiB
       case 3: return wg_launch<BM, 1, 5, EPI, NORM, 4>(a, w, p, st);     // 160 KiB
@@ -455,7 +481,7 @@ hipError_t wg_launch_v(const GemmArgs& a, const WgArgs& w, const WgPlan& p, hipS
       default: return wg_launch<BM, 2, 3, EPI, NORM, 4>(a, w, p, st);    // 160 KiB
     }
   } else {  // X stage 16 KiB, W stage 16 KiB
-    switch (g_wgemm_variant) {
+    switch (variant) {
       case 1: return wg_launch<BM, 3, 5, EPI, NORM, 0>(a, w, p, st);
       case 2: return wg_launch<BM, 3, 3, EPI, NORM, 4>(a, w, p, st);     // 128 KiB
       case 3: return wg_launch<BM, 2, 6, EPI, NORM, 4>(a, w, p, st);     // 160 KiB
@@ -489,6 +515,30 @@ CAIN_API int cain_wgemm_min_m() {
 CAIN_API void cain_wgemm_set_min_m(int m) { g_wgemm_min_m = m; }
 CAIN_API void cain_wgemm_set_variant(int v) { g_wgemm_variant = v; }
 CAIN_API void cain_wgemm_set_split(int target, int ksmax) { g_wg_target = target, g_wg_ksmax = ksmax; }
+// Per-shape plan: split count (<= 0: the default rule) and ring variant (< 0: the global one) for GEMMs of N
+// columns over K with the bm-row tile (128 or 256).  Returns 0, or -1 when the table is full.
+CAIN_API int cain_wgemm_set_shape(int N, int K, int bm, int ks, int variant) {
+  for (int i = 0; i < g_wg_nshapes; ++i) {
+    WgShape& s = g_wg_shapes[i];
+    if (s.N == N && s.K == K && s.bm == bm) {
+      s.ks = ks, s.variant = variant;
+      return 0;
+    }
+  }
+  if (g_wg_nshapes == WG_MAX_SHAPES) return -1;
+  g_wg_shapes[g_wg_nshapes++] = WgShape{N, K, bm, ks, variant};
+  return 0;
+}
+CAIN_API void cain_wgemm_clear_shapes() { g_wg_nshapes = 0; }
+CAIN_API int cain_wgemm_eligible(int N, int K, int M);
+// The plan the next launch of this shape would use: ks * 16 + variant (tests, tools).
+CAIN_API int cain_wgemm_plan(int N, int K, int M) {
+  if (!cain_wgemm_eligible(N, K, M)) return -1;
+  const WgPlan p = wg_plan(N, K, M);
+  if (g_wgemm_variant < 0) g_wgemm_variant = wg_env("CAIN_WGEMM_VARIANT", 0);
+  const WgShape* o = wg_shape(N, K, p.bm);
+  return p.ks * 16 + (o && o->variant >= 0 ? o->variant : g_wgemm_variant);
+}
 
 CAIN_API int cain_wgemm_eligible(int N, int K, int M) {
   const int mm = cain_wgemm_min_m();

@@ -160,4 +160,4 @@ def test_fanout_one_rank_over_rccl(tmp_path):
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     assert "backend nccl" in r.stdout, r.stdout[-2000:]
     rows = list(csv.DictReader(open(tmp_path / "dp" / "run_table.csv")))
-    assert sum(x["__done"] == "DONE" for x in rows) == 11 and {x["rank"] for x in rows if x["rank"]} == {"0"}
+    assert sum(x["__done"] == "DONE" for x in rows) == 11 and {x["rank"].strip() for x in rows if x["rank"].strip()} == {"0"}

@@ -114,3 +114,34 @@ def test_wide_splitk_repeatable_after_batched_path(N, K, norm, epi):
         outs = [ops.skinny_gemm(wp, x, N, ops.EPI_F32, norm=norm, eps=1e-6) for _ in range(3)]
         assert rel_err(outs[0], ref) < 2e-3
     assert all(torch.equal(o, outs[0]) for o in outs)
+
+
+@pytest.mark.parametrize("ks,variant", [(3, 2), (6, 0), (16, 2), (1, 0)])
+def test_shape_plan_override(ks, variant):
+    """A per-shape plan (split count, ring variant) from the autotune table changes the launch, not the result."""
+    torch.manual_seed(ks)
+    N, K, M = 4096, 4096, 256
+    W = (torch.randn(N, K, device=DEV) * 0.02).bfloat16()
+    x = (2 * torch.randn(M, K, device=DEV)).bfloat16()
+    wp = pack_mfma_a(W)
+    ref = ops.skinny_gemm(wp, x, N, ops.EPI_F32, norm=True)
+    try:
+        ops.set_wide_gemm_plan(N, K, 256, ks, variant)
+        assert ops.wide_gemm_plan(N, K, M) == (ks, variant)
+        y = ops.skinny_gemm(wp, x, N, ops.EPI_F32, norm=True)
+    finally:
+        ops.clear_wide_gemm_plans()
+    assert rel_err(y, ref) < 1e-5
+
+
+def test_autotune_installs_a_plan_per_shape():
+    torch.manual_seed(1)
+    K, N = 4096, 4096
+    wps = [pack_mfma_a((torch.randn(N, K, device=DEV) * 0.02).bfloat16()) for _ in range(3)]
+    try:
+        res = ops.tune_wide_gemm([(N, K, ops.EPI_RESID, False, wps)], 256, iters=1)
+        assert len(res) == 1 and res[0]["candidates"]
+        assert ops.wide_gemm_plan(N, K, 256) == (res[0]["ks"], res[0]["variant"])
+        assert res[0]["us"] == min(res[0]["candidates"].values())
+    finally:
+        ops.clear_wide_gemm_plans()
