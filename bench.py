@@ -93,7 +93,7 @@ def main() -> int:
     ap.add_argument("--steps-per-graph", type=int, default=16)
     ap.add_argument("--no-energy", action="store_true")
     ap.add_argument("--weights", choices=("bf16", "fp8"), default="bf16",
-                    help="GEMM weight storage: bf16 (headline) or fp8 e4m3 per-row scaled (W8A16, batch <= 64)")
+                    help="GEMM weight storage: bf16 (headline) or fp8 e4m3 per-row scaled (W8A8 above 16 rows, W8A16 below)")
     ap.add_argument("--kv", choices=("bf16", "fp8"), default="bf16",
                     help="KV-cache storage: bf16 (headline) or fp8 e4m3 (half the attention bytes; separate config)")
     ap.add_argument("--device", choices=("cuda", "cpu"), default="cuda",
@@ -233,7 +233,9 @@ def main() -> int:
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": round(value / base_tps, 2) if base_tps else None,
-            "dtype": ("bf16" if ns.weights == "bf16" else "bf16 activations, fp8-e4m3 weights")
+            "dtype": ("bf16" if ns.weights == "bf16" else
+                      "fp8-e4m3 weights and per-row e4m3 GEMM activations (W8A8), bf16 elsewhere"
+                      if getattr(eng, "w8a8", False) else "bf16 activations, fp8-e4m3 weights")
                      + (", fp8-e4m3 KV cache" if ns.kv == "fp8" else ""),
             "device": "cpu (torch oracle)" if cpu else "MI355X",
             "data": "synthetic (reference topics.csv prompts, random-init weights)",

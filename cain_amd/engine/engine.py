@@ -44,7 +44,8 @@ OLLAMA_DEFAULTS = dict(temperature=0.8, top_k=40, top_p=0.9, repeat_penalty=1.1,
 
 MAX_ROWS = 256  # rows per forward: decode batch (runtime.hip CAIN_MAX_ROWS)
 PREFILL_ROWS = 128  # prompt tokens per prefill forward
-W8_MAX_ROWS = 64  # fp8-weight kernels (gemm_w8.hip): rows per forward, decode and prefill
+W8_MAX_ROWS = 64  # W8A16 fp8-weight kernels (gemm_w8.hip): rows per forward when W8A8 is off
+W8A8_MIN_ROWS = 16  # fp8 engines run forwards of more rows on the W8A8 wide kernel (csrc/wgemm8.hip)
 
 
 @dataclass
@@ -118,7 +119,7 @@ def lt_min_rows(max_batch: int, weight_dtype: str = "bf16") -> int:
 # ============================================================== ctypes structs
 class _CainLayer(ctypes.Structure):
     _fields_ = [(n, ctypes.c_void_p) for n in ("wqkv", "bqkv", "wo", "wgu", "wdown", "sqkv", "so", "sgu", "sdown",
-                                                  "wo_lt", "wgu_lt")]
+                                                  "wo_lt", "wgu_lt", "wqkv8", "wo8", "wgu8", "wdown8")]
 
 
 class _CainPlanDesc(ctypes.Structure):
@@ -132,7 +133,8 @@ class _CainPlanDesc(ctypes.Structure):
                 + [("gemm_ws_bytes", ctypes.c_longlong), ("w8", ctypes.c_int), ("lm_head_scale", ctypes.c_void_p)]
                 + [("lt_min_rows", ctypes.c_int), ("gu", ctypes.c_void_p), ("lt_ws", ctypes.c_void_p),
                    ("lt_ws_bytes", ctypes.c_longlong), ("lm_head_lt", ctypes.c_void_p), ("xn", ctypes.c_void_p)]
-                + [("kv8", ctypes.c_int)])
+                + [("kv8", ctypes.c_int), ("lm_head8", ctypes.c_void_p), ("x8", ctypes.c_void_p),
+                   ("xs", ctypes.c_void_p), ("x8_ld", ctypes.c_int)])
 
 
 class _CainRows(ctypes.Structure):
@@ -170,8 +172,10 @@ class DecodeEngine:
                  max_batch: int = 16, max_context: int = 2048, seed: int = 0, backend: Optional[str] = None,
                  steps_per_graph: int = 8, weights: Optional[ModelWeights] = None, tokenizer=None,
                  keep_natural: bool = False, weight_dtype: str = "bf16", kv_dtype: str = "bf16"):
-        """``weight_dtype="fp8"``: GEMM weights quantised per row to e4m3 (W8A16, half the weight bytes
-        per decode step -- the single-stream / small-batch option); limits rows per forward to 64.
+        """``weight_dtype="fp8"``: GEMM weights quantised per row to e4m3 (half the weight bytes per decode step):
+        forwards of up to 16 rows run W8A16 (gemm_w8.hip, bf16 activations), wider ones W8A8 (wgemm8.hip: the
+        activations quantised per row to e4m3, fp8 MFMA) up to 256 rows; CAIN_W8A8=0 keeps W8A16 only (<= 64
+        rows).
         ``kv_dtype="fp8"``: the KV cache holds e4m3 elements (half the attention bytes per decode step and half
         the cache memory; csrc/attention.hip KV8)."""
         self.cfg = get_config(model) if isinstance(model, str) else model
@@ -181,7 +185,10 @@ class DecodeEngine:
             raise ValueError(f"kv_dtype must be 'bf16' or 'fp8', got {kv_dtype!r}")
         self.weight_dtype = weight_dtype
         self.kv_dtype = kv_dtype
-        row_cap = W8_MAX_ROWS if weight_dtype == "fp8" else MAX_ROWS
+        # W8A8 needs whole 128-deep stages, >= 4 of them, on every GEMM's K (all real configs; not the tiny ones)
+        self.w8a8 = (weight_dtype == "fp8" and os.environ.get("CAIN_W8A8", "1") != "0"
+                     and all(k % 128 == 0 and k >= 512 for k in (self.cfg.d_model, self.cfg.q_dim, self.cfg.ffn)))
+        row_cap = W8_MAX_ROWS if weight_dtype == "fp8" and not self.w8a8 else MAX_ROWS
         self.device = torch.device(device)
         if backend is None:
             backend = "hip" if self.device.type == "cuda" else "torch"
@@ -224,8 +231,9 @@ class DecodeEngine:
         # 23 vs 39 us and 66 vs 103 us at 256 rows on llama3.1:8b, profiles/lt_gemm.md); it needs plain
         # row-major copies of those two weights beside the MFMA packing
         lt_rows = lt_min_rows(self.max_batch, self.weight_dtype)
+        w8a8 = self.w8a8 and max(self.max_batch, self.prefill_chunk) > W8A8_MIN_ROWS
         packed = pack_for_engine(self.weights, free_natural=not self.keep_natural, weight_dtype=self.weight_dtype,
-                                 plain_lt=lt_rows > 0,
+                                 plain_lt=lt_rows > 0, w8a8=w8a8,
                                  plain_lm_head=lt_rows > 0 and os.environ.get("CAIN_LT_LM_HEAD", "1") != "0")
         torch.cuda.synchronize(dev)
         S, T, L = self.max_batch, self.T_max, cfg.n_layers
@@ -261,7 +269,7 @@ class DecodeEngine:
         for i, lp in enumerate(packed["layers"]):
             self._layers[i] = _CainLayer(*(_ptr(lp.get(k)) for k in ("wqkv", "bqkv", "wo", "wgu", "wdown",
                                                                      "sqkv", "so", "sgu", "sdown", "wo_lt",
-                                                                     "wgu_lt")))
+                                                                     "wgu_lt", "wqkv8", "wo8", "wgu8", "wdown8")))
         self._packed = packed
         d = _CainPlanDesc()
         d.n_layers, d.d, d.H, d.Hkv, d.hd = L, cfg.d_model, cfg.n_heads, cfg.n_kv_heads, cfg.head_dim
@@ -284,6 +292,12 @@ class DecodeEngine:
         shapes = [(cfg.qkv_dim, cfg.d_model), (cfg.d_model, cfg.q_dim), (2 * cfg.ffn, cfg.d_model),
                   (cfg.d_model, cfg.ffn), (cfg.vocab, cfg.d_model)]
         ws = max([ops.gemm_ws_bytes(n, k, m) for n, k in shapes for m in range(17, R + 1)] + [0])
+        if w8a8:
+            ws = max([ws] + [int(self.lib.cain_w8a8_ws_bytes(n, k, m)) for n, k in shapes for m in range(17, R + 1)])
+            kmax = max(cfg.d_model, cfg.q_dim, cfg.ffn)
+            self.x8 = torch.zeros(R, kmax, device=dev, dtype=torch.uint8)
+            self.xs = torch.zeros(R, device=dev, dtype=torch.float32)
+            d.lm_head8, d.x8, d.xs, d.x8_ld = _ptr(packed.get("lm_head8")), _ptr(self.x8), _ptr(self.xs), kmax
         self.gemm_ws = torch.zeros(max(ws, 16) // 4 + 1, device=dev, dtype=torch.int32)
         d.gemm_ws, d.gemm_ws_bytes = _ptr(self.gemm_ws), ws
         d.w8, d.lm_head_scale = int(self.weight_dtype == "fp8"), _ptr(packed.get("lm_head_scale"))
@@ -346,7 +360,8 @@ class DecodeEngine:
         rc = self.lib.cain_plan_forward(ctypes.c_void_p(self._plan(M)), M, ctypes.byref(rs), int(want_logits),
                                         int(want_sample), ctypes.c_void_p(self.stream.cuda_stream))
         if rc != 0:
-            raise RuntimeError(f"cain_plan_forward failed rc={rc}")
+            where = self.lib.cain_plan_last_failure()
+            raise RuntimeError(f"cain_plan_forward failed rc={rc}" + (f" at {where.decode()}" if where else ""))
 
     def _graph(self, M: int, steps: int) -> int:
         key = (M, steps)

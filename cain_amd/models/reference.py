@@ -50,6 +50,14 @@ def fp8_kv_roundtrip(t: torch.Tensor) -> torch.Tensor:
     return t.to(torch.bfloat16).float().clamp(-448.0, 448.0).to(torch.float8_e4m3fn).float()
 
 
+def fp8_act_roundtrip(t: torch.Tensor) -> torch.Tensor:
+    """Per-row e4m3 quantisation of a bf16 GEMM input, widened: e4m3(x / s) * s with s = amax / 448."""
+    xb = t.to(torch.bfloat16).float()
+    amax = xb.abs().amax(-1, keepdim=True)
+    s = torch.where(amax > 0, amax / 448.0, torch.ones_like(amax))
+    return (xb / s).clamp(-448.0, 448.0).to(torch.float8_e4m3fn).float() * s
+
+
 class ReferenceModel:
     """Causal forward: tokens [B, T] → logits [B, T, V] (fp32).
 
@@ -58,12 +66,15 @@ class ReferenceModel:
     ``memo_weights`` keeps the compute-dtype copies of the weights (CPU serving: no per-call conversion)."""
 
     def __init__(self, mw: ModelWeights, compute_dtype=torch.float32, memo_weights: bool = False,
-                 kv_dtype: str = "bf16"):
+                 kv_dtype: str = "bf16", act_dtype: str = "bf16"):
         self.mw = mw
         self.cfg = mw.cfg
         self.dt = compute_dtype
         # "fp8": K (after RoPE) and V pass through bf16 -> e4m3 as the engine's fp8 KV cache stores them
         self.kv_fp8 = kv_dtype == "fp8"
+        # "fp8": every GEMM input is quantised per row to e4m3 as the W8A8 kernels do (ops/csrc/wgemm8.hip
+        # quant_rows_kernel: bf16 row, scale amax / 448; the RMSNorm factor from the unquantised row)
+        self.act_fp8 = act_dtype == "fp8"
         self._memo = {} if memo_weights else None
 
     def _w(self, t: torch.Tensor) -> torch.Tensor:
@@ -75,6 +86,17 @@ class ReferenceModel:
             w = self._memo[key] = t.to(self.dt)
         return w
 
+    def _in(self, t: torch.Tensor) -> torch.Tensor:
+        """A GEMM input as the kernels see it (per-row e4m3 with act_dtype="fp8")."""
+        return fp8_act_roundtrip(t).to(self.dt) if self.act_fp8 else t
+
+    def _norm_in(self, x: torch.Tensor, gain: torch.Tensor) -> torch.Tensor:
+        h = rms_norm(x, gain, self.cfg.norm_eps)
+        if self.act_fp8:  # quantised row times the exact RMSNorm factor of the bf16 row
+            xb = x.to(torch.bfloat16).float()
+            h = fp8_act_roundtrip(x) * torch.rsqrt(xb.pow(2).mean(-1, keepdim=True) + self.cfg.norm_eps) * gain.float()
+        return h.to(self.dt)
+
     def embed(self, tokens: torch.Tensor) -> torch.Tensor:
         x = self.mw.embed[tokens].to(self.dt)
         if self.cfg.embed_scale:
@@ -85,7 +107,7 @@ class ReferenceModel:
               cache: Optional[list] = None):
         cfg, lw = self.cfg, self.mw.layers[li]
         B, T, _ = x.shape
-        h = rms_norm(x, effective_gain(cfg, lw.attn_norm), cfg.norm_eps).to(self.dt)
+        h = self._norm_in(x, effective_gain(cfg, lw.attn_norm))
         qkv = h @ self._w(lw.wqkv).t()
         if lw.bqkv is not None:
             qkv = qkv + lw.bqkv.to(self.dt)
@@ -114,12 +136,12 @@ class ReferenceModel:
         mask = causal if attn_mask is None else causal & attn_mask
         att = att.masked_fill(~mask, float("-inf")).softmax(-1)
         o = torch.einsum("bhqk,bkhd->bqhd", att, v.float()).reshape(B, T, cfg.q_dim).to(self.dt)
-        x = x + (o @ self._w(lw.wo).t())
-        h = rms_norm(x, effective_gain(cfg, lw.mlp_norm), cfg.norm_eps).to(self.dt)
+        x = x + (self._in(o) @ self._w(lw.wo).t())
+        h = self._norm_in(x, effective_gain(cfg, lw.mlp_norm))
         g = h @ self._w(lw.w_gate).t()
         u = h @ self._w(lw.w_up).t()
         a = (activation(cfg, g.float()) * u.float()).to(self.dt)
-        return x + a @ self._w(lw.w_down).t()
+        return x + self._in(a) @ self._w(lw.w_down).t()
 
     @torch.no_grad()
     def forward(self, tokens: torch.Tensor, positions: Optional[torch.Tensor] = None,
@@ -133,7 +155,7 @@ class ReferenceModel:
             x = self.layer(x, li, positions, cache=cache)
         if last_only:
             x = x[:, -1:]
-        x = rms_norm(x, effective_gain(self.cfg, self.mw.final_norm), self.cfg.norm_eps).to(self.dt)
+        x = self._norm_in(x, effective_gain(self.cfg, self.mw.final_norm))
         return (x @ self._w(self.mw.lm_head).t()).float()
 
     @torch.no_grad()

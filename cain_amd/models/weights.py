@@ -84,6 +84,17 @@ def pack_mfma_a_fp8(q: torch.Tensor) -> torch.Tensor:
     return t.contiguous().reshape(n // 16, k // 64, 64, 16)
 
 
+def pack_mfma_a_fp8_k128(q: torch.Tensor) -> torch.Tensor:
+    """e4m3 [N, K] -> uint8 [N/16, K/64, 64, 16] for the W8A8 wide kernel (ops/csrc/wgemm8.hip): lane = g*16 + r
+    holds bytes j = element (16t + r, 64p + 16g + j); two consecutive 1-KiB blocks (p = 2s, 2s + 1) are the
+    32-B A operands of one v_mfma_scale_f32_16x16x128_f8f6f4 over k 128s .. 128s + 127."""
+    n, k = q.shape
+    if n % 16 or k % 128:
+        raise ValueError(f"pack_mfma_a_fp8_k128 needs N%16==0 and K%128==0, got {tuple(q.shape)}")
+    t = q.view(torch.uint8).reshape(n // 16, 16, k // 64, 4, 16)    # [t, r, p, g, j]
+    return t.permute(0, 2, 3, 1, 4).contiguous().reshape(n // 16, k // 64, 64, 16)
+
+
 def unpack_mfma_a_fp8(p: torch.Tensor) -> torch.Tensor:
     nt, kp = p.shape[0], p.shape[1]
     t = p.reshape(nt, kp, 4, 16, 2, 8).permute(0, 3, 1, 4, 2, 5)   # [t, r, p, h, g, j]
@@ -195,12 +206,13 @@ def fp8_roundtrip_weights(mw: ModelWeights) -> ModelWeights:
 
 
 def pack_for_engine(mw: ModelWeights, free_natural: bool = False, weight_dtype: str = "bf16",
-                    plain_lt: bool = False, plain_lm_head: bool = False) -> Dict[str, object]:
+                    plain_lt: bool = False, plain_lm_head: bool = False, w8a8: bool = False) -> Dict[str, object]:
     """Build the decode engine's packed tensors (see module doc); norm gains are folded into the GEMM
     weights they feed (attn_norm -> wqkv, mlp_norm -> gate/up, final_norm -> lm_head).
 
     ``weight_dtype="fp8"``: every GEMM weight (LM head included) is quantised per row after the gain
-    fold; each matrix entry becomes the fp8 packing and its scales are stored under ``s<name>``."""
+    fold; each matrix entry becomes the fp8 packing and its scales are stored under ``s<name>``.  With
+    ``w8a8`` the same e4m3 bytes are also stored in the W8A8 wide kernel's packing under ``<name>8``."""
     if weight_dtype not in ("bf16", "fp8"):
         raise ValueError(f"weight_dtype must be 'bf16' or 'fp8', got {weight_dtype!r}")
     cfg = mw.cfg
@@ -211,6 +223,8 @@ def pack_for_engine(mw: ModelWeights, free_natural: bool = False, weight_dtype: 
         if fp8:
             q, sc = quantize_fp8_rows(w)
             dst[name], dst["s" + name[1:]] = pack_mfma_a_fp8(q), sc
+            if w8a8:
+                dst[name + "8"] = pack_mfma_a_fp8_k128(q)
         else:
             dst[name] = pack_mfma_a(w)
 
@@ -238,6 +252,8 @@ def pack_for_engine(mw: ModelWeights, free_natural: bool = False, weight_dtype: 
     packed["lm_head"] = packed.pop("wlm_head")
     if fp8:
         packed["lm_head_scale"] = packed.pop("slm_head")
+        if w8a8:
+            packed["lm_head8"] = packed.pop("wlm_head8")
     if free_natural and not cfg.tie_embeddings:
         mw.lm_head = None
     mw.packed = packed

@@ -73,6 +73,12 @@ def load() -> ctypes.CDLL:
                                   + [ci] * 4 + [vp, ctypes.c_longlong, ci, ci, vp])
         lib.cain_gemm_w8.argtypes = ([vp, vp, vp, ci, ci, ci, ci, vp, ci, vp, ci, cf, vp, vp, vp, vp, vp, vp]
                                      + [ci] * 5 + [vp])
+        lib.cain_gemm_w8a8.argtypes = ([vp, vp, vp, ci, vp, ci, ci, ci, vp, ci, vp, vp, vp, vp, vp, vp, vp]
+                                       + [ci] * 4 + [vp, ctypes.c_longlong, ci, vp])
+        lib.cain_quant_rows.argtypes = [vp, ci, ci, ci, vp, ci, vp, ci, cf, vp]
+        lib.cain_w8a8_eligible.argtypes = [ci, ci, ci]
+        lib.cain_w8a8_ws_bytes.restype = ctypes.c_longlong
+        lib.cain_w8a8_ws_bytes.argtypes = [ci, ci, ci]
         lib.cain_gemm_ws_bytes.restype = ctypes.c_longlong
         lib.cain_gemm_ws_bytes.argtypes = [ci, ci, ci]
         lib.cain_wgemm_set_min_m.argtypes = [ci]
@@ -92,6 +98,7 @@ def load() -> ctypes.CDLL:
         lib.cain_plan_create.argtypes = [vp]
         lib.cain_plan_destroy.argtypes = [vp]
         lib.cain_plan_forward.argtypes = [vp, ci, vp, ci, ci, vp]
+        lib.cain_plan_last_failure.restype = ctypes.c_char_p
         lib.cain_plan_capture.restype = vp
         lib.cain_plan_capture.argtypes = [vp, ci, vp, ci, vp, ctypes.POINTER(ci)]
         lib.cain_graph_launch.argtypes = [vp, vp]
@@ -306,6 +313,56 @@ def gemm_w8(wq: torch.Tensor, scale: torch.Tensor, x: torch.Tensor, n: int, epi:
                           _p(r.get("sin_t")), _p(r.get("kc")), _p(r.get("vtc")), r.get("H", 0), r.get("Hkv", 0),
                           r.get("hd", 0), T_max, epi, _stream())
     _check(rc, "gemm_w8")
+    return out
+
+
+def quant_rows(x: torch.Tensor, norm: bool = False, eps: float = 1e-6):
+    """Per-row e4m3 quantisation of bf16 activations (csrc/wgemm8.hip quant_rows_kernel): returns (x8 uint8
+    [M, K], xs fp32 [M]) with x ~= e4m3(x8) * amax/448 and xs = amax/448 * (rsqrt(mean(x^2) + eps) if norm)."""
+    lib = load()
+    _gpu(x)
+    M, K = x.shape
+    assert x.dtype == torch.bfloat16 and x.stride(1) == 1
+    x8 = torch.empty(M, K, device=x.device, dtype=torch.uint8)
+    xs = torch.empty(M, device=x.device, dtype=torch.float32)
+    _check(lib.cain_quant_rows(_p(x), x.stride(0), K, M, _p(x8), K, _p(xs), int(bool(norm)), eps, _stream()),
+           "quant_rows")
+    return x8, xs
+
+
+def w8a8_eligible(n: int, k: int, m: int) -> bool:
+    return bool(load().cain_w8a8_eligible(n, k, m))
+
+
+def gemm_w8a8(wq8: torch.Tensor, scale: torch.Tensor, x: torch.Tensor, n: int, epi: int = EPI_BF16, bias=None,
+              out: Optional[torch.Tensor] = None, norm: bool = False, eps: float = 1e-6, rope=None) -> torch.Tensor:
+    """W8A8 wide GEMM (csrc/wgemm8.hip, 16 < M <= 256): the bf16 rows of ``x`` are quantised per row to e4m3
+    (``quant_rows``, the RMSNorm folded into the row scale when ``norm``), then y = epi(xs * scale * x8 . q^T)
+    with q packed by ``models.weights.pack_mfma_a_fp8_k128``.  Epilogues and ``rope`` as ``gemm_w8``."""
+    lib = load()
+    _gpu(wq8, scale, x)
+    M, K = x.shape
+    assert wq8.dtype == torch.uint8 and wq8.shape[0] * 16 == n and wq8.shape[1] * 64 == K, (tuple(wq8.shape), K, n)
+    assert w8a8_eligible(n, K, M), (n, K, M)
+    n_out = n // 2 if epi in (EPI_SILU, EPI_GELU) else n
+    if epi == EPI_RESID:
+        assert out is not None and out.shape == (M, n_out), "EPI_RESID updates `out` (the residual) in place"
+    if out is None:
+        out = torch.empty(M, n_out, device=x.device, dtype=torch.float32 if epi == EPI_F32 else torch.bfloat16)
+    x8, xs = quant_rows(x, norm, eps)
+    r = rope or {}
+    if epi == EPI_QKV_ROPE:
+        assert rope is not None, "EPI_QKV_ROPE needs the rope/cache arguments"
+        if is_fp8_cache(r["kc"]):
+            epi |= EPI_KV_FP8
+    T_max = r["kc"].shape[-2] if rope else 0
+    nbytes = int(lib.cain_w8a8_ws_bytes(n, K, M))
+    ws = _workspace(x.device, nbytes)
+    rc = lib.cain_gemm_w8a8(_p(wq8), _p(scale), _p(x8), K, _p(xs), K, n, M, _p(out), out.stride(0), _p(bias),
+                            _p(r.get("slot")), _p(r.get("pos")), _p(r.get("cos_t")), _p(r.get("sin_t")),
+                            _p(r.get("kc")), _p(r.get("vtc")), r.get("H", 0), r.get("Hkv", 0), r.get("hd", 0), T_max,
+                            _p(ws), nbytes, epi, _stream())
+    _check(rc, "gemm_w8a8")
     return out
 
 

@@ -16,6 +16,7 @@
 // the device, a whole generation is a handful of graph launches with no host
 // round trip per token (graph-replay floor instead of ~290 host launches per
 // token: MI355X_MICROARCH.md rows 'boundary', 'graph-replay-floor').
+#include <cstdio>
 #include <vector>
 
 #include "common.h"
@@ -36,6 +37,13 @@ CAIN_API int cain_lt_prepare(int N, int K, int M, int ldx, int ldy, int accumula
 CAIN_API int cain_lt_gemm_f32(const void* W, const void* X, int ldx, int K, int N, int M, float* Y, int ldy, void* ws,
                               long long ws_bytes, hipStream_t st);
 CAIN_API int cain_lt_prepare_f32(int N, int K, int M, int ldx, int ldy, long long ws_bytes);
+CAIN_API int cain_gemm_w8a8(const void* Wp8, const float* wscale, const void* X8, int ld8, const float* xs, int K,
+                            int N, int M, void* Y, int ldy, const float* bias, const int* slot, const int* pos,
+                            const float* cos_t, const float* sin_t, void* kc, void* vtc, int H, int Hkv, int hd,
+                            int T_max, void* ws, long long ws_bytes, int epi_flags, hipStream_t st);
+CAIN_API int cain_quant_rows(const void* x, int ldx, int K, int M, void* x8, int ld8, float* xs, int norm, float eps,
+                             hipStream_t st);
+CAIN_API int cain_w8a8_eligible(int N, int K, int M);
 CAIN_API int cain_rownorm(const void* x, int ldx, int d, float eps, void* xn, int ldxn, int M, hipStream_t st);
 CAIN_API int cain_rownorm_act(const void* x, int ldx, int d, float eps, int norm, const void* gu, int ldgu, void* act,
                               int ldact, int M, int ffn, int kind, hipStream_t st);
@@ -70,6 +78,11 @@ struct CainLayer {
   // the 8-row-interleaved gate/up [2 ffn, d]
   const void* wo_lt;
   const void* wgu_lt;
+  // fp8 weights in the W8A8 wide kernel's packing (wgemm8.hip; null: W8A16 only), same scales as above
+  const void* wqkv8;
+  const void* wo8;
+  const void* wgu8;
+  const void* wdown8;
 };
 
 struct CainPlanDesc {
@@ -108,6 +121,12 @@ struct CainPlanDesc {
   // 1: the KV caches hold fp8 e4m3 elements (same fragment-major offsets, one byte each, unscaled and
   // saturated at +-448): the QKV epilogue writes them (gemm_epi.h EPI_KV_FP8), attention widens them
   int kv8;
+  // W8A8 (w8 with the <name>8 packings): forwards of more than 16 rows quantise each GEMM input per row into
+  // x8 [Mpad][x8_ld] e4m3 + xs [Mpad] (wgemm8.hip quant_rows_kernel) and run the fp8-MFMA wide kernel
+  const void* lm_head8;
+  void* x8;
+  float* xs;
+  int x8_ld;
 };
 
 struct CainRows {
@@ -133,10 +152,16 @@ struct Plan {
   std::vector<CainLayer> layers;
 };
 
-#define CK(x)                     \
-  do {                            \
-    int _e = (x);                 \
-    if (_e != 0) return _e;       \
+// first failing call of the last failed forward (source text + line), for the Python error message
+thread_local char g_fail[160] = {0};
+
+#define CK(x)                                                                    \
+  do {                                                                           \
+    int _e = (x);                                                                \
+    if (_e != 0) {                                                               \
+      if (!g_fail[0]) snprintf(g_fail, sizeof(g_fail), "runtime.hip:%d %s", __LINE__, #x); \
+      return _e;                                                                 \
+    }                                                                            \
   } while (0)
 
 bool lt_rows(const CainPlanDesc& d, int M) { return d.lt_min_rows > 0 && M >= d.lt_min_rows && !d.w8 && d.gu; }
@@ -161,8 +186,14 @@ int forward(const Plan& p, int M, const CainRows& r, int want_logits, int want_s
   const int q_dim = d.H * d.hd;
   const int epi_act = d.act_kind == 1 ? 4 : 3;
   // one GEMM of the schedule: the bf16 kernels (gemm.hip) or the fp8-weight ones (gemm_w8.hip)
-  auto gemm = [&](const void* W, const float* ws, const void* X, int ldx, int K, int N, void* Y, int ldy,
-                  const float* bias, int norm, const void* kc, const void* vc, int epi) -> int {
+  auto gemm = [&](const void* W, const void* W8, const float* ws, const void* X, int ldx, int K, int N, void* Y,
+                  int ldy, const float* bias, int norm, const void* kc, const void* vc, int epi) -> int {
+    if (d.w8 && W8 && d.x8 && cain_w8a8_eligible(N, K, M)) {  // W8A8: per-row fp8 activations, fp8 MFMA
+      CK(cain_quant_rows(X, ldx, K, M, d.x8, d.x8_ld, d.xs, norm, d.eps, st));
+      return cain_gemm_w8a8(W8, ws, d.x8, d.x8_ld, d.xs, K, N, M, Y, ldy, bias, r.slot, r.pos, d.cos_t, d.sin_t,
+                            const_cast<void*>(kc), const_cast<void*>(vc), d.H, d.Hkv, d.hd, d.T_max, d.gemm_ws,
+                            d.gemm_ws_bytes, epi, st);
+    }
     if (d.w8)
       return cain_gemm_w8(W, ws, X, ldx, K, N, M, Y, ldy, bias, norm, d.eps, r.slot, r.pos, d.cos_t, d.sin_t,
                           const_cast<void*>(kc), const_cast<void*>(vc), d.H, d.Hkv, d.hd, d.T_max, epi, st);
@@ -177,21 +208,22 @@ int forward(const Plan& p, int M, const CainRows& r, int want_logits, int want_s
     const size_t kv_off = (size_t)l * d.kv_layer_elems * (d.kv8 ? 1 : 2);  // bytes
     char* kc = static_cast<char*>(d.kcache) + kv_off;
     char* vc = static_cast<char*>(d.vtcache) + kv_off;
-    CK(gemm(L.wqkv, L.sqkv, d.x, d.d, d.d, qkv_dim, d.q, q_dim, L.bqkv, 1, kc, vc,
+    CK(gemm(L.wqkv, L.wqkv8, L.sqkv, d.x, d.d, d.d, qkv_dim, d.q, q_dim, L.bqkv, 1, kc, vc,
             /*EPI_QKV_ROPE*/ 5 | (d.kv8 ? /*EPI_KV_FP8*/ 0x100 : 0)));
     CK(cain_attention_ex(d.q, kc, vc, r.slot, r.pos, d.part_o, d.part_ml, d.counters, d.attn, q_dim, M, d.H, d.Hkv,
                          d.hd, d.T_max, d.nsplit, d.attn_scale, d.kv8, 1.f, 1.f, st));
     if (lt && L.wo_lt)
       CK(cain_lt_gemm(L.wo_lt, d.attn, q_dim, q_dim, d.d, M, d.x, d.d, 1, d.lt_ws, d.lt_ws_bytes, st));
     else
-      CK(gemm(L.wo, L.so, d.attn, q_dim, q_dim, d.d, d.x, d.d, nullptr, 0, nullptr, nullptr, /*EPI_RESID*/ 1));
+      CK(gemm(L.wo, L.wo8, L.so, d.attn, q_dim, q_dim, d.d, d.x, d.d, nullptr, 0, nullptr, nullptr, /*EPI_RESID*/ 1));
     if (lt && L.wgu_lt) {
       CK(cain_lt_gemm(L.wgu_lt, d.x, d.d, d.d, 2 * d.ffn, M, d.gu, 2 * d.ffn, 0, d.lt_ws, d.lt_ws_bytes, st));
       CK(cain_rownorm_act(d.x, d.d, d.d, d.eps, 1, d.gu, 2 * d.ffn, d.act, d.ffn, M, d.ffn, d.act_kind, st));
     } else {
-      CK(gemm(L.wgu, L.sgu, d.x, d.d, d.d, 2 * d.ffn, d.act, d.ffn, nullptr, 1, nullptr, nullptr, epi_act));
+      CK(gemm(L.wgu, L.wgu8, L.sgu, d.x, d.d, d.d, 2 * d.ffn, d.act, d.ffn, nullptr, 1, nullptr, nullptr, epi_act));
     }
-    CK(gemm(L.wdown, L.sdown, d.act, d.ffn, d.ffn, d.d, d.x, d.d, nullptr, 0, nullptr, nullptr, /*EPI_RESID*/ 1));
+    CK(gemm(L.wdown, L.wdown8, L.sdown, d.act, d.ffn, d.ffn, d.d, d.x, d.d, nullptr, 0, nullptr, nullptr,
+            /*EPI_RESID*/ 1));
   }
   if (want_logits) {
     int e = -2;
@@ -200,8 +232,8 @@ int forward(const Plan& p, int M, const CainRows& r, int want_logits, int want_s
       e = cain_lt_gemm_f32(d.lm_head_lt, d.xn, d.d, d.d, d.V, M, d.logits, d.V, d.lt_ws, d.lt_ws_bytes, st);
       if (e > 0) CK(e);  // a library failure; no plan / unsupported shape (< 0) falls back
     }
-    if (e != 0) CK(gemm(d.lm_head, d.lm_head_scale, d.x, d.d, d.d, d.V, d.logits, d.V, nullptr, 1, nullptr, nullptr,
-            /*EPI_F32*/ 2));
+    if (e != 0) CK(gemm(d.lm_head, d.lm_head8, d.lm_head_scale, d.x, d.d, d.d, d.V, d.logits, d.V, nullptr, 1, nullptr,
+                        nullptr, /*EPI_F32*/ 2));
   }
   if (want_sample) {
     CK(cain_sample(d.logits, d.V, d.V, r.tok, r.pos, r.gen, r.ldg, r.n_gen, r.max_new, r.done, r.hist, r.slot,
@@ -224,10 +256,14 @@ CAIN_API void* cain_plan_create(const CainPlanDesc* desc) {
 
 CAIN_API void cain_plan_destroy(void* plan) { delete static_cast<Plan*>(plan); }
 
+CAIN_API const char* cain_plan_last_failure() { return g_fail; }
+
 CAIN_API int cain_plan_forward(void* plan, int M, const CainRows* rows, int want_logits, int want_sample,
                                hipStream_t st) {
   auto* p = static_cast<Plan*>(plan);
-  if (M < 1 || M > CAIN_MAX_ROWS || M > p->d.Mpad || (p->d.w8 && M > 64)) return -1;
+  g_fail[0] = 0;
+  // W8A16 alone (no W8A8 buffers) takes at most 64 rows
+  if (M < 1 || M > CAIN_MAX_ROWS || M > p->d.Mpad || (p->d.w8 && !p->d.x8 && M > 64)) return -1;
   return forward(*p, M, *rows, want_logits, want_sample, st);
 }
 
@@ -235,7 +271,7 @@ CAIN_API int cain_plan_forward(void* plan, int M, const CainRows* rows, int want
 CAIN_API void* cain_plan_capture(void* plan, int M, const CainRows* rows, int steps, hipStream_t st, int* err) {
   auto* p = static_cast<Plan*>(plan);
   *err = 0;
-  if (M < 1 || M > CAIN_MAX_ROWS || M > p->d.Mpad || (p->d.w8 && M > 64) || steps < 1) {
+  if (M < 1 || M > CAIN_MAX_ROWS || M > p->d.Mpad || (p->d.w8 && !p->d.x8 && M > 64) || steps < 1) {
     *err = -1;
     return nullptr;
   }

@@ -46,63 +46,9 @@
 
 #include "common.h"
 #include "gemm_epi.h"
+#include "wgemm_ring.h"
 
-namespace {
-
-typedef __attribute__((address_space(3))) void lds_void_t;
-typedef __attribute__((address_space(1))) const void gbl_void_t;
-
-constexpr int WG_NT = 8;    // output columns per workgroup: 8 tiles of 16
-constexpr int WG_BK = 64;   // k per ring stage (2 slices of 32)
-
-template <int BM>
-struct WgGeo {
-  static constexpr int WM = BM == 256 ? 4 : 2;  // waves along M
-  static constexpr int WN = 8 / WM;             // waves along N
-  static constexpr int MB = BM / 16 / WM;       // 16-row blocks per wave
-  static constexpr int TN = WG_NT / WN;         // 16-column tiles per wave
-  static constexpr int W_BYTES = WG_NT * 2 * 1024;  // one W stage: 8 tiles x 2 slices of 1 KiB
-  static constexpr int X_BYTES = BM * WG_BK * 2;    // one X stage: BM rows x 128 B
-  static constexpr int XPW = BM / 8 / 8;        // X LDS-DMA instructions per wave per stage (8 rows each)
-  static constexpr int RB = BM / 16;            // row blocks per tile (split-K slab units)
-};
-
-template <int N>
-__device__ __forceinline__ void wait_vmcnt() {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-// wave-uniform runtime count (the pipeline tail issues fewer stages): one uniform branch per value
-template <int N = 0>
-__device__ __forceinline__ void wait_vmcnt_rt(int n) {
-  if constexpr (N >= 30) {
-    wait_vmcnt<N>();
-  } else {
-    if (n <= N) wait_vmcnt<N>();
-    else wait_vmcnt_rt<N + 1>(n);
-  }
-}
-
-// every wave's LDS-DMA of the stage being consumed has landed (its own counted wait before this), and every
-// wave has finished reading the slot about to be refilled
-__device__ __forceinline__ void ring_barrier() {
-  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-}
-
-__device__ __forceinline__ void glds16(const void* src, char* lds_wave_base, int aux_nt) {
-  if (aux_nt)
-    __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)lds_wave_base, 16, 0, 2);
-  else
-    __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)lds_wave_base, 16, 0, 0);
-}
-
-}  // namespace
-
-struct WgArgs {
-  int ks;           // k-splits (workgroups per column block)
-  int kst;          // ring stages (64-deep k-steps) per split
-  float* part;      // [ks][n_units][64 lanes] f32x4 (ks > 1)
-  float* part_ss;   // [nblk][ks][BM] per-row partial sums of squares (ks > 1 && NORM)
-};
+using namespace wg;
 
 constexpr int WG_CTR_BYTES = 16 * 1024;  // the workspace region before the slabs (gemm.hip WG_COUNTER_BYTES)
 
@@ -390,11 +336,6 @@ struct WgPlan {
   int bm, nblk, ks, kst;
   size_t part_floats, ss_floats;
 };
-
-int wg_env(const char* name, int dflt) {
-  const char* e = getenv(name);
-  return e ? atoi(e) : dflt;
-}
 
 // Split count: ~256 streaming workgroups (one per CU: the ring takes 128-144 KiB of LDS), at most 8 splits and
 // at least 4 stages per split.  Column-block counts >= 128 (gate/up, LM head) run unsplit.

@@ -41,3 +41,15 @@ def test_vcache_pack_roundtrip_and_offsets(hd):
         d, hq = lane & 15, lane >> 4
         want = torch.cat([v[0, 4 * hq: 4 * hq + 4, d], v[0, 16 + 4 * hq: 16 + 4 * hq + 4, d]])
         assert torch.equal(frag[lane], want)
+
+
+def test_pack_mfma_a_fp8_k128_layout():
+    """W8A8 packing: lane g*16 + r of block (t, p) holds W[16t + r][64p + 16g .. +15]."""
+    from cain_amd.models.weights import pack_mfma_a_fp8_k128
+    torch.manual_seed(0)
+    q = torch.randn(32, 256).to(torch.float8_e4m3fn)
+    p = pack_mfma_a_fp8_k128(q)
+    assert p.shape == (2, 4, 64, 16) and p.dtype == torch.uint8
+    u = q.view(torch.uint8)
+    for t, pp, g, r in [(0, 0, 0, 0), (1, 3, 2, 5), (0, 2, 3, 15), (1, 1, 1, 9)]:
+        assert torch.equal(p[t, pp, g * 16 + r], u[16 * t + r, 64 * pp + 16 * g: 64 * pp + 16 * g + 16])
