@@ -236,14 +236,18 @@ __global__ __launch_bounds__(64 * (8 + NDMA), (8 + NDMA) / 4) void wgemm_kernel(
       __builtin_amdgcn_sched_barrier(0);
       mfma_slice(0, a0, b0, [&] { read_slice(t, 1, a1, b1); });
       __builtin_amdgcn_sched_barrier(0);
-      if (t + 1 < nst) {
+      const bool more = t + 1 < nst;
+      if (more) {
         land(t + 1);
         ring_barrier();
         if constexpr (!NDMA) issue_step(t + 1);
-        read_slice(t + 1, 0, a0, b0);
       }
       __builtin_amdgcn_sched_barrier(0);
-      mfma_slice(1, a1, b1, [] {});
+      // the next stage's slice-0 reads go in after slice 1's first MFMA: issued before it, they made the
+      // compiler wait for them (lgkmcnt(0)) ahead of slice 1 as well
+      mfma_slice(1, a1, b1, [&] {
+        if (more) read_slice(t + 1, 0, a0, b0);
+      });
       __builtin_amdgcn_sched_barrier(0);
     }
   }
