@@ -37,6 +37,7 @@
 // barrier -> relaxed agent ticket; no release/acquire fences, counter reset by the
 // reducer: cdna_hip_programming.md §5 'In-launch split-K reduction'), so there
 // is no separate combine launch.
+#include <cstdlib>
 #include <type_traits>
 
 #include "common.h"
@@ -58,7 +59,7 @@ __device__ __forceinline__ bf16x8 fp8x8_to_bf16(u32x2 v, float sc) {
   return r;
 }
 
-template <int HD, int AW, bool KV8>
+template <int HD, int AW, bool KV8, bool NT_KV = true>
 __global__ __launch_bounds__(AW * 64) void attn_decode_kernel(
     const __bf16* __restrict__ q, const __bf16* __restrict__ kc, const __bf16* __restrict__ vtc,
     const int* __restrict__ slot, const int* __restrict__ pos, float* __restrict__ part_o,
@@ -106,16 +107,21 @@ __global__ __launch_bounds__(AW * 64) void attn_decode_kernel(
     constexpr int ESZ = KV8 ? 1 : 2;  // bytes per cache element
     const char* kbase = reinterpret_cast<const char*>(kc) + (((size_t)s * Hkv + kh) * T_max * HD + lane * 8) * ESZ;
     const char* vbase = reinterpret_cast<const char*>(vtc) + (((size_t)s * Hkv + kh) * HD * T_max + lane * 8) * ESZ;
+    // the caches stream once per step: non-temporal loads (MI355X_MICROARCH.md 'nt-weights': once-read bytes)
+    auto ld = [](const char* p) -> frag_t {
+      if constexpr (NT_KV) return __builtin_nontemporal_load(reinterpret_cast<const frag_t*>(p));
+      else return *reinterpret_cast<const frag_t*>(p);
+    };
     auto load_blk = [&](int blk, frag_t (&k_a)[NKS], frag_t (&k_b)[NKS], frag_t (&v)[NDT]) {
       const char* k0 = kbase + (size_t)blk * (2 * NKS * 512 * ESZ);
 #pragma unroll
       for (int i = 0; i < NKS; ++i) {
-        k_a[i] = *reinterpret_cast<const frag_t*>(k0 + i * 512 * ESZ);
-        k_b[i] = *reinterpret_cast<const frag_t*>(k0 + (NKS + i) * 512 * ESZ);
+        k_a[i] = ld(k0 + i * 512 * ESZ);
+        k_b[i] = ld(k0 + (NKS + i) * 512 * ESZ);
       }
       const char* v0 = vbase + (size_t)blk * (NDT * 512 * ESZ);
 #pragma unroll
-      for (int dt = 0; dt < NDT; ++dt) v[dt] = *reinterpret_cast<const frag_t*>(v0 + dt * 512 * ESZ);
+      for (int dt = 0; dt < NDT; ++dt) v[dt] = ld(v0 + dt * 512 * ESZ);
     };
     auto widen = [&](const frag_t& f, float sc) -> bf16x8 {
       if constexpr (KV8) return fp8x8_to_bf16(f, sc);
@@ -279,19 +285,42 @@ __global__ __launch_bounds__(AW * 64) void attn_decode_kernel(
   }
 }
 
+// CAIN_ATTN_NT=0: default-policy cache loads instead of non-temporal ones (A/B runs)
+static bool attn_nt() {
+  static const bool nt = [] {
+    const char* e = getenv("CAIN_ATTN_NT");
+    return !(e && e[0] == '0');
+  }();
+  return nt;
+}
+
+template <int HD, int AW, bool KV8, bool NT>
+static void launch_attn_t(const void* q, const void* kc, const void* vtc, const int* slot, const int* pos,
+                          float* part_o, float* part_ml, unsigned* counters, void* out, int ldo, int M, int H, int Hkv,
+                          int T_max, int nsplit, float scale, float kscale, float vscale, hipStream_t st) {
+  hipLaunchKernelGGL((attn_decode_kernel<HD, AW, KV8, NT>), dim3(M * Hkv, nsplit), dim3(AW * 64), 0, st,
+                     (const __bf16*)q, (const __bf16*)kc, (const __bf16*)vtc, slot, pos, part_o, part_ml, counters,
+                     (__bf16*)out, ldo, M, H, Hkv, T_max, nsplit, scale, kscale, vscale);
+}
+
 template <int HD, int AW>
 static hipError_t launch_attn(const void* q, const void* kc, const void* vtc, const int* slot, const int* pos,
                               float* part_o, float* part_ml, unsigned* counters, void* out, int ldo, int M, int H,
                               int Hkv, int T_max, int nsplit, float scale, int kv8, float kscale, float vscale,
                               hipStream_t st) {
-  if (kv8)
-    hipLaunchKernelGGL((attn_decode_kernel<HD, AW, true>), dim3(M * Hkv, nsplit), dim3(AW * 64), 0, st,
-                       (const __bf16*)q, (const __bf16*)kc, (const __bf16*)vtc, slot, pos, part_o, part_ml, counters,
-                       (__bf16*)out, ldo, M, H, Hkv, T_max, nsplit, scale, kscale, vscale);
+  const bool nt = attn_nt();
+  if (kv8 && nt)
+    launch_attn_t<HD, AW, true, true>(q, kc, vtc, slot, pos, part_o, part_ml, counters, out, ldo, M, H, Hkv, T_max,
+                                      nsplit, scale, kscale, vscale, st);
+  else if (kv8)
+    launch_attn_t<HD, AW, true, false>(q, kc, vtc, slot, pos, part_o, part_ml, counters, out, ldo, M, H, Hkv, T_max,
+                                       nsplit, scale, kscale, vscale, st);
+  else if (nt)
+    launch_attn_t<HD, AW, false, true>(q, kc, vtc, slot, pos, part_o, part_ml, counters, out, ldo, M, H, Hkv, T_max,
+                                       nsplit, scale, 1.f, 1.f, st);
   else
-    hipLaunchKernelGGL((attn_decode_kernel<HD, AW, false>), dim3(M * Hkv, nsplit), dim3(AW * 64), 0, st,
-                       (const __bf16*)q, (const __bf16*)kc, (const __bf16*)vtc, slot, pos, part_o, part_ml, counters,
-                       (__bf16*)out, ldo, M, H, Hkv, T_max, nsplit, scale, 1.f, 1.f);
+    launch_attn_t<HD, AW, false, false>(q, kc, vtc, slot, pos, part_o, part_ml, counters, out, ldo, M, H, Hkv, T_max,
+                                        nsplit, scale, 1.f, 1.f, st);
   return hipGetLastError();
 }
 
