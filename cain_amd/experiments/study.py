@@ -104,8 +104,10 @@ class StudySettings:
     # tracing: the on-device server records each generation with torch.profiler and the
     # Chrome trace is filed as run_dir/kernel_trace.json (adds profiler overhead to the measured window)
     trace: bool = False
-    # on-device weight storage: bf16, or fp8 (e4m3 per-row scaled weights, W8A16 kernels; max_batch <= 64)
+    # on-device weight storage: bf16, or fp8 (e4m3 per-row scaled weights; W8A8 above 16 rows, W8A16 below)
     weights: str = "bf16"
+    # on-device KV-cache storage: bf16, or fp8 (e4m3)
+    kv: str = "bf16"
 
     @classmethod
     def from_env(cls, base: Optional["StudySettings"] = None) -> "StudySettings":
@@ -299,6 +301,8 @@ class _StudyBase:
                 args.append("--preload")
             if s.weights != "bf16":
                 args += ["--weights", s.weights]
+            if s.kv != "bf16":
+                args += ["--kv", s.kv]
             if s.trace:
                 args += ["--trace-dir", str(self.results_output_path / s.name / "traces" / f"rank{self.rank}")]
             env = {}

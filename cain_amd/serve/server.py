@@ -99,8 +99,10 @@ class EngineBackend(Backend):
 
     def __init__(self, models: List[str], device: str = "cuda:0", max_batch: int = 16, max_context: int = 2048,
                  backend: Optional[str] = None, seed: int = 0, preload: bool = False, steps_per_graph: int = 8,
-                 trace_dir: Optional[str] = None, weight_dtype: str = "bf16", continuous: bool = True):
+                 trace_dir: Optional[str] = None, weight_dtype: str = "bf16", continuous: bool = True,
+                 kv_dtype: str = "bf16"):
         self._models = list(models)
+        self.kv_dtype = kv_dtype
         # continuous batching needs the HIP engine; tracing records whole static batches
         self.continuous = continuous and not trace_dir
         self.weight_dtype = weight_dtype
@@ -134,7 +136,8 @@ class EngineBackend(Backend):
                     raise KeyError(f"model '{model}' not found, try pulling it first")
                 eng = DecodeEngine(model, device=self.device, max_batch=self._max_batch,
                                    max_context=self.max_context, backend=self.backend, seed=self.seed,
-                                   steps_per_graph=self.steps_per_graph, weight_dtype=self.weight_dtype)
+                                   steps_per_graph=self.steps_per_graph, weight_dtype=self.weight_dtype,
+                                   kv_dtype=self.kv_dtype)
                 self.engines[model] = eng
             return eng
 
@@ -553,7 +556,8 @@ def main(argv: Optional[List[str]] = None) -> None:
     ap.add_argument("--fake-prefill-s", type=float, default=0.0, help="fake backend: modelled time to first token")
     ap.add_argument("--trace-dir", default=None, help="write a torch.profiler Chrome trace of every decode batch here")
     ap.add_argument("--weights", choices=["bf16", "fp8"], default="bf16",
-                    help="GEMM weight storage (fp8: e4m3 per-row scaled, W8A16 kernels, batch <= 64)")
+                    help="GEMM weight storage (fp8: e4m3 per-row scaled; W8A8 above 16 rows, W8A16 below)")
+    ap.add_argument("--kv", choices=["bf16", "fp8"], default="bf16", help="KV-cache storage (fp8: e4m3)")
     ap.add_argument("--static-batching", action="store_true",
                     help="batch requests that arrive within --batch-window-ms and run each batch to completion "
                          "(default on the HIP engine: continuous batching)")
@@ -568,7 +572,7 @@ def main(argv: Optional[List[str]] = None) -> None:
     else:
         be = EngineBackend(models, device=ns.device, max_batch=ns.max_batch, max_context=ns.max_context,
                            backend=ns.backend, preload=ns.preload, trace_dir=ns.trace_dir, weight_dtype=ns.weights,
-                           continuous=not ns.static_batching)
+                           continuous=not ns.static_batching, kv_dtype=ns.kv)
     srv = make_server(be, ns.host, ns.port, ns.batch_window_ms, ns.verbose)
     print(f"[serve] Ollama-compatible API on http://{ns.host}:{srv.server_address[1]} models={models}", flush=True)
     try:
@@ -586,8 +590,10 @@ def generate_main(argv: Optional[List[str]] = None) -> None:
     ap.add_argument("--device", default="cuda:0")
     ap.add_argument("--temperature", type=float, default=None)
     ap.add_argument("--seed", type=int, default=None)
+    ap.add_argument("--weights", choices=["bf16", "fp8"], default="bf16")
+    ap.add_argument("--kv", choices=["bf16", "fp8"], default="bf16")
     ns = ap.parse_args(argv)
-    be = EngineBackend([ns.model], device=ns.device, max_batch=1)
+    be = EngineBackend([ns.model], device=ns.device, max_batch=1, weight_dtype=ns.weights, kv_dtype=ns.kv)
     opts = {k: v for k, v in (("temperature", ns.temperature), ("seed", ns.seed)) if v is not None}
     job = Job(ns.model, ns.prompt, ns.num_predict or default_num_predict(ns.prompt), opts)
     be.run(ns.model, [job])
