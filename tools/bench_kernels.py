@@ -49,6 +49,7 @@ def main():
                     help="attention cases M:L (rows : context length)")
     ap.add_argument("--attn-splits", default="auto", help="comma list of split counts ('auto' = the engine's)")
     ap.add_argument("--attn-tmax", type=int, default=1536)
+    ap.add_argument("--attn-kv", choices=("bf16", "fp8"), default="bf16", help="KV-cache element type")
     ns = ap.parse_args()
     cfg = get_config(ns.model)
     dev = torch.device("cuda")
@@ -105,6 +106,10 @@ def main():
         M, L = (int(x) for x in case.split(":"))
         kc = torch.randn(M, cfg.n_kv_heads, T_max, cfg.head_dim, device=dev).bfloat16()
         vt = torch.randn(M, cfg.n_kv_heads, cfg.head_dim, T_max, device=dev).bfloat16()
+        esz = 2
+        if ns.attn_kv == "fp8":  # e4m3 bytes (uint8 storage selects the kernel's fp8 path)
+            kc, vt = kc.to(torch.float8_e4m3fn).view(torch.uint8), vt.to(torch.float8_e4m3fn).view(torch.uint8)
+            esz = 1
         q = torch.randn(M, cfg.q_dim, device=dev).bfloat16()
         slot = torch.arange(M, device=dev, dtype=torch.int32)
         pos = torch.full((M,), L - 1, device=dev, dtype=torch.int32)
@@ -117,8 +122,8 @@ def main():
             us = timeit(lambda: ops.attention(q, kc, vt, slot, pos, cfg.n_heads, cfg.n_kv_heads, cfg.head_dim, ns_,
                                               1 / math.sqrt(cfg.head_dim), out=out, part_o=po, part_ml=pm,
                                               counters=cnt))
-            kv_bytes = 2 * M * cfg.n_kv_heads * L * cfg.head_dim * 2
-            r = dict(kind="attention", model=cfg.name, M=M, L=L, T_max=T_max, nsplit=ns_, split_arg=sp,
+            kv_bytes = 2 * M * cfg.n_kv_heads * L * cfg.head_dim * esz
+            r = dict(kind="attention", model=cfg.name, kv=ns.attn_kv, M=M, L=L, T_max=T_max, nsplit=ns_, split_arg=sp,
                      us=round(us, 2), TBps=round(kv_bytes / us / 1e6, 3))
             res.append(r)
             print(json.dumps(r), flush=True)
