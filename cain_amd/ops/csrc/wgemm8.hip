@@ -233,25 +233,37 @@ __global__ __launch_bounds__(256) void wgemm8_reduce_kernel(const GemmArgs a, co
 
 // Per-row fp8 quantisation of bf16 activations: x8 = e4m3(x / s), s = amax / 448; xs = s * (norm ?
 // rsqrt(mean(x^2) + eps) : 1) -- the RMSNorm of the bf16 rows folded into the row scale (gain in W).
-// One 256-thread workgroup per row, 8 elements per thread and pass (K % 8 == 0).
-__global__ __launch_bounds__(256) void quant_rows_kernel(const __bf16* __restrict__ x, int ldx, int K,
-                                                         uint8_t* __restrict__ x8, int ld8, float* __restrict__ xs,
-                                                         int norm, float eps) {
+// One 256-thread workgroup per row; the row stays in registers between the statistics and the store (one read
+// of the row: a second pass over it cost a second L2 round trip in a launch this short).  K % 8 == 0,
+// K <= QR_MAXK.
+constexpr int QR_THREADS = 256, QR_CHUNKS = 12;  // 16-B chunks per thread
+constexpr int QR_MAXK = QR_THREADS * QR_CHUNKS * 8;  // 24,576 = gemma:7b's ffn, the widest GEMM input
+__global__ __launch_bounds__(QR_THREADS) void quant_rows_kernel(const __bf16* __restrict__ x, int ldx, int K,
+                                                                uint8_t* __restrict__ x8, int ld8,
+                                                                float* __restrict__ xs, int norm, float eps) {
   const int m = blockIdx.x;
   const __bf16* row = x + (size_t)m * ldx;
-  float amax = 0.f, ss = 0.f;
-  for (int k = threadIdx.x * 8; k < K; k += 256 * 8) {
-    const bf16x8 v = *reinterpret_cast<const bf16x8*>(row + k);
+  bf16x8 v[QR_CHUNKS];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float f = bf2f(v[j]);
-      amax = fmaxf(amax, fabsf(f));
-      ss += f * f;
+  for (int c = 0; c < QR_CHUNKS; ++c) {
+    const int k = (c * QR_THREADS + threadIdx.x) * 8;
+    if (k < K) v[c] = *reinterpret_cast<const bf16x8*>(row + k);
+  }
+  float amax = 0.f, ss = 0.f;
+#pragma unroll
+  for (int c = 0; c < QR_CHUNKS; ++c) {
+    if ((c * QR_THREADS + threadIdx.x) * 8 < K) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float f = bf2f(v[c][j]);
+        amax = fmaxf(amax, fabsf(f));
+        ss += f * f;
+      }
     }
   }
   amax = wave_max(amax);
   ss = wave_sum(ss);
-  __shared__ float s_a[4], s_s[4];
+  __shared__ float s_a[QR_THREADS / 64], s_s[QR_THREADS / 64];
   const int wave = threadIdx.x >> 6;
   if ((threadIdx.x & 63) == 0) s_a[wave] = amax, s_s[wave] = ss;
   __syncthreads();
@@ -260,13 +272,16 @@ __global__ __launch_bounds__(256) void quant_rows_kernel(const __bf16* __restric
   const float scale = amax > 0.f ? amax / 448.f : 1.f;
   const float inv = 1.f / scale;
   uint8_t* orow = x8 + (size_t)m * ld8;
-  for (int k = threadIdx.x * 8; k < K; k += 256 * 8) {
-    const bf16x8 v = *reinterpret_cast<const bf16x8*>(row + k);
-    typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
-    u32x2_t o;
-    o[0] = fp8x4(bf2f(v[0]) * inv, bf2f(v[1]) * inv, bf2f(v[2]) * inv, bf2f(v[3]) * inv);
-    o[1] = fp8x4(bf2f(v[4]) * inv, bf2f(v[5]) * inv, bf2f(v[6]) * inv, bf2f(v[7]) * inv);
-    *reinterpret_cast<u32x2_t*>(orow + k) = o;
+  typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
+#pragma unroll
+  for (int c = 0; c < QR_CHUNKS; ++c) {
+    const int k = (c * QR_THREADS + threadIdx.x) * 8;
+    if (k < K) {
+      u32x2_t o;
+      o[0] = fp8x4(bf2f(v[c][0]) * inv, bf2f(v[c][1]) * inv, bf2f(v[c][2]) * inv, bf2f(v[c][3]) * inv);
+      o[1] = fp8x4(bf2f(v[c][4]) * inv, bf2f(v[c][5]) * inv, bf2f(v[c][6]) * inv, bf2f(v[c][7]) * inv);
+      *reinterpret_cast<u32x2_t*>(orow + k) = o;
+    }
   }
   if (threadIdx.x == 0) xs[m] = scale * (norm ? rsqrtf(ss / float(K) + eps) : 1.f);
 }
@@ -343,8 +358,8 @@ CAIN_API long long cain_w8a8_ws_bytes(int N, int K, int M) {
 
 CAIN_API int cain_quant_rows(const void* x, int ldx, int K, int M, void* x8, int ld8, float* xs, int norm, float eps,
                              hipStream_t st) {
-  if (K % 8 || ldx % 8 || ld8 % 8 || M < 1) return -1;
-  hipLaunchKernelGGL(quant_rows_kernel, dim3(M), dim3(256), 0, st, (const __bf16*)x, ldx, K, (uint8_t*)x8, ld8, xs,
+  if (K % 8 || K > QR_MAXK || ldx % 8 || ld8 % 8 || M < 1) return -1;
+  hipLaunchKernelGGL(quant_rows_kernel, dim3(M), dim3(QR_THREADS), 0, st, (const __bf16*)x, ldx, K, (uint8_t*)x8, ld8, xs,
                      norm, eps);
   return int(hipGetLastError());
 }
