@@ -282,3 +282,33 @@ def test_sample_distribution_matches_topk_softmax():
     p = torch.softmax(torch.tensor([3.0, 2.5, 2.0]), 0)
     freq = counts[:3] / counts.sum()
     assert torch.allclose(freq, p, atol=0.06), (freq, p)
+
+
+@pytest.mark.parametrize("H,Hkv,hd", [(32, 8, 128), (32, 32, 96), (28, 4, 128), (16, 8, 64)])
+@pytest.mark.parametrize("kv", ["bf16", "fp8"])
+def test_attention_many_rows(H, Hkv, hd, kv):
+    """Single-split attention over many (row, kv head) pairs (the decode batch shape): rows of different lengths,
+    an idle row, bf16 and fp8 caches."""
+    torch.manual_seed(21)
+    T_max, M = 512, 200
+    lengths = torch.randint(1, T_max, (M,)).tolist()
+    kc = torch.randn(M, Hkv, T_max, hd, device=DEV)
+    vt = torch.randn(M, Hkv, T_max, hd, device=DEV)
+    if kv == "fp8":
+        kc, vt = kc.to(torch.float8_e4m3fn).float(), vt.to(torch.float8_e4m3fn).float()
+        kp = ops.pack_kcache(kc.to(torch.float8_e4m3fn).view(torch.uint8))
+        vp = ops.pack_vcache(vt.to(torch.float8_e4m3fn).view(torch.uint8))
+    else:
+        kc, vt = kc.bfloat16().float(), vt.bfloat16().float()
+        kp, vp = ops.pack_kcache(kc.bfloat16()), ops.pack_vcache(vt.bfloat16())
+    q = torch.randn(M, H * hd, device=DEV).bfloat16()
+    slot = torch.arange(M, device=DEV, dtype=torch.int32)
+    slot[7] = -1  # an idle row: no output written, no cache read
+    pos = torch.tensor([L - 1 for L in lengths], device=DEV, dtype=torch.int32)
+    out = torch.full((M, H * hd), 7.0, device=DEV).bfloat16()
+    ops.attention(q, kp, vp, slot, pos, H, Hkv, hd, 1, 1.0 / math.sqrt(hd), out=out)
+    for m in range(0, M, 9):
+        if m == 7:
+            continue
+        ref = _attn_ref(q[m].view(H, hd), kc[m], vt[m], lengths[m], H // Hkv)
+        assert rel_err(out[m].view(H, hd), ref) < 2e-2, (m, lengths[m])
