@@ -123,9 +123,11 @@ int smi_open() {
   }
   sym(g_smi.lib, "amdsmi_get_cpu_handles", g_smi.cpu_handles);
   sym(g_smi.lib, "amdsmi_get_cpu_socket_energy", g_smi.cpu_energy);
-  // CPU sockets need the HSMP driver (usually root-only on a shared host): try GPUs + CPUs, then GPUs alone
+  // CPU sockets need the HSMP driver (usually root-only on a shared host): try GPUs + CPUs, then GPUs alone.
+  // Without a readable /dev/hsmp the CPU init only prints "ESMI Not initialized" and fails: skip it.
   bool cpus_ok = false;
-  if (g_smi.cpu_handles && g_smi.cpu_energy &&
+  const bool hsmp = access("/dev/hsmp", R_OK) == 0;
+  if (hsmp && g_smi.cpu_handles && g_smi.cpu_energy &&
       g_smi.init(AMDSMI_INIT_AMD_GPUS | AMDSMI_INIT_AMD_CPUS) == AMDSMI_STATUS_SUCCESS) {
     cpus_ok = true;
   } else if (g_smi.init(AMDSMI_INIT_AMD_GPUS) != AMDSMI_STATUS_SUCCESS) {
