@@ -220,7 +220,15 @@ class ExperimentController:
         try:
             EventSubscriptionController.raise_event(RunnerEvents.BEFORE_EXPERIMENT)
             todo = self.pending()
+            # session budget (seconds; config `run_budget_s` or CAIN_RUN_BUDGET_S): no run starts after it, the
+            # rest stays TODO for the next invocation of the same command (allocation windows shorter than a study)
+            budget = float(os.environ.get("CAIN_RUN_BUDGET_S", getattr(self.config, "run_budget_s", 0) or 0))
+            t_start = time.monotonic()
             for n, variation in enumerate(todo):
+                if budget > 0 and n > 0 and time.monotonic() - t_start > budget:  # >= 1 run per session
+                    output.console_log_WARNING(f"session budget of {budget:.0f} s reached: {len(todo) - n} runs left "
+                                               "TODO; run the same command again to resume")
+                    return
                 self.run_variation(variation)
                 if n + 1 < len(todo):
                     self.cooldown()

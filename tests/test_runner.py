@@ -288,6 +288,21 @@ def test_timeout_kills_run_and_continues(exp_config, monkeypatch):
     assert sum(r["__done"] is RunProgress.DONE for r in rows.values()) == 3
 
 
+def test_session_budget_leaves_rest_todo_then_resumes(exp_config, tmp_path, monkeypatch):
+    """CAIN_RUN_BUDGET_S: no run starts once the session budget is spent; the next invocation of the same
+    command resumes the TODO rows (studies longer than one allocation window)."""
+    monkeypatch.setenv("CAIN_TEST_HANG", "")  # no hang
+    monkeypatch.setenv("CAIN_RUN_BUDGET_S", "1e-9")  # spent after the first run
+    cfg = _run(exp_config, isolation="inline")
+    rows = CSVOutputManager(cfg.experiment_path).read_run_table()
+    assert sum(r["__done"] is RunProgress.DONE for r in rows) == 1
+    assert "after_experiment" not in (tmp_path / "events.log").read_text().split()
+    monkeypatch.delenv("CAIN_RUN_BUDGET_S")
+    cfg = _run(exp_config, isolation="inline")
+    assert all(r["__done"] is RunProgress.DONE for r in CSVOutputManager(cfg.experiment_path).read_run_table())
+    assert (tmp_path / "events.log").read_text().split().count("after_experiment") == 1
+
+
 def test_resume_md5_mismatch_requires_consent(exp_config, monkeypatch):
     monkeypatch.setenv("CAIN_TEST_FAIL", "run_2_repetition_0")
     _run(exp_config)
