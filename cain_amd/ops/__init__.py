@@ -34,7 +34,8 @@ from typing import Optional
 import torch
 
 HERE = Path(__file__).resolve().parent
-LIB_PATH = HERE / "libcain_kernels.so"
+# CAIN_KERNELS_LIB: another build of the library (A/B runs of a kernel change on one box)
+LIB_PATH = Path(os.environ.get("CAIN_KERNELS_LIB") or HERE / "libcain_kernels.so")
 
 EPI_BF16, EPI_RESID, EPI_F32, EPI_SILU, EPI_GELU, EPI_QKV_ROPE = 0, 1, 2, 3, 4, 5
 EPI_KV_FP8 = 0x100  # or-ed into EPI_QKV_ROPE: the KV cache is fp8 e4m3 (csrc/gemm_epi.h)

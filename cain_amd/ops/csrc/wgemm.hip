@@ -308,8 +308,12 @@ __global__ __launch_bounds__(64 * (8 + NDMA), (8 + NDMA) / 4) void wgemm_kernel(
   }
 }
 
-// Split-K combine + fused epilogue: one wave per 16 x 16 output unit.
-template <int BM, int EPI, bool NORM>
+// Split-K combine + fused epilogue: one wave per 16 x 16 output unit.  The kernel is a few dependent memory
+// round trips long, so every load goes out before the first add: the epilogue inputs (residual row, RoPE position
+// and then its cos / sin) first, then all KS slab pieces and row sums (KS a compile-time split count; KS = 0 is
+// the runtime-count fallback).  Issued after the sum, as before, the epilogue loads were one more round trip
+// (two for QKV: position, then the tables).
+template <int BM, int EPI, bool NORM, int KS>
 __global__ __launch_bounds__(256) void wgemm_reduce_kernel(const GemmArgs a, const WgArgs w, int n_units) {
   constexpr int RB = BM / 16;
   const int lane = threadIdx.x & 63;
@@ -318,20 +322,51 @@ __global__ __launch_bounds__(256) void wgemm_reduce_kernel(const GemmArgs a, con
   const int gt = unit / RB, rb = unit - gt * RB;
   const int ntiles = a.N >> 4;
   const int m = rb * 16 + (lane & 15);
+  const bool live = gt < ntiles;
+  const EpiIn e = live ? epi_load_at<EPI>(a, gt, m, lane) : EpiIn{};
+  const int ks = KS ? KS : w.ks;
+  const f32x4* src = reinterpret_cast<const f32x4*>(w.part) + (size_t)unit * 64 + lane;
+  const float* ssrc = w.part_ss + (size_t)(gt / WG_NT) * ks * BM + m;
   f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int k = 0; k < w.ks; ++k) v += *reinterpret_cast<const f32x4*>(w.part + (((size_t)k * n_units + unit) * 64 + lane) * 4);
-  if constexpr (NORM) {
-    const int blk = gt / WG_NT;
-    float ss = 0.f;
-    for (int k = 0; k < w.ks; ++k) ss += w.part_ss[((size_t)blk * w.ks + k) * BM + m];
-    v *= rsqrtf(ss / float(a.K) + a.eps);
+  float ss = 0.f;
+  if constexpr (KS > 0) {
+    f32x4 p[KS];
+    float q[KS];
+#pragma unroll
+    for (int k = 0; k < KS; ++k) p[k] = src[(size_t)k * n_units * 64];
+    if constexpr (NORM) {
+#pragma unroll
+      for (int k = 0; k < KS; ++k) q[k] = ssrc[k * BM];
+    }
+#pragma unroll
+    for (int k = 0; k < KS; ++k) {
+      v += p[k];
+      if constexpr (NORM) ss += q[k];
+    }
+  } else {
+    for (int k = 0; k < ks; ++k) v += src[(size_t)k * n_units * 64];
+    if constexpr (NORM) {
+      for (int k = 0; k < ks; ++k) ss += ssrc[k * BM];
+    }
   }
+  if constexpr (NORM) v *= rsqrtf(ss / float(a.K) + a.eps);
   f32x4 pv;
 #pragma unroll
   for (int i = 0; i < 4; ++i) pv[i] = __shfl_xor(v[i], 32, 64);
-  if (gt >= ntiles) return;
-  const EpiIn e = epi_load_at<EPI>(a, gt, m, lane);
+  if (!live) return;
   epi_store<EPI>(a, gt, m, lane, e, [&](int off) { return off ? pv : v; });
+}
+
+template <int BM, int EPI, bool NORM>
+void wg_reduce_launch(const GemmArgs& a, const WgArgs& w, int n_units, hipStream_t st) {
+  const dim3 grid((n_units + 3) / 4), blk(256);
+  switch (w.ks) {
+#define CAIN_WG_RED(K) \
+  case K: hipLaunchKernelGGL((wgemm_reduce_kernel<BM, EPI, NORM, K>), grid, blk, 0, st, a, w, n_units); return;
+    CAIN_WG_RED(2) CAIN_WG_RED(3) CAIN_WG_RED(4) CAIN_WG_RED(5) CAIN_WG_RED(6) CAIN_WG_RED(7) CAIN_WG_RED(8)
+#undef CAIN_WG_RED
+    default: hipLaunchKernelGGL((wgemm_reduce_kernel<BM, EPI, NORM, 0>), grid, blk, 0, st, a, w, n_units);
+  }
 }
 
 namespace {
@@ -400,8 +435,7 @@ hipError_t wg_launch(const GemmArgs& a, const WgArgs& w, const WgPlan& p, hipStr
                      st, a, w);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || p.ks == 1) return e;
-  const int n_units = p.nblk * WG_NT * G::RB;
-  hipLaunchKernelGGL((wgemm_reduce_kernel<BM, EPI, NORM>), dim3((n_units + 3) / 4), dim3(256), 0, st, a, w, n_units);
+  wg_reduce_launch<BM, EPI, NORM>(a, w, p.nblk * WG_NT * G::RB, st);
   return hipGetLastError();
 }
 
