@@ -59,8 +59,15 @@ __device__ __forceinline__ bf16x8 fp8x8_to_bf16(u32x2 v, float sc) {
   return r;
 }
 
-template <int HD, int AW, bool KV8, bool NT_KV = true>
-__global__ __launch_bounds__(AW * 64) void attn_decode_kernel(
+// ONESET: one register set of K / V fragments per wave instead of the two-set ping-pong, so more workgroups are
+// resident (OCC: minimum waves per SIMD the register allocation must allow).  The two-set body needs ~220
+// registers (2 waves per SIMD, 2 workgroups per CU: the 2,048-workgroup grid of 256 rows x 8 kv heads runs in 4
+// rounds); the one-set body held to 128 registers (no spills) runs 4 workgroups per CU, 2 rounds, 16 waves each
+// with one block in flight.  Measured (llama3.1:8b, 256 rows, tools/bench_kernels.py --attn-only, one box):
+// 49.4 -> 33.2 us at 192 positions, 79.7 -> 58.1 at 350, 136.5 -> 113.4 at 700, 258.2 -> 220.9 at 1400 (6.6 TB/s);
+// fp8 cache 65.3 -> 56.7 at 700; headline bench 25.1k -> 26.3k tok/s (profiles/r2/attn_occupancy.md).
+template <int HD, int AW, bool KV8, bool NT_KV = true, bool ONESET = false, int OCC = 1>
+__global__ __launch_bounds__(AW * 64, OCC) void attn_decode_kernel(
     const __bf16* __restrict__ q, const __bf16* __restrict__ kc, const __bf16* __restrict__ vtc,
     const int* __restrict__ slot, const int* __restrict__ pos, float* __restrict__ part_o,
     float* __restrict__ part_ml, unsigned* __restrict__ counters, __bf16* __restrict__ out, int ldo, int M, int H,
@@ -166,7 +173,7 @@ __global__ __launch_bounds__(AW * 64) void attn_decode_kernel(
     };
 
     const int first = b0 + wave;
-    if constexpr (HD <= 128) {
+    if constexpr (HD <= 128 && !ONESET) {
       frag_t ka[NKS], kb[NKS], va[NDT];
       load_blk(first, ka, kb, va);
       // two register sets ping-pong, the next block's loads issued before the current block computes;
@@ -182,7 +189,7 @@ __global__ __launch_bounds__(AW * 64) void attn_decode_kernel(
         __builtin_amdgcn_sched_barrier(0);
         if (blk + AW < b1) process(blk + AW, kc2, kd2, vb2);
       }
-    } else {  // hd 256: one register set (two would spill)
+    } else {  // hd 256: one register set (two would spill); ONESET: 3 waves per SIMD instead of 2
       frag_t ka[NKS], kb[NKS], va[NDT];
       load_blk(first, ka, kb, va);
       for (int blk = first; blk < b1; blk += AW) {
@@ -296,14 +303,34 @@ static bool attn_nt() {
   return nt;
 }
 
+// Body for hd <= 128 (CAIN_ATTN_VARIANT, A/B runs): 2 = one register set held to 128 registers (4 waves per
+// SIMD; default), 1 = one set (3 waves per SIMD), 0 = two register sets (2 waves per SIMD; round 1's body).
+static int attn_variant() {
+  static const int v = [] {
+    const char* e = getenv("CAIN_ATTN_VARIANT");
+    return e && *e ? atoi(e) : 2;
+  }();
+  return v;
+}
+
 template <int HD, int AW, bool KV8, bool NT>
 static void launch_attn_t(const void* q, const void* kc, const void* vtc, const int* slot, const int* pos,
                           float* part_o, float* part_ml, unsigned* counters, void* out, int ldo, int M, int H, int Hkv,
                           int T_max, int nsplit, float scale, float kscale, float vscale, hipStream_t st) {
   // (a four-set prefetch for the half-size fp8 blocks measured slower: 90 vs 68 us at 256 rows x 700 positions)
-  hipLaunchKernelGGL((attn_decode_kernel<HD, AW, KV8, NT>), dim3(M * Hkv, nsplit), dim3(AW * 64), 0, st,
-                     (const __bf16*)q, (const __bf16*)kc, (const __bf16*)vtc, slot, pos, part_o, part_ml, counters,
-                     (__bf16*)out, ldo, M, H, Hkv, T_max, nsplit, scale, kscale, vscale);
+  const int var = HD <= 128 ? attn_variant() : 0;
+  if (var == 1)
+    hipLaunchKernelGGL((attn_decode_kernel<HD, AW, KV8, NT, true>), dim3(M * Hkv, nsplit), dim3(AW * 64), 0, st,
+                       (const __bf16*)q, (const __bf16*)kc, (const __bf16*)vtc, slot, pos, part_o, part_ml, counters,
+                       (__bf16*)out, ldo, M, H, Hkv, T_max, nsplit, scale, kscale, vscale);
+  else if (var == 2)
+    hipLaunchKernelGGL((attn_decode_kernel<HD, AW, KV8, NT, true, 4>), dim3(M * Hkv, nsplit), dim3(AW * 64), 0,
+                       st, (const __bf16*)q, (const __bf16*)kc, (const __bf16*)vtc, slot, pos, part_o, part_ml,
+                       counters, (__bf16*)out, ldo, M, H, Hkv, T_max, nsplit, scale, kscale, vscale);
+  else
+    hipLaunchKernelGGL((attn_decode_kernel<HD, AW, KV8, NT>), dim3(M * Hkv, nsplit), dim3(AW * 64), 0, st,
+                       (const __bf16*)q, (const __bf16*)kc, (const __bf16*)vtc, slot, pos, part_o, part_ml, counters,
+                       (__bf16*)out, ldo, M, H, Hkv, T_max, nsplit, scale, kscale, vscale);
 }
 
 template <int HD, int AW>
