@@ -319,6 +319,8 @@ static void launch_attn_t(const void* q, const void* kc, const void* vtc, const 
                           int T_max, int nsplit, float scale, float kscale, float vscale, hipStream_t st) {
   // (a four-set prefetch for the half-size fp8 blocks measured slower: 90 vs 68 us at 256 rows x 700 positions)
   const int var = HD <= 128 ? attn_variant() : 0;
+  // (hd 256 keeps 1 wave per SIMD: held to 256 registers, 2 waves per SIMD, gemma:7b's 256-row attention
+  // measured 144.5 vs 139.6 us at 192 positions and 454 vs 438 at 700 -- it already streams 6.7 TB/s)
   if (var == 1)
     hipLaunchKernelGGL((attn_decode_kernel<HD, AW, KV8, NT, true>), dim3(M * Hkv, nsplit), dim3(AW * 64), 0, st,
                        (const __bf16*)q, (const __bf16*)kc, (const __bf16*)vtc, slot, pos, part_o, part_ml, counters,

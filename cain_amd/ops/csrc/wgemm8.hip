@@ -209,8 +209,9 @@ __global__ __launch_bounds__(64 * (8 + NDMA), (8 + NDMA) / 4) void wgemm8_kernel
   }
 }
 
-// Split-K combine + scales + fused epilogue: one wave per 16 x 16 output unit.
-template <int BM, int EPI>
+// Split-K combine + scales + fused epilogue: one wave per 16 x 16 output unit.  As wgemm.hip's reduce: the
+// epilogue inputs, the scales and all KS slab pieces are issued before the first add (KS = 0: runtime count).
+template <int BM, int EPI, int KS>
 __global__ __launch_bounds__(256) void wgemm8_reduce_kernel(const GemmArgs a, const WgArgs w, const W8Scales q,
                                                             int n_units) {
   constexpr int RB = BM / 16;
@@ -220,14 +221,24 @@ __global__ __launch_bounds__(256) void wgemm8_reduce_kernel(const GemmArgs a, co
   const int gt = unit / RB, rb = unit - gt * RB;
   const int ntiles = a.N >> 4;
   const int m = rb * 16 + (lane & 15);
+  const bool live = gt < ntiles;
+  const EpiIn e = live ? epi_load_at<EPI>(a, gt, m, lane) : EpiIn{};
+  const f32x4* src = reinterpret_cast<const f32x4*>(w.part) + (size_t)unit * 64 + lane;
   f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int k = 0; k < w.ks; ++k) v += *reinterpret_cast<const f32x4*>(w.part + (((size_t)k * n_units + unit) * 64 + lane) * 4);
-  if (gt < ntiles) v = w8_scaled(v, q, gt, m, lane, a.M);
+  if constexpr (KS > 0) {
+    f32x4 p[KS];
+#pragma unroll
+    for (int k = 0; k < KS; ++k) p[k] = src[(size_t)k * n_units * 64];
+#pragma unroll
+    for (int k = 0; k < KS; ++k) v += p[k];
+  } else {
+    for (int k = 0; k < w.ks; ++k) v += src[(size_t)k * n_units * 64];
+  }
+  if (live) v = w8_scaled(v, q, gt, m, lane, a.M);
   f32x4 pv;
 #pragma unroll
   for (int i = 0; i < 4; ++i) pv[i] = __shfl_xor(v[i], 32, 64);
-  if (gt >= ntiles) return;
-  const EpiIn e = epi_load_at<EPI>(a, gt, m, lane);
+  if (!live) return;
   epi_store<EPI>(a, gt, m, lane, e, [&](int off) { return off ? pv : v; });
 }
 
@@ -321,7 +332,14 @@ hipError_t w8_launch(const GemmArgs& a, const WgArgs& w, const W8Scales& q, cons
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || p.ks == 1) return e;
   const int n_units = p.nblk * WG_NT * G::RB;
-  hipLaunchKernelGGL((wgemm8_reduce_kernel<BM, EPI>), dim3((n_units + 3) / 4), dim3(256), 0, st, a, w, q, n_units);
+  const dim3 grid((n_units + 3) / 4), blk(256);
+  switch (w.ks) {
+#define CAIN_W8_RED(K) \
+  case K: hipLaunchKernelGGL((wgemm8_reduce_kernel<BM, EPI, K>), grid, blk, 0, st, a, w, q, n_units); break;
+    CAIN_W8_RED(2) CAIN_W8_RED(3) CAIN_W8_RED(4) CAIN_W8_RED(5) CAIN_W8_RED(6) CAIN_W8_RED(7) CAIN_W8_RED(8)
+#undef CAIN_W8_RED
+    default: hipLaunchKernelGGL((wgemm8_reduce_kernel<BM, EPI, 0>), grid, blk, 0, st, a, w, q, n_units);
+  }
   return hipGetLastError();
 }
 
