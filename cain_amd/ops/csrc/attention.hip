@@ -363,21 +363,10 @@ CAIN_API int cain_attention_ex(const void* q, const void* kc, const void* vtc, c
                                int Hkv, int hd, int T_max, int nsplit, float scale, int kv8, float kscale,
                                float vscale, hipStream_t st) {
   if (H % Hkv || H / Hkv > 16 || T_max % 32 || nsplit < 1 || nsplit > 64 || M > 256) return -1;
-  // 8-wave workgroups for few (row, kv head) pairs, 16-wave ones for <= 16 pairs (single-stream decode: 8 kv
-  // heads -> 8 workgroups on a 256-CU chip, so more waves per pair is the only parallelism left; llama3.1:8b at
-  // one row measured 15.6 -> 10.2 us at 700 positions, 15.7 -> 11.0 at 1,400, gpurun_out/r7); hd <= 128 only: the
-  // hd-256 body needs one wave per SIMD.  CAIN_ATTN_AW16=0: 8-wave workgroups there too (A/B runs).
+  // 8-wave workgroups for few (row, kv head) pairs (hd <= 128: the hd-256 body needs one wave per SIMD)
   const bool wide = M * Hkv <= 64;
-  static const bool aw16 = [] {
-    const char* e = getenv("CAIN_ATTN_AW16");
-    return !(e && e[0] == '0');
-  }();
-  const bool widest = aw16 && M * Hkv <= 16;
 #define CAIN_ATTN_CASE(HDV)                                                                                        \
   case HDV:                                                                                                      \
-    if (widest)                                                                                                  \
-      return int(launch_attn<HDV, 16>(q, kc, vtc, slot, pos, part_o, part_ml, counters, out, ldo, M, H, Hkv,     \
-                                      T_max, nsplit, scale, kv8, kscale, vscale, st));                           \
     return wide ? int(launch_attn<HDV, 8>(q, kc, vtc, slot, pos, part_o, part_ml, counters, out, ldo, M, H, Hkv,  \
                                           T_max, nsplit, scale, kv8, kscale, vscale, st))                        \
                 : int(launch_attn<HDV, 4>(q, kc, vtc, slot, pos, part_o, part_ml, counters, out, ldo, M, H, Hkv,  \
