@@ -151,8 +151,13 @@ def main() -> int:
         if not cpu:
             torch.cuda.synchronize(dev)
 
+    def progress(what: str) -> None:  # stderr heartbeat (long runs must keep writing; the JSON stays on stdout)
+        if rank == 0:
+            print(f"[bench] {what} {time.strftime('%H:%M:%S')}", file=sys.stderr, flush=True)
+
     for w in range(ns.warmup):
         one_step(-1 - w)
+        progress(f"warmup {w + 1}/{ns.warmup}")
 
     meter = None
     if not ns.no_energy and not cpu:
@@ -182,6 +187,7 @@ def main() -> int:
     toks = 0
     for s in range(ns.steps):
         toks += one_step(s)
+        progress(f"step {s + 1}/{ns.steps}")
     barrier()
     dt = time.perf_counter() - t0
     reading = meter.stop() if meter else None
