@@ -156,10 +156,14 @@ def attention_splits(M: int, Hkv: int, T_max: int) -> int:
     if forced > 0:
         return min(64, forced)
     if M * Hkv <= 64:
-        # few (row, kv head) pairs run 8-wave workgroups (attention.hip): one split up to 64 blocks of 32
-        # positions (8 per wave) -- the split combine costs ~4 us of dependent memory round trips, more than
-        # it saves below that (profiles/single_stream_r1.md)
-        return int(max(1, min(64, math.ceil((T_max // 32) / 64))))
+        # few (row, kv head) pairs run 8-wave workgroups (attention.hip): position splits up to ~64 workgroups
+        # (<= 8 splits, >= 4 blocks of 32 positions per split at full context), and at most 64 blocks per split.
+        # Measured in the graph-replayed batch-1 decode (rocprof, profiles/r2/attn_occupancy.md): llama3.1:8b
+        # 10.9 -> 7.7 us per call at 8 splits (4: 9.1, 16: 8.5), qwen2:1.5b 11.2 -> 8.2, gemma:2b 18.9 -> 13.2,
+        # phi3 (32 pairs, 2 splits) 9.7 -> 9.2, llama at 2 rows (4 splits) 11.2 -> 9.4 -- the in-kernel combine's
+        # round trips cost less than one workgroup per pair walking the whole context.
+        few = min(8, T_max // 128, 64 // (M * Hkv))
+        return int(max(1, min(64, max(few, math.ceil((T_max // 32) / 64)))))
     ns = max(1, min(T_max // 128, math.ceil(256 / (M * Hkv))))
     per = int(os.environ.get("CAIN_ATTN_SPLIT_BLOCKS", "0") or 0)
     if per > 0:
