@@ -87,13 +87,17 @@ __global__ __launch_bounds__(64 * (8 + NDMA), (8 + NDMA) / 4) void wgemm_kernel(
   const int nblk = (ntiles + WG_NT - 1) / WG_NT;
 
   // block -> (column block, k-split); the k-split partners of one column block read disjoint X panels, the
-  // column blocks of one k-split read the SAME X panel: keep those on one XCD (blocks b and b + 8 share an XCD
-  // under round-robin dispatch; speed only, any placement is correct)
+  // column blocks of one k-split read the SAME X panel: split-major placement keeps those on one XCD (blocks b
+  // and b + 8 share an XCD under round-robin dispatch); the default xcd_blk placement keeps a column block's
+  // split partners together instead, for the reduce (wgemm_dispatch).  Speed only, any placement is correct.
   int blk, kc;
   {
     const int bid = blockIdx.x, ks = w.ks;
     if (ks == 1) blk = bid, kc = 0;
-    else if ((8 % ks) == 0) kc = bid % ks, blk = bid / ks;
+    else if (w.xcd_blk) {  // XCD x = bid % 8 owns column blocks x, x + 8, ... with all their splits (nblk % 8 == 0)
+      const int j = bid >> 3;
+      blk = (bid & 7) + 8 * (j / ks), kc = j % ks;
+    } else if ((8 % ks) == 0) kc = bid % ks, blk = bid / ks;
     else kc = bid / nblk, blk = bid - kc * nblk;
   }
   const int tile0 = blk * WG_NT;
@@ -317,7 +321,13 @@ template <int BM, int EPI, bool NORM, int KS>
 __global__ __launch_bounds__(256) void wgemm_reduce_kernel(const GemmArgs a, const WgArgs w, int n_units) {
   constexpr int RB = BM / 16;
   const int lane = threadIdx.x & 63;
-  const int unit = blockIdx.x * 4 + (threadIdx.x >> 6);
+  int rbid = blockIdx.x;
+  if (w.xcd_blk) {  // this workgroup's units on the XCD that wrote their column block's slabs (see wgemm_kernel)
+    constexpr int PER_BLK = WG_NT * RB / 4;  // reduce workgroups per column block
+    const int j = blockIdx.x >> 3;
+    rbid = ((blockIdx.x & 7) + 8 * (j / PER_BLK)) * PER_BLK + j % PER_BLK;
+  }
+  const int unit = rbid * 4 + (threadIdx.x >> 6);
   if (unit >= n_units) return;
   const int gt = unit / RB, rb = unit - gt * RB;
   const int ntiles = a.N >> 4;
@@ -539,6 +549,13 @@ int wgemm_dispatch(const GemmArgs& a, int epi, bool norm, void* ws, long long ws
   WgArgs w{};
   w.ks = p.ks;
   w.kst = p.kst;
+  // XCD-local split-K: the split partners of a column block, and the reduce workgroups of its units, run on one
+  // XCD (blocks b and b + 8 share one under round-robin dispatch), so the reduce reads the slabs from the L2
+  // that holds them instead of across the fabric.  Measured on the headline (rocprof, gpurun_out/r15): O / down
+  // reduce 8.7 -> 6.9 us, QKV 22.5 + 11.2 -> 20.1 + 10.9 us, O / down main +1.1 us (their X panels are now
+  // fetched per XCD); 25.8k -> 26.3k tok/s.  CAIN_WGEMM_XCD=0: the split-major placement (A/B runs).
+  static const int xcd = wg_env("CAIN_WGEMM_XCD", 1);
+  w.xcd_blk = xcd && p.ks > 1 && p.nblk % 8 == 0;
   // [reserved counter region][slabs][sums]
   w.part = reinterpret_cast<float*>(static_cast<char*>(ws) + WG_CTR_BYTES);
   w.part_ss = w.part + p.part_floats;

@@ -58,6 +58,7 @@ struct WgArgs {
   int kst;          // ring stages (64-deep k-steps) per split
   float* part;      // [ks][n_units][64 lanes] f32x4 (ks > 1)
   float* part_ss;   // [nblk][ks][BM] per-row partial sums of squares (ks > 1 && NORM)
+  int xcd_blk;      // 1: a column block's split partners and its reducers share one XCD (wgemm.hip)
 };
 
 
