@@ -92,13 +92,7 @@ __global__ __launch_bounds__(64 * (8 + NDMA), (8 + NDMA) / 4) void wgemm_kernel(
   // split partners together instead, for the reduce (wgemm_dispatch).  Speed only, any placement is correct.
   int blk, kc;
   {
-    const int bid = blockIdx.x, ks = w.ks;
-    if (ks == 1) blk = bid, kc = 0;
-    else if (w.xcd_blk) {  // XCD x = bid % 8 owns column blocks x, x + 8, ... with all their splits (nblk % 8 == 0)
-      const int j = bid >> 3;
-      blk = (bid & 7) + 8 * (j / ks), kc = j % ks;
-    } else if ((8 % ks) == 0) kc = bid % ks, blk = bid / ks;
-    else kc = bid / nblk, blk = bid - kc * nblk;
+    wg_block_of(blockIdx.x, w.ks, nblk, w.xcd_blk, blk, kc);
   }
   const int tile0 = blk * WG_NT;
   const int st0 = kc * w.kst;                    // first stage (64-deep k-step) of this split
@@ -321,13 +315,8 @@ template <int BM, int EPI, bool NORM, int KS>
 __global__ __launch_bounds__(256) void wgemm_reduce_kernel(const GemmArgs a, const WgArgs w, int n_units) {
   constexpr int RB = BM / 16;
   const int lane = threadIdx.x & 63;
-  int rbid = blockIdx.x;
-  if (w.xcd_blk) {  // this workgroup's units on the XCD that wrote their column block's slabs (see wgemm_kernel)
-    constexpr int PER_BLK = WG_NT * RB / 4;  // reduce workgroups per column block
-    const int j = blockIdx.x >> 3;
-    rbid = ((blockIdx.x & 7) + 8 * (j / PER_BLK)) * PER_BLK + j % PER_BLK;
-  }
-  const int unit = rbid * 4 + (threadIdx.x >> 6);
+  // this workgroup's 4 units on the XCD that wrote their column block's slabs (wg_block_of)
+  const int unit = wg_reduce_block(blockIdx.x, WG_NT * RB / 4, w.xcd_blk) * 4 + (threadIdx.x >> 6);
   if (unit >= n_units) return;
   const int gt = unit / RB, rb = unit - gt * RB;
   const int ntiles = a.N >> 4;

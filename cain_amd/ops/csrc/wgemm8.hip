@@ -70,10 +70,7 @@ __global__ __launch_bounds__(64 * (8 + NDMA), (8 + NDMA) / 4) void wgemm8_kernel
 
   int blk, kc;
   {
-    const int bid = blockIdx.x, ks = w.ks;
-    if (ks == 1) blk = bid, kc = 0;
-    else if ((8 % ks) == 0) kc = bid % ks, blk = bid / ks;
-    else kc = bid / nblk, blk = bid - kc * nblk;
+    wg_block_of(blockIdx.x, w.ks, nblk, w.xcd_blk, blk, kc);
   }
   const int tile0 = blk * WG_NT;
   const int st0 = kc * w.kst;
@@ -216,7 +213,7 @@ __global__ __launch_bounds__(256) void wgemm8_reduce_kernel(const GemmArgs a, co
                                                             int n_units) {
   constexpr int RB = BM / 16;
   const int lane = threadIdx.x & 63;
-  const int unit = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int unit = wg_reduce_block(blockIdx.x, WG_NT * RB / 4, w.xcd_blk) * 4 + (threadIdx.x >> 6);
   if (unit >= n_units) return;
   const int gt = unit / RB, rb = unit - gt * RB;
   const int ntiles = a.N >> 4;
@@ -402,6 +399,8 @@ CAIN_API int cain_gemm_w8a8(const void* Wp8, const float* wscale, const void* X8
   a.H = H, a.Hkv = Hkv, a.hd = hd, a.T_max = T_max, a.kv8 = (epi_flags & EPI_KV_FP8) ? 1 : 0;
   WgArgs w{};
   w.ks = p.ks, w.kst = p.kst, w.part = ws ? reinterpret_cast<float*>(static_cast<char*>(ws) + W8_SLAB_OFFSET) : nullptr;
+  static const int xcd = wg_env("CAIN_WGEMM_XCD", 1);  // XCD-local split-K (wgemm_ring.h wg_block_of)
+  w.xcd_blk = xcd && p.ks > 1 && p.nblk % 8 == 0;
   const W8Scales q{xs, wscale};
   const hipError_t e = p.bm == 256 ? w8_launch_e<256>(epi, a, w, q, p, st) : w8_launch_e<128>(epi, a, w, q, p, st);
   return int(e);

@@ -51,6 +51,25 @@ __device__ __forceinline__ void glds16(const void* src, char* lds_wave_base, int
     __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)lds_wave_base, 16, 0, 0);
 }
 
+// Workgroup -> (column block, k-split) of the wide GEMMs.  xcd_blk (nblk % 8 == 0): XCD x = bid % 8 (round-robin
+// dispatch) owns column blocks x, x + 8, ... with all their splits, so the split-K reduce can read the slabs from
+// that XCD's L2 (wg_reduce_block); otherwise split-major: the column blocks of one split (which read the same X
+// panel) share an XCD.  Speed only, any placement is correct.
+__device__ __forceinline__ void wg_block_of(int bid, int ks, int nblk, int xcd_blk, int& blk, int& kc) {
+  if (ks == 1) blk = bid, kc = 0;
+  else if (xcd_blk) {
+    const int j = bid >> 3;
+    blk = (bid & 7) + 8 * (j / ks), kc = j % ks;
+  } else if ((8 % ks) == 0) kc = bid % ks, blk = bid / ks;
+  else kc = bid / nblk, blk = bid - kc * nblk;
+}
+// Reduce workgroup index (units of per_blk consecutive workgroups per column block) on the XCD of its block.
+__device__ __forceinline__ int wg_reduce_block(int bid, int per_blk, int xcd_blk) {
+  if (!xcd_blk) return bid;
+  const int j = bid >> 3;
+  return ((bid & 7) + 8 * (j / per_blk)) * per_blk + j % per_blk;
+}
+
 }  // namespace wg
 
 struct WgArgs {
