@@ -198,7 +198,10 @@ class DecodeEngine:
             backend = "hip" if self.device.type == "cuda" else "torch"
         self.backend = backend
         self.max_batch = int(min(max_batch, row_cap))
-        self.prefill_chunk = min(PREFILL_ROWS, row_cap)
+        # prompt tokens per prefill forward: the engine's own row count when that is wider (a 256-row engine
+        # prefills 256 tokens per forward on the wide GEMM: half the launches of 128-row chunks)
+        self.prefill_chunk = int(min(int(os.environ.get("CAIN_PREFILL_ROWS", "0") or 0)
+                                     or max(PREFILL_ROWS, self.max_batch), row_cap))
         self.T_max = int(math.ceil(min(max_context, self.cfg.max_context) / 32) * 32)
         self.seed = seed
         self.steps_per_graph = max(1, int(steps_per_graph))
