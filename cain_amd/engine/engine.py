@@ -330,6 +330,10 @@ class DecodeEngine:
         vs 23.9k tok/s untuned on the same box -- the isolated winner is not the in-graph winner, so the default
         rule stays.  Runs before any graph capture and before the GEMM workspace is sized."""
         from .. import ops
+        # CAIN_WGEMM_PLANS="N:K:BM:KS[:VARIANT],...": explicit per-shape plans (in-graph A/B of split counts)
+        for spec in filter(None, os.environ.get("CAIN_WGEMM_PLANS", "").split(",")):
+            f = [int(x) for x in spec.split(":")]
+            ops.set_wide_gemm_plan(f[0], f[1], f[2], f[3], f[4] if len(f) > 4 else -1)
         if self.weight_dtype != "bf16" or os.environ.get("CAIN_WGEMM_TUNE", "0") != "1":
             return []
         cfg = self.cfg

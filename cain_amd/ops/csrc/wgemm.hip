@@ -407,6 +407,10 @@ WgPlan wg_plan(int N, int K, int M) {
   p.nblk = ((N >> 4) + WG_NT - 1) / WG_NT;
   const int stages = K / WG_BK;
   int ks = p.nblk >= 128 ? 1 : std::max(1, std::min(ksmax, (target + p.nblk / 2) / p.nblk));
+  // 256-row tiles with short splits (< 16 stages): ~3/4 of the workgroups, longer splits and fewer slabs.  In the
+  // graph-replayed headline (llama3.1:8b, gpurun_out/r20-r21, same box, interleaved): O 8 -> 6 splits and QKV
+  // 5 -> 4 took 26.5k -> 26.7k tok/s (each alone +1 %); down (28 stages per split at 8) lost at 6.
+  if (p.bm == 256 && ks > 1 && stages / ks < 16) ks = std::max(1, std::min(ks, (target * 3 / 4 + p.nblk / 2) / p.nblk));
   if (const WgShape* o = wg_shape(N, K, p.bm)) {
     if (o->ks > 0) ks = o->ks;
   }
