@@ -96,6 +96,7 @@ class EnergyReading:
     per_gpu_energy_j: List[float] = field(default_factory=list)
     host_share: float = 1.0
     idle_cpu_power_w: float = float("nan")
+    sampler_core: int = -1    # CPU core the native sampler thread was pinned to
     samples: List[dict] = field(default_factory=list)
 
     @property
@@ -107,6 +108,27 @@ class EnergyReading:
         if not with_samples:
             d.pop("samples")
         return d
+
+
+def sampler_core(local_rank: Optional[int] = None, cpus: Optional[Sequence[int]] = None) -> int:
+    """CPU core for this process's sampler thread: the ``local_rank``-th highest core of the affinity mask
+    (``LOCAL_RANK`` by default), so the samplers of the ranks of one node each get a core of their own instead
+    of all polling amd-smi on the mask's last core (the native default).  Wraps when there are more ranks than
+    allowed cores; -1 when the mask is unknown (the native sampler then picks)."""
+    if local_rank is None:
+        try:
+            local_rank = int(os.environ.get("LOCAL_RANK", "0") or 0)
+        except ValueError:
+            local_rank = 0
+    if cpus is None:
+        try:
+            cpus = sorted(os.sched_getaffinity(0))
+        except (AttributeError, OSError):
+            return -1
+    cpus = sorted(int(c) for c in cpus)
+    if not cpus:
+        return -1
+    return cpus[-1 - (max(0, int(local_rank)) % len(cpus))]
 
 
 def resolve_smi_indices(devices: Optional[Sequence[int]] = None) -> List[int]:
@@ -169,6 +191,9 @@ class EnergyMeter:
         self.ram_w_per_gb = ram_w_per_gb
         self.host_share = float(host_share)
         self.keep_samples = keep_samples
+        if cpu_core is None or cpu_core < 0:
+            cpu_core = sampler_core()
+        self.cpu_core = int(cpu_core)
         self.sampler = native.NativeSampler(self.smi, period_ms=period_ms, fast_period_ms=fast_period_ms,
                                             cpu_core=cpu_core)
         self.sampler.start()
@@ -283,7 +308,7 @@ class EnergyMeter:
             gpu_power_w=gpu_j / dur if self.n_gpus else float("nan"), vram_usage=vram,
             idle_power_w=self.idle_power_w, idle_subtracted_j=idle_sub, gpu_counter_updates=updates,
             per_gpu_energy_j=per_gpu, host_share=self.host_share, idle_cpu_power_w=self.idle_cpu_power_w,
-            samples=samples if self.keep_samples else [])
+            sampler_core=self.cpu_core, samples=samples if self.keep_samples else [])
 
     def _cpu_energy(self, samples: List[dict], dur: float, cpu_pct: float):
         """(joules, source) of host CPU energy charged to a window of ``dur`` s: the readable counter's increase

@@ -15,6 +15,10 @@ MI355X-native differences:
 
 * the on-device arm is this framework's own decode engine behind an Ollama-compatible server started per
   data-parallel rank on that rank's GPU (``python -m cain_amd serve``, port ``port_base + 1 + rank``);
+* a ``local:<device>`` remote arm is ONE engine server per node (port ``port_base + 101``): rank 0 starts it
+  after a memory-fit check and publishes its URL on the job's store, every other rank reuses it -- the
+  reference's one remote server (README.md:15-16); ``gpu_usage`` stays the client's own GPU residency and a
+  server sharing the client's GPU reports its activity in ``server_gpu_usage``;
 * energy is the amd-smi hardware accumulator of the measured GPU plus host CPU (HSMP / RAPL counters or the
   CPU-load TDP model, this rank's share of the host) and the client's RAM, on a native sampler thread
   (``cain_amd.energy``); the remote arm measures the client only (the rank's GPU when the server lives on
@@ -59,7 +63,45 @@ DEFAULT_TOPICS = REPO_ROOT / "experiments" / "topics.csv"
 
 REFERENCE_COLUMNS = ["topic", "execution_time", "cpu_usage", "gpu_usage", "memory_usage"]
 EXTRA_COLUMNS = ["tokens_generated", "prompt_tokens", "J_per_token", "tok_per_s", "ttft_s", "gen_time_s",
-                 "server_total_s", "server_eval_s", "client_wall_s", "device", "server"]
+                 "server_total_s", "server_eval_s", "client_wall_s", "device", "server", "server_gpu_usage"]
+
+#: c10d store key under which rank 0 publishes the node's one remote server URL ("error:<msg>" on failure)
+REMOTE_URL_KEY = "cain/remote_url/{name}"
+#: HBM of one MI355X: the budget of the co-located servers' memory-fit check
+GPU_MEM_BYTES = 288 * 10**9
+
+
+def server_footprint_bytes(models: List[str], max_batch: int, max_context: int, weights: str = "bf16",
+                           kv: str = "bf16") -> int:
+    """Device memory of one ``cain_amd serve --preload`` process: every model's weights (bf16 = 2 B / param,
+    fp8 = 1 B / param for the projections plus bf16 embeddings) and KV cache for max_batch x max_context,
+    plus ~2 GB of workspaces and allocator slack per model."""
+    from ..models.config import get_config
+
+    total = 0
+    for m in models:
+        cfg = get_config(m)
+        wb = cfg.weight_bytes(1 if weights == "fp8" else 2)
+        if weights == "fp8":
+            wb += cfg.vocab * cfg.d_model  # bf16 embedding beside the fp8 projections
+        if cfg.tie_embeddings:
+            wb += cfg.vocab * cfg.d_model * 2  # the engine packs its own LM-head copy of a tied embedding
+        total += wb + cfg.kv_bytes_per_token(1 if kv == "fp8" else 2) * max_batch * max_context + (2 << 30)
+    return total
+
+
+def _dist_store():
+    """The c10d key-value store of the data-parallel job (None outside one)."""
+    try:
+        import torch.distributed as dist
+
+        if dist.is_available() and dist.is_initialized():
+            return dist.distributed_c10d._get_default_store()
+    except Exception:  # pragma: no cover
+        pass
+    return None
+
+
 ENERGY_COLUMNS = [DataColumns.ENERGY_CONSUMED, DataColumns.ENERGY_USAGE_J, DataColumns.GPU_ENERGY_J,
                   DataColumns.CPU_ENERGY_J, DataColumns.RAM_ENERGY_J, DataColumns.IDLE_SUBTRACTED_J,
                   DataColumns.AVG_GPU_POWER_W, DataColumns.WINDOW_S, DataColumns.CPU_ENERGY_SOURCE]
@@ -86,6 +128,9 @@ class StudySettings:
     # remote arm: "" -> SERVER_IP from .env, else "fake" (modelled remote GPU server on this host's CPU),
     # "local:<device>" (an engine server on another device of this host) or an explicit URL
     remote: str = ""
+    # backend of a "local:<device>" remote server ("" = the server's default for its device: hip on a GPU);
+    # "fake" serves modelled generations (tests of the multi-rank plumbing)
+    remote_backend: str = ""
     remote_fake_tok_s: float = 70.0       # RTX 4070-class llama-8B decode rate for the modelled server
     remote_fake_prefill_s: float = 0.15
     client: str = "curl"                  # curl (reference parity) | http (in-process client)
@@ -343,20 +388,64 @@ class _StudyBase:
             self._threads.append(th)
             return th.url
         if spec.startswith("local:"):
-            dev = spec.split(":", 1)[1]
-            port = s.port_base + 101 + self.rank
+            return self._node_remote_server(spec.split(":", 1)[1], log_dir)
+        return spec if "://" in spec else f"http://{spec}"
+
+    def _node_remote_server(self, dev: str, log_dir: Path) -> str:
+        """ONE remote server per node, as the reference has one server every trial talks to
+        (README.md:15-16, experiment/RunnerConfig.py:122-131): rank 0 starts it on device ``dev`` and publishes
+        its URL on the job's c10d store; the other ranks wait for that URL and reuse the server.  Before
+        preloading, the server's footprint (plus the co-located on-device server's, when ``dev`` is also a
+        client GPU) is checked against the card's HBM."""
+        s = self.settings
+        self.remote_shares_gpu = dev.isdigit() and self._gpu_index() == int(dev)
+        store = _dist_store() if int(getattr(self, "dp_world", 1) or 1) > 1 else None
+        key = REMOTE_URL_KEY.format(name=s.name)
+        if self.rank != 0:
+            if store is None:
+                raise RuntimeError("a data-parallel rank > 0 needs the job's store to find the remote server")
+            val = store.get(key).decode()  # blocks until rank 0 publishes (bounded by the store timeout)
+            if val.startswith("error:"):
+                raise RuntimeError(f"rank 0 could not start the remote server: {val[6:]}")
+            _wait_alive(val, s.server_start_timeout_s, None, list(s.models))
+            return val
+        try:
+            backend = s.remote_backend or ""
+            if backend != "fake" and dev.isdigit():
+                need = server_footprint_bytes(list(s.models), s.max_batch, s.max_context)
+                world = int(getattr(self, "dp_world", 1) or 1)
+                # rank r's on-device server lives on GPU r (LOCAL_RANK) in a data-parallel job
+                co_located = "on_device" in s.methods and (int(dev) < world if world > 1 else self.remote_shares_gpu)
+                if co_located:
+                    need += server_footprint_bytes(list(s.models), s.max_batch, s.max_context, s.weights, s.kv)
+                if need > GPU_MEM_BYTES:
+                    raise RuntimeError(f"remote server on GPU {dev} needs {need / 1e9:.0f} GB"
+                                       f"{' with the co-located on-device server' if co_located else ''}"
+                                       f" > {GPU_MEM_BYTES / 1e9:.0f} GB of HBM")
+            port = s.port_base + 101
             env = {"HIP_VISIBLE_DEVICES": dev} if dev.isdigit() else {}
             device = "cuda:0" if dev.isdigit() else dev
-            self.remote_shares_gpu = dev.isdigit() and self._gpu_index() == int(dev)
-            srv = _ServerProc(["--host", "127.0.0.1", "--port", str(port), "--models", ",".join(s.models),
-                               "--device", device, "--max-batch", str(s.max_batch), "--max-context",
-                               str(s.max_context), "--preload"], log_dir / f"remote_rank{self.rank}.log", env)
+            args = ["--host", "127.0.0.1", "--port", str(port), "--models", ",".join(s.models), "--device", device,
+                    "--max-batch", str(s.max_batch), "--max-context", str(s.max_context)]
+            if backend:
+                args += ["--backend", backend]
+            if backend == "fake":
+                args += ["--fake-tok-s", str(s.remote_fake_tok_s), "--fake-prefill-s", str(s.remote_fake_prefill_s)]
+            else:
+                args.append("--preload")
+            srv = _ServerProc(args, log_dir / "remote_node.log", env)
             self._servers.append(srv)
             atexit.register(srv.stop)
             url = f"http://127.0.0.1:{port}"
             _wait_alive(url, s.server_start_timeout_s, srv.proc, list(s.models))
-            return url
-        return spec if "://" in spec else f"http://{spec}"
+        except Exception as exc:
+            if store is not None:
+                store.set(key, f"error:{exc}")
+            raise
+        if store is not None:
+            store.set(key, url)
+        output.console_log(f"remote server {url} on device {dev} (one per node, shared by {getattr(self, 'dp_world', 1)} ranks)")
+        return url
 
     def teardown_rank(self) -> None:
         for srv in self._servers:
@@ -449,11 +538,18 @@ class _StudyBase:
 
     def populate_run_data(self, context: RunnerContext) -> Optional[Dict[str, Any]]:
         r = getattr(self, "__energy_reading__", None)
+        gpu = round(r.gpu_usage, 3) if r is not None and r.gpu_usage == r.gpu_usage else 0.0
+        # gpu_usage is the CLIENT device's GPU residency (reference experiment/RunnerConfig.py:207-226: the M2's
+        # own GPU while curl waited on the remote server).  When the remote server shares this rank's GPU the
+        # board's activity is the server's: the client process never opens the GPU, so its own residency is 0 and
+        # the measured activity goes to server_gpu_usage instead.
+        shared = context.run_variation.get("method") == "remote" and self.remote_shares_gpu
+        self._server_gpu_usage = gpu if shared else ""
         data: Dict[str, Any] = {
             "topic": self.topic,
             "execution_time": (self.timestamp_end - self.timestamp_start).total_seconds(),
             "cpu_usage": round(r.cpu_usage, 3) if r is not None else "",
-            "gpu_usage": round(r.gpu_usage, 3) if r is not None and r.gpu_usage == r.gpu_usage else 0.0,
+            "gpu_usage": 0.0 if shared else gpu,
             "memory_usage": round(r.memory_usage, 3) if r is not None else "",
         }
         self._last_stats = self.response.stats() if self.response is not None else {}
@@ -523,5 +619,6 @@ class StudyConfig(_MeasuredStudy):
             "gen_time_s": round(st.get("server_eval_s", 0.0) + st.get("server_prompt_eval_s", 0.0), 6),
             "device": str(getattr(self, "energy_devices", [""])[0]) if getattr(self, "energy_devices", None) else "",
             "server": self.url,
+            "server_gpu_usage": getattr(self, "_server_gpu_usage", ""),
         })
         return data

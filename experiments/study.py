@@ -4,7 +4,8 @@ repetitions (1,260 runs, reference experiment/RunnerConfig.py:66-87), trials fan
     python -m cain_amd experiments/study.py --gpus 8
 
 Every rank starts its own on-device server on its GPU; the remote arm talks to ``SERVER_IP`` from ``.env``
-(or a modelled server when unset; ``CAIN_STUDY_REMOTE=local:<gpu>`` serves it from another GPU of the node).
+(or a modelled server when unset; ``CAIN_STUDY_REMOTE=local:<gpu>`` serves it from one engine server on that GPU
+of the node, started once by rank 0 and shared by every rank).
 """
 from cain_amd.experiments import StudyConfig, StudySettings
 

@@ -54,6 +54,48 @@ def test_study_config_runs_both_arms(tmp_path, gpus):
     assert (tmp_path / "full_factorial" / "analysis" / "results.json").exists()
 
 
+def test_study_eight_ranks_share_one_remote_server(tmp_path):
+    """The real StudyConfig at 8 data-parallel ranks (gloo, modelled servers): ONE remote server for the node
+    (rank 0 starts it and publishes its URL on the job's store; the reference has one server every trial talks
+    to), each rank's energy sampler on a core of its own, and a single writer of run_table.csv."""
+    import json
+
+    from cain_amd.energy.meter import sampler_core
+
+    base = 23000 + os.getpid() % 1000
+    r = subprocess.run([sys.executable, "-m", "cain_amd", str(ROOT / "experiments" / "study.py"), "--gpus", "8"],
+                       capture_output=True, text=True, timeout=900, cwd=ROOT,
+                       env=_env(tmp_path, CAIN_STUDY_PORT_BASE=str(base), CAIN_STUDY_REPETITIONS="8",
+                                CAIN_STUDY_DEVICE_BACKEND="fake", CAIN_STUDY_REMOTE="local:cpu",
+                                CAIN_STUDY_REMOTE_BACKEND="fake", CAIN_STUDY_REMOTE_FAKE_TOK_S="2000",
+                                CAIN_STUDY_REMOTE_FAKE_PREFILL_S="0", CAIN_STUDY_IDLE_BASELINE_S="0"))
+    assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-4000:]
+    out = tmp_path / "full_factorial"
+    rows = list(csv.DictReader(open(out / "run_table.csv")))
+    assert len(rows) == 16 and all(x["__done"] == "DONE" for x in rows)
+    remote = [x for x in rows if x["method"] == "remote"]
+    assert len({x["server"] for x in remote}) == 1, {x["server"] for x in remote}
+    logs = sorted(p.name for p in (out / "servers").iterdir())
+    assert "remote_node.log" in logs and not any(n.startswith("remote_rank") for n in logs), logs
+    assert sum(n.startswith("on_device_rank") for n in logs) == 8
+    # single writer: only rank 0 commits rows
+    commits = [ln for ln in r.stdout.splitlines() if "committed" in ln]
+    assert commits and all("rank 0/8" in ln for ln in commits), commits[:5]
+    # distinct sampler cores: on-device rows name their rank's server port (port_base + 1 + rank)
+    cores = {}
+    for x in rows:
+        if x["method"] != "on_device":
+            continue
+        rank = int(x["server"].rsplit(":", 1)[1]) - base - 1
+        core = json.load(open(out / x["__run_id"] / "energy.json"))["sampler_core"]
+        assert core == sampler_core(rank), (rank, core)
+        cores.setdefault(rank, set()).add(core)
+    assert len(cores) >= 2
+    if len(os.sched_getaffinity(0)) >= 8:
+        flat = [next(iter(c)) for c in cores.values()]
+        assert len(set(flat)) == len(flat), cores
+
+
 @pytest.mark.gpu
 def test_study_on_device_arm_on_gpu_measures_energy(tmp_path):
     """On the GPU box: the per-rank server runs the HIP engine, the window reads the amd-smi accumulator."""
@@ -100,4 +142,8 @@ def test_study_both_arms_against_real_engine_servers(tmp_path):
     assert all(float(x["tok_per_s"]) > 150 for x in remote), [x["tok_per_s"] for x in remote]
     assert all(float(x["gpu_energy_J"]) == 0.0 for x in remote)
     assert all(float(x["gpu_energy_J"]) > 0 for x in local)
+    # gpu_usage keeps the reference meaning (the client's own GPU residency: none, the client never opens the
+    # GPU); the shared board's activity is the server's and goes to server_gpu_usage
+    assert all(float(x["gpu_usage"]) == 0.0 and float(x["server_gpu_usage"]) > 0 for x in remote)
+    assert all(x["server_gpu_usage"] == "" for x in local)
     assert all(x["server"] != local[0]["server"] for x in remote)

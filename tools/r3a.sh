@@ -1,0 +1,9 @@
+set -o pipefail
+export TMPDIR=/tmp
+mkdir -p gpurun_out/r3a
+tools/gpu_steps.sh r3a \
+ "b1_qwen|300|rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r3a/pq -o run -- python3 bench.py --model qwen2:1.5b --batch 1 --steps 1 --warmup 1 --no-energy --no-single" \
+ "b1_gemma|300|rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r3a/pg -o run -- python3 bench.py --model gemma:2b --batch 1 --steps 1 --warmup 1 --no-energy --no-single" \
+ "b1_llama_fp8|300|python3 bench.py --batch 1 --steps 2 --warmup 1 --weights fp8 --no-single" \
+ "b1_llama|300|python3 bench.py --batch 1 --steps 2 --warmup 1 --no-single"
+find gpurun_out/r3a -name "*kernel_trace.csv" -delete
