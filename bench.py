@@ -262,9 +262,9 @@ def main() -> int:
                                         if base_jpt and not math.isnan(energy) and energy > 0 else None),
             "single_stream_vs_baseline_J_per_token": (round(base_jpt / ss_j_mean, 3)
                                                       if base_jpt and not math.isnan(ss_j_mean) else None),
-            # start-up autotune of the wide-batch GEMM plans: N x K @ rows -> splits x ring variant (us)
-            "wgemm_plans": {f"{t['n']}x{t['k']}@{t['m']}": f"{t['ks']}x{t['variant']} ({t['us']} us)"
-                            for t in getattr(eng, "wgemm_tuning", [])},
+            # wide-batch GEMM plans in use: N x K @ rows -> k-splits x ring variant (csrc/wgemm.hip)
+            "wgemm_plans": {f"{t['n']}x{t['k']}@{t['m']}": f"{t['ks']}x{t['variant']}"
+                            for t in getattr(eng, "wgemm_plans", [])},
         }
         print(json.dumps(out), flush=True)
     if meter:

@@ -108,8 +108,9 @@ def lt_min_rows(max_batch: int, weight_dtype: str = "bf16") -> int:
     """Row count from which a forward runs its O and gate/up projections on hipBLASLt (0: never, the default).
 
     Off by default since the hand-written wide-batch kernel (csrc/wgemm.hip) took over 64 < M <= 256
-    (profiles/wgemm_r2.md); ``CAIN_LT_MIN_ROWS=128`` brings the library path back for A/B runs.  The fp8 weight
-    path has no library equivalent."""
+    (profiles/wgemm_r2.md); ``CAIN_LT_MIN_ROWS=128`` brings the library path back for A/B runs, which loads the
+    opt-in ``libcain_blas.so`` (``python -m cain_amd.build --blas``; the default library links no vendor GEMM).
+    The fp8 weight path has no library equivalent."""
     v = int(os.environ.get("CAIN_LT_MIN_ROWS", "0"))
     if v <= 0 or weight_dtype != "bf16" or max_batch < v:
         return 0
@@ -238,6 +239,8 @@ class DecodeEngine:
         # 23 vs 39 us and 66 vs 103 us at 256 rows on llama3.1:8b, profiles/lt_gemm.md); it needs plain
         # row-major copies of those two weights beside the MFMA packing
         lt_rows = lt_min_rows(self.max_batch, self.weight_dtype)
+        if lt_rows > 0:
+            ops.enable_lt()  # the opt-in hipBLASLt library (A/B runs only; csrc_blas/blas.hip)
         w8a8 = self.w8a8 and max(self.max_batch, self.prefill_chunk) > W8A8_MIN_ROWS
         packed = pack_for_engine(self.weights, free_natural=not self.keep_natural, weight_dtype=self.weight_dtype,
                                  plain_lt=lt_rows > 0, w8a8=w8a8,
@@ -293,9 +296,9 @@ class DecodeEngine:
         for k in ("x", "q", "attn", "act", "logits", "counters"):
             setattr(d, k, _ptr(self.buf[k]))
         d.part_o, d.part_ml = _ptr(self.part_o), _ptr(self.part_ml)
-        self.wgemm_tuning = self._tune_wide_gemm(packed, R)
-        # batched GEMM (16 < M <= 128) split-K workspace: largest need over this model's GEMM shapes (after the
-        # autotune, which may pick larger split counts than the default rule)
+        self.wgemm_plans = self._wide_gemm_plans(R)
+        # batched GEMM (16 < M <= 128) split-K workspace: largest need over this model's GEMM shapes (after any
+        # CAIN_WGEMM_PLANS override, which may pick larger split counts than the default rule)
         shapes = [(cfg.qkv_dim, cfg.d_model), (cfg.d_model, cfg.q_dim), (2 * cfg.ffn, cfg.d_model),
                   (cfg.d_model, cfg.ffn), (cfg.vocab, cfg.d_model)]
         ws = max([ops.gemm_ws_bytes(n, k, m) for n, k in shapes for m in range(17, R + 1)] + [0])
@@ -322,32 +325,25 @@ class DecodeEngine:
         self._graphs: Dict[tuple, int] = {}
         self.stream = torch.cuda.Stream(device=dev)
 
-    def _tune_wide_gemm(self, packed, R: int) -> list:
-        """Start-up autotune of the wide-batch GEMM plans (split count, ring variant) for this model's projection
-        shapes, timed on its own layer weights (ops.tune_wide_gemm) at the row tiles the engine will run: the
-        max batch (256-row tile when > 128) and the 128-row prefill chunk.  Opt-in (CAIN_WGEMM_TUNE=1): on the
-        headline bench the tuned plans (faster in isolation, e.g. O at 5 splits 25.5 us vs 30.5) measured 23.5k
-        vs 23.9k tok/s untuned on the same box -- the isolated winner is not the in-graph winner, so the default
-        rule stays.  Runs before any graph capture and before the GEMM workspace is sized."""
+    def _wide_gemm_plans(self, R: int) -> list:
+        """Split plans of the wide-batch GEMM (csrc/wgemm.hip) this engine runs, per projection shape at its
+        widest forward: the default rule, or ``CAIN_WGEMM_PLANS="N:K:BM:KS[:VARIANT],..."`` (explicit per-shape
+        plans for in-graph A/B runs; measured in the graph-replayed decode, never by isolated timings -- an
+        isolated autotune's winners did not move the headline, profiles/wgemm_r2.md)."""
         from .. import ops
-        # CAIN_WGEMM_PLANS="N:K:BM:KS[:VARIANT],...": explicit per-shape plans (in-graph A/B of split counts)
         for spec in filter(None, os.environ.get("CAIN_WGEMM_PLANS", "").split(",")):
             f = [int(x) for x in spec.split(":")]
             ops.set_wide_gemm_plan(f[0], f[1], f[2], f[3], f[4] if len(f) > 4 else -1)
-        if self.weight_dtype != "bf16" or os.environ.get("CAIN_WGEMM_TUNE", "0") != "1":
-            return []
         cfg = self.cfg
-        layers = packed["layers"]
-        act = ops.EPI_GELU if cfg.act == "gelu_tanh" else ops.EPI_SILU
-        cases = [(cfg.qkv_dim, cfg.d_model, ops.EPI_BF16, True, [lp["wqkv"] for lp in layers]),
-                 (cfg.d_model, cfg.q_dim, ops.EPI_RESID, False, [lp["wo"] for lp in layers]),
-                 (2 * cfg.ffn, cfg.d_model, act, True, [lp["wgu"] for lp in layers]),
-                 (cfg.d_model, cfg.ffn, ops.EPI_RESID, False, [lp["wdown"] for lp in layers])]
-        if self.max_batch > 128:
-            cases.append((cfg.vocab, cfg.d_model, ops.EPI_F32, True, [packed["lm_head"]]))
-        rows = sorted({m for m in (self.max_batch, min(R, 128)) if m > 64})
-        with torch.cuda.device(self.device):
-            return [r for m in rows for r in ops.tune_wide_gemm(cases, m)]
+        shapes = [(cfg.qkv_dim, cfg.d_model), (cfg.d_model, cfg.q_dim), (2 * cfg.ffn, cfg.d_model),
+                  (cfg.d_model, cfg.ffn), (cfg.vocab, cfg.d_model)]
+        out = []
+        if self.weight_dtype == "bf16" and R > 64:
+            for n, k in shapes:
+                if ops.wide_gemm_eligible(n, k, R):
+                    ks, v = ops.wide_gemm_plan(n, k, R)
+                    out.append(dict(n=n, k=k, m=R, ks=ks, variant=v))
+        return out
 
     def _plan(self, M: int) -> int:
         """One native plan per attention split count (nsplit depends on the row count)."""
@@ -736,10 +732,12 @@ class ContinuousBatch:
         for h in dead:
             self.free_slots.append(self.row_slot[h])
         if moves:
-            src = torch.tensor(list(moves.keys()), device=eng.device, dtype=torch.long)
-            dst = torch.tensor(list(moves.values()), device=eng.device, dtype=torch.long)
             r = eng.rows
             with torch.cuda.stream(eng.stream):
+                # index tensors made on the engine's stream: the copies below run there, so the caching allocator
+                # cannot hand these blocks out again before the gathers have read them
+                src = torch.tensor(list(moves.keys()), device=eng.device, dtype=torch.long)
+                dst = torch.tensor(list(moves.values()), device=eng.device, dtype=torch.long)
                 for key in ("tok", "pos", "slot", "n_gen", "max_new", "done"):
                     r[key][dst] = r[key][src]
                 h64 = r["hist"].view(-1, 64)

@@ -14,8 +14,8 @@ op                     source                      replaces (Ollama/llama.cpp)
                        csrc/wgemm.hip              fused RMSNorm, residual epilogue (wgemm: the
                                                    LDS-DMA ring kernel for 64 < M <= 256 rows)
 ``qkv_rope``           csrc/gemm.hip               QKV GEMV + bias + RoPE + KV-cache append
-``lt_gemm``            csrc/blas.hip               O / gate-up GEMM at >= 128 rows (hipBLASLt)
-``rownorm_act``        csrc/blas.hip               RMSNorm scale + SiLU/GeLU*up after lt_gemm
+``lt_gemm``            csrc_blas/blas.hip          hipBLASLt GEMM (opt-in libcain_blas.so, A/B runs only)
+``rownorm_act``        csrc_blas/blas.hip          RMSNorm scale + SiLU/GeLU*up after lt_gemm (opt-in)
 ``rmsnorm``            csrc/norm.hip               RMSNorm (standalone; the engine fuses it)
 ``embed``              csrc/norm.hip               embedding gather (+Gemma scale)
 ``attention``          csrc/attention.hip          decode / prefill attention (split-K, in-kernel combine)
@@ -86,9 +86,7 @@ def load() -> ctypes.CDLL:
         lib.cain_wgemm_eligible.argtypes = [ci, ci, ci]
         lib.cain_wgemm_set_shape.argtypes = [ci, ci, ci, ci, ci]
         lib.cain_wgemm_plan.argtypes = [ci, ci, ci]
-        lib.cain_lt_gemm.argtypes = [vp, vp, ci, ci, ci, ci, vp, ci, ci, vp, ctypes.c_longlong, vp]
-        lib.cain_lt_prepare.argtypes = [ci, ci, ci, ci, ci, ci, ctypes.c_longlong]
-        lib.cain_rownorm_act.argtypes = [vp, ci, ci, cf, ci, vp, ci, vp, ci, ci, ci, ci, vp]
+        lib.cain_set_lt_api.argtypes = [vp]
         lib.cain_rmsnorm.argtypes = [vp, ci, vp, vp, ci, ci, ci, cf, vp]
         lib.cain_embed.argtypes = [vp, vp, vp, ci, ci, ci, cf, vp]
         lib.cain_attention.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp, ci, ci, ci, ci, ci, ci, ci, cf, vp]
@@ -169,56 +167,6 @@ def wide_gemm_plan(n: int, k: int, m: int) -> Optional[tuple]:
     """(split count, ring variant) the next wide-GEMM launch of this shape uses; None if not eligible."""
     v = int(load().cain_wgemm_plan(n, k, m))
     return None if v < 0 else (v // 16, v % 16)
-
-
-#: ring variants the autotune tries (csrc/wgemm.hip wg_launch_v): 0 = default ring, 2 = shallower W ring
-TUNE_VARIANTS = (0, 2)
-
-
-def tune_wide_gemm(cases, m: int, iters: int = 2, candidates=(2, 3, 4, 5, 6, 8, 10, 12, 16)) -> list:
-    """Pick each wide-GEMM shape's split count and ring variant by timing the candidates on real weights.
-
-    ``cases``: (n, k, epi, norm, [packed weights]) -- one packed matrix per layer; every candidate cycles through
-    all of them so, as in a decode step, each launch streams its weights from HBM rather than a warm cache.
-    ``m``: rows (the tile class 128 / 256 follows from it).  Unsplit shapes (>= 128 column blocks) only get the
-    ring variant tuned.  Returns one dict per shape (chosen plan, time per call of every candidate, in us) and
-    installs the winners with ``set_wide_gemm_plan``.
-    """
-    load()
-    bm = 256 if m > 128 else 128
-    out = []
-    for n, k, epi, norm, wps in cases:
-        if not wide_gemm_eligible(n, k, m) or not wps:
-            continue
-        dev = wps[0].device
-        g = torch.Generator(device=dev).manual_seed(n ^ k)
-        x = (torch.randn(m, k, device=dev, generator=g) * 2).bfloat16()
-        n_out = n // 2 if epi in (EPI_SILU, EPI_GELU) else n
-        y = torch.zeros(m, n_out, device=dev, dtype=torch.float32 if epi == EPI_F32 else torch.bfloat16)
-        nblk = (n // 16 + 7) // 8
-        splits = [1] if nblk >= 128 else [c for c in candidates if k // 64 // c >= 4]
-        times = {}
-        for ks in splits:
-            for v in TUNE_VARIANTS:
-                set_wide_gemm_plan(n, k, bm, ks, v)
-                if wide_gemm_plan(n, k, m) != (ks, v):
-                    continue  # clamped to a plan already timed
-                for wp in wps[:2]:
-                    skinny_gemm(wp, x, n, epi, out=y, norm=norm)
-                torch.cuda.synchronize(dev)
-                a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                a.record()
-                for _ in range(iters):
-                    for wp in wps:
-                        skinny_gemm(wp, x, n, epi, out=y, norm=norm)
-                b.record()
-                torch.cuda.synchronize(dev)
-                times[(ks, v)] = a.elapsed_time(b) * 1000.0 / (iters * len(wps))
-        best = min(times, key=times.get)
-        set_wide_gemm_plan(n, k, bm, *best)
-        out.append(dict(n=n, k=k, m=m, ks=best[0], variant=best[1], us=round(times[best], 2),
-                        candidates={f"{a}x{b}": round(t, 2) for (a, b), t in sorted(times.items())}))
-    return out
 
 
 def _workspace(device, nbytes: int) -> Optional[torch.Tensor]:
@@ -486,12 +434,49 @@ def sample(logits, tok, pos, gen, n_gen, max_new, done, hist, slot, params, T_ma
 
 
 _LT_WS: dict = {}
+BLAS_LIB_PATH = HERE / "libcain_blas.so"
+_blas: Optional[ctypes.CDLL] = None
+
+
+def load_blas() -> ctypes.CDLL:
+    """The opt-in hipBLASLt A/B library (``python -m cain_amd.build --blas``); the default build has none."""
+    global _blas
+    with _lock:
+        if _blas is not None:
+            return _blas
+        if not BLAS_LIB_PATH.exists():
+            if os.environ.get("CAIN_AUTOBUILD", "1") != "0":
+                from .. import build
+                build.build_blas()
+            if not BLAS_LIB_PATH.exists():
+                raise NativeOpsUnavailable(f"{BLAS_LIB_PATH} missing: `python -m cain_amd.build --blas` (opt-in)")
+        lib = ctypes.CDLL(str(BLAS_LIB_PATH))
+        lib.cain_lt_gemm.argtypes = [vp, vp, ci, ci, ci, ci, vp, ci, ci, vp, ctypes.c_longlong, vp]
+        lib.cain_lt_prepare.argtypes = [ci, ci, ci, ci, ci, ci, ctypes.c_longlong]
+        lib.cain_rownorm_act.argtypes = [vp, ci, ci, cf, ci, vp, ci, vp, ci, ci, ci, ci, vp]
+        _blas = lib
+        return lib
+
+
+class _LtApi(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_void_p) for n in ("gemm", "prepare", "gemm_f32", "prepare_f32", "rownorm",
+                                                "rownorm_act")]
+
+
+def enable_lt() -> None:
+    """Register the hipBLASLt entries with the decode runtime (runtime.hip cain_set_lt_api): forwards with
+    >= CAIN_LT_MIN_ROWS rows then run O and gate/up on the library (A/B runs against the hand kernels)."""
+    blas = load_blas()
+    fp = lambda f: ctypes.cast(f, ctypes.c_void_p).value  # noqa: E731
+    api = _LtApi(fp(blas.cain_lt_gemm), fp(blas.cain_lt_prepare), fp(blas.cain_lt_gemm_f32),
+                 fp(blas.cain_lt_prepare_f32), fp(blas.cain_rownorm), fp(blas.cain_rownorm_act))
+    load().cain_set_lt_api(ctypes.byref(api))
 
 
 def lt_gemm(w: torch.Tensor, x: torch.Tensor, out: Optional[torch.Tensor] = None,
             accumulate: bool = False) -> torch.Tensor:
     """``out = x @ w.T`` (``out += x @ w.T`` with ``accumulate``) on hipBLASLt: w [N, K], x [M, K] bf16
-    row-major; the engine's wide-batch O and gate/up projections (csrc/blas.hip)."""
+    row-major, on the opt-in library (csrc_blas/blas.hip, ``load_blas``)."""
     _gpu(w, x, out)
     N, K = w.shape
     M = x.shape[0]
@@ -501,7 +486,7 @@ def lt_gemm(w: torch.Tensor, x: torch.Tensor, out: Optional[torch.Tensor] = None
     ws = _LT_WS.get(x.device)
     if ws is None:
         ws = _LT_WS[x.device] = torch.zeros((64 << 20) // 4, device=x.device, dtype=torch.int32)
-    _check(load().cain_lt_gemm(_p(w), _p(x), x.stride(0), K, N, M, _p(out), out.stride(0), int(accumulate), _p(ws),
+    _check(load_blas().cain_lt_gemm(_p(w), _p(x), x.stride(0), K, N, M, _p(out), out.stride(0), int(accumulate), _p(ws),
                                ws.numel() * 4, _stream()), "cain_lt_gemm")
     return out
 
@@ -516,6 +501,6 @@ def rownorm_act(x: torch.Tensor, gu: torch.Tensor, eps: float, kind: int = 0, no
     if out is None:
         out = torch.empty(M, ffn, device=x.device, dtype=torch.bfloat16)
     assert x.stride(1) == 1 and gu.stride(1) == 1 and out.stride(1) == 1 and gu.shape[0] == M
-    _check(load().cain_rownorm_act(_p(x), x.stride(0), d, eps, int(norm), _p(gu), gu.stride(0), _p(out),
+    _check(load_blas().cain_rownorm_act(_p(x), x.stride(0), d, eps, int(norm), _p(gu), gu.stride(0), _p(out),
                                    out.stride(0), M, ffn, kind, _stream()), "cain_rownorm_act")
     return out

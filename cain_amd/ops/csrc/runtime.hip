@@ -31,12 +31,6 @@ CAIN_API int cain_gemm_w8(const void* Wp, const float* wscale, const void* X, in
                           int ldy, const float* bias, int norm, float eps, const int* slot, const int* pos,
                           const float* cos_t, const float* sin_t, void* kc, void* vtc, int H, int Hkv, int hd,
                           int T_max, int epi, hipStream_t st);
-CAIN_API int cain_lt_gemm(const void* W, const void* X, int ldx, int K, int N, int M, void* Y, int ldy, int accumulate,
-                          void* ws, long long ws_bytes, hipStream_t st);
-CAIN_API int cain_lt_prepare(int N, int K, int M, int ldx, int ldy, int accumulate, long long ws_bytes);
-CAIN_API int cain_lt_gemm_f32(const void* W, const void* X, int ldx, int K, int N, int M, float* Y, int ldy, void* ws,
-                              long long ws_bytes, hipStream_t st);
-CAIN_API int cain_lt_prepare_f32(int N, int K, int M, int ldx, int ldy, long long ws_bytes);
 CAIN_API int cain_gemm_w8a8(const void* Wp8, const float* wscale, const void* X8, int ld8, const float* xs, int K,
                             int N, int M, void* Y, int ldy, const float* bias, const int* slot, const int* pos,
                             const float* cos_t, const float* sin_t, void* kc, void* vtc, int H, int Hkv, int hd,
@@ -44,9 +38,6 @@ CAIN_API int cain_gemm_w8a8(const void* Wp8, const float* wscale, const void* X8
 CAIN_API int cain_quant_rows(const void* x, int ldx, int K, int M, void* x8, int ld8, float* xs, int norm, float eps,
                              hipStream_t st);
 CAIN_API int cain_w8a8_eligible(int N, int K, int M);
-CAIN_API int cain_rownorm(const void* x, int ldx, int d, float eps, void* xn, int ldxn, int M, hipStream_t st);
-CAIN_API int cain_rownorm_act(const void* x, int ldx, int d, float eps, int norm, const void* gu, int ldgu, void* act,
-                              int ldact, int M, int ffn, int kind, hipStream_t st);
 CAIN_API int cain_embed(const int* tok, const void* E, void* out, int ldo, int M, int d, float scale, hipStream_t st);
 CAIN_API int cain_attention_ex(const void* q, const void* kc, const void* vtc, const int* slot, const int* pos,
                                float* part_o, float* part_ml, unsigned* counters, void* out, int ldo, int M, int H,
@@ -58,6 +49,20 @@ CAIN_API int cain_attention(const void* q, const void* kc, const void* vtc, cons
 CAIN_API int cain_sample(float* logits, int ldl, int V, int* tok, int* pos, int* gen, int ldg, int* n_gen,
                          const int* max_new, int* done, int* hist, const int* slot, int T_max, int M,
                          const void* params, hipStream_t st);
+
+// hipBLASLt A/B path (opt-in library libcain_blas.so, csrc_blas/blas.hip): not linked into this library; its
+// entry points are registered at run time by cain_amd.ops.enable_lt().  Unregistered (the default), every
+// forward runs the hand-written kernels.
+struct CainLtApi {
+  int (*gemm)(const void*, const void*, int, int, int, int, void*, int, int, void*, long long, hipStream_t);
+  int (*prepare)(int, int, int, int, int, int, long long);
+  int (*gemm_f32)(const void*, const void*, int, int, int, int, float*, int, void*, long long, hipStream_t);
+  int (*prepare_f32)(int, int, int, int, int, long long);
+  int (*rownorm)(const void*, int, int, float, void*, int, int, hipStream_t);
+  int (*rownorm_act)(const void*, int, int, float, int, const void*, int, void*, int, int, int, int, hipStream_t);
+};
+static CainLtApi g_lt{};
+CAIN_API void cain_set_lt_api(const CainLtApi* a) { g_lt = a ? *a : CainLtApi{}; }
 
 extern "C" {
 
@@ -164,17 +169,17 @@ thread_local char g_fail[160] = {0};
     }                                                                            \
   } while (0)
 
-bool lt_rows(const CainPlanDesc& d, int M) { return d.lt_min_rows > 0 && M >= d.lt_min_rows && !d.w8 && d.gu; }
+bool lt_rows(const CainPlanDesc& d, int M) { return g_lt.gemm && d.lt_min_rows > 0 && M >= d.lt_min_rows && !d.w8 && d.gu; }
 
 // hipBLASLt heuristics allocate and synchronise: resolve them before a stream capture
 int lt_prepare(const Plan& p, int M) {
   const CainPlanDesc& d = p.d;
   if (!lt_rows(d, M) || p.layers.empty()) return 0;
   const int q_dim = d.H * d.hd;
-  if (p.layers[0].wo_lt) CK(cain_lt_prepare(d.d, q_dim, M, q_dim, d.d, 1, d.lt_ws_bytes));
-  if (p.layers[0].wgu_lt) CK(cain_lt_prepare(2 * d.ffn, d.d, M, d.d, 2 * d.ffn, 0, d.lt_ws_bytes));
+  if (p.layers[0].wo_lt) CK(g_lt.prepare(d.d, q_dim, M, q_dim, d.d, 1, d.lt_ws_bytes));
+  if (p.layers[0].wgu_lt) CK(g_lt.prepare(2 * d.ffn, d.d, M, d.d, 2 * d.ffn, 0, d.lt_ws_bytes));
   // no library algorithm for the fp32-output LM head is not an error: forward() falls back to the hand GEMM
-  if (d.lm_head_lt && d.xn) (void)cain_lt_prepare_f32(d.V, d.d, M, d.d, d.V, d.lt_ws_bytes);
+  if (d.lm_head_lt && d.xn) (void)g_lt.prepare_f32(d.V, d.d, M, d.d, d.V, d.lt_ws_bytes);
   return 0;
 }
 
@@ -213,12 +218,12 @@ int forward(const Plan& p, int M, const CainRows& r, int want_logits, int want_s
     CK(cain_attention_ex(d.q, kc, vc, r.slot, r.pos, d.part_o, d.part_ml, d.counters, d.attn, q_dim, M, d.H, d.Hkv,
                          d.hd, d.T_max, d.nsplit, d.attn_scale, d.kv8, 1.f, 1.f, st));
     if (lt && L.wo_lt)
-      CK(cain_lt_gemm(L.wo_lt, d.attn, q_dim, q_dim, d.d, M, d.x, d.d, 1, d.lt_ws, d.lt_ws_bytes, st));
+      CK(g_lt.gemm(L.wo_lt, d.attn, q_dim, q_dim, d.d, M, d.x, d.d, 1, d.lt_ws, d.lt_ws_bytes, st));
     else
       CK(gemm(L.wo, L.wo8, L.so, d.attn, q_dim, q_dim, d.d, d.x, d.d, nullptr, 0, nullptr, nullptr, /*EPI_RESID*/ 1));
     if (lt && L.wgu_lt) {
-      CK(cain_lt_gemm(L.wgu_lt, d.x, d.d, d.d, 2 * d.ffn, M, d.gu, 2 * d.ffn, 0, d.lt_ws, d.lt_ws_bytes, st));
-      CK(cain_rownorm_act(d.x, d.d, d.d, d.eps, 1, d.gu, 2 * d.ffn, d.act, d.ffn, M, d.ffn, d.act_kind, st));
+      CK(g_lt.gemm(L.wgu_lt, d.x, d.d, d.d, 2 * d.ffn, M, d.gu, 2 * d.ffn, 0, d.lt_ws, d.lt_ws_bytes, st));
+      CK(g_lt.rownorm_act(d.x, d.d, d.d, d.eps, 1, d.gu, 2 * d.ffn, d.act, d.ffn, M, d.ffn, d.act_kind, st));
     } else {
       CK(gemm(L.wgu, L.wgu8, L.sgu, d.x, d.d, d.d, 2 * d.ffn, d.act, d.ffn, nullptr, 1, nullptr, nullptr, epi_act));
     }
@@ -228,8 +233,8 @@ int forward(const Plan& p, int M, const CainRows& r, int want_logits, int want_s
   if (want_logits) {
     int e = -2;
     if (lt && d.lm_head_lt && d.xn) {
-      CK(cain_rownorm(d.x, d.d, d.d, d.eps, d.xn, d.d, M, st));
-      e = cain_lt_gemm_f32(d.lm_head_lt, d.xn, d.d, d.d, d.V, M, d.logits, d.V, d.lt_ws, d.lt_ws_bytes, st);
+      CK(g_lt.rownorm(d.x, d.d, d.d, d.eps, d.xn, d.d, M, st));
+      e = g_lt.gemm_f32(d.lm_head_lt, d.xn, d.d, d.d, d.V, M, d.logits, d.V, d.lt_ws, d.lt_ws_bytes, st);
       if (e > 0) CK(e);  // a library failure; no plan / unsupported shape (< 0) falls back
     }
     if (e != 0) CK(gemm(d.lm_head, d.lm_head8, d.lm_head_scale, d.x, d.d, d.d, d.V, d.logits, d.V, nullptr, 1, nullptr,

@@ -226,7 +226,11 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(
       }
       float zc = 0.f;
       for (int i = 0; i < cut; ++i) zc += __expf(sv[i] * invT - mx);
-      const uint64_t r = mix64(P.seed ^ mix64(uint64_t(m) * 0x632BE59BD9B4E019ull + uint64_t(ng)));
+      // the random stream is keyed by the request's seed and its token index only, not by the batch row: a
+      // request that continuous batching moves to another row (ContinuousBatch.retire) keeps its stream, so an
+      // Ollama `seed` reproduces the same tokens however the batch is packed (rows without a seed get a unique
+      // one on the host, engine._row_options)
+      const uint64_t r = mix64(P.seed ^ mix64(uint64_t(ng) * 0x632BE59BD9B4E019ull + 0x9E3779B97F4A7C15ull));
       const float u = float(r >> 40) * (1.0f / 16777216.0f) * zc;
       float c = 0.f;
       int pick = si[cut - 1];

@@ -379,8 +379,8 @@ struct WgPlan {
 // at least 4 stages per split.  Column-block counts >= 128 (gate/up, LM head) run unsplit.
 int g_wg_target = -1, g_wg_ksmax = -1;
 
-// Per-shape plan overrides (split count, ring variant) keyed by (N, K, row tile): written by the engine's start-up
-// autotune (ops.tune_wide_gemm times the candidates on the model's own weights) before any graph is captured.
+// Per-shape plan overrides (split count, ring variant) keyed by (N, K, row tile): set before any graph is captured
+// (engine CAIN_WGEMM_PLANS, tools/wgemm_bench.py) for in-graph A/B runs of split plans.
 // The default split rule is a heuristic; measured on one box at 256 rows, the O projection (N = K = 4096) ran
 // 24.7 us at 6 splits against 29.4 at 8 and 29.5 at 4, and the best split and ring differ per shape.
 struct WgShape {

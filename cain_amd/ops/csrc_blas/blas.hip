@@ -1,3 +1,8 @@
+// OPT-IN A/B build (``python -m cain_amd.build --blas`` -> cain_amd/ops/libcain_blas.so): the default kernel
+// library has no hipBLASLt dependency and the headline runs hand-written kernels only.  Loading this library
+// (cain_amd.ops.enable_lt) registers these entries with the runtime (runtime.hip cain_set_lt_api), which then
+// sends O and gate/up of forwards with >= CAIN_LT_MIN_ROWS rows here -- for A/B runs against the hand kernels.
+//
 // Library-GEMM path for the wide decode batches (M >= 128 rows): hipBLASLt for the plain GEMM, one
 // hand-written row kernel for what the fused MFMA bodies did in their epilogue.
 //
@@ -22,7 +27,7 @@
 #include <mutex>
 #include <tuple>
 
-#include "common.h"
+#include "../csrc/common.h"
 
 namespace {
 

@@ -119,14 +119,17 @@ def run_rank(config_path: str, rank: int, world: int, isolation: Optional[str] =
         EventSubscriptionController.raise_event(RunnerEvents.BEFORE_EXPERIMENT)
         passes = 1 + max(0, int(retry_failed))
         store = dist.distributed_c10d._get_default_store()
+        hb = _Heartbeat(store, rank)
         for p in range(passes):
-            failed = _work_queue(store, f"cain/{p}/", todo_ids, by_id, ctrl, config, writer, world)
+            failed = _work_queue(store, f"cain/{p}/", todo_ids, by_id, ctrl, config, writer, world, rank=rank,
+                                 deadline_s=pg_timeout_s)
             retry = [failed if writer else None]
             dist.broadcast_object_list(retry, src=0)
             todo_ids = retry[0]
             if not todo_ids or p + 1 >= passes:
                 break
             output.console_log_WARNING(f"retrying {len(todo_ids)} failed runs (pass {p + 2}/{passes})")
+        hb.close()
         dist.barrier()
         if writer:
             output.console_log_OK("Experiment completed...")
@@ -147,12 +150,41 @@ def run_rank(config_path: str, rank: int, world: int, isolation: Optional[str] =
             pass
 
 
+class _Heartbeat:
+    """A rank's liveness counter on the job's store (``cain/hb/<rank>``), bumped by a daemon thread: the writer
+    tells a rank that died (its counter stops) from one that is merely busy with a long run."""
+
+    def __init__(self, store, rank: int, period_s: float = 2.0):
+        import threading
+
+        self.store, self.key, self.period = store, f"cain/hb/{rank}", period_s
+        self._stop = threading.Event()
+        self._t = threading.Thread(target=self._run, daemon=True)
+        self._t.start()
+
+    def _run(self) -> None:
+        while not self._stop.is_set():
+            try:
+                self.store.add(self.key, 1)
+            except Exception:  # pragma: no cover - the store went away with the job
+                return
+            self._stop.wait(self.period)
+
+    def close(self) -> None:
+        self._stop.set()
+
+
 def _work_queue(store, prefix: str, todo_ids: List[str], by_id: Dict[str, Dict[str, Any]], ctrl, config,
-                writer: bool, world: int, poll_s: float = 0.2) -> List[str]:
-    """One pass over ``todo_ids`` as a shared queue.  Every rank claims indices with ``store.add`` and publishes
-    each finished row (pickled; None = the run failed) under ``<prefix>res/<index>``; the writer commits what is
-    published between its own runs and, after its last one, until every index is in.  Returns, on the writer,
-    the run ids that failed in this pass."""
+                writer: bool, world: int, poll_s: float = 0.2, rank: int = 0, hb_timeout_s: float = 60.0,
+                deadline_s: float = 3600.0) -> List[str]:
+    """One pass over ``todo_ids`` as a shared queue.  Every rank claims indices with ``store.add`` (recording
+    the claim under ``<prefix>claim/<index>``) and publishes each finished row (pickled; None = the run failed)
+    under ``<prefix>res/<index>``; the writer commits what is published between its own runs and, after its last
+    one, until every index is in.  That final wait is bounded: an index whose claimant's heartbeat
+    (``_Heartbeat``) has stopped for ``hb_timeout_s`` is recorded as failed (its row stays TODO for a resume or
+    retry), and when nothing at all is published for ``deadline_s`` the writer records every missing index as
+    failed, names the claimants and raises (the job exits non-zero).  Returns, on the writer, the run ids that
+    failed in this pass."""
     import pickle
     import time
 
@@ -186,6 +218,7 @@ def _work_queue(store, prefix: str, todo_ids: List[str], by_id: Dict[str, Dict[s
         i = int(store.add(f"{prefix}next", 1)) - 1
         if i >= n:
             break
+        store.set(f"{prefix}claim/{i}", str(rank))
         if ran:
             ctrl.cooldown()  # per rank: overlaps with the other ranks' runs
         rid = todo_ids[i]
@@ -197,8 +230,43 @@ def _work_queue(store, prefix: str, todo_ids: List[str], by_id: Dict[str, Dict[s
         if config.operation_type is OperationType.SEMI:
             EventSubscriptionController.raise_event(RunnerEvents.CONTINUE)
     if writer:
+        last_progress = time.monotonic()
+        beats: Dict[int, tuple] = {}  # rank -> (last counter value, when it changed, writer clock)
+
+        def claimant(i: int) -> int:
+            key = f"{prefix}claim/{i}"
+            return int(store.get(key)) if store.check([key]) else -1
+
+        def alive(r: int, now: float) -> bool:
+            key = f"cain/hb/{r}"
+            v = int(store.add(key, 0)) if r >= 0 else 0
+            old = beats.get(r)
+            if old is None or old[0] != v:
+                beats[r] = (v, now)
+                return True
+            return now - old[1] < hb_timeout_s
+
         while pending:
+            before = len(pending)
             commit_published()
+            now = time.monotonic()
+            if len(pending) < before:
+                last_progress = now
+            if not pending:
+                break
+            dead = [i for i in sorted(pending) if not alive(claimant(i), now)]
+            for i in dead:
+                output.console_log_FAIL(f"run {todo_ids[i]} (queue index {i}) was claimed by rank {claimant(i)}, "
+                                        f"whose heartbeat stopped: left TODO")
+                pending.discard(i)
+                failed.append(todo_ids[i])
+            if pending and now - last_progress > deadline_s:
+                lost = sorted(pending)
+                for i in lost:
+                    failed.append(todo_ids[i])
+                pending.clear()
+                raise RuntimeError(f"no run published for {deadline_s:.0f} s; unpublished runs (left TODO): "
+                                   + ", ".join(f"{todo_ids[i]} (rank {claimant(i)})" for i in lost))
             if pending:
                 time.sleep(poll_s)
     output.console_log(f"rank ran {ran} of {n} runs in this pass ({world} ranks)")

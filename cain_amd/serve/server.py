@@ -178,14 +178,13 @@ class EngineBackend(Backend):
     def serve_queue(self, model: str, q: "queue.Queue[Job]") -> bool:
         """Continuous batching loop of one model (never returns on the HIP engine; False: not supported here,
         the scheduler falls back to static batches)."""
-        from ..engine.engine import GenResult
-
         eng = self.engine(model)
         if eng.backend != "hip":
             return False
         cb = eng.continuous()
         tok = eng.tokenizer
-        live: Dict[int, Dict[str, Any]] = {}  # row -> {job, prefill_ns, t_first}
+        # row -> {job, t0 (admission start), t_pre (prefill done), t_first (first token on the host)}
+        live: Dict[int, Dict[str, Any]] = {}
         while True:
             pending: List[Job] = []
             if cb.n == 0:
@@ -195,53 +194,74 @@ class EngineBackend(Backend):
                     pending.append(q.get_nowait())
                 except queue.Empty:
                     break
-            if pending:
-                t0 = time.perf_counter_ns()
-                try:
-                    rows = cb.admit([j.prompt for j in pending], [j.num_predict for j in pending],
-                                    [j.options for j in pending])
-                    eng.stream.synchronize()
-                except BaseException as exc:  # noqa: BLE001 - reported per job
-                    for j in pending:
-                        j.error = exc
-                        j.done.set()
-                    continue
-                dt = time.perf_counter_ns() - t0
-                for r, j in zip(rows, pending):
-                    live[r] = {"job": j, "prefill_ns": dt, "t_first": None}
             try:
-                cb.step()
-                new, fin = cb.poll()
-            except BaseException as exc:  # noqa: BLE001 - fail the live requests, start a fresh batch
+                self._cb_iteration(model, eng, cb, tok, live, pending)
+            except Exception as exc:  # noqa: BLE001 - fail every request in flight, start a fresh batch
                 for st in live.values():
                     st["job"].error = exc
                     st["job"].done.set()
-                live = {}
+                for j in pending:
+                    if not j.done.is_set():
+                        j.error = exc
+                        j.done.set()
+                live.clear()
                 cb = eng.continuous()
-                continue
-            now = time.perf_counter_ns()
-            for r, ids in enumerate(new):
-                st = live[r]
-                if ids and st["t_first"] is None:
-                    st["t_first"] = now
-                if ids and st["job"].stream is not None:
-                    st["job"].stream("".join(tok.piece(t) for t in ids))
-            done_rows = [r for r, f in enumerate(fin) if f]
-            for r in done_rows:
-                st, j = live[r], live[r]["job"]
-                toks = cb.tokens(r)
-                eos = cb.options[r]["eos_id"]
-                reason = "stop" if (eos >= 0 and toks and toks[-1] == eos) else "length"
-                t_first = st["t_first"] or now
-                j.result = GenResult(model, list(cb.prompt_tokens[r]), toks, tok.decode(toks), reason,
-                                     load_duration_ns=0, prompt_eval_duration_ns=st["prefill_ns"],
-                                     eval_duration_ns=int(now - t_first),
-                                     total_duration_ns=int(now - j.t_submit * 1e9))
-                j.ttft_ns = int(t_first - j.t_submit * 1e9)
+
+    @staticmethod
+    def _cb_iteration(model: str, eng, cb, tok, live: Dict[int, Dict[str, Any]], pending: List[Job]) -> None:
+        """One continuous-batching iteration: admit ``pending`` (each request validated on its own: a prompt over
+        the context fails that request only), then one graph chunk over every live row, then hand out tokens and
+        finish the rows that are done.  Timing matches the static path (engine._generate_hip): the newly admitted
+        rows' first token is decoded by a one-step graph and synchronised, so ``t_first`` is exact;
+        ``eval_duration`` runs from the end of admission (first token included), ``ttft`` from its start."""
+        from ..engine.engine import GenResult
+
+        ok: List[Job] = []
+        ids: List[List[int]] = []
+        for j in pending:
+            try:
+                p = eng.encode(j.prompt) or [eng.cfg.bos_id]
+                if len(p) >= eng.T_max:
+                    raise ValueError(f"prompt of {len(p)} tokens exceeds the context ({eng.T_max})")
+            except Exception as exc:  # noqa: BLE001 - reported to this request only
+                j.error = exc
                 j.done.set()
-            if done_rows:
-                moves = cb.retire(done_rows)
-                live = {moves.get(r, r): st for r, st in live.items() if r not in set(done_rows)}
+                continue
+            ok.append(j)
+            ids.append(p)
+        if ok:
+            t0 = time.perf_counter_ns()
+            rows = cb.admit(ids, [j.num_predict for j in ok], [j.options for j in ok])
+            eng.stream.synchronize()
+            t_pre = time.perf_counter_ns()
+            cb.step(1)  # the new rows' first token on its own (the live rows advance one step with them)
+            eng.stream.synchronize()
+            t_first = time.perf_counter_ns()
+            for r, j in zip(rows, ok):
+                live[r] = {"job": j, "t0": t0, "t_pre": t_pre, "t_first": t_first}
+        cb.step()
+        new, fin = cb.poll()
+        now = time.perf_counter_ns()
+        for r, new_ids in enumerate(new):
+            if new_ids and live[r]["job"].stream is not None:
+                live[r]["job"].stream("".join(tok.piece(t) for t in new_ids))
+        done_rows = [r for r, f in enumerate(fin) if f]
+        for r in done_rows:
+            st, j = live[r], live[r]["job"]
+            toks = cb.tokens(r)
+            eos = cb.options[r]["eos_id"]
+            reason = "stop" if (eos >= 0 and toks and toks[-1] == eos) else "length"
+            j.result = GenResult(model, list(cb.prompt_tokens[r]), toks, tok.decode(toks), reason,
+                                 load_duration_ns=0, prompt_eval_duration_ns=int(st["t_pre"] - st["t0"]),
+                                 eval_duration_ns=int(now - st["t_pre"]),
+                                 total_duration_ns=int(now - j.t_submit * 1e9))
+            j.ttft_ns = int(st["t_first"] - st["t0"])
+            j.done.set()
+        if done_rows:
+            moves = cb.retire(done_rows)
+            kept = {moves.get(r, r): st for r, st in live.items() if r not in set(done_rows)}
+            live.clear()
+            live.update(kept)
 
     def _traced(self, model: str, fn):
         """Run ``fn`` under torch.profiler (CPU + GPU activity) and export a Chrome trace."""

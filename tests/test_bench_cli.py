@@ -25,7 +25,7 @@ def _line(out):
     return json.loads([ln for ln in out.splitlines() if ln.startswith("{")][-1])
 
 
-@pytest.mark.parametrize("n", [1, 2, 4])
+@pytest.mark.parametrize("n", [1, 2, 4, 8])
 def test_bench_spawns_n_ranks(n):
     r = _run(["--gpus", str(n)])
     assert r.returncode == 0, r.stderr[-2000:]

@@ -89,3 +89,59 @@ def test_server_late_request_is_not_held_behind_the_running_batch():
     # the short request finished while the long one was still decoding
     assert t_short < 0.5 * t_long, (t_short, t_long)
     assert short["cain_ttft_ns"] < 0.25 * long_["total_duration"], (short["cain_ttft_ns"], long_["total_duration"])
+
+
+def test_moved_row_keeps_its_sequence():
+    """A request that retire() moves into a hole left by a finished row continues the same token stream: its
+    full sequence (sampled, fixed seed) equals a static engine.generate of the same prompt and options, because
+    the sampler keys its random stream by the request's seed, not by the row (sample.hip)."""
+    eng = DecodeEngine("tiny-llama3.1:8b", device="cuda", max_batch=4, max_context=256, seed=4, steps_per_graph=4)
+    opts = dict(temperature=0.8, top_k=40, top_p=0.9, repeat_penalty=1.1, eos_id=-1, seed=1234)
+    want = eng.generate(["the mover"], 30, [opts])[0].tokens
+    cb = eng.continuous()
+    rows = cb.admit(["short a", "short b", "the mover"], [4, 4, 30], [GREEDY, GREEDY, opts])
+    assert rows == [0, 1, 2]
+    owner = {0: "a", 1: "b", 2: "m"}
+    got = []
+    moved = False
+    for _ in range(40):
+        cb.step()
+        new, fin = cb.poll()
+        got += new[[r for r, o in owner.items() if o == "m"][0]]
+        dead = [r for r, f in enumerate(fin) if f]
+        if dead:
+            moves = cb.retire(dead)
+            moved |= any(owner[j] == "m" for j in moves)
+            owner = {moves.get(r, r): o for r, o in owner.items() if r not in dead}
+        if cb.n == 0:
+            break
+    assert moved, "the long request was expected to move into a freed row"
+    assert got == want
+    eng.close()
+
+
+def test_continuous_timing_matches_static_path():
+    """ttft / eval_duration of one request under continuous batching are taken like the static path's: the first
+    token decoded on its own (exact t_first), eval_duration from the end of admission, covering every token."""
+    be = EngineBackend(["tiny-llama3.1:8b"], device="cuda:0", max_batch=4, max_context=1024, preload=True,
+                       steps_per_graph=8)
+    body = {"model": "tiny-llama3.1:8b", "prompt": "timing probe", "stream": False,
+            "options": {"num_predict": 200, "eos_id": -1}}
+    with ServerThread(be, port=0) as srv:
+        _post(srv.url, body, {}, "w")
+        out = {}
+        _post(srv.url, body, out, "c")
+    cont = out["c"][0]
+    st = EngineBackend(["tiny-llama3.1:8b"], device="cuda:0", max_batch=4, max_context=1024, preload=True,
+                       steps_per_graph=8, continuous=False)
+    with ServerThread(st, port=0) as srv:
+        _post(srv.url, body, {}, "w")
+        out = {}
+        _post(srv.url, body, out, "s")
+    stat = out["s"][0]
+    assert cont["eval_count"] == stat["eval_count"] == 200
+    # the first token is not stamped a whole chunk late, and eval_duration covers all 200 tokens
+    assert cont["cain_ttft_ns"] < 3 * stat["cain_ttft_ns"] + 2_000_000, (cont["cain_ttft_ns"], stat["cain_ttft_ns"])
+    assert 0.5 * stat["eval_duration"] < cont["eval_duration"] < 2.0 * stat["eval_duration"] + 5_000_000, \
+        (cont["eval_duration"], stat["eval_duration"])
+    assert cont["eval_duration"] <= cont["total_duration"]

@@ -27,3 +27,14 @@ def test_energy_library_loads_without_gpu():
     lib = native.load()
     assert lib.es_sample_size() == ctypes.sizeof(native.ESample)
     assert native.init() >= 0
+
+
+def test_default_kernel_library_links_no_vendor_gemm():
+    """hipBLASLt is an opt-in A/B build (libcain_blas.so): the default library the engine and the headline load
+    needs no vendor GEMM library and exports no library-GEMM entry."""
+    import subprocess
+
+    lib = ops.load()
+    assert not hasattr(lib, "cain_lt_gemm") and hasattr(lib, "cain_set_lt_api")
+    needed = subprocess.run(["readelf", "-d", str(ops.LIB_PATH)], capture_output=True, text=True).stdout
+    assert "hipblaslt" not in needed.lower() and "rocblas" not in needed.lower(), needed

@@ -161,3 +161,91 @@ def test_fanout_one_rank_over_rccl(tmp_path):
     assert "backend nccl" in r.stdout, r.stdout[-2000:]
     rows = list(csv.DictReader(open(tmp_path / "dp" / "run_table.csv")))
     assert sum(x["__done"] == "DONE" for x in rows) == 11 and {x["rank"].strip() for x in rows if x["rank"].strip()} == {"0"}
+
+
+class _DictStore:
+    """In-process stand-in for the c10d store (add / set / get / check)."""
+
+    def __init__(self):
+        self.d = {}
+
+    def add(self, k, v):
+        self.d[k] = int(self.d.get(k, 0)) + int(v)
+        return self.d[k]
+
+    def set(self, k, v):
+        self.d[k] = v.encode() if isinstance(v, str) else v
+
+    def get(self, k):
+        v = self.d[k]
+        return v if isinstance(v, bytes) else str(v).encode()
+
+    def check(self, keys):
+        return all(k in self.d for k in keys)
+
+
+def _writer_pass(monkeypatch, store, todo, **kw):
+    from cain_amd.parallel import fanout
+    from cain_amd.runner import store as store_mod
+    from cain_amd.runner.models import OperationType
+
+    committed = []
+
+    class _CSV:
+        def __init__(self, path):
+            pass
+
+        def update_rows(self, rows):
+            committed.extend(r["__run_id"] for r in rows)
+
+    monkeypatch.setattr(store_mod, "CSVOutputManager", _CSV)
+
+    class _Ctrl:
+        path = None
+
+        def cooldown(self):
+            pass
+
+        def run_variation(self, v, commit):
+            return dict(v)
+
+    class _Cfg:
+        operation_type = OperationType.AUTO
+
+    by_id = {t: {"__run_id": t} for t in todo}
+    return fanout._work_queue(store, "cain/0/", todo, by_id, _Ctrl(), _Cfg(), True, 2, poll_s=0.01, **kw), committed
+
+
+def test_writer_does_not_wait_forever_for_a_dead_claimant(monkeypatch):
+    """a rank that claims a queue index and dies without publishing it no longer makes the writer spin
+    forever -- once the claimant's heartbeat stops, the index is recorded as failed (row left TODO)."""
+    store = _DictStore()
+    store.add("cain/0/next", 1)      # rank 1 claimed index 0 ...
+    store.set("cain/0/claim/0", "1")
+    store.add("cain/hb/1", 1)        # ... and its heartbeat never moves again
+    failed, committed = _writer_pass(monkeypatch, store, ["a", "b"], rank=0, hb_timeout_s=0.3, deadline_s=30)
+    assert failed == ["a"] and committed == ["b"]
+
+
+def test_writer_deadline_raises_and_names_the_claimant(monkeypatch):
+    """With the claimant alive but nothing published for the deadline, the writer records the missing runs and
+    raises, so the job exits non-zero instead of hanging."""
+    import threading
+
+    store = _DictStore()
+    store.add("cain/0/next", 1)
+    store.set("cain/0/claim/0", "1")
+    stop = threading.Event()
+
+    def beat():
+        while not stop.is_set():
+            store.add("cain/hb/1", 1)
+            stop.wait(0.02)
+
+    t = threading.Thread(target=beat, daemon=True)
+    t.start()
+    try:
+        with pytest.raises(RuntimeError, match=r"a \(rank 1\)"):
+            _writer_pass(monkeypatch, store, ["a", "b"], rank=0, hb_timeout_s=30, deadline_s=0.3)
+    finally:
+        stop.set()

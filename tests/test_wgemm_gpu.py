@@ -132,16 +132,3 @@ def test_shape_plan_override(ks, variant):
     finally:
         ops.clear_wide_gemm_plans()
     assert rel_err(y, ref) < 1e-5
-
-
-def test_autotune_installs_a_plan_per_shape():
-    torch.manual_seed(1)
-    K, N = 4096, 4096
-    wps = [pack_mfma_a((torch.randn(N, K, device=DEV) * 0.02).bfloat16()) for _ in range(3)]
-    try:
-        res = ops.tune_wide_gemm([(N, K, ops.EPI_RESID, False, wps)], 256, iters=1)
-        assert len(res) == 1 and res[0]["candidates"]
-        assert ops.wide_gemm_plan(N, K, 256) == (res[0]["ks"], res[0]["variant"])
-        assert res[0]["us"] == min(res[0]["candidates"].values())
-    finally:
-        ops.clear_wide_gemm_plans()
