@@ -297,11 +297,12 @@ class DecodeEngine:
             setattr(d, k, _ptr(self.buf[k]))
         d.part_o, d.part_ml = _ptr(self.part_o), _ptr(self.part_ml)
         self.wgemm_plans = self._wide_gemm_plans(R)
-        # batched GEMM (16 < M <= 128) split-K workspace: largest need over this model's GEMM shapes (after any
+        # split-K workspace of the batched / wide GEMMs and of the skinny kernel's split grids (M <= 16 on narrow
+        # outputs): largest need over this model's GEMM shapes at every row count (after any
         # CAIN_WGEMM_PLANS override, which may pick larger split counts than the default rule)
         shapes = [(cfg.qkv_dim, cfg.d_model), (cfg.d_model, cfg.q_dim), (2 * cfg.ffn, cfg.d_model),
                   (cfg.d_model, cfg.ffn), (cfg.vocab, cfg.d_model)]
-        ws = max([ops.gemm_ws_bytes(n, k, m) for n, k in shapes for m in range(17, R + 1)] + [0])
+        ws = max([ops.gemm_ws_bytes(n, k, m) for n, k in shapes for m in range(1, R + 1)] + [0])
         if w8a8:
             ws = max([ws] + [int(self.lib.cain_w8a8_ws_bytes(n, k, m)) for n, k in shapes for m in range(17, R + 1)])
             kmax = max(cfg.d_model, cfg.q_dim, cfg.ffn)

@@ -61,6 +61,9 @@ def fp8_act_roundtrip(t: torch.Tensor) -> torch.Tensor:
 class ReferenceModel:
     """Causal forward: tokens [B, T] → logits [B, T, V] (fp32).
 
+    ``compute_dtype=torch.bfloat16`` is the PyTorch bf16-eager baseline of the numerics tests: the HIP engine's
+    error against the fp32 oracle must stay within a small factor of this baseline's on the same weights.
+
     ``cache`` (a list, one ``[k, v]`` per layer, filled on first use) turns it into an incremental decoder:
     the CPU serving path of the engine uses it so a generation costs one token of compute per step.
     ``memo_weights`` keeps the compute-dtype copies of the weights (CPU serving: no per-call conversion)."""
@@ -156,6 +159,10 @@ class ReferenceModel:
         if last_only:
             x = x[:, -1:]
         x = self._norm_in(x, effective_gain(self.cfg, self.mw.final_norm))
+        if self.dt != torch.float32:
+            # reduced-precision eager baseline (tests' relative numerics criterion): bf16 everywhere the engine keeps
+            # bf16, but fp32 logits like the engine's LM head (fp32 accumulation, no bf16 rounding of the logits)
+            return x.float() @ self.mw.lm_head.float().t()
         return (x @ self._w(self.mw.lm_head).t()).float()
 
     @torch.no_grad()

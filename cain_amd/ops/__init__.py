@@ -93,6 +93,10 @@ def load() -> ctypes.CDLL:
         lib.cain_attention_ex.argtypes = ([vp, vp, vp, vp, vp, vp, vp, vp, vp, ci, ci, ci, ci, ci, ci, ci, cf, ci, cf, cf]
                                           + [vp])
         lib.cain_sample.argtypes = [vp, ci, ci, vp, vp, vp, ci, vp, vp, vp, vp, vp, ci, ci, vp, vp]
+        lib.cain_sample_ex.argtypes = [vp, ci, ci, vp, vp, vp, ci, vp, vp, vp, vp, vp, ci, ci, vp, vp,
+                                       ctypes.c_longlong, vp]
+        lib.cain_sample_ws_bytes.restype = ctypes.c_longlong
+        lib.cain_sample_ws_bytes.argtypes = [ci]
         lib.cain_plan_create.restype = vp
         lib.cain_plan_create.argtypes = [vp]
         lib.cain_plan_destroy.argtypes = [vp]
@@ -426,11 +430,32 @@ def sample_params_tensor(rows, device) -> torch.Tensor:
     return torch.from_numpy(arr.view(np.uint8).copy()).to(device)
 
 
-def sample(logits, tok, pos, gen, n_gen, max_new, done, hist, slot, params, T_max) -> None:
+def sample(logits, tok, pos, gen, n_gen, max_new, done, hist, slot, params, T_max, split: bool = False) -> None:
+    """On-device sampling + decode-state update (csrc/sample.hip).  ``split``: the two-stage kernel (vocabulary
+    slices on 16 workgroups per row, last-arriver merge) that decode forwards of <= 64 rows use; otherwise the
+    one-workgroup-per-row kernel."""
     lib = load()
     M, V = logits.shape[0], logits.shape[1]
+    if split:
+        nb = int(lib.cain_sample_ws_bytes(M))
+        ws = _sample_ws(logits.device, nb)
+        _check(lib.cain_sample_ex(_p(logits), logits.stride(0), V, _p(tok), _p(pos), _p(gen), gen.stride(0),
+                                  _p(n_gen), _p(max_new), _p(done), _p(hist), _p(slot), T_max, M, _p(params), _p(ws),
+                                  nb, _stream()), "sample")
+        return
     _check(lib.cain_sample(_p(logits), logits.stride(0), V, _p(tok), _p(pos), _p(gen), gen.stride(0), _p(n_gen),
                            _p(max_new), _p(done), _p(hist), _p(slot), T_max, M, _p(params), _stream()), "sample")
+
+
+_SAMPLE_WS: dict = {}
+
+
+def _sample_ws(device, nbytes: int) -> torch.Tensor:
+    """Zeroed sampler workspace per device (its tickets self-reset), grown on demand."""
+    t = _SAMPLE_WS.get(device)
+    if t is None or t.numel() * 4 < nbytes:
+        t = _SAMPLE_WS[device] = torch.zeros((nbytes + 3) // 4, device=device, dtype=torch.int32)
+    return t
 
 
 _LT_WS: dict = {}

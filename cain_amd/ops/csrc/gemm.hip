@@ -41,8 +41,20 @@
 
 #include "gemm_epi.h"
 
-template <int NT, int NB, int WAVES, int U, int EPI, bool NORM, bool PP>
-__global__ __launch_bounds__(WAVES * 64) void skinny_gemm_kernel(const GemmArgs a) {
+// Split-K of the skinny kernel (SPLIT): a grid of N/16 tiles smaller than the chip (the O / down projections
+// of qwen2:1.5b and gemma:2b at one row: 96-128 workgroups on 256 CUs, 2.7 TB/s) also splits K over ks
+// workgroups.  Each publishes its fp32 16x16 partial (and the RMSNorm partial sums of squares) with
+// write-through stores; the last arriver of the tile (ticket) adds the ks partials in fixed order and runs the
+// fused epilogue -- the in-launch combine of cdna_hip_programming.md §5 item 2, as in bgemm_kernel.
+struct SkArgs {
+  int ks;              // workgroups per tile (k ranges)
+  unsigned* counters;  // [ntiles], zero between launches (the reducer resets its own)
+  float* part;         // [ntiles][ks][64 lanes] f32x4
+  float* part_ss;      // [ntiles][ks][16]
+};
+
+template <int NT, int NB, int WAVES, int U, int EPI, bool NORM, bool PP, bool SPLIT = false>
+__global__ __launch_bounds__(WAVES * 64) void skinny_gemm_kernel(const GemmArgs a, const SkArgs sk) {
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int K = a.K;
@@ -50,24 +62,31 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_gemm_kernel(const GemmArgs 
   // XCD-aware block -> (row tile, M split) mapping: blocks b and b + 8 share an XCD under the
   // round-robin dispatch, so the msplit workgroups of one weight tile are given ids that differ by
   // multiples of 8 and their repeated tile reads hit the same L2 (speed only: any placement is correct).
-  int tg, ms;
+  // SPLIT (msplit = 1): the same mapping over the ks k-ranges, so a tile's partials and its reducer share an L2.
+  int tg, ms, kc = 0;
   {
-    const int bid = blockIdx.x, msp = a.msplit;
+    const int bid = blockIdx.x, msp = SPLIT ? sk.ks : a.msplit;
     const int ntg = gridDim.x / msp;
+    int sub;
     if (msp == 1) {
-      tg = bid, ms = 0;
+      tg = bid, sub = 0;
     } else if ((ntg & 7) == 0) {
       const int r = bid >> 3;
-      ms = r % msp;
+      sub = r % msp;
       tg = (r / msp) * 8 + (bid & 7);
     } else {
-      tg = bid / msp, ms = bid - (bid / msp) * msp;
+      tg = bid / msp, sub = bid - (bid / msp) * msp;
     }
+    if constexpr (SPLIT) ms = 0, kc = sub;
+    else ms = sub;
   }
   const int tile0 = tg * NT;
   const int mo = ms * 16 * NB;  // first row of this workgroup
-  const int s_beg = (wave * KS) / WAVES;
-  const int s_end = ((wave + 1) * KS) / WAVES;
+  // k-slices of this workgroup (all of K unless SPLIT), dealt to its waves
+  const int ksp = SPLIT ? (KS + sk.ks - 1) / sk.ks : KS;
+  const int k_beg = min(KS, kc * ksp), k_n = min(KS, k_beg + ksp) - k_beg;
+  const int s_beg = k_beg + (wave * k_n) / WAVES;
+  const int s_end = k_beg + ((wave + 1) * k_n) / WAVES;
   constexpr int UNITS = NT * NB * 64;
   constexpr bool PRE = UNITS <= WAVES * 64;  // each wave finalises at most one 64-unit chunk
 
@@ -227,6 +246,67 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_gemm_kernel(const GemmArgs 
   }
   __syncthreads();
 
+  if constexpr (SPLIT) {
+    // NT = NB = 1: one 64-lane unit per tile.  Wave 0 publishes this k-range's partial, takes the ticket; the
+    // last of the tile's ks arrivals sums the partials (k-range order: deterministic) and finishes the tile.
+    static_assert(NT == 1 && NB == 1, "split-K skinny body: one 16x16 unit per workgroup");
+    __shared__ unsigned s_ticket;
+    __shared__ float s_inv[16];
+    if (wave == 0) {
+      f32x4 v = red[0][lane];
+#pragma unroll
+      for (int w = 1; w < WAVES; ++w) v += red[w][lane];
+      const size_t pi = (size_t)tg * sk.ks + kc;
+      st_wt(slab_rsrc(sk.part), int((pi * 64 + lane) * 16), v);
+      if constexpr (NORM) {
+        if (lane < 16) {
+          float ss = 0.f;
+#pragma unroll
+          for (int w = 0; w < WAVES; ++w) ss += red_ss[w][lane];
+          st_wt_f32(slab_rsrc(sk.part_ss), int((pi * 16 + lane) * 4), ss);
+        }
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (lane == 0)
+        s_ticket = __hip_atomic_fetch_add(sk.counters + tg, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (s_ticket != unsigned(sk.ks - 1) || wave != 0) return;
+    // reducer: every partial load issued before the first add (clamped index, surplus weighted 0)
+    const __amdgpu_buffer_rsrc_t pr = slab_rsrc(sk.part), sr = slab_rsrc(sk.part_ss);
+    f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
+    float ss = 0.f;
+    for (int k0 = 0; k0 < sk.ks; k0 += 4) {
+      f32x4 l[4];
+      float q[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const size_t pi = (size_t)tg * sk.ks + min(k0 + j, sk.ks - 1);
+        l[j] = ld_wt(pr, int((pi * 64 + lane) * 16));
+        q[j] = NORM ? ld_wt_f32(sr, int((pi * 16 + (lane & 15)) * 4)) : 0.f;
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float wj = (k0 + j < sk.ks) ? 1.f : 0.f;
+        v += wj * l[j];
+        ss += wj * q[j];
+      }
+    }
+    red[0][lane] = v;
+    if constexpr (NORM) {
+      if (lane < 16) s_inv[lane] = rsqrtf(ss / float(a.K) + a.eps);
+    }
+    if (lane == 0) sk.counters[tg] = 0u;  // ready for the next launch (launch-ordered)
+    const int m = mo + (lane & 15);
+    const EpiIn e = epi_load<NT, NB, EPI>(a, tile0, mo, lane);
+    epi_store<EPI>(a, tile0, m, lane, e, [&](int off) {
+      f32x4 r = red[0][lane + off];
+      if constexpr (NORM) r *= s_inv[(lane + off) & 15];
+      return r;
+    });
+    return;
+  }
+
   auto unit_sum = [&](int u) -> f32x4 {
     f32x4 v = red[0][u];
 #pragma unroll
@@ -254,45 +334,71 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_gemm_kernel(const GemmArgs 
 }
 
 template <int NT, int NB, int WAVES, int EPI, bool NORM>
-static hipError_t launch_t(const GemmArgs& a, hipStream_t st) {
+static hipError_t launch_t(const GemmArgs& a, const SkArgs& sk, hipStream_t st) {
   constexpr int U = (NB >= 2) ? 2 : 4;  // x2 register sets (pipelined)
   static const int pp = [] {
     const char* e = getenv("CAIN_SKINNY_PP");
     return e ? atoi(e) : 0;
   }();
+  if (sk.ks > 1) {
+    if constexpr (NT == 1 && NB == 1) {
+      hipLaunchKernelGGL((skinny_gemm_kernel<NT, NB, WAVES, U, EPI, NORM, false, true>), dim3(a.N / 16 * sk.ks),
+                         dim3(WAVES * 64), 0, st, a, sk);
+      return hipGetLastError();
+    }
+    return hipErrorInvalidValue;
+  }
   if (pp)
     hipLaunchKernelGGL((skinny_gemm_kernel<NT, NB, WAVES, U, EPI, NORM, true>), dim3(a.N / (16 * NT) * a.msplit),
-                       dim3(WAVES * 64), 0, st, a);
+                       dim3(WAVES * 64), 0, st, a, sk);
   else
     hipLaunchKernelGGL((skinny_gemm_kernel<NT, NB, WAVES, U, EPI, NORM, false>), dim3(a.N / (16 * NT) * a.msplit),
-                       dim3(WAVES * 64), 0, st, a);
+                       dim3(WAVES * 64), 0, st, a, sk);
   return hipGetLastError();
 }
 
 template <int NT, int NB, int EPI, bool NORM>
-static hipError_t launch_w(int waves, const GemmArgs& a, hipStream_t st) {
+static hipError_t launch_w(int waves, const GemmArgs& a, const SkArgs& sk, hipStream_t st) {
   // the LDS reduction buffer is WAVES * NT * NB KiB: cap it at 64 KiB at compile time
   constexpr int WMAX = 64 / (NT * NB);
   if constexpr (WMAX >= 16) {
-    if (waves >= 16) return launch_t<NT, NB, 16, EPI, NORM>(a, st);
+    if (waves >= 16) return launch_t<NT, NB, 16, EPI, NORM>(a, sk, st);
   }
   if constexpr (WMAX >= 8) {
-    if (waves >= 8) return launch_t<NT, NB, 8, EPI, NORM>(a, st);
+    if (waves >= 8) return launch_t<NT, NB, 8, EPI, NORM>(a, sk, st);
   }
-  return launch_t<NT, NB, 4, EPI, NORM>(a, st);
+  return launch_t<NT, NB, 4, EPI, NORM>(a, sk, st);
 }
 
 template <bool NORM>
-static hipError_t launch_e(int epi, int waves, const GemmArgs& a, hipStream_t st) {
+static hipError_t launch_e(int epi, int waves, const GemmArgs& a, const SkArgs& sk, hipStream_t st) {
   switch (epi) {
-    case EPI_BF16: return launch_w<1, 1, EPI_BF16, NORM>(waves, a, st);
-    case EPI_RESID: return launch_w<1, 1, EPI_RESID, NORM>(waves, a, st);
-    case EPI_F32: return launch_w<1, 1, EPI_F32, NORM>(waves, a, st);
-    case EPI_SILU: return launch_w<1, 1, EPI_SILU, NORM>(waves, a, st);
-    case EPI_GELU: return launch_w<1, 1, EPI_GELU, NORM>(waves, a, st);
-    case EPI_QKV_ROPE: return launch_w<1, 1, EPI_QKV_ROPE, NORM>(waves, a, st);
+    case EPI_BF16: return launch_w<1, 1, EPI_BF16, NORM>(waves, a, sk, st);
+    case EPI_RESID: return launch_w<1, 1, EPI_RESID, NORM>(waves, a, sk, st);
+    case EPI_F32: return launch_w<1, 1, EPI_F32, NORM>(waves, a, sk, st);
+    case EPI_SILU: return launch_w<1, 1, EPI_SILU, NORM>(waves, a, sk, st);
+    case EPI_GELU: return launch_w<1, 1, EPI_GELU, NORM>(waves, a, sk, st);
+    case EPI_QKV_ROPE: return launch_w<1, 1, EPI_QKV_ROPE, NORM>(waves, a, sk, st);
     default: return hipErrorInvalidValue;
   }
+}
+
+// Split rule of the skinny kernel (M <= 16 rows, one workgroup per 16-row tile): a grid under ~3/4 of the CUs
+// whose tiles are long (K > 128 slices: the down projections of qwen2:1.5b / gemma:2b, 96-128 tiles of 280-512
+// slices) takes ks = ceil(K / 128 slices) k-ranges, so every workgroup streams <= 128 slices and ~3x the CUs
+// stream.  Short tiles stay whole: there the split's combine round trip (measured +1 us on
+// qwen2:1.5b's QKV) costs more than it spreads.  (Also measured and not kept: "one-shot" waves that load all of
+// their <= 16 slices in one burst before any MFMA -- the 128 staging VGPRs halve the resident waves, and with
+// them the bytes in flight: qwen2:1.5b gate/up 11.9 -> 12.5 us, split down 9.0 -> 10.4 us, gpurun_out/r3d.)
+// CAIN_SKINNY_SPLIT=0 disables it.
+static int skinny_split(int N, int K, int M) {
+  static const int on = [] {
+    const char* e = getenv("CAIN_SKINNY_SPLIT");
+    return e ? atoi(e) : 1;
+  }();
+  const int nt = N / 16, KS = K / 32;
+  if (!on || M > 16 || nt >= 192 || nt < 1 || KS <= 128) return 1;
+  return std::min(8, (KS + 127) / 128);
 }
 
 // Waves per workgroup: 8 (the tuned choice on every llama3.1:8b decode shape, profiles/gemm_tune.md)
@@ -305,8 +411,11 @@ static int pick_waves(int n_wg, int ks) {
   return w;
 }
 
-static int gemm_dispatch(GemmArgs a, int epi, int norm, int waves, hipStream_t st) {
+static int gemm_dispatch(GemmArgs a, int epi, int norm, int waves, hipStream_t st, const SkArgs* split = nullptr) {
   if (a.K % 32 || a.N % 16 || a.M < 1 || a.M > 64) return -1;
+  SkArgs sk{};
+  sk.ks = 1;
+  if (split && split->ks > 1 && a.M <= 16) sk = *split;
   const bool pair = (epi == EPI_SILU || epi == EPI_GELU);
   // Rows beyond 16 are split over workgroups (msplit) rather than widening a workgroup's
   // B operand: per k-step a wave then loads one weight and one activation fragment, and
@@ -315,13 +424,13 @@ static int gemm_dispatch(GemmArgs a, int epi, int norm, int waves, hipStream_t s
   const int nb = 1;
   const int nt = 1;
   a.msplit = (a.M + 15) / 16;
-  const int n_wg = a.N / 16 * a.msplit;
-  if (waves <= 0) waves = pick_waves(n_wg, a.K / 32);
+  const int n_wg = a.N / 16 * a.msplit * sk.ks;
+  if (waves <= 0) waves = pick_waves(n_wg, a.K / 32 / sk.ks);
   while (waves > 4 && waves * nt * nb > 64) waves /= 2;  // LDS reduction buffer <= 64 KiB
   // 16-wave groups cap registers at 128/lane: the RoPE / norm-prologue / NB=4 bodies would spill
   if (waves > 8 && (epi == EPI_QKV_ROPE || norm || nb >= 4)) waves = 8;
   (void)pair;
-  const hipError_t e = norm ? launch_e<true>(epi, waves, a, st) : launch_e<false>(epi, waves, a, st);
+  const hipError_t e = norm ? launch_e<true>(epi, waves, a, sk, st) : launch_e<false>(epi, waves, a, sk, st);
   return int(e);
 }
 
@@ -939,10 +1048,18 @@ CAIN_API int cain_wgemm_eligible(int N, int K, int M);
 CAIN_API long long cain_wgemm_ws_bytes(int N, int K, int M);
 int wgemm_dispatch(const GemmArgs& a, int epi, bool norm, void* ws, long long ws_bytes, hipStream_t st);
 
-// Workspace the batched paths need for a GEMM of this shape (0 when the skinny kernel runs it).
+// Skinny split-K slabs: [tiles][ks][64] f32x4 partials + [tiles][ks][16] row sums of squares, after the counters
+static size_t skinny_split_ws_bytes(int N, int ks) {
+  return GEMM_SLAB_OFFSET + (size_t)(N / 16) * ks * (256 + 16) * sizeof(float);
+}
+
+// Workspace the batched paths need for a GEMM of this shape (0 when the unsplit skinny kernel runs it).
 CAIN_API long long cain_gemm_ws_bytes(int N, int K, int M) {
   if (cain_wgemm_eligible(N, K, M)) return (long long)BG_COUNTER_BYTES + cain_wgemm_ws_bytes(N, K, M);
-  if (!bgemm_eligible(N, K, M)) return 0;
+  if (!bgemm_eligible(N, K, M)) {
+    const int ks = (M <= 16) ? skinny_split(N, K, M) : 1;
+    return ks > 1 ? (long long)skinny_split_ws_bytes(N, ks) : 0;
+  }
   return (long long)bgemm_ws_bytes(bgemm_plan(N, K, M, bgemm_ntw()));
 }
 
@@ -1000,6 +1117,26 @@ CAIN_API int cain_gemm(const void* Wp, const void* X, int ldx, int K, int N, int
       a.H = H, a.Hkv = Hkv, a.hd = hd, a.T_max = T_max, a.kv8 = kv8;
       if (epi == EPI_QKV_ROPE && (hd % 16 || (hd / 2) % 8)) return -1;
       return bgemm_dispatch(a, epi, norm != 0, p, ws, st);
+    }
+  }
+  if (ws && M <= 16 && K % 32 == 0 && N % 16 == 0) {
+    const int ks = skinny_split(N, K, M);
+    if (ks > 1 && (long long)skinny_split_ws_bytes(N, ks) <= ws_bytes && (N / 16) * 4 <= (int)BG_COUNTER_BYTES) {
+      if (epi == EPI_QKV_ROPE && (hd % 16 || (hd / 2) % 8)) return -1;
+      GemmArgs a{};
+      a.Wp = reinterpret_cast<const bf16x8*>(Wp);
+      a.X = reinterpret_cast<const __bf16*>(X);
+      a.ldx = ldx, a.K = K, a.N = N, a.M = M, a.Y = Y, a.ldy = ldy, a.bias = bias;
+      a.eps = eps;
+      a.slot = slot, a.pos = pos, a.cos_t = cos_t, a.sin_t = sin_t;
+      a.kc = reinterpret_cast<__bf16*>(kc), a.vtc = reinterpret_cast<__bf16*>(vtc);
+      a.H = H, a.Hkv = Hkv, a.hd = hd, a.T_max = T_max, a.kv8 = kv8;
+      SkArgs sk{};
+      sk.ks = ks;
+      sk.counters = reinterpret_cast<unsigned*>(ws);  // the batched path's tickets (both reset their own)
+      sk.part = reinterpret_cast<float*>(static_cast<char*>(ws) + GEMM_SLAB_OFFSET);
+      sk.part_ss = sk.part + (size_t)(N / 16) * ks * 256;
+      return gemm_dispatch(a, epi, norm != 0, waves, st, &sk);
     }
   }
   return cain_skinny_gemm_ex(Wp, X, ldx, K, N, M, Y, ldy, bias, norm, eps, slot, pos, cos_t, sin_t, kc, vtc, H, Hkv,

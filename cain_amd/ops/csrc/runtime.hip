@@ -49,6 +49,10 @@ CAIN_API int cain_attention(const void* q, const void* kc, const void* vtc, cons
 CAIN_API int cain_sample(float* logits, int ldl, int V, int* tok, int* pos, int* gen, int ldg, int* n_gen,
                          const int* max_new, int* done, int* hist, const int* slot, int T_max, int M,
                          const void* params, hipStream_t st);
+CAIN_API long long cain_sample_ws_bytes(int M);
+CAIN_API int cain_sample_ex(float* logits, int ldl, int V, int* tok, int* pos, int* gen, int ldg, int* n_gen,
+                            const int* max_new, int* done, int* hist, const int* slot, int T_max, int M,
+                            const void* params, void* ws, long long ws_bytes, hipStream_t st);
 
 // hipBLASLt A/B path (opt-in library libcain_blas.so, csrc_blas/blas.hip): not linked into this library; its
 // entry points are registered at run time by cain_amd.ops.enable_lt().  Unregistered (the default), every
@@ -155,6 +159,12 @@ namespace {
 struct Plan {
   CainPlanDesc d;
   std::vector<CainLayer> layers;
+  // two-stage sampler workspace (sample.hip cain_sample_ex) for decode forwards of <= 64 rows, zeroed once
+  void* sample_ws = nullptr;
+  long long sample_ws_bytes = 0;
+  ~Plan() {
+    if (sample_ws) (void)hipFree(sample_ws);
+  }
 };
 
 // first failing call of the last failed forward (source text + line), for the Python error message
@@ -241,8 +251,8 @@ int forward(const Plan& p, int M, const CainRows& r, int want_logits, int want_s
                         nullptr, /*EPI_F32*/ 2));
   }
   if (want_sample) {
-    CK(cain_sample(d.logits, d.V, d.V, r.tok, r.pos, r.gen, r.ldg, r.n_gen, r.max_new, r.done, r.hist, r.slot,
-                   d.T_max, M, r.sample_params, st));
+    CK(cain_sample_ex(d.logits, d.V, d.V, r.tok, r.pos, r.gen, r.ldg, r.n_gen, r.max_new, r.done, r.hist, r.slot,
+                      d.T_max, M, r.sample_params, p.sample_ws, p.sample_ws_bytes, st));
   }
   return 0;
 }
@@ -256,6 +266,16 @@ CAIN_API void* cain_plan_create(const CainPlanDesc* desc) {
   p->d = *desc;
   p->layers.assign(desc->layers, desc->layers + desc->n_layers);
   p->d.layers = p->layers.data();
+  const int ms = desc->Mpad < 64 ? desc->Mpad : 64;
+  if (ms > 0) {
+    const long long nb = cain_sample_ws_bytes(ms);
+    if (hipMalloc(&p->sample_ws, nb) == hipSuccess && hipMemset(p->sample_ws, 0, nb) == hipSuccess) {
+      p->sample_ws_bytes = nb;
+    } else {
+      if (p->sample_ws) (void)hipFree(p->sample_ws);
+      p->sample_ws = nullptr;  // the one-workgroup sampler needs no workspace
+    }
+  }
   return p;
 }
 

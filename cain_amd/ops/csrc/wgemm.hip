@@ -264,21 +264,94 @@ __global__ __launch_bounds__(64 * (8 + NDMA), (8 + NDMA) / 4) void wgemm_kernel(
 
   if (w.ks > 1) {
     // fp32 slab of this split (unit (gt, rb) = 16 x 16 outputs, lane-major f32x4: the reducer's layout) and this
-    // split's per-row sums of squares; wgemm_reduce_kernel, the next launch on the stream, combines them.
-    // (Measured: a combine inside this launch -- write-through slabs, arrival tickets, row groups claimed by the
-    // block's workgroups -- took 2-8 us longer per GEMM than the separate launch on QKV / O / down at 256 rows.)
+    // split's per-row sums of squares.
+    const int n_units = nblk * WG_NT * G::RB;
+    if (!w.combine) {
+      // wgemm_reduce_kernel, the next launch on the stream, combines them
+      if (compute) {
+#pragma unroll
+        for (int tn = 0; tn < G::TN; ++tn)
+#pragma unroll
+          for (int mb = 0; mb < G::MB; ++mb) {
+            const int unit = (tile0 + wn * G::TN + tn) * G::RB + wm * G::MB + mb;
+            *reinterpret_cast<f32x4*>(w.part + (((size_t)kc * n_units + unit) * 64 + lane) * 4) = acc[tn][mb];
+          }
+      }
+      if constexpr (NORM) {
+        for (int r = threadIdx.x; r < BM; r += NTHR)
+          w.part_ss[((size_t)blk * w.ks + kc) * BM + r] = s_ss[r] + s_ss[BM + r];
+      }
+      return;
+    }
+    // In-launch combine (w.combine): the ks split partners of the column block publish their slabs write-through
+    // (sc1: no release fence, cdna_hip_programming.md §5 item 2), arrive on the block's counter, wait for each
+    // other, and then EACH reduces 1/ks of the block's 16 x 16 units (reduce-scatter among the partners) and runs
+    // the fused epilogue for them -- the separate reduce launch, its kernel boundary and its whole-grid ramp are
+    // gone, and the reduction work stays spread over every workgroup.  The wait needs all partners resident:
+    // the grid is <= 256 workgroups at one per CU (wgemm_dispatch), and the spin is bounded.
+    const __amdgpu_buffer_rsrc_t pr = slab_rsrc(w.part), sr = slab_rsrc(w.part_ss);
     if (compute) {
-      const int n_units = nblk * WG_NT * G::RB;
 #pragma unroll
       for (int tn = 0; tn < G::TN; ++tn)
 #pragma unroll
         for (int mb = 0; mb < G::MB; ++mb) {
           const int unit = (tile0 + wn * G::TN + tn) * G::RB + wm * G::MB + mb;
-          *reinterpret_cast<f32x4*>(w.part + (((size_t)kc * n_units + unit) * 64 + lane) * 4) = acc[tn][mb];
+          st_wt(pr, int((((size_t)kc * n_units + unit) * 64 + lane) * 16), acc[tn][mb]);
         }
     }
     if constexpr (NORM) {
-      for (int r = threadIdx.x; r < BM; r += NTHR) w.part_ss[((size_t)blk * w.ks + kc) * BM + r] = s_ss[r] + s_ss[BM + r];
+      for (int r = threadIdx.x; r < BM; r += NTHR)
+        st_wt_f32(sr, int((((size_t)blk * w.ks + kc) * BM + r) * 4), s_ss[r] + s_ss[BM + r]);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    unsigned* ctr = w.counters + blk * 2;
+    if (threadIdx.x == 0) {
+      __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      for (int spin = 0; spin < (1 << 24); ++spin) {  // bounded: ~seconds, never a hang
+        if (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= unsigned(w.ks)) break;
+        __builtin_amdgcn_s_sleep(1);
+      }
+      // the last partner out resets both counters for the next launch (every partner has seen ks arrivals)
+      if (__hip_atomic_fetch_add(ctr + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == unsigned(w.ks - 1)) {
+        __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(ctr + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    __syncthreads();
+    if (!compute) return;
+    // units of this column block: blk * 128 + [0, 128); partner kc takes [kc * 128 / ks, (kc + 1) * 128 / ks)
+    constexpr int BU = WG_NT * G::RB;
+    const int u0 = (kc * BU) / w.ks, u1 = ((kc + 1) * BU) / w.ks;
+    for (int lu = u0 + wave; lu < u1; lu += 8) {
+      const int unit = blk * BU + lu;
+      const int gt = unit / G::RB, rb = unit - gt * G::RB;
+      const int m = rb * 16 + c;
+      const bool live = gt < ntiles;
+      const EpiIn e = live ? epi_load_at<EPI>(a, gt, m, lane) : EpiIn{};
+      f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
+      float ss = 0.f;
+      for (int k0 = 0; k0 < w.ks; k0 += 4) {  // every partial load in flight before the adds
+        f32x4 l[4];
+        float q[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int k = min(k0 + j, w.ks - 1);
+          l[j] = ld_wt(pr, int((((size_t)k * n_units + unit) * 64 + lane) * 16));
+          q[j] = NORM ? ld_wt_f32(sr, int((((size_t)blk * w.ks + k) * BM + m) * 4)) : 0.f;
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float wj = (k0 + j < w.ks) ? 1.f : 0.f;
+          v += wj * l[j];
+          ss += wj * q[j];
+        }
+      }
+      if constexpr (NORM) v *= rsqrtf(ss / float(a.K) + a.eps);
+      f32x4 pv;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) pv[i] = __shfl_xor(v[i], 32, 64);
+      if (live) epi_store<EPI>(a, gt, m, lane, e, [&](int off) { return off ? pv : v; });
     }
     return;
   }
@@ -437,7 +510,7 @@ hipError_t wg_launch(const GemmArgs& a, const WgArgs& w, const WgPlan& p, hipStr
   hipLaunchKernelGGL((wgemm_kernel<BM, DX, DW, EPI, NORM, NDMA, ABL>), dim3(p.nblk * p.ks), dim3(64 * (8 + NDMA)), lds,
                      st, a, w);
   hipError_t e = hipGetLastError();
-  if (e != hipSuccess || p.ks == 1) return e;
+  if (e != hipSuccess || p.ks == 1 || w.combine) return e;
   wg_reduce_launch<BM, EPI, NORM>(a, w, p.nblk * WG_NT * G::RB, st);
   return hipGetLastError();
 }
@@ -549,7 +622,19 @@ int wgemm_dispatch(const GemmArgs& a, int epi, bool norm, void* ws, long long ws
   // fetched per XCD); 25.8k -> 26.3k tok/s.  CAIN_WGEMM_XCD=0: the split-major placement (A/B runs).
   static const int xcd = wg_env("CAIN_WGEMM_XCD", 1);
   w.xcd_blk = xcd && p.ks > 1 && p.nblk % 8 == 0;
-  // [reserved counter region][slabs][sums]
+  // in-launch split-K combine (CAIN_WGEMM_COMBINE=1, A/B runs): the partners wait for each other, so the whole grid
+  // must be resident -- at most one workgroup per CU (the ring's LDS) on every CU.  Off by default: on the headline
+  // (llama3.1:8b, 256 rows, same box, back to back) 26.06k tok/s with it vs 26.90k with the separate reduce launch
+  // (gpurun_out/r3c) -- the write-through slabs and the partners' wait cost more than the launch boundary saved.
+  static const int combine = wg_env("CAIN_WGEMM_COMBINE", 0);
+  static const int n_cu = [] {
+    int dev = 0, n = 0;
+    (void)hipGetDevice(&dev);
+    return hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess ? n : 0;
+  }();
+  w.combine = combine && p.ks > 1 && p.nblk * p.ks <= n_cu && p.nblk * 2 * 4 <= WG_CTR_BYTES;
+  // [counter region: 2 per column block, zero at rest][slabs][sums]
+  w.counters = static_cast<unsigned*>(ws);
   w.part = reinterpret_cast<float*>(static_cast<char*>(ws) + WG_CTR_BYTES);
   w.part_ss = w.part + p.part_floats;
   hipError_t e;

@@ -78,6 +78,8 @@ struct WgArgs {
   float* part;      // [ks][n_units][64 lanes] f32x4 (ks > 1)
   float* part_ss;   // [nblk][ks][BM] per-row partial sums of squares (ks > 1 && NORM)
   int xcd_blk;      // 1: a column block's split partners and its reducers share one XCD (wgemm.hip)
+  int combine;      // 1: in-launch split-K combine by the partners (wgemm.hip); 0: wgemm_reduce_kernel
+  unsigned* counters;  // [nblk][2] arrivals / exits of the in-launch combine, zero at rest
 };
 
 

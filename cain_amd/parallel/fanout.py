@@ -46,6 +46,9 @@ import traceback
 from typing import Any, Dict, List, Optional
 
 
+_SESSION_T0 = [0.0]  # monotonic start of this rank (run_rank), for CAIN_RUN_BUDGET_S
+
+
 def _free_port() -> int:
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -80,6 +83,9 @@ def run_rank(config_path: str, rank: int, world: int, isolation: Optional[str] =
     from ..runner.store import CSVOutputManager
     from ..runner.validator import ConfigValidator
 
+    import time
+
+    _SESSION_T0[0] = time.monotonic()
     backend = _backend()
     local = int(os.environ.get("LOCAL_RANK", rank))
     device = None
@@ -214,7 +220,13 @@ def _work_queue(store, prefix: str, todo_ids: List[str], by_id: Dict[str, Dict[s
             output.console_log_WARNING(f"CSVManager: committed {len(done)} rows ({n - len(pending)}/{n})")
 
     ran = 0
+    # CAIN_RUN_BUDGET_S > 0: stop claiming runs that long after the rank started (chunked sessions of a long study:
+    # the rest stays TODO and the next session resumes it)
+    budget = float(os.environ.get("CAIN_RUN_BUDGET_S", "0") or 0)
     while True:
+        if budget > 0 and time.monotonic() - _SESSION_T0[0] > budget:
+            output.console_log_WARNING(f"run budget of {budget:.0f} s used: the remaining runs stay TODO (resume)")
+            break
         i = int(store.add(f"{prefix}next", 1)) - 1
         if i >= n:
             break
@@ -230,6 +242,10 @@ def _work_queue(store, prefix: str, todo_ids: List[str], by_id: Dict[str, Dict[s
         if config.operation_type is OperationType.SEMI:
             EventSubscriptionController.raise_event(RunnerEvents.CONTINUE)
     if writer:
+        if budget > 0:
+            # indices nobody claimed (every rank stopped at its budget) stay TODO: wait for the claimed ones only
+            claimed = min(n, int(store.add(f"{prefix}next", 0)))
+            pending.difference_update(range(claimed, n))
         last_progress = time.monotonic()
         beats: Dict[int, tuple] = {}  # rank -> (last counter value, when it changed, writer clock)
 

@@ -129,11 +129,25 @@ def test_greedy_decode_tracks_oracle_token_by_token(name):
 
 
 def test_greedy_decode_tracks_oracle_full_size():
+    """Full-size greedy decode: the engine's tokens disagree with the fp32 oracle's teacher-forced argmax no
+    more often than a PyTorch bf16-eager model's argmax does on the same sequences (relative criterion,
+    tests/numerics.py), and only at near-ties."""
+    from numerics import eager_bf16
+
     eng = DecodeEngine("llama3.1:8b", device="cuda", max_batch=4, max_context=256, keep_natural=True, seed=13,
                        steps_per_graph=16)
     ref = ReferenceModel(eng.weights, memo_weights=True)
     exact, total = _teacher_forced_agreement(eng, ref, PROMPTS[:2], 64, range(2), tie=0.3)
-    assert exact / total > 0.8, (exact, total)  # measured 112 / 128; every other step a near-tie
+    eager = eager_bf16(eng.weights)
+    base_bad = 0
+    res = eng.generate(PROMPTS[:2], 64, [dict(temperature=0.0, repeat_penalty=1.0, eos_id=-1)] * 2)
+    for i in range(2):
+        p_ids = eng.encode(PROMPTS[i])
+        seq = torch.tensor([p_ids + res[i].tokens[:-1]], device="cuda")
+        a = ref.forward(seq)[0, len(p_ids) - 1:].argmax(-1)
+        b = eager.forward(seq)[0, len(p_ids) - 1:].argmax(-1)
+        base_bad += int((a != b).sum())
+    assert total - exact <= 1.25 * base_bad + 2, (total - exact, base_bad, total)
     eng.close()
-    del ref
+    del ref, eager
     torch.cuda.empty_cache()

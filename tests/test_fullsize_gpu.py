@@ -3,7 +3,12 @@ weights, for every real configuration of the study, at 1, 64 and 
 single-stream, mid-batch (bgemm) and wide-batch (wgemm) GEMM paths, the 32k-256k-vocab LM heads, Gemma's MQA at
 head_dim 256 through a full stack -- plus the fp8-weight path against its dequantised oracle.
 
-The oracle is checked on a sample of the rows (every row runs through the engine)."""
+The oracle is checked on a sample of the rows (every row runs through the engine).  Criterion (tests/numerics.py):
+the engine's relative logit error against the fp32 oracle is at most 1.25x that of a PyTorch bf16-eager model on
+the same weights and prompts -- an absolute cosine bound would admit a real precision regression.
+
+``test_headline_operating_point`` pins the configuration that produces the headline number: llama3.1:8b, 256
+rows, a 1,334-token greedy generation, teacher-forced against the oracle on 4 rows at their full context."""
 import pytest
 import torch
 
@@ -16,6 +21,7 @@ from cain_amd.engine import DecodeEngine  # noqa: E402
 from cain_amd.models.config import MODELS  # noqa: E402
 from cain_amd.models.reference import ReferenceModel  # noqa: E402
 from cain_amd.models.weights import fp8_roundtrip_weights  # noqa: E402
+from numerics import assert_within_eager, eager_bf16, rel  # noqa: E402
 
 TOPICS = ["India", "World War II", "Elizabeth II", "United States", "Cristiano Ronaldo", "The Beatles",
           "Barack Obama", "Donald Trump", "Michael Jackson", "Lady Gaga", "Eminem", "Adolf Hitler"]
@@ -26,27 +32,33 @@ def _prompts(n):
             + " and more" * (i % 4) for i in range(n)]
 
 
-def _check(eng, ref, prompts, rows, tag):
+def _check(eng, ref, eager, prompts, rows, tag):
     got = eng.last_logits(prompts)
+    e_eng, e_eager = [], []
     for i in rows:
-        want = ref.forward(torch.tensor([eng.encode(prompts[i])], device="cuda"), last_only=True)[0, -1]
+        toks = torch.tensor([eng.encode(prompts[i])], device="cuda")
+        want = ref.forward(toks, last_only=True)[0, -1]
+        base = eager.forward(toks, last_only=True)[0, -1]
         g = got[i].float()
-        cos = float(torch.nn.functional.cosine_similarity(g, want, dim=0))
-        assert cos > 0.995, (tag, i, cos)
+        e_eng.append(rel(g, want))
+        e_eager.append(rel(base, want))
+        assert float(torch.nn.functional.cosine_similarity(g, want, dim=0)) > 0.98, (tag, i)  # sanity floor
         top2 = want.topk(2)
         # argmax must agree where the oracle's top-2 gap is well outside the bf16 error of this row
         if float(top2.values[0] - top2.values[1]) > 4 * float((g - want).std()):
             assert int(g.argmax()) == int(top2.indices[0]), (tag, i)
+    assert_within_eager(e_eng, e_eager, tag)
 
 
 @pytest.mark.parametrize("name", sorted(MODELS))
 def test_fullsize_logits_match_oracle(name):
     eng = DecodeEngine(name, device="cuda", max_batch=256, max_context=128, keep_natural=True, seed=17)
     ref = ReferenceModel(eng.weights, memo_weights=True)
+    eager = eager_bf16(eng.weights)
     for m, rows in ((1, [0]), (64, [0, 21, 63]), (256, [0, 77, 130, 255])):
-        _check(eng, ref, _prompts(m), rows, f"{name} M={m}")
+        _check(eng, ref, eager, _prompts(m), rows, f"{name} M={m}")
     eng.close()
-    del ref
+    del ref, eager
     torch.cuda.empty_cache()
 
 
@@ -57,9 +69,54 @@ def test_fullsize_fp8_weights_match_dequantised_oracle(name, monkeypatch):
     monkeypatch.setenv("CAIN_W8A8", "0")
     eng = DecodeEngine(name, device="cuda", max_batch=64, max_context=128, keep_natural=True, seed=19,
                        weight_dtype="fp8")
-    ref = ReferenceModel(fp8_roundtrip_weights(eng.weights), memo_weights=True)
+    wq = fp8_roundtrip_weights(eng.weights)
+    ref = ReferenceModel(wq, memo_weights=True)
+    eager = eager_bf16(wq)  # the torch path on the same fp8-rounded weights
     for m, rows in ((1, [0]), (64, [0, 40, 63])):
-        _check(eng, ref, _prompts(m), rows, f"{name} fp8 M={m}")
+        _check(eng, ref, eager, _prompts(m), rows, f"{name} fp8 M={m}")
     eng.close()
-    del ref
+    del ref, eager, wq
+    torch.cuda.empty_cache()
+
+
+def test_headline_operating_point():
+    """The bench's configuration end to end (bench.py: llama3.1:8b, 256 concurrent rows, a 1000-word request =
+    1,334 generated tokens): every row decodes greedily through the graph-replayed wide-batch path; 4 rows are
+    then teacher-forced through the fp32 oracle over their FULL context (prompt + 1,334 tokens) and the engine's
+    tokens must disagree with the oracle's argmax no more often than a PyTorch bf16-eager model's argmax does
+    (relative criterion), and only at near-ties."""
+    n_new = 1334
+    eng = DecodeEngine("llama3.1:8b", device="cuda", max_batch=256, max_context=1536, keep_natural=True, seed=23,
+                       steps_per_graph=16)
+    prompts = _prompts(256)
+    res = eng.generate(prompts, n_new, [dict(temperature=0.0, repeat_penalty=1.0, eos_id=-1)] * 256)
+    assert all(r.eval_count == n_new for r in res)
+    rows = (0, 85, 170, 255)
+    p_ids = {i: eng.encode(prompts[i]) for i in rows}
+    w = eng.weights
+    eng.close()
+    del eng  # frees the 256-row KV cache before the fp32 oracle
+    torch.cuda.empty_cache()
+    ref = ReferenceModel(w, memo_weights=True)
+    eager = eager_bf16(w)
+    mism_eng = mism_eager = total = 0
+    for i in rows:
+        toks = res[i].tokens
+        seq = torch.tensor([p_ids[i] + toks[:-1]], device="cuda")
+        lg = ref.forward(seq)[0, len(p_ids[i]) - 1:]  # the oracle's logits at every generated position
+        best = lg.argmax(-1)
+        base = eager.forward(seq)[0, len(p_ids[i]) - 1:].argmax(-1)
+        t = torch.tensor(toks, device="cuda")
+        bad = best != t
+        mism_eng += int(bad.sum())
+        mism_eager += int((base != best).sum())
+        total += len(toks)
+        # a disagreement is a near-tie of the oracle: the engine's token within 0.3 std of its best logit
+        if bool(bad.any()):
+            idx = bad.nonzero()[:, 0]
+            margin = lg[idx, best[idx]] - lg[idx, t[idx]]
+            assert bool((margin < 0.3 * lg[idx].std(-1)).all()), (i, float(margin.max()))
+        del lg
+    assert mism_eng <= 1.25 * mism_eager + 0.01 * total, (mism_eng, mism_eager, total)
+    del ref, eager
     torch.cuda.empty_cache()

@@ -312,3 +312,90 @@ def test_attention_many_rows(H, Hkv, hd, kv):
             continue
         ref = _attn_ref(q[m].view(H, hd), kc[m], vt[m], lengths[m], H // Hkv)
         assert rel_err(out[m].view(H, hd), ref) < 2e-2, (m, lengths[m])
+
+
+@pytest.mark.parametrize("M", [1, 4, 16])
+@pytest.mark.parametrize("N,K,epi,norm", [(1536, 8960, ops.EPI_RESID, False),     # qwen2:1.5b down (96 tiles)
+                                          (1536, 1536, ops.EPI_RESID, False),     # qwen2:1.5b O
+                                          (2048, 16384, ops.EPI_RESID, False),    # gemma:2b down
+                                          (2048, 2048, ops.EPI_F32, True),        # fused RMSNorm, 128 tiles
+                                          (2 * 1280, 2048, ops.EPI_SILU, True)])  # gate/up pairs, 160 tiles
+def test_skinny_split_k_matches_fp32_and_unsplit(M, N, K, epi, norm):
+    """Split-K skinny grids (narrow outputs at <= 16 rows: ks k-ranges per tile, last-arriver combine in fixed
+    order) against the fp32 reference and against the unsplit kernel on the same inputs."""
+    torch.manual_seed(N + K + M)
+    W = (torch.randn(N, K, device=DEV) / K ** 0.5).bfloat16()
+    x = (2 * torch.randn(M, K, device=DEV)).bfloat16()
+    g = (1 + 0.2 * torch.randn(K, device=DEV)).bfloat16()
+    Wf = fold_gain(W, g) if norm else W
+    if epi == ops.EPI_SILU:
+        Wp = pack_mfma_a(interleave_tiles(Wf[: N // 2], Wf[N // 2:], tile=8))
+    else:
+        Wp = pack_mfma_a(Wf)
+    xr = x.float()
+    if norm:
+        xr = xr * torch.rsqrt(xr.pow(2).mean(-1, keepdim=True) + 1e-6) * g.float()
+    if epi == ops.EPI_SILU:
+        ref = torch.nn.functional.silu(xr @ W[: N // 2].float().t()) * (xr @ W[N // 2:].float().t())
+    else:
+        ref = xr @ W.float().t()
+    outs = []
+    for batched in (True, False):
+        r0 = torch.randn(M, N, device=DEV).bfloat16() if epi == ops.EPI_RESID else None
+        if r0 is not None:
+            torch.manual_seed(5)
+            r0 = torch.randn(M, N, device=DEV).bfloat16()
+            out = r0.clone()
+            ops.skinny_gemm(Wp, x, N, epi, out=out, norm=norm, eps=1e-6, batched=batched)
+            want = ref + r0.float()
+        else:
+            out = ops.skinny_gemm(Wp, x, N, epi, norm=norm, eps=1e-6, batched=batched)
+            want = ref
+        assert rel_err(out, want) < 1e-2, (batched, rel_err(out, want))
+        outs.append(out.float())
+    if N // 16 < 192 and K // 32 > 128:
+        assert ops.gemm_ws_bytes(N, K, M) > 0  # the split grid was taken with batched=True
+    assert rel_err(outs[0], outs[1]) < 5e-3
+
+
+@pytest.mark.parametrize("V", [151936, 32064, 600, 257])
+@pytest.mark.parametrize("M", [1, 3, 64])
+def test_split_sampler_draws_the_same_tokens(V, M):
+    """The two-stage sampler (16 vocabulary slices per row, last-arriver merge) draws exactly the token of the
+    one-workgroup kernel for the same logits, options and seed -- greedy, top-k 1..256, top-p, repeat penalty
+    with a history -- and advances the decode state the same way."""
+    torch.manual_seed(V + M)
+    T_max = 2048
+
+    def state():
+        return dict(tok=torch.zeros(M, device=DEV, dtype=torch.int32),
+                    pos=torch.full((M,), 10, device=DEV, dtype=torch.int32),
+                    gen=torch.zeros(M, 32, device=DEV, dtype=torch.int32),
+                    n_gen=torch.full((M,), 5, device=DEV, dtype=torch.int32),
+                    max_new=torch.full((M,), 20, device=DEV, dtype=torch.int32),
+                    done=torch.zeros(M, device=DEV, dtype=torch.int32),
+                    hist=torch.randint(0, V, (M * 64,), device=DEV, dtype=torch.int32),
+                    slot=torch.arange(M, device=DEV, dtype=torch.int32))
+
+    for rep in range(6):
+        logits = torch.randn(M, V, device=DEV) * (0.5 + rep)
+        logits[:, :3] += 4.0  # a few dominant entries, with a tie at rep 0
+        if rep == 0:
+            logits[:, 7] = logits[:, 1]
+        kinds = [(0.0, 40, 1.0), (0.8, 40, 0.9), (1.0, 1, 1.0), (1.2, 256, 0.95), (0.7, 0, 1.0), (1.0, 7, 0.5)]
+        rows = [dict(temperature=kinds[i % 6][0], top_k=kinds[i % 6][1], top_p=kinds[i % 6][2],
+                     repeat_penalty=1.1 if i % 2 else 1.0, repeat_last_n=64, eos_id=-1, seed=rep * 7919 + i)
+                for i in range(M)]
+        params = ops.sample_params_tensor(rows, DEV)
+        out = []
+        for split in (False, True):
+            st = state()
+            torch.manual_seed(rep)
+            st["hist"] = torch.randint(0, V, (M * 64,), device=DEV, dtype=torch.int32, generator=None)
+            ops.sample(logits.clone(), st["tok"], st["pos"], st["gen"], st["n_gen"], st["max_new"], st["done"],
+                       st["hist"], st["slot"], params, T_max, split=split)
+            out.append({k: v.cpu() for k, v in st.items()})
+        for k in ("tok", "pos", "gen", "n_gen", "done", "hist"):
+            assert torch.equal(out[0][k], out[1][k]), (rep, k)
+    # greedy rows are the argmax (lowest index on ties)
+    assert int(out[1]["tok"][0]) == int(torch.argmax(logits[0]).item()) or rows[0]["repeat_penalty"] != 1.0

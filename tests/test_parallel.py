@@ -249,3 +249,22 @@ def test_writer_deadline_raises_and_names_the_claimant(monkeypatch):
             _writer_pass(monkeypatch, store, ["a", "b"], rank=0, hb_timeout_s=30, deadline_s=0.3)
     finally:
         stop.set()
+
+
+def test_run_budget_leaves_unclaimed_runs_todo(monkeypatch):
+    """CAIN_RUN_BUDGET_S: once the session's budget is used, ranks stop claiming and the writer waits only for
+    the runs that were claimed -- the rest stay TODO for the next (resumed) session."""
+    import time
+
+    from cain_amd.parallel import fanout
+
+    monkeypatch.setenv("CAIN_RUN_BUDGET_S", "5")
+    store = _DictStore()
+    monkeypatch.setattr(fanout, "_SESSION_T0", [time.monotonic()])
+    failed, committed = _writer_pass(monkeypatch, store, ["a", "b", "c"], rank=0, hb_timeout_s=30, deadline_s=30)
+    assert failed == [] and committed == ["a", "b", "c"]  # within the budget: everything runs
+    store = _DictStore()
+    monkeypatch.setattr(fanout, "_SESSION_T0", [time.monotonic() - 10])
+    t0 = time.monotonic()
+    failed, committed = _writer_pass(monkeypatch, store, ["a", "b", "c"], rank=0, hb_timeout_s=30, deadline_s=30)
+    assert failed == [] and committed == [] and time.monotonic() - t0 < 5
