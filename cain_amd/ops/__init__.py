@@ -92,6 +92,8 @@ def load() -> ctypes.CDLL:
         lib.cain_attention.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp, ci, ci, ci, ci, ci, ci, ci, cf, vp]
         lib.cain_attention_ex.argtypes = ([vp, vp, vp, vp, vp, vp, vp, vp, vp, ci, ci, ci, ci, ci, ci, ci, cf, ci, cf, cf]
                                           + [vp])
+        lib.cain_front_eligible.argtypes = [ci] * 8
+        lib.cain_front.argtypes = ([vp] * 12 + [ci] * 6 + [cf, ci, vp, vp, vp, ci, cf, vp, vp, vp])
         lib.cain_sample.argtypes = [vp, ci, ci, vp, vp, vp, ci, vp, vp, vp, vp, vp, ci, ci, vp, vp]
         lib.cain_sample_ex.argtypes = [vp, ci, ci, vp, vp, vp, ci, vp, vp, vp, vp, vp, ci, ci, vp, vp,
                                        ctypes.c_longlong, vp]
@@ -412,6 +414,38 @@ def attention(q, kc, vtc, slot, pos, H, Hkv, hd, nsplit, scale, out=None, part_o
                                  vscale, _stream()),
            "attention")
     return out
+
+
+def front_eligible(M: int, d: int, H: int, Hkv: int, hd: int, nsplit: int, kv8: bool = False) -> bool:
+    return bool(load().cain_front_eligible(M, d, H * hd, hd, H, Hkv, nsplit, int(kv8)))
+
+
+def layer_front(wqkv, bqkv, wo, x, q, attn, kc, vtc, slot, pos, cos_t, sin_t, H, Hkv, hd, nsplit, scale,
+                eps: float = 1e-6, norm: bool = True, part_o=None, part_ml=None, counters=None, flags=None,
+                trace=None) -> None:
+    """QKV (+RMSNorm, bias, RoPE, KV append) -> attention -> O (+residual) of one layer in ONE launch
+    (csrc/front.hip; <= 4 rows, bf16 caches, ``front_eligible``).  Same operands as ``qkv_rope`` ->
+    ``attention`` -> ``skinny_gemm(EPI_RESID)``: ``x`` [M, d] is the residual stream (updated in place), ``q`` /
+    ``attn`` [M, H*hd] the intermediate buffers.  ``counters`` / ``flags`` must be zero (they are again after).
+    ``trace``: optional int64 [grid, 4] per-workgroup timestamps (10 ns ticks: start, wait begin, wait end, end;
+    workgroups [0, n_qkv) QKV, then M*Hkv*nsplit attention, then d/16 O)."""
+    lib = load()
+    _gpu(wqkv, wo, x, q, attn, kc, vtc)
+    M, d = x.shape
+    T_max = kc.shape[-2]
+    assert not is_fp8_cache(kc) and x.dtype == torch.bfloat16 and x.stride(0) == d and q.stride(0) == H * hd
+    assert attn.stride(0) == H * hd and front_eligible(M, d, H, Hkv, hd, nsplit), (M, d, H, Hkv, hd, nsplit)
+    if part_o is None:
+        part_o = torch.empty(M * H * nsplit * hd, device=x.device, dtype=torch.float32)
+        part_ml = torch.empty(attention_ml_floats(M, H, Hkv, nsplit), device=x.device, dtype=torch.float32)
+    if counters is None:
+        counters = torch.zeros(M * Hkv, device=x.device, dtype=torch.int32)
+    if flags is None:
+        flags = torch.zeros(16, device=x.device, dtype=torch.int32)
+    _check(lib.cain_front(_p(wqkv), _p(bqkv), _p(wo), _p(x), _p(q), _p(attn), _p(kc), _p(vtc), _p(slot), _p(pos),
+                          _p(cos_t), _p(sin_t), M, d, H, Hkv, hd, T_max, eps, int(bool(norm)), _p(part_o),
+                          _p(part_ml), _p(counters), nsplit, scale, _p(flags), _p(trace), _stream()),
+           "layer_front")
 
 
 SAMPLE_DTYPE = [("temperature", "f4"), ("top_p", "f4"), ("repeat_penalty", "f4"), ("top_k", "i4"),

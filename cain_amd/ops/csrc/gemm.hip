@@ -385,8 +385,7 @@ static hipError_t launch_e(int epi, int waves, const GemmArgs& a, const SkArgs& 
 
 // Split rule of the skinny kernel (M <= 16 rows, one workgroup per 16-row tile): a grid under ~3/4 of the CUs
 // whose tiles are long (K > 128 slices: the down projections of qwen2:1.5b / gemma:2b, 96-128 tiles of 280-512
-// slices) takes ks = ceil(K / 128 slices) k-ranges, so every workgroup streams <= 128 slices and ~3x the CUs
-// stream.  Short tiles stay whole: there the split's combine round trip (measured +1 us on
+// slices) takes ks ~ K / 80 slices k-ranges (at most 8 and ~512 workgroups), so ~4x the CUs stream.  Short tiles stay whole: there the split's combine round trip (measured +1 us on
 // qwen2:1.5b's QKV) costs more than it spreads.  (Also measured and not kept: "one-shot" waves that load all of
 // their <= 16 slices in one burst before any MFMA -- the 128 staging VGPRs halve the resident waves, and with
 // them the bytes in flight: qwen2:1.5b gate/up 11.9 -> 12.5 us, split down 9.0 -> 10.4 us, gpurun_out/r3d.)
@@ -398,7 +397,8 @@ static int skinny_split(int N, int K, int M) {
   }();
   const int nt = N / 16, KS = K / 32;
   if (!on || M > 16 || nt >= 192 || nt < 1 || KS <= 128) return 1;
-  return std::min(8, (KS + 127) / 128);
+  // ~80 slices per workgroup, at most ~512 workgroups (qwen2:1.5b down: ks 4 = 9.0 us vs ks 3 = 10.4 us)
+  return std::max(1, std::min(std::min(8, (KS + 79) / 80), 512 / nt));
 }
 
 // Waves per workgroup: 8 (the tuned choice on every llama3.1:8b decode shape, profiles/gemm_tune.md)

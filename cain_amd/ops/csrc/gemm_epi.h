@@ -81,10 +81,25 @@ __device__ __forceinline__ EpiIn epi_load(const GemmArgs& a, int tile0, int mo, 
   return epi_load_at<EPI>(a, tile0 + t, mo + b * 16 + (lane & 15), lane);
 }
 
+// One epilogue store; WT: write-through (relaxed agent-scope atomic store = global_store ... sc1), for outputs
+// another workgroup of the same launch reads with sc1 loads (front.hip's in-launch hand-offs).
+template <bool WT, class T>
+__device__ __forceinline__ void st_epi(void* p, const T& v) {
+  if constexpr (WT) {
+    static_assert(sizeof(T) <= 8, "write-through epilogue stores are at most 8 bytes");
+    using U = std::conditional_t<sizeof(T) == 8, uint64_t,
+                                 std::conditional_t<sizeof(T) == 4, uint32_t,
+                                                    std::conditional_t<sizeof(T) == 2, uint16_t, uint8_t>>>;
+    __hip_atomic_store(reinterpret_cast<U*>(p), __builtin_bit_cast(U, v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else {
+    *reinterpret_cast<T*>(p) = v;
+  }
+}
+
 // Finish and store one 64-unit chunk (one 16x16 output block: n in tile gt, 16 rows m).
 // get(off) returns the final fp32 accumulator of the unit held by lane (lane + off) of the
 // chunk; the pair epilogues read their partner rows (+8 of the tile) at off = 32.
-template <int EPI, class Get>
+template <int EPI, bool WT = false, class Get>
 __device__ __forceinline__ void epi_store(const GemmArgs& a, int gt, int m, int lane, const EpiIn& e, Get get) {
   const int nsub = (lane >> 4) * 4;
   const bool mvalid = m < a.M;
@@ -100,7 +115,7 @@ __device__ __forceinline__ void epi_store(const GemmArgs& a, int gt, int m, int 
         const float av = (EPI == EPI_SILU) ? silu_f(g[i]) : gelu_tanh_f(g[i]);
         o[i] = f2bf(av * up[i]);
       }
-      if (mvalid) *reinterpret_cast<bf16x4*>(reinterpret_cast<__bf16*>(a.Y) + (size_t)m * a.ldy + n) = o;
+      if (mvalid) st_epi<WT>(reinterpret_cast<__bf16*>(a.Y) + (size_t)m * a.ldy + n, o);
     }
   } else if constexpr (EPI == EPI_QKV_ROPE) {
     const int tph = a.hd >> 4;  // tiles per head
@@ -125,21 +140,19 @@ __device__ __forceinline__ void epi_store(const GemmArgs& a, int gt, int m, int 
         }
         if (head < a.H) {
           __bf16* dst = reinterpret_cast<__bf16*>(a.Y) + (size_t)m * a.ldy + head * a.hd;
-          *reinterpret_cast<bf16x4*>(dst + j0) = y1;
-          *reinterpret_cast<bf16x4*>(dst + j0 + half) = y2;
+          st_epi<WT>(dst + j0, y1);
+          st_epi<WT>(dst + j0 + half, y2);
         } else {
           // fragment-major K cache (attention.hip): 4 consecutive head dims of one position are contiguous
           const size_t base = ((size_t)sl * a.Hkv + (head - a.H)) * a.T_max * a.hd;
           if (a.kv8) {  // the bf16-rounded values, as e4m3: one dword per 4 head dims
             uint8_t* kb = reinterpret_cast<uint8_t*>(a.kc) + base;
-            *reinterpret_cast<uint32_t*>(kb + kfrag_off(e.p, j0, a.hd)) =
-                fp8x4(bf2f(y1[0]), bf2f(y1[1]), bf2f(y1[2]), bf2f(y1[3]));
-            *reinterpret_cast<uint32_t*>(kb + kfrag_off(e.p, j0 + half, a.hd)) =
-                fp8x4(bf2f(y2[0]), bf2f(y2[1]), bf2f(y2[2]), bf2f(y2[3]));
+            st_epi<WT>(kb + kfrag_off(e.p, j0, a.hd), fp8x4(bf2f(y1[0]), bf2f(y1[1]), bf2f(y1[2]), bf2f(y1[3])));
+            st_epi<WT>(kb + kfrag_off(e.p, j0 + half, a.hd), fp8x4(bf2f(y2[0]), bf2f(y2[1]), bf2f(y2[2]), bf2f(y2[3])));
           } else {
             __bf16* kb = a.kc + base;
-            *reinterpret_cast<bf16x4*>(kb + kfrag_off(e.p, j0, a.hd)) = y1;
-            *reinterpret_cast<bf16x4*>(kb + kfrag_off(e.p, j0 + half, a.hd)) = y2;
+            st_epi<WT>(kb + kfrag_off(e.p, j0, a.hd), y1);
+            st_epi<WT>(kb + kfrag_off(e.p, j0 + half, a.hd), y2);
           }
         }
       }
@@ -154,12 +167,12 @@ __device__ __forceinline__ void epi_store(const GemmArgs& a, int gt, int m, int 
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int p8 = __builtin_amdgcn_cvt_pk_fp8_f32(fp8_sat(bf2f(f2bf(v[i] + e.b1[i]))), 0.f, 0, false);
-          dst[i * 8] = uint8_t(p8 & 0xff);
+          st_epi<WT>(dst + i * 8, uint8_t(p8 & 0xff));
         }
       } else {
         __bf16* dst = a.vtc + off;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) dst[i * 8] = f2bf(v[i] + e.b1[i]);
+        for (int i = 0; i < 4; ++i) st_epi<WT>(dst + i * 8, f2bf(v[i] + e.b1[i]));
       }
     }
   } else {
@@ -171,13 +184,13 @@ __device__ __forceinline__ void epi_store(const GemmArgs& a, int gt, int m, int 
       bf16x4 o;
 #pragma unroll
       for (int i = 0; i < 4; ++i) o[i] = f2bf(v[i] + e.b1[i]);
-      if (mvalid) *reinterpret_cast<bf16x4*>(reinterpret_cast<__bf16*>(a.Y) + (size_t)m * a.ldy + n) = o;
+      if (mvalid) st_epi<WT>(reinterpret_cast<__bf16*>(a.Y) + (size_t)m * a.ldy + n, o);
     } else {  // EPI_RESID: in-place residual update
       if (mvalid) {
         bf16x4 o;
 #pragma unroll
         for (int i = 0; i < 4; ++i) o[i] = f2bf(v[i] + bf2f(e.r[i]));
-        *reinterpret_cast<bf16x4*>(reinterpret_cast<__bf16*>(a.Y) + (size_t)m * a.ldy + n) = o;
+        st_epi<WT>(reinterpret_cast<__bf16*>(a.Y) + (size_t)m * a.ldy + n, o);
       }
     }
   }

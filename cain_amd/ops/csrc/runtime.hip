@@ -7,7 +7,7 @@
 // prompt token, each with its own cache slot and position):
 //
 //   embed -> L x [QKV GEMM(+RMSNorm, +bias, RoPE, KV append)
-//                 -> attention(+split combine) -> O GEMM(+residual)
+//                 -> attention(+split combine) -> O GEMM(+residual)      (<= 4 bf16 rows: ONE launch, front.hip)
 //                 -> gate/up GEMM(+RMSNorm, act*mul) -> down GEMM(+residual)]
 //                 -> LM-head GEMM(+RMSNorm) -> sample
 //
@@ -17,6 +17,7 @@
 // round trip per token (graph-replay floor instead of ~290 host launches per
 // token: MI355X_MICROARCH.md rows 'boundary', 'graph-replay-floor').
 #include <cstdio>
+#include <cstdlib>
 #include <vector>
 
 #include "common.h"
@@ -50,6 +51,12 @@ CAIN_API int cain_sample(float* logits, int ldl, int V, int* tok, int* pos, int*
                          const int* max_new, int* done, int* hist, const int* slot, int T_max, int M,
                          const void* params, hipStream_t st);
 CAIN_API long long cain_sample_ws_bytes(int M);
+CAIN_API int cain_front_eligible(int M, int d, int q_dim, int hd, int H, int Hkv, int nsplit, int kv8);
+CAIN_API int cain_front(const void* wqkv, const float* bqkv, const void* wo, void* x, void* q, void* attn,
+                        void* kc, void* vtc, const int* slot, const int* pos, const float* cos_t, const float* sin_t,
+                        int M, int d, int H, int Hkv, int hd, int T_max, float eps, int norm, float* part_o,
+                        float* part_ml, unsigned* att_ctr, int nsplit, float scale, unsigned* flags,
+                        unsigned long long* trace, hipStream_t st);
 CAIN_API int cain_sample_ex(float* logits, int ldl, int V, int* tok, int* pos, int* gen, int ldg, int* n_gen,
                             const int* max_new, int* done, int* hist, const int* slot, int T_max, int M,
                             const void* params, void* ws, long long ws_bytes, hipStream_t st);
@@ -162,8 +169,11 @@ struct Plan {
   // two-stage sampler workspace (sample.hip cain_sample_ex) for decode forwards of <= 64 rows, zeroed once
   void* sample_ws = nullptr;
   long long sample_ws_bytes = 0;
+  // layer-front launch (front.hip) hand-off counters for forwards of <= 4 rows, zeroed once (null: never used)
+  unsigned* front_flags = nullptr;
   ~Plan() {
     if (sample_ws) (void)hipFree(sample_ws);
+    if (front_flags) (void)hipFree(front_flags);
   }
 };
 
@@ -178,6 +188,15 @@ thread_local char g_fail[160] = {0};
       return _e;                                                                 \
     }                                                                            \
   } while (0)
+
+// CAIN_FRONT=0: the three launches QKV / attention / O instead of the fused layer front (A/B runs)
+bool front_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("CAIN_FRONT");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
 
 bool lt_rows(const CainPlanDesc& d, int M) { return g_lt.gemm && d.lt_min_rows > 0 && M >= d.lt_min_rows && !d.w8 && d.gu; }
 
@@ -217,20 +236,32 @@ int forward(const Plan& p, int M, const CainRows& r, int want_logits, int want_s
                      d.gemm_ws_bytes, epi, d.waves, st);
   };
   const bool lt = lt_rows(d, M);
+  // few-row bf16 forwards: QKV -> attention -> O of a layer as ONE launch (front.hip)
+  const bool front = p.front_flags && !d.w8 && !lt && front_enabled() &&
+                     cain_front_eligible(M, d.d, q_dim, d.hd, d.H, d.Hkv, d.nsplit, d.kv8);
   CK(cain_embed(r.tok, d.embed, d.x, d.d, M, d.d, d.embed_scale, st));
   for (int l = 0; l < d.n_layers; ++l) {
     const CainLayer& L = p.layers[l];
     const size_t kv_off = (size_t)l * d.kv_layer_elems * (d.kv8 ? 1 : 2);  // bytes
     char* kc = static_cast<char*>(d.kcache) + kv_off;
     char* vc = static_cast<char*>(d.vtcache) + kv_off;
-    CK(gemm(L.wqkv, L.wqkv8, L.sqkv, d.x, d.d, d.d, qkv_dim, d.q, q_dim, L.bqkv, 1, kc, vc,
-            /*EPI_QKV_ROPE*/ 5 | (d.kv8 ? /*EPI_KV_FP8*/ 0x100 : 0)));
-    CK(cain_attention_ex(d.q, kc, vc, r.slot, r.pos, d.part_o, d.part_ml, d.counters, d.attn, q_dim, M, d.H, d.Hkv,
-                         d.hd, d.T_max, d.nsplit, d.attn_scale, d.kv8, 1.f, 1.f, st));
-    if (lt && L.wo_lt)
-      CK(g_lt.gemm(L.wo_lt, d.attn, q_dim, q_dim, d.d, M, d.x, d.d, 1, d.lt_ws, d.lt_ws_bytes, st));
-    else
-      CK(gemm(L.wo, L.wo8, L.so, d.attn, q_dim, q_dim, d.d, d.x, d.d, nullptr, 0, nullptr, nullptr, /*EPI_RESID*/ 1));
+    if (front) {
+      CK(cain_front(L.wqkv, L.bqkv, L.wo, d.x, d.q, d.attn, kc, vc, r.slot, r.pos, d.cos_t, d.sin_t, M, d.d, d.H,
+                    d.Hkv, d.hd, d.T_max, d.eps, 1, d.part_o, d.part_ml, d.counters, d.nsplit, d.attn_scale,
+                    p.front_flags, nullptr, st));
+    } else {
+      CK(gemm(L.wqkv, L.wqkv8, L.sqkv, d.x, d.d, d.d, qkv_dim, d.q, q_dim, L.bqkv, 1, kc, vc,
+              /*EPI_QKV_ROPE*/ 5 | (d.kv8 ? /*EPI_KV_FP8*/ 0x100 : 0)));
+      CK(cain_attention_ex(d.q, kc, vc, r.slot, r.pos, d.part_o, d.part_ml, d.counters, d.attn, q_dim, M, d.H,
+                           d.Hkv, d.hd, d.T_max, d.nsplit, d.attn_scale, d.kv8, 1.f, 1.f, st));
+    }
+    if (!front) {  // (the front launch ran the O projection too)
+      if (lt && L.wo_lt)
+        CK(g_lt.gemm(L.wo_lt, d.attn, q_dim, q_dim, d.d, M, d.x, d.d, 1, d.lt_ws, d.lt_ws_bytes, st));
+      else
+        CK(gemm(L.wo, L.wo8, L.so, d.attn, q_dim, q_dim, d.d, d.x, d.d, nullptr, 0, nullptr, nullptr,
+                /*EPI_RESID*/ 1));
+    }
     if (lt && L.wgu_lt) {
       CK(g_lt.gemm(L.wgu_lt, d.x, d.d, d.d, 2 * d.ffn, M, d.gu, 2 * d.ffn, 0, d.lt_ws, d.lt_ws_bytes, st));
       CK(g_lt.rownorm_act(d.x, d.d, d.d, d.eps, 1, d.gu, 2 * d.ffn, d.act, d.ffn, M, d.ffn, d.act_kind, st));
@@ -275,6 +306,14 @@ CAIN_API void* cain_plan_create(const CainPlanDesc* desc) {
       if (p->sample_ws) (void)hipFree(p->sample_ws);
       p->sample_ws = nullptr;  // the one-workgroup sampler needs no workspace
     }
+  }
+  if (!desc->w8 && hipMalloc(&p->front_flags, 64) == hipSuccess) {
+    if (hipMemset(p->front_flags, 0, 64) != hipSuccess) {
+      (void)hipFree(p->front_flags);
+      p->front_flags = nullptr;
+    }
+  } else {
+    p->front_flags = nullptr;
   }
   return p;
 }

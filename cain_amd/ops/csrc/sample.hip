@@ -91,6 +91,21 @@ __device__ void advance_row(int m, int choice, int ng, const SampleParams& P, in
   }
 }
 
+// Overflow of the candidate buffer (more than MAXC elements >= tau, possible for top_k >= ~128): the K-th largest
+// of the MAXC stored candidates (all >= tau) is a tighter threshold that still keeps every top-K element (the
+// row's K-th largest is >= the K-th largest of any subset); the caller re-gathers with it.  Returns the new tau
+// through *s_tau (every thread of the workgroup calls it; ends with a barrier).
+__device__ void tighten_tau(const float* cval, const int* cidx, int K, int nthreads, float* s_tau) {
+  for (int a = threadIdx.x; a < MAXC; a += nthreads) {
+    const float va = cval[a];
+    const int ia = cidx[a];
+    int r = 0;
+    for (int b = 0; b < MAXC; ++b) r += (cval[b] > va) || (cval[b] == va && cidx[b] < ia);
+    if (r == K - 1) *s_tau = va;
+  }
+  __syncthreads();
+}
+
 __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(
     float* __restrict__ logits, int ldl, int V, int* __restrict__ tok, int* __restrict__ pos,
     int* __restrict__ gen, int ldg, int* __restrict__ n_gen, const int* __restrict__ max_new,
@@ -141,7 +156,10 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(
   for (int base = tid; base < V4; base += 4 * SAMPLE_THREADS) {
     f32x4 c[4];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) c[u] = lg4[min(base + u * SAMPLE_THREADS, V4 - 1)];  // unconditional (clamped)
+    for (int u = 0; u < 4; ++u) {  // unconditional loads; chunks past the row re-read chunk tid % V4
+      const int i4 = base + u * SAMPLE_THREADS;
+      c[u] = lg4[i4 < V4 ? i4 : tid % V4];
+    }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const bool in = base + u * SAMPLE_THREADS < V4;
@@ -219,14 +237,20 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(
       }
       if (r == K - 1) s_tau = kv;
     }
+    __syncthreads();
+    // ---- pass 2: gather candidates >= tau (few; LDS atomics only for them); on an overflow of the candidate
+    // buffer the threshold is tightened and the row gathered again (tighten_tau)
+    for (int attempt = 0; attempt < 4; ++attempt) {
     if (tid == 0) s_nc = 0;
     __syncthreads();
     const float tau = s_tau;
-    // ---- pass 2: gather candidates >= tau (few; LDS atomics only for them)
     for (int base = tid; base < V4; base += 4 * SAMPLE_THREADS) {
       f32x4 c[4];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) c[u] = lg4[min(base + u * SAMPLE_THREADS, V4 - 1)];  // unconditional (clamped)
+      for (int u = 0; u < 4; ++u) {  // unconditional loads; chunks past the row re-read chunk tid % V4
+        const int i4 = base + u * SAMPLE_THREADS;
+        c[u] = lg4[i4 < V4 ? i4 : tid % V4];
+      }
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const bool in = base + u * SAMPLE_THREADS < V4;
@@ -250,6 +274,9 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(
       }
     }
     __syncthreads();
+    if (s_nc <= MAXC) break;
+    tighten_tau(cval, cidx, K, SAMPLE_THREADS, &s_tau);
+    }
     // ---- rank the candidates (value desc, index asc); keep the top K in sorted order
     const int nc = min(s_nc, MAXC);
     for (int a = tid; a < nc; a += SAMPLE_THREADS) {
@@ -274,21 +301,24 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(
 // =====================================================================================================
 // Two-stage sampler for few rows (single-stream decode, continuous batches of a few requests).
 //
-// The one-workgroup-per-row kernel above streams a row's logits through ONE CU twice: 39-48 us per token at
-// batch 1 for 128-256 k vocabularies (profiles/r2/prof_b1_r2_kernel_stats.csv) -- as long as three decode
-// layers of qwen2:1.5b.  Here SS_P workgroups share a row: each scans 1/SS_P of the vocabulary (repeat penalty
-// for the ids it owns, then its exact local top-K by the same thread-maxima threshold + gather + rank as above,
-// or its argmax when greedy) and publishes the sorted list with write-through stores; the LAST arriving
-// workgroup of the row (ticket) merges the SS_P sorted lists -- each candidate's global rank is its position in
-// its own list plus a binary search in every other list -- and runs the same temperature / top-p / draw and
-// decode-state update as the one-workgroup kernel.  The union of local top-K lists holds the global top-K and
-// (value desc, index asc) is a strict order, so both kernels draw the same token from the same logits and seed.
+// The one-workgroup-per-row kernel above streams a row's logits through ONE CU twice: 39-67 us per token at batch
+// 1 for 128-256 k vocabularies -- as long as several decode layers of qwen2:1.5b.  Here SS_P workgroups share a
+// row.  Each holds 1/SS_P of the vocabulary in registers (one memory round trip), applies the repeat penalty to the
+// ids it owns and finds its exact local top-K with the same threshold argument as the one-workgroup kernel, at
+// workgroup scale: tau = the K-th largest of its 256 thread maxima (wave bitonic sorts + binary searches) keeps
+// every local top-K element, the few elements >= tau (typically K..3K) go to LDS and are ranked there.  The slice
+// publishes its sorted list write-through; the LAST arriving workgroup of the row (ticket) gathers the SS_P lists
+// above tau_m = the largest K-th entry of any full list (again a lower bound of the row's K-th largest), ranks
+// them and runs the same temperature / top-p / draw and decode-state update as the one-workgroup kernel.  The union
+// of the local top-K lists holds the global top-K and (value desc, index asc) is a strict order, so both kernels
+// draw the same token from the same logits and seed.  (An earlier version found each top-K by K rounds of a
+// wave argmax: 105-341 us per token, profiles/r3/.)
 // =====================================================================================================
 constexpr int SS_THREADS = 256;
+constexpr int SS_NW = SS_THREADS / 64;
 constexpr int SS_P = 16;      // vocabulary slices (workgroups) per row
 constexpr int SS_KMAX = 256;  // top-k clamp, as the one-workgroup kernel
 constexpr int SS_NJ = 16;     // 16-byte chunks per thread: a slice holds <= SS_NJ * 4 * SS_THREADS elements
-constexpr int SS_G = 4;       // sub-maxima per thread (threshold granularity)
 
 struct SampleWs {  // per row: SS_P sorted candidate lists + their lengths; one ticket counter per row
   float* cv;       // [M][SS_P][SS_KMAX]
@@ -296,6 +326,59 @@ struct SampleWs {  // per row: SS_P sorted candidate lists + their lengths; one 
   int* cn;         // [M][SS_P]
   unsigned* ctr;   // [M], zero between launches (the merger resets it)
 };
+
+__device__ __forceinline__ bool ss_before(float av, int ai, float bv, int bi) {
+  return av > bv || (av == bv && ai < bi);
+}
+
+// The K-th largest (value desc, index asc) of the workgroup's SS_THREADS keys (bv, bi), all distinct in that order;
+// every thread calls it, the value lands in *s_tau (ends with a barrier).  Each wave bitonic-sorts its 64 keys in
+// registers; a key's rank is its lane plus, per other wave, a 6-step binary search in that wave's sorted list.
+__device__ void ss_kth(float bv, int bi, int K, float (*ws_v)[64], int (*ws_i)[64], float* s_tau) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  float kv = bv;
+  int ki = bi;
+  for (int k = 2; k <= 64; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      const float ov = __shfl_xor(kv, j, 64);
+      const int oi = __shfl_xor(ki, j, 64);
+      const bool o_before = ss_before(ov, oi, kv, ki);
+      const bool keep_before = ((lane & j) == 0) == ((lane & k) == 0);
+      if (keep_before ? o_before : !o_before) { kv = ov; ki = oi; }
+    }
+  }
+  ws_v[wv][lane] = kv;
+  ws_i[wv][lane] = ki;
+  __syncthreads();
+  if (lane < K) {
+    int r = lane;
+    for (int w2 = 0; w2 < SS_NW; ++w2) {
+      if (w2 == wv) continue;
+      int lo = 0, hi = 64;
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (ss_before(ws_v[w2][mid], ws_i[w2][mid], kv, ki)) lo = mid + 1; else hi = mid;
+      }
+      r += lo;
+    }
+    if (r == K - 1) *s_tau = kv;
+  }
+  __syncthreads();
+}
+
+// Rank the n candidates cval/cidx[0..n) and write the first K in order to sv / si (every thread calls it; ends with
+// a barrier).  Returns min(n, K).
+__device__ int ss_rank(const float* cval, const int* cidx, int n, int K, float* sv, int* si) {
+  for (int a = threadIdx.x; a < n; a += SS_THREADS) {
+    const float va = cval[a];
+    const int ia = cidx[a];
+    int r = 0;
+    for (int b = 0; b < n; ++b) r += ss_before(cval[b], cidx[b], va, ia);
+    if (r < K) { sv[r] = va; si[r] = ia; }
+  }
+  __syncthreads();
+  return min(n, K);
+}
 
 __global__ __launch_bounds__(SS_THREADS) void sample_split_kernel(
     float* __restrict__ logits, int ldl, int V, int* __restrict__ tok, int* __restrict__ pos,
@@ -306,8 +389,7 @@ __global__ __launch_bounds__(SS_THREADS) void sample_split_kernel(
   if (slot[m] < 0 || done[m]) return;  // the same for every workgroup of the row: no ticket is taken
   const SampleParams P = params[m];
   float* lg = logits + (size_t)m * ldl;
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  constexpr int NW = SS_THREADS / 64;
+  const int tid = threadIdx.x;
   // this workgroup's slice [v0, v1) of the vocabulary (16-byte aligned starts)
   const int chunk = (((V + SS_P - 1) / SS_P) + 3) & ~3;
   const int v0 = min(V, part * chunk), v1 = min(V, v0 + chunk);
@@ -315,24 +397,19 @@ __global__ __launch_bounds__(SS_THREADS) void sample_split_kernel(
   int K = P.top_k;
   if (K <= 0 || K > SS_KMAX) K = SS_KMAX;
   if (K > V) K = V;
-  const int KL = greedy ? 1 : K;  // list length published per slice (at most)
+  const int KL = greedy ? 1 : K;  // list length a slice publishes (at most)
 
   __shared__ int s_hist[HIST];
-  __shared__ float ws_v[NW][64];
-  __shared__ int ws_i[NW][64];
-  __shared__ float sub_v[NW * SS_G][64];
-  __shared__ int sub_i[NW * SS_G][64];
+  __shared__ float ws_v[SS_NW][64];
+  __shared__ int ws_i[SS_NW][64];
+  __shared__ float cval[MAXC];
+  __shared__ int cidx[MAXC];
+  __shared__ float sv[SS_KMAX];
+  __shared__ int si[SS_KMAX];
   __shared__ float s_tau;
   __shared__ int s_nc;
   __shared__ unsigned s_ticket;
-  __shared__ float cval[MAXC];
-  __shared__ int cidx[MAXC];
-  __shared__ float mv[SS_P * SS_KMAX];  // merger: all lists (the stage-1 ranks reuse it as scratch)
-  __shared__ int mi[SS_P * SS_KMAX];
   __shared__ int mn[SS_P];
-  __shared__ float sv[SS_KMAX];
-  __shared__ int si[SS_KMAX];
-  __shared__ int s_choice;
 
   // ---- repeat penalty of the history ids this slice owns (llama.cpp semantics: once per distinct id)
   const int* hr = hist + (size_t)m * HIST;
@@ -353,209 +430,119 @@ __global__ __launch_bounds__(SS_THREADS) void sample_split_kernel(
     __syncthreads();
   }
 
-  // ---- the slice in registers: thread t holds 16-byte chunks t, t + 256, ... (SS_NJ of them, all loads in
-  // flight at once -- one memory round trip), every later pass reads registers, not memory
-  const int n4 = (v1 - v0) >> 2;  // whole chunks; the < 4-element tail (V % 4, last slice only) runs scalar
+  // ---- the slice in registers: thread t holds 16-byte chunks t, t + 256, ... (all loads in flight at once --
+  // one memory round trip).  Every load is unconditional, masked after it returns (a select between a load and a
+  // constant makes hipcc branch around each load and wait for it alone, cdna_hip_programming.md §5 item 4(c));
+  // chunks past the slice re-read chunk tid % n4, spread over the slice (not all on one address).  Element
+  // (j, q) of thread t is id v0 + 4 * (t + 256 j) + q; slot SS_NJ * 4 is the < 4-element tail (last slice only).
+  const int n4 = (v1 - v0) >> 2;
   const f32x4* lg4 = reinterpret_cast<const f32x4*>(lg + v0);
-  // every load unconditional from a clamped chunk, masked after it returns: a select between a load and a
-  // constant makes hipcc branch around each load and wait for it alone (16 dependent round trips; measured
-  // 104 us per token this way at one row) -- cdna_hip_programming.md §5 item 4(c)
-  f32x4 c[SS_NJ];
-  if (n4 > 0) {
+  float e[SS_NJ * 4 + 1];
+  {
+    const int spare = n4 > 0 ? tid % n4 : 0;
 #pragma unroll
-    for (int j = 0; j < SS_NJ; ++j) c[j] = lg4[min(tid + j * SS_THREADS, n4 - 1)];
+    for (int j = 0; j < SS_NJ; ++j) {
+      const int i4 = tid + j * SS_THREADS;
+      const f32x4 c = lg4[i4 < n4 ? i4 : spare];  // n4 == 0: a slice of < 4 elements, chunk 0 is in the row
+#pragma unroll
+      for (int q = 0; q < 4; ++q) e[4 * j + q] = i4 < n4 ? c[q] : -INFINITY;
+    }
   }
-#pragma unroll
-  for (int j = 0; j < SS_NJ; ++j) {
-    const bool in = tid + j * SS_THREADS < n4;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) c[j][e] = in ? c[j][e] : -INFINITY;
-  }
-  float tail = -INFINITY;
   const int ti = v0 + (n4 << 2) + tid;
-  if (ti < v1) tail = lg[ti];
-  auto elem_index = [&](int j, int e) { return v0 + (tid + j * SS_THREADS) * 4 + e; };
+  e[SS_NJ * 4] = ti < v1 ? lg[ti < V ? ti : tid] : -INFINITY;
+  auto eid = [&](int k) { return k < SS_NJ * 4 ? v0 + 4 * (tid + (k >> 2) * SS_THREADS) + (k & 3) : ti; };
 
-  float* my_v = ws.cv + ((size_t)m * SS_P + part) * SS_KMAX;
-  int* my_i = ws.ci + ((size_t)m * SS_P + part) * SS_KMAX;
-  if (greedy) {
-    float bv = tail;
-    int bi = ti < v1 ? ti : 0x7fffffff;
+  // ---- thread max (lowest id on ties: ids grow with k); an empty thread gets a unique sentinel id
+  float bv = -INFINITY;
+  int bk = -1;
 #pragma unroll
-    for (int j = 0; j < SS_NJ; ++j)
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-        if (c[j][e] > bv) { bv = c[j][e]; bi = elem_index(j, e); }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      const float ov = __shfl_xor(bv, o, 64);
-      const int oi = __shfl_xor(bi, o, 64);
-      if (ov > bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
-    }
-    if (lane == 0) { ws_v[wv][0] = bv; ws_i[wv][0] = bi; }
-    __syncthreads();
-    if (tid == 0) {
-      float v = ws_v[0][0];
-      int ix = ws_i[0][0];
-      for (int w = 1; w < NW; ++w)
-        if (ws_v[w][0] > v || (ws_v[w][0] == v && ws_i[w][0] < ix)) { v = ws_v[w][0]; ix = ws_i[w][0]; }
-      __hip_atomic_store(my_v, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(my_i, ix, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(ws.cn + (size_t)m * SS_P + part, v1 > v0 ? 1 : 0, __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-    }
-  } else {
-    // threshold tau = K-th largest of the SS_G * 256 sub-maxima (each thread's chunks in SS_G groups; ties
-    // broken by sub-maximum id, a strict order): K distinct elements are >= tau, so every top-K element of the
-    // slice is.  With SS_G = 4 sub-maxima per thread, the elements >= tau stay few even at top_k = 256.
-    // Each wave bitonic-sorts each of its SS_G lists of 64 (value desc, id asc); a value's rank is its own
-    // position plus a binary search in every other list.
-    constexpr int JG = SS_NJ / SS_G;
-#pragma unroll
-    for (int g = 0; g < SS_G; ++g) {
-      float kv = -INFINITY;
-#pragma unroll
-      for (int j = g * JG; j < (g + 1) * JG; ++j)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) kv = fmaxf(kv, c[j][e]);
-      if (g == SS_G - 1) kv = fmaxf(kv, tail);
-      int ki = tid * SS_G + g;
-      for (int k = 2; k <= 64; k <<= 1) {
-        for (int jj = k >> 1; jj > 0; jj >>= 1) {
-          const float ov = __shfl_xor(kv, jj, 64);
-          const int oi = __shfl_xor(ki, jj, 64);
-          const bool o_before = (ov > kv) || (ov == kv && oi < ki);
-          const bool keep_before = ((lane & jj) == 0) == ((lane & k) == 0);
-          if (keep_before ? o_before : !o_before) { kv = ov; ki = oi; }
-        }
-      }
-      sub_v[wv * SS_G + g][lane] = kv;
-      sub_i[wv * SS_G + g][lane] = ki;
-    }
-    if (tid == 0) { s_nc = 0; s_tau = -INFINITY; }
-    __syncthreads();
-    constexpr int NL = NW * SS_G;  // sorted lists of 64
-#pragma unroll
-    for (int g = 0; g < SS_G; ++g) {
-      const int l = wv * SS_G + g;
-      if (lane < K) {
-        const float kv = sub_v[l][lane];
-        const int ki = sub_i[l][lane];
-        int r = lane;
-        for (int l2 = 0; l2 < NL; ++l2) {
-          if (l2 == l) continue;
-          int lo = 0, hi = 64;
-          while (lo < hi) {
-            const int mid = (lo + hi) >> 1;
-            const float xv = sub_v[l2][mid];
-            const bool before = (xv > kv) || (xv == kv && sub_i[l2][mid] < ki);
-            if (before) lo = mid + 1; else hi = mid;
-          }
-          r += lo;
-          if (r >= K) break;
-        }
-        if (r == K - 1) s_tau = kv;
-      }
-    }
+  for (int k = 0; k < SS_NJ * 4 + 1; ++k)
+    if (e[k] > bv) { bv = e[k]; bk = k; }
+  const int bi = bk >= 0 ? eid(bk) : 0x7fffff00 + tid;
+
+  // ---- tau: K-th largest thread max; gather the elements >= tau, rank them; on an overflow of the candidate
+  // buffer tighten tau (tighten_tau) and gather again from the registers
+  if (tid == 0) s_tau = -INFINITY;
+  ss_kth(bv, bi, min(KL, SS_THREADS), ws_v, ws_i, &s_tau);
+  for (int attempt = 0; attempt < 4; ++attempt) {
+    if (tid == 0) s_nc = 0;
     __syncthreads();
     const float tau = s_tau;
-    // gather the slice's elements >= tau from registers
 #pragma unroll
-    for (int j = 0; j < SS_NJ; ++j)
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-        if (c[j][e] >= tau) {
-          const int k = atomicAdd(&s_nc, 1);
-          if (k < MAXC) { cval[k] = c[j][e]; cidx[k] = elem_index(j, e); }
-        }
-    if (ti < v1 && tail >= tau) {
-      const int k = atomicAdd(&s_nc, 1);
-      if (k < MAXC) { cval[k] = tail; cidx[k] = ti; }
-    }
+    for (int k = 0; k < SS_NJ * 4 + 1; ++k)
+      if (e[k] >= tau && e[k] > -INFINITY) {
+        const int c = atomicAdd(&s_nc, 1);
+        if (c < MAXC) { cval[c] = e[k]; cidx[c] = eid(k); }
+      }
     __syncthreads();
-    const int nc = min(s_nc, MAXC);
-    const int nl = min(nc, K);
-    for (int a = tid; a < nc; a += SS_THREADS) {
-      const float va = cval[a];
-      const int ia = cidx[a];
-      int r = 0;
-      for (int b = 0; b < nc; ++b) {
-        const float vb = cval[b];
-        r += (vb > va) || (vb == va && cidx[b] < ia);
-      }
-      if (r < nl) {  // publish in rank order (write-through: the merger may sit on another XCD)
-        __hip_atomic_store(my_v + r, va, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(my_i + r, ia, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
-    if (tid == 0) __hip_atomic_store(ws.cn + (size_t)m * SS_P + part, nl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (s_nc <= MAXC) break;
+    tighten_tau(cval, cidx, KL, SS_THREADS, &s_tau);
   }
+  const int nl = ss_rank(cval, cidx, min(s_nc, MAXC), KL, sv, si);
 
-  // ---- every storing wave drains, one lane takes the row's ticket; the last slice merges
+  // ---- publish the sorted list (write-through: the merger may sit on another XCD), drain, take the row's ticket
+  float* my_v = ws.cv + ((size_t)m * SS_P + part) * SS_KMAX;
+  int* my_i = ws.ci + ((size_t)m * SS_P + part) * SS_KMAX;
+  if (tid < nl) {
+    __hip_atomic_store(my_v + tid, sv[tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(my_i + tid, si[tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (tid == 0) __hip_atomic_store(ws.cn + (size_t)m * SS_P + part, nl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (tid == 0) s_ticket = __hip_atomic_fetch_add(ws.ctr + m, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
   if (s_ticket != unsigned(SS_P - 1)) return;
 
-  if (tid < SS_P) mn[tid] = __hip_atomic_load(ws.cn + (size_t)m * SS_P + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __syncthreads();
+  // ---- merger: list lengths, tau_m = the largest KL-th entry of a full list (sc1 loads throughout)
   const float* rv = ws.cv + (size_t)m * SS_P * SS_KMAX;
   const int* ri = ws.ci + (size_t)m * SS_P * SS_KMAX;
-  for (int e = tid; e < SS_P * KL; e += SS_THREADS) {
-    const int q = e / KL, j = e - q * KL;
-    if (j < mn[q]) {
-      mv[q * SS_KMAX + j] = __hip_atomic_load(rv + q * SS_KMAX + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      mi[q * SS_KMAX + j] = __hip_atomic_load(ri + q * SS_KMAX + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+  if (tid < SS_P) {
+    const int n = __hip_atomic_load(ws.cn + (size_t)m * SS_P + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    mn[tid] = n;
+    const float last = __hip_atomic_load(rv + tid * SS_KMAX + (KL - 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    float t = n >= KL ? last : -INFINITY;
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) t = fmaxf(t, __shfl_xor(t, o, 64));
+    if (tid == 0) s_tau = t;
   }
   if (tid == 0) ws.ctr[m] = 0u;  // ready for the next launch (launch-ordered)
   __syncthreads();
-
-  int choice;
-  if (greedy) {
-    if (tid == 0) {
-      float v = -INFINITY;
-      int ix = 0x7fffffff;
-      for (int q = 0; q < SS_P; ++q)
-        if (mn[q] > 0 && (mv[q * SS_KMAX] > v || (mv[q * SS_KMAX] == v && mi[q * SS_KMAX] < ix))) {
-          v = mv[q * SS_KMAX];
-          ix = mi[q * SS_KMAX];
-        }
-      s_choice = ix;
-    }
+  // candidate slot k = q * KL + r (list q, rank r); thread t takes slots t, t + 256, ... (<= 16 each)
+  const int nslot = SS_P * KL;
+  for (int attempt = 0; attempt < 4; ++attempt) {
+    if (tid == 0) s_nc = 0;
     __syncthreads();
-    choice = s_choice;
-  } else {
-    // global rank of each listed candidate: its own position + binary search in every other list
-    int total = 0;
-    for (int q = 0; q < SS_P; ++q) total += mn[q];
-    const int n = min(total, K);
-    for (int e = tid; e < SS_P * KL; e += SS_THREADS) {
-      const int q = e / KL, j = e - q * KL;
-      if (j >= mn[q]) continue;
-      const float va = mv[q * SS_KMAX + j];
-      const int ia = mi[q * SS_KMAX + j];
-      int r = j;
-      for (int q2 = 0; q2 < SS_P; ++q2) {
-        if (q2 == q) continue;
-        int lo = 0, hi = mn[q2];
-        while (lo < hi) {
-          const int mid = (lo + hi) >> 1;
-          const float xv = mv[q2 * SS_KMAX + mid];
-          const bool before = (xv > va) || (xv == va && mi[q2 * SS_KMAX + mid] < ia);
-          if (before) lo = mid + 1; else hi = mid;
-        }
-        r += lo;
+    const float tau = s_tau;
+    for (int k0 = 0; k0 < nslot; k0 += 4 * SS_THREADS) {
+      float x[4];
+      int xi[4];
+      bool in[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {  // unconditional loads from clamped, spread offsets; masked afterwards
+        const int k = k0 + u * SS_THREADS + tid;
+        const int q = k / KL, r = k - (k / KL) * KL;
+        in[u] = k < nslot && r < mn[q < SS_P ? q : 0];
+        const int off = k < nslot ? q * SS_KMAX + r : tid;
+        x[u] = __hip_atomic_load(rv + off, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        xi[u] = __hip_atomic_load(ri + off, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
-      if (r < n) { sv[r] = va; si[r] = ia; }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (in[u] && x[u] >= tau) {
+          const int c = atomicAdd(&s_nc, 1);
+          if (c < MAXC) { cval[c] = x[u]; cidx[c] = xi[u]; }
+        }
     }
     __syncthreads();
-    if (tid == 0) s_choice = draw_topk(sv, si, n, P, ng);
-    __syncthreads();
-    choice = s_choice;
+    if (s_nc <= MAXC) break;
+    tighten_tau(cval, cidx, KL, SS_THREADS, &s_tau);
   }
-  if (tid == 0) advance_row(m, choice, ng, P, tok, pos, gen, ldg, n_gen, max_new, done, hist, T_max);
+  const int n = ss_rank(cval, cidx, min(s_nc, MAXC), KL, sv, si);
+  if (tid == 0) {
+    const int choice = greedy ? si[0] : draw_topk(sv, si, n, P, ng);
+    advance_row(m, choice, ng, P, tok, pos, gen, ldg, n_gen, max_new, done, hist, T_max);
+  }
 }
 
 // params: device array of M SampleParams (per-row options, so one captured graph
