@@ -97,6 +97,7 @@ def load() -> ctypes.CDLL:
         lib.cain_sample.argtypes = [vp, ci, ci, vp, vp, vp, ci, vp, vp, vp, vp, vp, ci, ci, vp, vp]
         lib.cain_sample_ex.argtypes = [vp, ci, ci, vp, vp, vp, ci, vp, vp, vp, vp, vp, ci, ci, vp, vp,
                                        ctypes.c_longlong, vp]
+        lib.cain_sample_set_trace.argtypes = [vp]
         lib.cain_sample_ws_bytes.restype = ctypes.c_longlong
         lib.cain_sample_ws_bytes.argtypes = [ci]
         lib.cain_plan_create.restype = vp
@@ -441,7 +442,7 @@ def layer_front(wqkv, bqkv, wo, x, q, attn, kc, vtc, slot, pos, cos_t, sin_t, H,
     if counters is None:
         counters = torch.zeros(M * Hkv, device=x.device, dtype=torch.int32)
     if flags is None:
-        flags = torch.zeros(16, device=x.device, dtype=torch.int32)
+        flags = torch.zeros(4096, device=x.device, dtype=torch.int32)
     _check(lib.cain_front(_p(wqkv), _p(bqkv), _p(wo), _p(x), _p(q), _p(attn), _p(kc), _p(vtc), _p(slot), _p(pos),
                           _p(cos_t), _p(sin_t), M, d, H, Hkv, hd, T_max, eps, int(bool(norm)), _p(part_o),
                           _p(part_ml), _p(counters), nsplit, scale, _p(flags), _p(trace), _stream()),

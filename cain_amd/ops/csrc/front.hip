@@ -11,10 +11,11 @@
 //
 //   role QKV  (blocks [0, n_qkv)):            one 16-row tile of W_qkv per workgroup, 8 waves split K; fused
 //                                             RMSNorm, bias, RoPE, K/V append (gemm_epi.h EPI_QKV_ROPE) with
-//                                             write-through stores; then arrive on flags[0]
+//                                             write-through stores; then sets its own tile flag
 //   role ATT  ([n_qkv, n_qkv + n_att)):       one (row, kv head, position split) per workgroup, one 32-position
 //                                             block per wave: blocks of past positions are loaded BEFORE waiting
-//                                             for flags[0]; then q and the block holding the new position (sc1
+//                                             for the flags of the q / K / V tiles of its kv head; then q and the
+//                                             block holding the new position (sc1
 //                                             loads), both products on MFMA, in-register online softmax, LDS merge
 //                                             of the waves, last-arriver merge of the splits (attention.hip's
 //                                             scheme); the output row goes out write-through, then flags[1]
@@ -40,8 +41,11 @@ constexpr int W = 8;          // waves per workgroup (every role)
 constexpr int NTHR = W * 64;
 constexpr int U = 4;          // slices per load group (QKV role pipeline)
 constexpr int OPF = 16;       // O role: weight fragments per wave prefetched (K <= 16 * 8 * 32 = 4096)
+constexpr int NSPLIT_MAX = 8; // attention splits per (row, kv head)
 constexpr float LOG2E = 1.4426950408889634f;
 constexpr int SPIN_MAX = 1 << 22;  // bounded waits (a few hundred ms): never a hang
+constexpr int FL_ATT = 0, FL_O = 1, FL_TILE = 64;
+constexpr int MAX_TILES = 4096 - FL_TILE;  // flags buffer: 4096 words
 
 struct Args {
   GemmArgs qkv;   // EPI_QKV_ROPE (+NORM), X = residual x, Y = q buffer, caches in kc / vtc
@@ -53,7 +57,8 @@ struct Args {
   int nsplit;
   float scale;
   int n_qkv, n_att, n_o;
-  unsigned* flags;  // [0] QKV workgroups done, [1] (row, kv head) groups done, [2] O workgroups done; zero at rest
+  // [FL_ATT] (row, kv head) groups done, [FL_O] O workgroups done, [FL_TILE + t] QKV tile t done; zero at rest
+  unsigned* flags;
   unsigned long long* trace;  // optional [grid][4] timestamps (s_memrealtime, 100 MHz): start, wait begin, wait end, end
 };
 
@@ -84,7 +89,7 @@ __device__ __forceinline__ bf16x8 ld_sc1_16(const void* base, int byte_off) {
 
 // ---- cross-wave reduction of a 16x16 accumulator unit through LDS and the fused epilogue (wave 0)
 template <int EPI, bool NORM, bool WT>
-__device__ void gemv_finish(const GemmArgs& a, int tile, const f32x4& acc, float ssq, float* lds) {
+__device__ void gemv_finish(const GemmArgs& a, int tile, const f32x4& acc, float ssq, float* lds, const EpiIn& e) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   f32x4* red = reinterpret_cast<f32x4*>(lds);           // [W][64]
   float* red_ss = lds + W * 64 * 4;                     // [W][16]
@@ -97,7 +102,6 @@ __device__ void gemv_finish(const GemmArgs& a, int tile, const f32x4& acc, float
   }
   __syncthreads();
   if (wave == 0) {
-    const EpiIn e = epi_load_at<EPI>(a, tile, lane & 15, lane);
     epi_store<EPI, WT>(a, tile, lane & 15, lane, e, [&](int off) {
       const int u = lane + off;
       f32x4 v = red[u];
@@ -123,6 +127,8 @@ __device__ void role_qkv(const Args& A, int tile, float* lds) {
   const int s_beg = (wave * KS) / W, s_end = ((wave + 1) * KS) / W;
   const bf16x8* wb = a.Wp + (size_t)tile * KS * 64 + lane;
   const __bf16* xb = a.X + (size_t)min(lane & 15, a.M - 1) * a.ldx + ((lane >> 4) << 3);
+  // epilogue inputs (bias, RoPE tables, slot / position) in flight under the weight stream
+  const EpiIn e = wave == 0 ? epi_load_at<EPI_QKV_ROPE>(a, tile, lane & 15, lane) : EpiIn{};
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
   float ssq = 0.f;
   typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -162,8 +168,11 @@ __device__ void role_qkv(const Args& A, int tile, float* lds) {
   }
   stamp(A, 1);
   stamp(A, 2);
-  gemv_finish<EPI_QKV_ROPE, NORM, true>(a, tile, acc, ssq, lds);
-  arrive(A.flags + 0);
+  gemv_finish<EPI_QKV_ROPE, NORM, true>(a, tile, acc, ssq, lds, e);
+  // every storing wave drains its write-through stores, then one lane sets this tile's flag (sc1 store)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store(A.flags + FL_TILE + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // ---- role O: all of the wave's weight fragments prefetched before the wait, then the attention output
@@ -177,8 +186,10 @@ __device__ void role_o(const Args& A, int tile, float* lds, unsigned att_groups)
   bf16x8 wp[OPF];
 #pragma unroll
   for (int u = 0; u < OPF; ++u) wp[u] = __builtin_nontemporal_load(wb + (size_t)(s_beg + min(u, max(n - 1, 0))) * 64);
+  // the residual rows (not written by this launch before this epilogue)
+  const EpiIn e = wave == 0 ? epi_load_at<EPI_RESID>(a, tile, lane & 15, lane) : EpiIn{};
   stamp(A, 1);
-  if (threadIdx.x == 0) spin_until(A.flags + 1, att_groups);
+  if (threadIdx.x == 0) spin_until(A.flags + FL_ATT, att_groups);
   __syncthreads();
   stamp(A, 2);
   const int xoff = (min(lane & 15, a.M - 1) * a.ldx + ((lane >> 4) << 3)) * 2;  // bytes
@@ -196,17 +207,19 @@ __device__ void role_o(const Args& A, int tile, float* lds, unsigned att_groups)
       acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wm, x[u], acc, 0, 0, 0);
     }
   }
-  gemv_finish<EPI_RESID, false, false>(a, tile, acc, 0.f, lds);
-  // the last O workgroup resets the flags: every consumer has passed its wait by then (the attention groups all
-  // arrived before any O workgroup could start computing, and every O workgroup arrives here after its own wait)
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  gemv_finish<EPI_RESID, false, false>(a, tile, acc, 0.f, lds, e);
+  // the last O workgroup resets the flags: every consumer has passed its wait by then (each attention workgroup
+  // polled its tile flags before its group could arrive, all groups arrived before any O workgroup got past its
+  // wait, and every O workgroup takes this ticket after its own wait)
   __syncthreads();
-  if (threadIdx.x == 0) {
-    if (__hip_atomic_fetch_add(A.flags + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == unsigned(A.n_o - 1)) {
-      __hip_atomic_store(A.flags + 0, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(A.flags + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(A.flags + 2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+  unsigned* s_last = reinterpret_cast<unsigned*>(lds);
+  if (threadIdx.x == 0)
+    *s_last = __hip_atomic_fetch_add(A.flags + FL_O, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+              unsigned(A.n_o - 1);
+  __syncthreads();
+  if (*s_last) {
+    for (int i = threadIdx.x; i < FL_TILE + A.n_qkv; i += NTHR)
+      __hip_atomic_store(A.flags + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -248,7 +261,21 @@ __device__ void role_att(const Args& A, int unit, float* lds) {
     for (int dt = 0; dt < NDT; ++dt) va[dt] = __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(vbase + blk_v(blk, dt)));
   }
   stamp(A, 1);
-  if (threadIdx.x == 0) spin_until(A.flags + 0, unsigned(A.n_qkv));
+  // the last wave polls the flags of the q tiles of heads kh*G.. and of the K / V tiles of head kh (the last wave:
+  // the one least likely to hold a prefetch, which its first poll would wait for -- loads retire in order)
+  if (wave == W - 1) {
+    const int tph = HD / 16, nt = (G + 2) * tph;
+    for (int it = 0; it < SPIN_MAX; ++it) {
+      bool ok = true;
+      for (int i = lane; i < nt; i += 64) {
+        const int t = i < G * tph ? kh * G * tph + i
+                                  : (i < (G + 1) * tph ? (H + kh) * tph + i - G * tph : (H + Hkv + kh) * tph + i - (G + 1) * tph);
+        ok &= __hip_atomic_load(A.flags + FL_TILE + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
+      }
+      if (__all(ok)) break;
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
   __syncthreads();
   stamp(A, 2);
 
@@ -373,7 +400,7 @@ __device__ void role_att(const Args& A, int unit, float* lds) {
     }
   }
   if (nsplit == 1) {
-    arrive(A.flags + 1);
+    arrive(A.flags + FL_ATT);
     return;
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -382,10 +409,18 @@ __device__ void role_att(const Args& A, int unit, float* lds) {
     *s_ticket = __hip_atomic_fetch_add(A.att_ctr + mk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
   if (*s_ticket != unsigned(nsplit - 1)) return;
-  // last arriver of (m, kh): merge the splits (sc1 loads), write the output rows write-through, arrive
-  float* s_w = s_o;            // [16][64] merge weights, reusing the wave merge area
+  // last arriver of (m, kh): merge the splits, write the output rows write-through, arrive.  The partial rows and
+  // the (max, sum) pairs are requested together (sc1 loads, one round trip): <= NSPLIT_MAX partials per thread in
+  // registers while the merge weights are formed in LDS
+  float* s_w = s_o;  // [16][64] merge weights, reusing the wave merge area
   float* s_den = s_o + 16 * 64;
   const int nw = G * nsplit;
+  const int e4 = threadIdx.x < nout4 ? threadIdx.x : 0;  // nout4 <= 16 * 128 / 4 = 512 = NTHR
+  const int gg4 = (e4 * 4) / HD, d04 = e4 * 4 - gg4 * HD;
+  const int po0 = int(((pbase + (size_t)gg4 * nsplit) * HD + d04) * 4);  // bytes
+  f32x4 pv[NSPLIT_MAX];
+#pragma unroll
+  for (int j = 0; j < NSPLIT_MAX; ++j) pv[j] = ld_wt(rpo, po0 + min(j, nsplit - 1) * HD * 4);
   for (int e = threadIdx.x; e < nw; e += NTHR) {
     const int gg = e / nsplit, j = e - (e / nsplit) * nsplit;
     s_w[gg * 64 + j] = __hip_atomic_load(pml + e * 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -407,17 +442,17 @@ __device__ void role_att(const Args& A, int unit, float* lds) {
   }
   if (threadIdx.x == 0) A.att_ctr[mk] = 0u;  // ready for the next launch (launch-ordered)
   __syncthreads();
-  for (int e = threadIdx.x; e < nout4; e += NTHR) {
-    const int gg = (e * 4) / HD, d0 = e * 4 - gg * HD;
-    const int po = int(((pbase + (size_t)gg * nsplit) * HD + d0) * 4);  // bytes
+  if (threadIdx.x < nout4) {
     f32x4 num = {0.f, 0.f, 0.f, 0.f};
-    for (int j = 0; j < nsplit; ++j) num += s_w[gg * 64 + j] * ld_wt(rpo, po + j * HD * 4);
+#pragma unroll
+    for (int j = 0; j < NSPLIT_MAX; ++j)
+      if (j < nsplit) num += s_w[gg4 * 64 + j] * pv[j];
     bf16x4 ov;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) ov[i] = f2bf(num[i] * s_l[gg]);
-    st_epi<true>(A.attn + (size_t)m * ldo + (kh * G + gg) * HD + d0, ov);
+    for (int i = 0; i < 4; ++i) ov[i] = f2bf(num[i] * s_l[gg4]);
+    st_epi<true>(A.attn + (size_t)m * ldo + (kh * G + gg4) * HD + d04, ov);
   }
-  arrive(A.flags + 1);
+  arrive(A.flags + FL_ATT);
 }
 
 // LDS: the attention role's wave merge is the largest user (W x HD x 16 floats + W x 32 + a ticket)
@@ -444,20 +479,22 @@ __global__ __launch_bounds__(NTHR, 2) void front_kernel(const Args A) {
 }  // namespace front
 
 // Eligible shapes: <= 4 rows, bf16 weights and caches, head_dim 64 / 96 / 128, the O projection's whole K covered
-// by the 8 waves' register prefetch (q_dim <= 4096), <= 64 attention workgroups.
+// by the 8 waves' register prefetch (q_dim <= 4096), <= 8 attention splits and <= 64 attention workgroups.
 CAIN_API int cain_front_eligible(int M, int d, int q_dim, int hd, int H, int Hkv, int nsplit, int kv8) {
   if (M < 1 || M > 4 || kv8) return 0;
   if (hd != 64 && hd != 96 && hd != 128) return 0;
   if (d % 32 || q_dim % 32) return 0;
   if (q_dim / 32 > front::OPF * front::W) return 0;
-  if (Hkv < 1 || H % Hkv || H / Hkv > 16 || nsplit < 1 || nsplit > 64 || M * Hkv * nsplit > 64) return 0;
+  if (Hkv < 1 || H % Hkv || H / Hkv > 16 || nsplit < 1 || nsplit > front::NSPLIT_MAX || M * Hkv * nsplit > 64)
+    return 0;
+  if ((H + 2 * Hkv) * hd / 16 > front::MAX_TILES) return 0;
   return 1;
 }
 
 // One launch for QKV (+RMSNorm, bias, RoPE, KV append) -> attention -> O (+residual) of a layer.  Same operands
 // as the three launches it replaces (runtime.hip forward): wqkv / wo packed bf16 (gemm.hip layout), x the residual
 // stream [M][d] (read by QKV, updated in place by O), q [M][q_dim], attn [M][q_dim], part_o / part_ml / att_ctr
-// the attention split workspace (att_ctr zero at rest), flags 3 zeroed counters (zero again when the launch ends).
+// the attention split workspace (att_ctr zero at rest), flags 4096 zeroed words (zero again when the launch ends).
 CAIN_API int cain_front(const void* wqkv, const float* bqkv, const void* wo, void* x, void* q, void* attn,
                         void* kc, void* vtc, const int* slot, const int* pos, const float* cos_t, const float* sin_t,
                         int M, int d, int H, int Hkv, int hd, int T_max, float eps, int norm, float* part_o,

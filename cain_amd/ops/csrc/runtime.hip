@@ -307,8 +307,8 @@ CAIN_API void* cain_plan_create(const CainPlanDesc* desc) {
       p->sample_ws = nullptr;  // the one-workgroup sampler needs no workspace
     }
   }
-  if (!desc->w8 && hipMalloc(&p->front_flags, 64) == hipSuccess) {
-    if (hipMemset(p->front_flags, 0, 64) != hipSuccess) {
+  if (!desc->w8 && hipMalloc(&p->front_flags, 4096 * 4) == hipSuccess) {  // front.hip: 4096 flag words
+    if (hipMemset(p->front_flags, 0, 4096 * 4) != hipSuccess) {
       (void)hipFree(p->front_flags);
       p->front_flags = nullptr;
     }

@@ -43,34 +43,58 @@ constexpr int SAMPLE_THREADS = 1024;
 constexpr int HIST = 64;
 constexpr int MAXC = 1024;  // candidate cap after top-k (ties included)
 
-// Temperature / top-p / multinomial draw over the n candidates sv[0..n) (sorted: value desc, index asc).  The
-// random stream is keyed by the request's seed and its token index only, not by the batch row: a request that
-// continuous batching moves to another row (ContinuousBatch.retire) keeps its stream, so an Ollama `seed`
-// reproduces the same tokens however the batch is packed (rows without a seed get a unique one on the host,
-// engine._row_options).
-__device__ int draw_topk(const float* sv, const int* si, int n, const SampleParams& P, int ng) {
+// Temperature / top-p / multinomial draw over the n candidates sv[0..n) (sorted: value desc, index asc), by ONE
+// wave (every lane of the calling wave calls it; all get the pick): candidate i sits in lane i % 64 of chunk i / 64,
+// sums are wave reductions and the top-p cut / the pick are the first lanes whose inclusive prefix sum crosses the
+// bound (shuffle scans, ballots) -- no chain of dependent LDS reads.  Both sampler kernels use it, so they draw
+// the same token from the same candidates.  The random stream is keyed by the request's seed and its token index
+// only, not by the batch row: a request that continuous batching moves to another row (ContinuousBatch.retire)
+// keeps its stream, so an Ollama `seed` reproduces the same tokens however the batch is packed (rows without a
+// seed get a unique one on the host, engine._row_options).
+__device__ __forceinline__ float wave_incl_scan(float v) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const float t = __shfl_up(v, o, 64);
+    if (lane >= o) v += t;
+  }
+  return v;
+}
+
+__device__ int draw_topk_wave(const float* sv, const int* si, int n, const SampleParams& P, int ng) {
+  const int lane = threadIdx.x & 63;
   const float invT = 1.0f / P.temperature;
   const float mx = sv[0] * invT;
   float z = 0.f;
-  for (int i = 0; i < n; ++i) z += __expf(sv[i] * invT - mx);
+  for (int i = lane; i < n; i += 64) z += __expf(sv[i] * invT - mx);
+  z = wave_sum(z);
   // top-p: smallest prefix with cumulative probability >= top_p
   int cut = n;
   if (P.top_p > 0.f && P.top_p < 1.f) {
-    float c = 0.f;
-    for (int i = 0; i < n; ++i) {
-      c += __expf(sv[i] * invT - mx) / z;
-      if (c >= P.top_p) { cut = i + 1; break; }
+    float carry = 0.f;
+    for (int c0 = 0; c0 < n; c0 += 64) {
+      const int i = c0 + lane;
+      const float pi = i < n ? __expf(sv[i < n ? i : 0] * invT - mx) / z : 0.f;
+      const float c = carry + wave_incl_scan(pi);
+      const unsigned long long hit = __ballot(i < n && c >= P.top_p);
+      if (hit) { cut = c0 + __ffsll((long long)hit); break; }
+      carry = __shfl(c, 63, 64);
     }
   }
   float zc = 0.f;
-  for (int i = 0; i < cut; ++i) zc += __expf(sv[i] * invT - mx);
+  for (int i = lane; i < cut; i += 64) zc += __expf(sv[i] * invT - mx);
+  zc = wave_sum(zc);
   const uint64_t r = mix64(P.seed ^ mix64(uint64_t(ng) * 0x632BE59BD9B4E019ull + 0x9E3779B97F4A7C15ull));
   const float u = float(r >> 40) * (1.0f / 16777216.0f) * zc;
-  float c = 0.f;
   int pick = si[cut - 1];
-  for (int i = 0; i < cut; ++i) {
-    c += __expf(sv[i] * invT - mx);
-    if (u < c) { pick = si[i]; break; }
+  float carry = 0.f;
+  for (int c0 = 0; c0 < cut; c0 += 64) {
+    const int i = c0 + lane;
+    const float ei = i < cut ? __expf(sv[i < cut ? i : 0] * invT - mx) : 0.f;
+    const float c = carry + wave_incl_scan(ei);
+    const unsigned long long hit = __ballot(i < cut && u < c);
+    if (hit) { pick = si[c0 + __ffsll((long long)hit) - 1]; break; }
+    carry = __shfl(c, 63, 64);
   }
   return pick;
 }
@@ -106,6 +130,38 @@ __device__ void tighten_tau(const float* cval, const int* cidx, int K, int nthre
   __syncthreads();
 }
 
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+
+// Rank the n candidates cval/cidx[0..n) (value desc, index asc) and write the first K in order to sv / si (every
+// thread of the workgroup calls it; ends with a barrier).  The buffers hold n rounded up to 4 (+ 4 spare entries,
+// padded here with entries that rank last); each thread compares its candidate against 4 at a time with 16-byte
+// LDS reads, unrolled, so the reads pipeline instead of forming a chain.  Returns min(n, K).
+__device__ int rank_candidates(float* cval, int* cidx, int n, int K, float* sv, int* si, int nthreads) {
+  const int n4 = (n + 3) >> 2;
+  if (threadIdx.x < n4 * 4 - n) {
+    cval[n + threadIdx.x] = -INFINITY;
+    cidx[n + threadIdx.x] = 0x7fffffff;
+  }
+  __syncthreads();
+  const f32x4* cv4 = reinterpret_cast<const f32x4*>(cval);
+  const i32x4* ci4 = reinterpret_cast<const i32x4*>(cidx);
+  for (int a = threadIdx.x; a < n; a += nthreads) {
+    const float va = cval[a];
+    const int ia = cidx[a];
+    int r = 0;
+#pragma unroll 4
+    for (int b = 0; b < n4; ++b) {
+      const f32x4 v = cv4[b];
+      const i32x4 ix = ci4[b];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) r += (v[j] > va) || (v[j] == va && ix[j] < ia);
+    }
+    if (r < K) { sv[r] = va; si[r] = ia; }
+  }
+  __syncthreads();
+  return min(n, K);
+}
+
 __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(
     float* __restrict__ logits, int ldl, int V, int* __restrict__ tok, int* __restrict__ pos,
     int* __restrict__ gen, int ldg, int* __restrict__ n_gen, const int* __restrict__ max_new,
@@ -122,8 +178,8 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(
   __shared__ float s_tau;
   __shared__ float sv[256];
   __shared__ int si[256];
-  __shared__ float cval[MAXC];
-  __shared__ int cidx[MAXC];
+  __shared__ __attribute__((aligned(16))) float cval[MAXC + 4];
+  __shared__ __attribute__((aligned(16))) int cidx[MAXC + 4];
   __shared__ int s_nc;
   __shared__ float red_v[SAMPLE_THREADS / 64];
   __shared__ int red_i[SAMPLE_THREADS / 64];
@@ -240,7 +296,8 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(
     __syncthreads();
     // ---- pass 2: gather candidates >= tau (few; LDS atomics only for them); on an overflow of the candidate
     // buffer the threshold is tightened and the row gathered again (tighten_tau)
-    for (int attempt = 0; attempt < 4; ++attempt) {
+  #pragma unroll 1
+  for (int attempt = 0; attempt < 4; ++attempt) {
     if (tid == 0) s_nc = 0;
     __syncthreads();
     const float tau = s_tau;
@@ -278,19 +335,11 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(
     tighten_tau(cval, cidx, K, SAMPLE_THREADS, &s_tau);
     }
     // ---- rank the candidates (value desc, index asc); keep the top K in sorted order
-    const int nc = min(s_nc, MAXC);
-    for (int a = tid; a < nc; a += SAMPLE_THREADS) {
-      const float va = cval[a];
-      const int ia = cidx[a];
-      int r = 0;
-      for (int b = 0; b < nc; ++b) {
-        const float vb = cval[b];
-        r += (vb > va) || (vb == va && cidx[b] < ia);
-      }
-      if (r < K) { sv[r] = va; si[r] = ia; }
+    const int nk = rank_candidates(cval, cidx, min(s_nc, MAXC), K, sv, si, SAMPLE_THREADS);
+    if (tid < 64) {
+      const int pick = draw_topk_wave(sv, si, nk, P, ng);
+      if (tid == 0) s_choice = pick;
     }
-    __syncthreads();
-    if (tid == 0) s_choice = draw_topk(sv, si, min(nc, K), P, ng);
     __syncthreads();
     choice = s_choice;
   }
@@ -304,7 +353,7 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(
 // The one-workgroup-per-row kernel above streams a row's logits through ONE CU twice: 39-67 us per token at batch
 // 1 for 128-256 k vocabularies -- as long as several decode layers of qwen2:1.5b.  Here SS_P workgroups share a
 // row.  Each holds 1/SS_P of the vocabulary in registers (one memory round trip), applies the repeat penalty to the
-// ids it owns and finds its exact local top-K with the same threshold argument as the one-workgroup kernel, at
+// ids it owns (in registers: the logits stay unmodified) and finds its exact local top-K with the same threshold argument as the one-workgroup kernel, at
 // workgroup scale: tau = the K-th largest of its 256 thread maxima (wave bitonic sorts + binary searches) keeps
 // every local top-K element, the few elements >= tau (typically K..3K) go to LDS and are ranked there.  The slice
 // publishes its sorted list write-through; the LAST arriving workgroup of the row (ticket) gathers the SS_P lists
@@ -325,7 +374,15 @@ struct SampleWs {  // per row: SS_P sorted candidate lists + their lengths; one 
   int* ci;         // [M][SS_P][SS_KMAX]
   int* cn;         // [M][SS_P]
   unsigned* ctr;   // [M], zero between launches (the merger resets it)
+  // optional [M * SS_P][8] per-workgroup timestamps (s_memrealtime, 10 ns): start, slice loaded, tau, gathered,
+  // ranked, ticket, (merger) merged + ranked, end; entry 6 of non-mergers = stage-1 candidate count
+  unsigned long long* trace;
 };
+
+__device__ __forceinline__ void ss_stamp(const SampleWs& ws, int i) {
+  if (ws.trace && threadIdx.x == 0)
+    ws.trace[((size_t)blockIdx.x * SS_P + blockIdx.y) * 8 + i] = __builtin_amdgcn_s_memrealtime();
+}
 
 __device__ __forceinline__ bool ss_before(float av, int ai, float bv, int bi) {
   return av > bv || (av == bv && ai < bi);
@@ -335,6 +392,7 @@ __device__ __forceinline__ bool ss_before(float av, int ai, float bv, int bi) {
 // every thread calls it, the value lands in *s_tau (ends with a barrier).  Each wave bitonic-sorts its 64 keys in
 // registers; a key's rank is its lane plus, per other wave, a 6-step binary search in that wave's sorted list.
 __device__ void ss_kth(float bv, int bi, int K, float (*ws_v)[64], int (*ws_i)[64], float* s_tau) {
+  static_assert(sizeof(float) * 64 % 16 == 0, "16-byte rows");
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   float kv = bv;
   int ki = bi;
@@ -350,46 +408,95 @@ __device__ void ss_kth(float bv, int bi, int K, float (*ws_v)[64], int (*ws_i)[6
   ws_v[wv][lane] = kv;
   ws_i[wv][lane] = ki;
   __syncthreads();
-  if (lane < K) {
+  // a key's rank in another wave's sorted list by counting (16-byte LDS reads, all independent) rather than a
+  // binary search (a chain of dependent reads)
+  if (wv * 64 < SS_THREADS && K > 0) {
     int r = lane;
+    const f32x4* v4 = reinterpret_cast<const f32x4*>(&ws_v[0][0]);
+    const i32x4* i4 = reinterpret_cast<const i32x4*>(&ws_i[0][0]);
     for (int w2 = 0; w2 < SS_NW; ++w2) {
       if (w2 == wv) continue;
-      int lo = 0, hi = 64;
-      while (lo < hi) {
-        const int mid = (lo + hi) >> 1;
-        if (ss_before(ws_v[w2][mid], ws_i[w2][mid], kv, ki)) lo = mid + 1; else hi = mid;
+#pragma unroll
+      for (int b = 0; b < 16; ++b) {
+        const f32x4 v = v4[w2 * 16 + b];
+        const i32x4 ix = i4[w2 * 16 + b];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) r += ss_before(v[j], ix[j], kv, ki) ? 1 : 0;
       }
-      r += lo;
     }
     if (r == K - 1) *s_tau = kv;
   }
   __syncthreads();
 }
 
-// Rank the n candidates cval/cidx[0..n) and write the first K in order to sv / si (every thread calls it; ends with
-// a barrier).  Returns min(n, K).
-__device__ int ss_rank(const float* cval, const int* cidx, int n, int K, float* sv, int* si) {
-  for (int a = threadIdx.x; a < n; a += SS_THREADS) {
-    const float va = cval[a];
-    const int ia = cidx[a];
-    int r = 0;
-    for (int b = 0; b < n; ++b) r += ss_before(cval[b], cidx[b], va, ia);
-    if (r < K) { sv[r] = va; si[r] = ia; }
+
+// Append the elements e[k] (ids eid(k)) with keep(k) to cval / cidx: per wave one LDS atomic for the wave's base,
+// lanes' offsets from a wave prefix sum of their counts (no per-element atomics), and no per-element branch: an
+// element that is not kept (or past MAXC) is written to the lane's own trash slot cval / cidx[MAXC + 4 + lane]
+// (unrolled per-element branches cost an exec-mask save each and spilled the kernel's SGPRs).  Every thread calls
+// it; ends with a barrier; *s_nc = the total (may exceed MAXC: the caller tightens and gathers again).
+template <int NE, class Keep, class Id>
+__device__ void gather_candidates(const float (&e)[NE], Keep keep, Id eid, float* cval, int* cidx, int* s_nc) {
+  const int lane = threadIdx.x & 63;
+  // the keep flags as a per-lane bit mask in VGPRs (boolean lane masks would live in SGPR pairs between the two
+  // loops: 65 of them spilled)
+  constexpr int NW32 = (NE + 31) / 32;
+  uint32_t km[NW32];
+#pragma unroll
+  for (int w = 0; w < NW32; ++w) km[w] = 0u;
+#pragma unroll
+  for (int k = 0; k < NE; ++k) km[k >> 5] |= (keep(k) ? 1u : 0u) << (k & 31);
+  int cnt = 0;
+#pragma unroll
+  for (int w = 0; w < NW32; ++w) cnt += __builtin_popcount(km[w]);
+  // inclusive wave scan of cnt
+  int inc = cnt;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int t = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += t;
+  }
+  const int tot = __shfl(inc, 63, 64);
+  int base = 0;
+  if (lane == 63 && tot > 0) base = atomicAdd(s_nc, tot);
+  base = __shfl(base, 63, 64) + inc - cnt;
+  const int trash = MAXC + 4 + lane;
+#pragma unroll
+  for (int k = 0; k < NE; ++k) {
+    const int kk = (km[k >> 5] >> (k & 31)) & 1;
+    const int dst = (kk && base < MAXC) ? base : trash;
+    cval[dst] = e[k];
+    cidx[dst] = eid(k);
+    base += kk;
   }
   __syncthreads();
-  return min(n, K);
+}
+
+// Bitonic sort of one key per lane across the calling wave, (value desc, index asc): lane l ends with the l-th.
+__device__ __forceinline__ void wave_sort_desc(float& kv, int& ki) {
+  const int lane = threadIdx.x & 63;
+  for (int k = 2; k <= 64; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      const float ov = __shfl_xor(kv, j, 64);
+      const int oi = __shfl_xor(ki, j, 64);
+      const bool o_before = ss_before(ov, oi, kv, ki);
+      const bool keep_before = ((lane & j) == 0) == ((lane & k) == 0);
+      if (keep_before ? o_before : !o_before) { kv = ov; ki = oi; }
+    }
+  }
 }
 
 __global__ __launch_bounds__(SS_THREADS) void sample_split_kernel(
-    float* __restrict__ logits, int ldl, int V, int* __restrict__ tok, int* __restrict__ pos,
+    const float* __restrict__ logits, int ldl, int V, int* __restrict__ tok, int* __restrict__ pos,
     int* __restrict__ gen, int ldg, int* __restrict__ n_gen, const int* __restrict__ max_new,
     int* __restrict__ done, int* __restrict__ hist, const int* __restrict__ slot, int T_max,
     const SampleParams* __restrict__ params, const SampleWs ws) {
   const int m = blockIdx.x, part = blockIdx.y;
   if (slot[m] < 0 || done[m]) return;  // the same for every workgroup of the row: no ticket is taken
   const SampleParams P = params[m];
-  float* lg = logits + (size_t)m * ldl;
-  const int tid = threadIdx.x;
+  const float* lg = logits + (size_t)m * ldl;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  ss_stamp(ws, 0);
   // this workgroup's slice [v0, v1) of the vocabulary (16-byte aligned starts)
   const int chunk = (((V + SS_P - 1) / SS_P) + 3) & ~3;
   const int v0 = min(V, part * chunk), v1 = min(V, v0 + chunk);
@@ -399,11 +506,11 @@ __global__ __launch_bounds__(SS_THREADS) void sample_split_kernel(
   if (K > V) K = V;
   const int KL = greedy ? 1 : K;  // list length a slice publishes (at most)
 
-  __shared__ int s_hist[HIST];
-  __shared__ float ws_v[SS_NW][64];
-  __shared__ int ws_i[SS_NW][64];
-  __shared__ float cval[MAXC];
-  __shared__ int cidx[MAXC];
+  __shared__ __attribute__((aligned(16))) float ws_v[SS_NW][64];
+  __shared__ __attribute__((aligned(16))) int ws_i[SS_NW][64];
+  __shared__ __attribute__((aligned(16))) int s_hist[HIST];
+  __shared__ __attribute__((aligned(16))) float cval[MAXC + 4 + 64];  // + 4: rank padding, + 64: trash slots
+  __shared__ __attribute__((aligned(16))) int cidx[MAXC + 4 + 64];
   __shared__ float sv[SS_KMAX];
   __shared__ int si[SS_KMAX];
   __shared__ float s_tau;
@@ -411,30 +518,11 @@ __global__ __launch_bounds__(SS_THREADS) void sample_split_kernel(
   __shared__ unsigned s_ticket;
   __shared__ int mn[SS_P];
 
-  // ---- repeat penalty of the history ids this slice owns (llama.cpp semantics: once per distinct id)
-  const int* hr = hist + (size_t)m * HIST;
-  const int ng = n_gen[m];
-  const int nrep = (P.repeat_penalty != 1.0f && P.repeat_last_n > 0) ? min(min(P.repeat_last_n, HIST), ng) : 0;
-  if (nrep > 0) {
-    if (tid < HIST) s_hist[tid] = (tid < nrep) ? hr[(ng - 1 - tid) & (HIST - 1)] : -1;
-    __syncthreads();
-    if (tid < nrep) {
-      const int id = s_hist[tid];
-      bool first = id >= v0 && id < v1;
-      for (int j = 0; j < tid; ++j) first &= (s_hist[j] != id);
-      if (first) {
-        const float v = lg[id];
-        lg[id] = v > 0.f ? v / P.repeat_penalty : v * P.repeat_penalty;
-      }
-    }
-    __syncthreads();
-  }
-
-  // ---- the slice in registers: thread t holds 16-byte chunks t, t + 256, ... (all loads in flight at once --
-  // one memory round trip).  Every load is unconditional, masked after it returns (a select between a load and a
-  // constant makes hipcc branch around each load and wait for it alone, cdna_hip_programming.md §5 item 4(c));
-  // chunks past the slice re-read chunk tid % n4, spread over the slice (not all on one address).  Element
-  // (j, q) of thread t is id v0 + 4 * (t + 256 j) + q; slot SS_NJ * 4 is the < 4-element tail (last slice only).
+  // ---- the slice in registers, requested first: thread t holds 16-byte chunks t, t + 256, ... (one memory round
+  // trip).  Every load is unconditional, masked after it returns (a select between a load and a constant makes
+  // hipcc branch around each load and wait for it alone, cdna_hip_programming.md §5 item 4(c)); chunks past the
+  // slice re-read chunk tid % n4, spread over the slice.  Element (j, q) of thread t is id v0 + 4 (t + 256 j) + q;
+  // slot SS_NJ * 4 is the < 4-element tail (last slice only).
   const int n4 = (v1 - v0) >> 2;
   const f32x4* lg4 = reinterpret_cast<const f32x4*>(lg + v0);
   float e[SS_NJ * 4 + 1];
@@ -452,6 +540,20 @@ __global__ __launch_bounds__(SS_THREADS) void sample_split_kernel(
   e[SS_NJ * 4] = ti < v1 ? lg[ti < V ? ti : tid] : -INFINITY;
   auto eid = [&](int k) { return k < SS_NJ * 4 ? v0 + 4 * (tid + (k >> 2) * SS_THREADS) + (k & 3) : ti; };
 
+  // ---- repeat penalty (llama.cpp semantics: each distinct recent id once), applied to the CANDIDATES: it only
+  // lowers values, so with R = #history ids, at least K of the top K + R raw elements keep their value and the
+  // (K + R)-th largest raw thread maximum is a lower bound of the penalised K-th largest; gathering raw >= that
+  // bound keeps every penalised top-K element.  The history ids go to LDS while the slice is in flight.
+  const int ng = n_gen[m];
+  const int nrep = (P.repeat_penalty != 1.0f && P.repeat_last_n > 0) ? min(min(P.repeat_last_n, HIST), ng) : 0;
+  int rs = 0;  // history ids in this slice (with repeats: an upper bound of the distinct ones)
+  if (tid < HIST) {
+    const int id = tid < nrep ? hist[(size_t)m * HIST + ((ng - 1 - tid) & (HIST - 1))] : -1;
+    s_hist[tid] = id;
+    rs = __popcll(__ballot(id >= v0 && id < v1));
+  }
+  if (tid < 64 && tid == 0) s_nc = rs;  // handed to every wave through LDS (s_nc is reset before its own use)
+
   // ---- thread max (lowest id on ties: ids grow with k); an empty thread gets a unique sentinel id
   float bv = -INFINITY;
   int bk = -1;
@@ -459,26 +561,46 @@ __global__ __launch_bounds__(SS_THREADS) void sample_split_kernel(
   for (int k = 0; k < SS_NJ * 4 + 1; ++k)
     if (e[k] > bv) { bv = e[k]; bk = k; }
   const int bi = bk >= 0 ? eid(bk) : 0x7fffff00 + tid;
+  ss_stamp(ws, 1);
 
   // ---- tau: K-th largest thread max; gather the elements >= tau, rank them; on an overflow of the candidate
   // buffer tighten tau (tighten_tau) and gather again from the registers
   if (tid == 0) s_tau = -INFINITY;
-  ss_kth(bv, bi, min(KL, SS_THREADS), ws_v, ws_i, &s_tau);
+  __syncthreads();
+  const int KB = KL + s_nc;  // > SS_THREADS: no bound from the thread maxima (tau = -inf, tightened on overflow)
+  ss_kth(bv, bi, KB <= SS_THREADS ? KB : 0, ws_v, ws_i, &s_tau);
+  ss_stamp(ws, 2);
+#pragma unroll 1
   for (int attempt = 0; attempt < 4; ++attempt) {
     if (tid == 0) s_nc = 0;
     __syncthreads();
     const float tau = s_tau;
-#pragma unroll
-    for (int k = 0; k < SS_NJ * 4 + 1; ++k)
-      if (e[k] >= tau && e[k] > -INFINITY) {
-        const int c = atomicAdd(&s_nc, 1);
-        if (c < MAXC) { cval[c] = e[k]; cidx[c] = eid(k); }
-      }
-    __syncthreads();
+    gather_candidates(e, [&](int k) { return e[k] >= tau && e[k] > -INFINITY; }, eid, cval, cidx, &s_nc);
     if (s_nc <= MAXC) break;
-    tighten_tau(cval, cidx, KL, SS_THREADS, &s_tau);
+    tighten_tau(cval, cidx, min(KB, MAXC), SS_THREADS, &s_tau);  // raw values: the (K + R)-th is the bound
   }
-  const int nl = ss_rank(cval, cidx, min(s_nc, MAXC), KL, sv, si);
+  ss_stamp(ws, 3);
+  if (ws.trace && tid == 0) ws.trace[((size_t)m * SS_P + part) * 8 + 6] = (unsigned long long)s_nc;
+  const int nc1 = min(s_nc, MAXC);
+  if (nrep > 0) {  // penalise the candidates whose id is in the history (16-byte LDS reads of the id list)
+    const i32x4* h4 = reinterpret_cast<const i32x4*>(s_hist);
+    for (int a = tid; a < nc1; a += SS_THREADS) {
+      const int id = cidx[a];
+      bool hit = false;
+#pragma unroll
+      for (int h = 0; h < HIST / 4; ++h) {
+        const i32x4 hv = h4[h];
+        hit |= (hv[0] == id) | (hv[1] == id) | (hv[2] == id) | (hv[3] == id);
+      }
+      if (hit) {
+        const float v = cval[a];
+        cval[a] = v > 0.f ? v / P.repeat_penalty : v * P.repeat_penalty;
+      }
+    }
+    __syncthreads();
+  }
+  const int nl = rank_candidates(cval, cidx, nc1, KL, sv, si, SS_THREADS);
+  ss_stamp(ws, 4);
 
   // ---- publish the sorted list (write-through: the merger may sit on another XCD), drain, take the row's ticket
   float* my_v = ws.cv + ((size_t)m * SS_P + part) * SS_KMAX;
@@ -492,57 +614,71 @@ __global__ __launch_bounds__(SS_THREADS) void sample_split_kernel(
   __syncthreads();
   if (tid == 0) s_ticket = __hip_atomic_fetch_add(ws.ctr + m, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
+  ss_stamp(ws, 5);
   if (s_ticket != unsigned(SS_P - 1)) return;
 
-  // ---- merger: list lengths, tau_m = the largest KL-th entry of a full list (sc1 loads throughout)
+  // ---- merger.  tau_m, a lower bound of the row's K-th largest: for K <= 64 the K-th largest of the SS_P lists'
+  // first 64 / SS_P entries (64 actual elements: wave 0 sorts them), else the largest K-th entry of a full list.
+  // Everything from the lists is read with sc1 loads (published write-through by other workgroups).
   const float* rv = ws.cv + (size_t)m * SS_P * SS_KMAX;
   const int* ri = ws.ci + (size_t)m * SS_P * SS_KMAX;
-  if (tid < SS_P) {
-    const int n = __hip_atomic_load(ws.cn + (size_t)m * SS_P + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    mn[tid] = n;
-    const float last = __hip_atomic_load(rv + tid * SS_KMAX + (KL - 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    float t = n >= KL ? last : -INFINITY;
-#pragma unroll
-    for (int o = 8; o > 0; o >>= 1) t = fmaxf(t, __shfl_xor(t, o, 64));
-    if (tid == 0) s_tau = t;
+  if (wv == 0) {
+    constexpr int HEADS = 64 / SS_P;
+    const int q = lane / HEADS, r = lane - q * HEADS;
+    const int n = __hip_atomic_load(ws.cn + (size_t)m * SS_P + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int rr = KL <= 64 ? r : KL - 1;  // K > 64: each list's K-th entry
+    float hv = __hip_atomic_load(rv + q * SS_KMAX + rr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int hi = __hip_atomic_load(ri + q * SS_KMAX + rr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (r == 0) mn[q] = n;
+    if (KL <= 64) {
+      if (rr >= n) { hv = -INFINITY; hi = 0x7fffff00 + lane; }
+      wave_sort_desc(hv, hi);
+      const float t = __shfl(hv, KL - 1, 64);  // -inf when fewer than K heads exist: gather everything
+      if (lane == 0) s_tau = t;
+    } else {
+      float t = (r == 0 && n >= KL) ? hv : -INFINITY;
+      t = wave_max(t);
+      if (lane == 0) s_tau = t;
+    }
   }
   if (tid == 0) ws.ctr[m] = 0u;  // ready for the next launch (launch-ordered)
   __syncthreads();
-  // candidate slot k = q * KL + r (list q, rank r); thread t takes slots t, t + 256, ... (<= 16 each)
-  const int nslot = SS_P * KL;
+  // list q = tid / 16 (SS_THREADS / SS_P threads per list), ranks r = tid % 16 + 16 u: no division
+  static_assert(SS_THREADS / SS_P == 16 && SS_KMAX / 16 == 16, "merger slot mapping");
+  constexpr int MS = SS_KMAX / 16;
+  const int mq = tid >> 4, mr0 = tid & 15;
+  const int nq = min(mn[mq], KL);
+  const int nu = (KL + 15) >> 4;  // uniform
+  float x[MS];
+  int xi[MS];
+#pragma unroll
+  for (int u = 0; u < MS; ++u) {  // unconditional loads from clamped offsets; masked afterwards
+    x[u] = -INFINITY, xi[u] = 0x7fffffff;
+    if (u < nu) {
+      const int r = mr0 + 16 * u;
+      const int off = mq * SS_KMAX + min(r, max(nq - 1, 0));
+      const float v = __hip_atomic_load(rv + off, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      xi[u] = __hip_atomic_load(ri + off, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      x[u] = r < nq ? v : -INFINITY;
+    }
+  }
+#pragma unroll 1
   for (int attempt = 0; attempt < 4; ++attempt) {
     if (tid == 0) s_nc = 0;
     __syncthreads();
     const float tau = s_tau;
-    for (int k0 = 0; k0 < nslot; k0 += 4 * SS_THREADS) {
-      float x[4];
-      int xi[4];
-      bool in[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {  // unconditional loads from clamped, spread offsets; masked afterwards
-        const int k = k0 + u * SS_THREADS + tid;
-        const int q = k / KL, r = k - (k / KL) * KL;
-        in[u] = k < nslot && r < mn[q < SS_P ? q : 0];
-        const int off = k < nslot ? q * SS_KMAX + r : tid;
-        x[u] = __hip_atomic_load(rv + off, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        xi[u] = __hip_atomic_load(ri + off, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u)
-        if (in[u] && x[u] >= tau) {
-          const int c = atomicAdd(&s_nc, 1);
-          if (c < MAXC) { cval[c] = x[u]; cidx[c] = xi[u]; }
-        }
-    }
-    __syncthreads();
+    gather_candidates(x, [&](int u) { return x[u] >= tau && x[u] > -INFINITY; }, [&](int u) { return xi[u]; }, cval,
+                      cidx, &s_nc);
     if (s_nc <= MAXC) break;
     tighten_tau(cval, cidx, KL, SS_THREADS, &s_tau);
   }
-  const int n = ss_rank(cval, cidx, min(s_nc, MAXC), KL, sv, si);
-  if (tid == 0) {
-    const int choice = greedy ? si[0] : draw_topk(sv, si, n, P, ng);
-    advance_row(m, choice, ng, P, tok, pos, gen, ldg, n_gen, max_new, done, hist, T_max);
+  const int n = rank_candidates(cval, cidx, min(s_nc, MAXC), KL, sv, si, SS_THREADS);
+  ss_stamp(ws, 6);
+  if (tid < 64) {
+    const int choice = greedy ? si[0] : draw_topk_wave(sv, si, n, P, ng);
+    if (tid == 0) advance_row(m, choice, ng, P, tok, pos, gen, ldg, n_gen, max_new, done, hist, T_max);
   }
+  ss_stamp(ws, 7);
 }
 
 // params: device array of M SampleParams (per-row options, so one captured graph
@@ -554,6 +690,10 @@ CAIN_API int cain_sample(float* logits, int ldl, int V, int* tok, int* pos, int*
                      max_new, done, hist, slot, T_max, reinterpret_cast<const SampleParams*>(params));
   return int(hipGetLastError());
 }
+
+static unsigned long long* g_sample_trace = nullptr;
+// Timestamps of the next two-stage sampler launches ([M * 16][8] int64, SampleWs::trace; null: off).  Tools only.
+CAIN_API void cain_sample_set_trace(void* p) { g_sample_trace = static_cast<unsigned long long*>(p); }
 
 // Workspace of the two-stage sampler for M rows (cain_sample_ex); zero-initialised once (the tickets self-reset).
 CAIN_API long long cain_sample_ws_bytes(int M) {
@@ -577,6 +717,7 @@ CAIN_API int cain_sample_ex(float* logits, int ldl, int V, int* tok, int* pos, i
   w.ci = reinterpret_cast<int*>(p);
   p += (size_t)M * SS_P * SS_KMAX * 4;
   w.cn = reinterpret_cast<int*>(p);
+  w.trace = g_sample_trace;
   hipLaunchKernelGGL(sample_split_kernel, dim3(M, SS_P), dim3(SS_THREADS), 0, st, logits, ldl, V, tok, pos, gen, ldg,
                      n_gen, max_new, done, hist, slot, T_max, reinterpret_cast<const SampleParams*>(params), w);
   return int(hipGetLastError());

@@ -116,7 +116,7 @@ def test_front_matches_three_launches_and_fp32(d, H, Hkv, hd, M, mode):
             attn = torch.zeros(M, H * hd, device=DEV, dtype=torch.bfloat16)
             if fused:
                 if "flags" not in outs:
-                    outs["flags"] = torch.zeros(16, device=DEV, dtype=torch.int32)
+                    outs["flags"] = torch.zeros(4096, device=DEV, dtype=torch.int32)
                     outs["ctr"] = torch.zeros(M * Hkv, device=DEV, dtype=torch.int32)
                 ops.layer_front(L["Wp"], L["bp"], L["Wop"], x, q, attn, kc, vt, slot, pos, cos_t, sin_t, H, Hkv,
                                 hd, ns, scale, eps=eps, counters=outs["ctr"], flags=outs["flags"])

@@ -49,7 +49,7 @@ def main() -> None:
     part_o = torch.empty(M * H * ns * hd, device=dev)
     part_ml = torch.empty(ops.attention_ml_floats(M, H, Hkv, ns), device=dev)
     ctr = torch.zeros(M * Hkv, device=dev, dtype=torch.int32)
-    flags = torch.zeros(16, device=dev, dtype=torch.int32)
+    flags = torch.zeros(4096, device=dev, dtype=torch.int32)
     scale = 1.0 / math.sqrt(hd)
 
     def fused(trace=None):
