@@ -23,7 +23,8 @@ Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--model M] [--words 
 
 After the timed steps every rank also runs ONE trial alone (batch 1, the reference's one-request-at-a-time
 protocol) and the JSON reports it beside the batched number: ``single_stream_tok_per_s`` and
-``single_stream_J_per_token``.
+``single_stream_J_per_token``, then the same trial on fp8 (e4m3 per-row) weights, the
+analogue of the reference's 4-bit Ollama models: ``single_stream_fp8_tok_per_s`` / ``_J_per_token``.
 """
 from __future__ import annotations
 
@@ -100,6 +101,8 @@ def main() -> int:
                     help="cpu: the torch oracle backend over gloo (tests of the multi-rank plumbing; tiny models)")
     ap.add_argument("--settle", type=float, default=8.0, help="seconds of rest before the idle-power baseline")
     ap.add_argument("--no-single", action="store_true", help="skip the batch-1 (single-stream) measurement")
+    ap.add_argument("--no-single-fp8", action="store_true",
+                    help="skip the fp8-weight batch-1 trial (the analogue of the reference's 4-bit Ollama models)")
     ns = ap.parse_args()
 
     world_env = os.environ.get("WORLD_SIZE")
@@ -208,9 +211,32 @@ def main() -> int:
         if rd1 is not None:
             ss_j = rd1.gpu_energy_j / max(1, r1.eval_count)
 
+    # the same batch-1 trial on fp8 (e4m3, per-row scaled) weights: the closest analogue of the reference's
+    # 4-bit quantised Ollama models (outside the timed region; a second engine of the same architecture)
+    f8_tps, f8_j = float("nan"), float("nan")
+    if not ns.no_single and not ns.no_single_fp8 and not cpu and ns.weights == "bf16":
+        try:
+            e8 = DecodeEngine(ns.model, device=dev, max_batch=1, max_context=ns.context, seed=1234 + rank,
+                              steps_per_graph=ns.steps_per_graph, weight_dtype="fp8", kv_dtype=ns.kv)
+            e8.generate(prompts(-7)[:1], min(n_tok, 32), [dict(opts, seed=7)])
+            barrier()
+            if meter:
+                meter.start()
+            t2 = time.perf_counter()
+            r2 = e8.generate(prompts(-8)[:1], n_tok, [dict(opts, seed=8)])[0]
+            sync()
+            dt2 = time.perf_counter() - t2
+            rd2 = meter.stop() if meter else None
+            f8_tps = r2.eval_count / dt2
+            if rd2 is not None:
+                f8_j = rd2.gpu_energy_j / max(1, r2.eval_count)
+            e8.close()
+        except Exception as exc:  # auxiliary measurement
+            print(f"[bench] fp8 single stream unavailable: {exc}", file=sys.stderr)
+
     vals = torch.tensor([dt, float(toks), reading.gpu_energy_j if reading else float("nan"),
                          reading.idle_subtracted_j if reading else float("nan"),
-                         reading.total_energy_j if reading else float("nan"), ss_tps, ss_j],
+                         reading.total_energy_j if reading else float("nan"), ss_tps, ss_j, f8_tps, f8_j],
                         dtype=torch.float64, device=dev)
     if world > 1:
         allv = [torch.zeros_like(vals) for _ in range(world)]
@@ -225,6 +251,8 @@ def main() -> int:
     energy_total = float(allv[:, 4].sum())
     ss_tps_mean = float(allv[:, 5].mean())
     ss_j_mean = float(allv[:, 6].mean())
+    f8_tps_mean = float(allv[:, 7].mean())
+    f8_j_mean = float(allv[:, 8].mean())
     value = tokens / t_max
     base_tps, base_jpt = BASELINE.get((ns.model, ns.words), (None, None))
     if rank == 0:
@@ -257,6 +285,8 @@ def main() -> int:
             "avg_gpu_power_W": round(energy / t_max / world, 1) if not math.isnan(energy) else None,
             "single_stream_tok_per_s": round(ss_tps_mean, 2) if not math.isnan(ss_tps_mean) else None,
             "single_stream_J_per_token": round(ss_j_mean, 4) if not math.isnan(ss_j_mean) else None,
+            "single_stream_fp8_tok_per_s": round(f8_tps_mean, 2) if not math.isnan(f8_tps_mean) else None,
+            "single_stream_fp8_J_per_token": round(f8_j_mean, 4) if not math.isnan(f8_j_mean) else None,
             "baseline": {"tok_per_s": base_tps, "J_per_token": base_jpt, "hardware": "MacBook Pro M2 (est.)"},
             "vs_baseline_J_per_token": (round(base_jpt / (energy / tokens), 2)
                                         if base_jpt and not math.isnan(energy) and energy > 0 else None),

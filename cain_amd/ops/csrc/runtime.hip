@@ -7,7 +7,7 @@
 // prompt token, each with its own cache slot and position):
 //
 //   embed -> L x [QKV GEMM(+RMSNorm, +bias, RoPE, KV append)
-//                 -> attention(+split combine) -> O GEMM(+residual)      (<= 4 bf16 rows: ONE launch, front.hip)
+//                 -> attention(+split combine) -> O GEMM(+residual)      (CAIN_FRONT=1, <= 4 bf16 rows: ONE launch)
 //                 -> gate/up GEMM(+RMSNorm, act*mul) -> down GEMM(+residual)]
 //                 -> LM-head GEMM(+RMSNorm) -> sample
 //
@@ -189,11 +189,14 @@ thread_local char g_fail[160] = {0};
     }                                                                            \
   } while (0)
 
-// CAIN_FRONT=0: the three launches QKV / attention / O instead of the fused layer front (A/B runs)
+// CAIN_FRONT=1: the fused layer front (front.hip) instead of the three launches QKV / attention / O.  Off by
+// default: in the graph-replayed batch-1 decode it measured 16.9 vs 14.9 us per layer (qwen2:1.5b) and 28.7 vs
+// 25.8 (llama3.1:8b) -- its in-launch hand-offs cost more than the two kernel boundaries they remove
+// (profiles/r3/front_trace_*.log, profiles/r3/README.md).
 bool front_enabled() {
   static const bool on = [] {
     const char* e = getenv("CAIN_FRONT");
-    return !(e && e[0] == '0');
+    return e && e[0] == '1';
   }();
   return on;
 }
