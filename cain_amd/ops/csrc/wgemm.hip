@@ -65,26 +65,58 @@ constexpr int WG_CTR_BYTES = 16 * 1024;  // the workspace region before the slab
 // fragment reads are always in flight under 16 MFMAs and no wave restarts the matrix pipe behind a barrier.
 //
 // ABL (diagnostics only): 1 = DMA without the fragment reads and MFMAs, 2 = fragment reads and MFMAs without the
-// DMA.  Results are garbage in both.
-template <int BM, int DX, int DW, int EPI, bool NORM, int NDMA, int ABL = 0>
+// DMA.  Results are garbage in both.  3 = the full kernel plus timestamps (tools/wgemm_trace.py): lane 0 of wave 0
+// (compute) and of the first loader wave store s_memrealtime / s_memtime at fixed points to w.stamps.
+//
+// OPT (tuning alternatives, A/B runs), bit mask:
+//   1 LSQ (NORM, BM = 256, NDMA = 4): the per-row sums of squares come from the loader waves instead of the X X^T
+//     MFMAs -- after stage t lands, loader lw reads rows 64 lw + lane of the X stage (8 ds_read_b128 per lane, the
+//     read-side XOR swizzle keeps the 16-lane groups conflict-free) and accumulates them with v_dot2c_f32_bf16
+//     (exact bf16 products, fp32 sums, as the MFMA), so the compute waves issue only the GEMM's MFMAs;
+//   2 LSPLIT (NDMA = 4): loaders 0-1 issue only W pieces, loaders 2-3 only X pieces, so a wave's counted wait for
+//     its L2-served X never queues behind HBM-served W (vmcnt retires in issue order per wave);
+//   4 ROT: workgroup b walks its stages starting at ((b >> 3) * 7) mod nst, so the workgroups of one XCD do not
+//     all read the same X lines at the same time (any stage order gives the same sums up to fp32 rounding);
+//   8 XNT: X pieces non-temporal as well (no L1 allocation for lines a CU reads once per stage).
+template <int BM, int DX, int DW, int EPI, bool NORM, int NDMA, int ABL = 0, int OPT = 0>
 __global__ __launch_bounds__(64 * (8 + NDMA), (8 + NDMA) / 4) void wgemm_kernel(const GemmArgs a, const WgArgs w) {
   using G = WgGeo<BM>;
+  constexpr bool LSQ = NORM && (OPT & 1) && BM == 256 && NDMA == 4;  // loader-wave sums of squares
+  constexpr bool MSQ = NORM && !LSQ;                                 // MFMA X X^T sums of squares
+  constexpr bool LSPLIT = (OPT & 2) && NDMA == 4;
+  constexpr bool ROT = (OPT & 4) != 0;
+  constexpr int XAUX = (OPT & 8) ? 1 : 0;
   constexpr int NX = DX + 1, NW = DW + 1;
   constexpr int NLOAD = NDMA ? NDMA : 8;            // waves issuing LDS-DMA
-  constexpr int WPW = 16 / NLOAD;                   // W blocks (1 KiB) per loader wave per stage
-  constexpr int XPW = (BM / 8) / NLOAD;             // X row octets per loader wave per stage
+  constexpr int NWL = LSPLIT ? 2 : NLOAD;           // waves issuing W pieces
+  constexpr int NXL = LSPLIT ? 2 : NLOAD;           // waves issuing X pieces
+  constexpr int WPW = 16 / NWL;                     // W blocks (1 KiB) per W-loader wave per stage
+  constexpr int XPW = (BM / 8) / NXL;               // X row octets per X-loader wave per stage
   constexpr int NTHR = 64 * (8 + NDMA);
   static_assert(DW >= DX && DX >= 1, "W is issued no later than X of the same stage");
-  static_assert(WPW * NLOAD == 16 && XPW * NLOAD == BM / 8, "loader split");
+  static_assert(WPW * NWL == 16 && XPW * NXL == BM / 8, "loader split");
   extern __shared__ __attribute__((aligned(16))) char smem[];  // the one LDS array: [NW W slots][NX X slots]
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const bool compute = wave < 8;
   const bool loader = NDMA ? !compute : true;
   const int lw = NDMA ? wave - 8 : wave;  // loader index
+  const bool wload = loader && (!LSPLIT || lw < 2);
+  const bool xload = loader && (!LSPLIT || lw >= 2);
+  const int xl = LSPLIT ? max(lw - 2, 0) : lw;  // X-loader index
   const int wm = wave % G::WM, wn = (wave / G::WM) % G::WN;
   const int KS = a.K >> 5, ntiles = a.N >> 4;
   const int nblk = (ntiles + WG_NT - 1) / WG_NT;
+  // ABL 3: slots 0/1 start (realtime / memtime), 2 stage 0 ready, 3 stage nst/2 ready, 4 loop end, 5 slab stores
+  // drained, 6/7 end (realtime / memtime)
+  auto stamp = [&](int sl, bool cyc) {
+    if constexpr (ABL == 3) {
+      const unsigned long long v = cyc ? __builtin_amdgcn_s_memtime() : __builtin_amdgcn_s_memrealtime();
+      if (lane == 0 && (wave == 0 || wave == 8)) w.stamps[((size_t)blockIdx.x * 2 + (wave == 8)) * 8 + sl] = v;
+    }
+  };
+  stamp(0, false);
+  stamp(1, true);
 
   // block -> (column block, k-split); the k-split partners of one column block read disjoint X panels, the
   // column blocks of one k-split read the SAME X panel: split-major placement keeps those on one XCD (blocks b
@@ -97,6 +129,11 @@ __global__ __launch_bounds__(64 * (8 + NDMA), (8 + NDMA) / 4) void wgemm_kernel(
   const int tile0 = blk * WG_NT;
   const int st0 = kc * w.kst;                    // first stage (64-deep k-step) of this split
   const int nst = min(w.kst, (a.K >> 6) - st0);  // stages of this split
+  const int rot = ROT ? (int)((blockIdx.x >> 3) * 7u % (unsigned)nst) : 0;
+  auto kstage = [&](int t) {  // ring stage t -> stage of this split's k range
+    if constexpr (ROT) return t + rot < nst ? t + rot : t + rot - nst;
+    else return t;
+  };
 
   // ---- LDS-DMA sources of this loader (per stage: WPW W blocks + XPW X row-octets)
   // W block j of loader lw: tile (lw * WPW + j) / 2, slice (lw * WPW + j) & 1 (a tile's two slices are 2 KiB
@@ -113,7 +150,7 @@ __global__ __launch_bounds__(64 * (8 + NDMA), (8 + NDMA) / 4) void wgemm_kernel(
   const char* xsrc[XPW];
 #pragma unroll
   for (int j = 0; j < XPW; ++j) {
-    const int i = lw + NLOAD * j;
+    const int i = xl + NXL * j;
     const int r = 8 * i + (lane >> 3);
     const int p = (lane & 7) ^ ((r >> 1) & 7);
     xsrc[j] = reinterpret_cast<const char*>(a.X) + ((size_t)min(r, a.M - 1) * a.ldx + (size_t)st0 * WG_BK + p * 8) * 2;
@@ -121,22 +158,36 @@ __global__ __launch_bounds__(64 * (8 + NDMA), (8 + NDMA) / 4) void wgemm_kernel(
   char* const xring = smem + NW * G::W_BYTES;
   auto issue_w = [&](int t) {  // W stage t (relative to st0) into W slot t % NW
     if constexpr (ABL == 2) return;
+    if (!wload) return;
     char* base = smem + (t % NW) * G::W_BYTES;
+    const size_t off = (size_t)kstage(t) * 2048;
 #pragma unroll
-    for (int j = 0; j < WPW; ++j) glds16(wsrc[j] + (size_t)t * 2048, base + (lw * WPW + j) * 1024, 1);
+    for (int j = 0; j < WPW; ++j) glds16(wsrc[j] + off, base + (lw * WPW + j) * 1024, 1);
   };
   auto issue_x = [&](int t) {  // X stage t into X slot t % NX
     if constexpr (ABL == 2) return;
+    if (!xload) return;
     char* base = xring + (t % NX) * G::X_BYTES;
+    const size_t off = (size_t)kstage(t) * (WG_BK * 2);
 #pragma unroll
-    for (int j = 0; j < XPW; ++j) glds16(xsrc[j] + (size_t)t * (WG_BK * 2), base + (lw + NLOAD * j) * 1024, 0);
+    for (int j = 0; j < XPW; ++j) glds16(xsrc[j] + off, base + (xl + NXL * j) * 1024, XAUX);
   };
   // issue order: step u (u < 0: prologue) issues W(u + DW), then X(u + DX); so W(t) is always older than X(t) and
   // waiting for X(t) covers both (vmcnt retires in issue order).  Loads younger than X(t): steps t-DX+1 .. t-1.
   auto younger_than = [&](int t) {
     int n = 0;
+    if constexpr (LSPLIT) {  // a W loader's W(t+1) .. W(t+DW-1), an X loader's X(t+1) .. X(t+DX-1)
+      if (wload) {
 #pragma unroll
-    for (int u = t - DX + 1; u < t; ++u) n += WPW * (u + DW < nst) + XPW * (u + DX < nst);
+        for (int s = 1; s < DW; ++s) n += WPW * (t + s < nst);
+      } else {
+#pragma unroll
+        for (int s = 1; s < DX; ++s) n += XPW * (t + s < nst);
+      }
+    } else {
+#pragma unroll
+      for (int u = t - DX + 1; u < t; ++u) n += WPW * (u + DW < nst) + XPW * (u + DX < nst);
+    }
     return n;
   };
   auto land = [&](int t) {  // this loader's pieces of stage t have landed (a loader's own counted wait)
@@ -192,12 +243,31 @@ __global__ __launch_bounds__(64 * (8 + NDMA), (8 + NDMA) / 4) void wgemm_kernel(
           __builtin_amdgcn_sched_barrier(0);
         }
       }
-    if constexpr (NORM) {
+    if constexpr (MSQ) {
       if (wn == s) {
 #pragma unroll
         for (int mb = 0; mb < G::MB; ++mb)
           ssq[mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[mb], bfr[mb], ssq[mb], 0, 0, 0);
       }
+    }
+  };
+  // LSQ: loader lw's row 64 lw + lane of X stage t (its 8 pieces in swizzled order: 16-lane groups hit 16
+  // different 4-bank groups)
+  float lsq = 0.f;
+  auto loader_ssq = [&](int t) {
+    if constexpr (LSQ) {
+      const int r = lw * 64 + lane;
+      const char* row = xring + (t % NX) * G::X_BYTES + r * 128;
+      bf16x8 v[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v[q] = *reinterpret_cast<const bf16x8*>(row + ((q ^ ((r >> 1) & 7)) << 4));
+#pragma unroll
+      for (int q = 0; q < 8; ++q)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const bf16x2 p = {v[q][2 * j], v[q][2 * j + 1]};
+          lsq = __builtin_amdgcn_fdot2_f32_bf16(p, p, lsq, false);
+        }
     }
   };
 
@@ -216,7 +286,10 @@ __global__ __launch_bounds__(64 * (8 + NDMA), (8 + NDMA) / 4) void wgemm_kernel(
     for (int t = 0; t < nst; ++t) {
       land(t);
       ring_barrier();
+      if (t == 0) stamp(2, false);
+      if (t == nst / 2) stamp(3, false);
       issue_step(t);
+      loader_ssq(t);
     }
   } else if constexpr (ABL == 1) {
     for (int t = 0; t < nst; ++t) {
@@ -228,6 +301,7 @@ __global__ __launch_bounds__(64 * (8 + NDMA), (8 + NDMA) / 4) void wgemm_kernel(
     bf16x8 a0[G::TN], b0[G::MB], a1[G::TN], b1[G::MB];
     land(0);
     ring_barrier();
+    stamp(2, false);
     if constexpr (!NDMA) issue_step(0);
     read_slice(0, 0, a0, b0);
     for (int t = 0; t < nst; ++t) {
@@ -238,6 +312,7 @@ __global__ __launch_bounds__(64 * (8 + NDMA), (8 + NDMA) / 4) void wgemm_kernel(
       if (more) {
         land(t + 1);
         ring_barrier();
+        if (t + 1 == nst / 2) stamp(3, false);
         if constexpr (!NDMA) issue_step(t + 1);
       }
       __builtin_amdgcn_sched_barrier(0);
@@ -250,14 +325,21 @@ __global__ __launch_bounds__(64 * (8 + NDMA), (8 + NDMA) / 4) void wgemm_kernel(
     }
   }
   ring_barrier();  // every wave is done with the ring: its LDS becomes epilogue scratch
+  stamp(4, false);
 
   // ---- per-row sums of squares: the diagonal of each X X^T block (lane (c, g) holds C[4g + i][c], so the
   // diagonal element of row c sits in lane c + 16 * (c >> 2), register c & 3)
   float* s_ss = reinterpret_cast<float*>(smem);  // [2][BM]
-  if constexpr (NORM) {
+  if constexpr (MSQ) {
     if (compute && wn < 2 && (c >> 2) == g) {
 #pragma unroll
       for (int mb = 0; mb < G::MB; ++mb) s_ss[wn * BM + (wm * G::MB + mb) * 16 + c] = ssq[mb][c & 3];
+    }
+    __syncthreads();
+  } else if constexpr (LSQ) {
+    if (!compute) {
+      s_ss[lw * 64 + lane] = lsq;
+      s_ss[BM + lw * 64 + lane] = 0.f;
     }
     __syncthreads();
   }
@@ -280,6 +362,12 @@ __global__ __launch_bounds__(64 * (8 + NDMA), (8 + NDMA) / 4) void wgemm_kernel(
       if constexpr (NORM) {
         for (int r = threadIdx.x; r < BM; r += NTHR)
           w.part_ss[((size_t)blk * w.ks + kc) * BM + r] = s_ss[r] + s_ss[BM + r];
+      }
+      if constexpr (ABL == 3) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        stamp(5, false);
+        stamp(6, false);
+        stamp(7, true);
       }
       return;
     }
@@ -376,6 +464,12 @@ __global__ __launch_bounds__(64 * (8 + NDMA), (8 + NDMA) / 4) void wgemm_kernel(
         epi_store<EPI>(a, gt, m, lane, e, [&](int off) { return off ? pv : v; });
       }
     }
+  }
+  if constexpr (ABL == 3) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    stamp(5, false);
+    stamp(6, false);
+    stamp(7, true);
   }
 }
 
@@ -497,18 +591,18 @@ WgPlan wg_plan(int N, int K, int M) {
   return p;
 }
 
-template <int BM, int DX, int DW, int EPI, bool NORM, int NDMA, int ABL = 0>
+template <int BM, int DX, int DW, int EPI, bool NORM, int NDMA, int ABL = 0, int OPT = 0>
 hipError_t wg_launch(const GemmArgs& a, const WgArgs& w, const WgPlan& p, hipStream_t st) {
   using G = WgGeo<BM>;
   constexpr int lds = (DW + 1) * G::W_BYTES + (DX + 1) * G::X_BYTES;
   static_assert(lds <= 160 * 1024, "LDS");
   static bool attr = [] {
-    return hipFuncSetAttribute(reinterpret_cast<const void*>(&wgemm_kernel<BM, DX, DW, EPI, NORM, NDMA, ABL>),
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(&wgemm_kernel<BM, DX, DW, EPI, NORM, NDMA, ABL, OPT>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, lds) == hipSuccess;
   }();
   if (!attr) return hipErrorInvalidConfiguration;
-  hipLaunchKernelGGL((wgemm_kernel<BM, DX, DW, EPI, NORM, NDMA, ABL>), dim3(p.nblk * p.ks), dim3(64 * (8 + NDMA)), lds,
-                     st, a, w);
+  hipLaunchKernelGGL((wgemm_kernel<BM, DX, DW, EPI, NORM, NDMA, ABL, OPT>), dim3(p.nblk * p.ks), dim3(64 * (8 + NDMA)),
+                     lds, st, a, w);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || p.ks == 1 || w.combine) return e;
   wg_reduce_launch<BM, EPI, NORM>(a, w, p.nblk * WG_NT * G::RB, st);
@@ -531,6 +625,23 @@ hipError_t wg_launch_v(const GemmArgs& a, const WgArgs& w, const WgPlan& p, hipS
       case 1: return wg_launch<BM, 2, 3, EPI, NORM, 0>(a, w, p, st);     // MFMA waves load
       case 2: return wg_launch<BM, 2, 2, EPI, NORM, 4>(a, w, p, st);     // 144 KiB
       case 3: return wg_launch<BM, 1, 5, EPI, NORM, 4>(a, w, p, st);     // 160 KiB
+      case 5: return wg_launch<BM, 2, 3, EPI, NORM, 4, 0, 1>(a, w, p, st);  // loader-wave sums of squares
+      case 6: return wg_launch<BM, 2, 3, EPI, NORM, 4, 3, 1>(a, w, p, st);  // 5 + timestamps
+      case 10: return wg_launch<BM, 2, 3, EPI, NORM, 4, 0, 2>(a, w, p, st);  // W / X loader roles
+      case 11: return wg_launch<BM, 1, 5, EPI, NORM, 4, 0, 2>(a, w, p, st);  // roles, deep W ring
+      case 12: return wg_launch<BM, 2, 3, EPI, NORM, 4, 0, 4>(a, w, p, st);  // rotated k start
+      case 13: return wg_launch<BM, 1, 5, EPI, NORM, 4, 0, 6>(a, w, p, st);  // roles + deep W + rotation
+      case 21: return wg_launch<BM, 1, 5, EPI, NORM, 4, 3, 2>(a, w, p, st);  // 11 + timestamps
+      case 22: return wg_launch<BM, 2, 3, EPI, NORM, 4, 3, 4>(a, w, p, st);  // 12 + timestamps
+      case 23: return wg_launch<BM, 1, 5, EPI, NORM, 4, 3, 6>(a, w, p, st);  // 13 + timestamps
+      case 20: return wg_launch<BM, 2, 3, EPI, NORM, 4, 3, 2>(a, w, p, st);  // 10 + timestamps
+      case 14: return wg_launch<BM, 2, 3, EPI, NORM, 4, 0, 6>(a, w, p, st);   // roles + rotation
+      case 15: return wg_launch<BM, 2, 3, EPI, NORM, 4, 0, 14>(a, w, p, st);  // roles + rotation + X nt
+      case 16: return wg_launch<BM, 2, 3, EPI, NORM, 4, 0, 8>(a, w, p, st);   // X nt
+      case 24: return wg_launch<BM, 2, 3, EPI, NORM, 4, 3, 6>(a, w, p, st);   // 14 + timestamps
+      case 25: return wg_launch<BM, 2, 3, EPI, NORM, 4, 3, 14>(a, w, p, st);  // 15 + timestamps
+      case 26: return wg_launch<BM, 2, 3, EPI, NORM, 4, 3, 8>(a, w, p, st);   // 16 + timestamps
+      case 7: return wg_launch<BM, 2, 3, EPI, NORM, 4, 3>(a, w, p, st);  // default + timestamps
       case 8: return wg_launch<BM, 2, 3, EPI, NORM, 4, 1>(a, w, p, st);  // DMA only
       case 9: return wg_launch<BM, 2, 3, EPI, NORM, 4, 2>(a, w, p, st);  // compute only
       default: return wg_launch<BM, 2, 3, EPI, NORM, 4>(a, w, p, st);    // 160 KiB
@@ -585,6 +696,9 @@ CAIN_API int cain_wgemm_set_shape(int N, int K, int bm, int ks, int variant) {
   return 0;
 }
 CAIN_API void cain_wgemm_clear_shapes() { g_wg_nshapes = 0; }
+// Timestamp buffer of the diagnostic variant 7 (>= grid * 16 uint64; tools/wgemm_trace.py).
+static unsigned long long* g_wg_stamps = nullptr;
+CAIN_API void cain_wgemm_set_stamps(void* p) { g_wg_stamps = static_cast<unsigned long long*>(p); }
 CAIN_API int cain_wgemm_eligible(int N, int K, int M);
 // The plan the next launch of this shape would use: ks * 16 + variant (tests, tools).
 CAIN_API int cain_wgemm_plan(int N, int K, int M) {
@@ -635,6 +749,7 @@ int wgemm_dispatch(const GemmArgs& a, int epi, bool norm, void* ws, long long ws
   w.combine = combine && p.ks > 1 && p.nblk * p.ks <= n_cu && p.nblk * 2 * 4 <= WG_CTR_BYTES;
   // [counter region: 2 per column block, zero at rest][slabs][sums]
   w.counters = static_cast<unsigned*>(ws);
+  w.stamps = g_wg_stamps;
   w.part = reinterpret_cast<float*>(static_cast<char*>(ws) + WG_CTR_BYTES);
   w.part_ss = w.part + p.part_floats;
   hipError_t e;

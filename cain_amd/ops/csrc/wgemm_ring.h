@@ -80,6 +80,7 @@ struct WgArgs {
   int xcd_blk;      // 1: a column block's split partners and its reducers share one XCD (wgemm.hip)
   int combine;      // 1: in-launch split-K combine by the partners (wgemm.hip); 0: wgemm_reduce_kernel
   unsigned* counters;  // [nblk][2] arrivals / exits of the in-launch combine, zero at rest
+  unsigned long long* stamps;  // diagnostic build only (wgemm.hip ABL 3): [grid][2 waves][8] timestamps
 };
 
 
