@@ -173,7 +173,7 @@ def clear_wide_gemm_plans() -> None:
 def wide_gemm_plan(n: int, k: int, m: int) -> Optional[tuple]:
     """(split count, ring variant) the next wide-GEMM launch of this shape uses; None if not eligible."""
     v = int(load().cain_wgemm_plan(n, k, m))
-    return None if v < 0 else (v // 16, v % 16)
+    return None if v < 0 else (v // 64, v % 64)
 
 
 def _workspace(device, nbytes: int) -> Optional[torch.Tensor]:

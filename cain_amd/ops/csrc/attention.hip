@@ -237,7 +237,7 @@ __global__ __launch_bounds__(AW * 64, OCC) void attn_decode_kernel(
       osum += f * s_o[w][d][gg];
     }
     if (nsplit == 1) {
-      out[(size_t)m * ldo + (kh * G + gg) * HD + d] = f2bf(lsum > 0.f ? osum / lsum : 0.f);
+      out[(size_t)m * ldo + (kh * G + gg) * HD + d] = f2bf(lsum > 0.f ? osum * fast_rcp(lsum) : 0.f);
     } else {
       // publish write-through (sc1) so the reducer needs no release/acquire fences
       // (MI355X_MICROARCH.md 'Valid forms', first table row; cdna_hip_programming.md Guideline 16)

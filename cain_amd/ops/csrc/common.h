@@ -8,6 +8,7 @@ typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 typedef uint16_t u16x8 __attribute__((ext_vector_type(8)));
 typedef uint16_t u16x4 __attribute__((ext_vector_type(4)));
 
@@ -27,13 +28,22 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
-__device__ __forceinline__ float silu_f(float g) { return g / (1.0f + __expf(-g)); }
+// Epilogue math on the hardware reciprocal / reciprocal square root (v_rcp_f32 / v_rsq_f32, ~1 ulp): hipcc's IEEE
+// division and denormal-safe rsqrtf expand to ~10 dependent VALU instructions each, which made the 256-row gate/up
+// epilogue (4 SiLU divisions + 1 RMSNorm division per 16 x 16 tile) ~5 us of a ~70 us kernel
+// (tools/wgemm_trace.py, profiles/r3/).  Both stay far below bf16 output rounding.
+__device__ __forceinline__ float fast_rcp(float x) { return __builtin_amdgcn_rcpf(x); }
+__device__ __forceinline__ float silu_f(float g) { return g * fast_rcp(1.0f + __expf(-g)); }
 __device__ __forceinline__ float gelu_tanh_f(float g) {
   const float k0 = 0.7978845608028654f, k1 = 0.044715f;
   float u = k0 * (g + k1 * g * g * g);
   // tanh(u) = 1 - 2/(exp(2u)+1)
-  float t = 1.0f - 2.0f / (__expf(2.0f * u) + 1.0f);
+  float t = 1.0f - 2.0f * fast_rcp(__expf(2.0f * u) + 1.0f);
   return 0.5f * g * (1.0f + t);
+}
+// RMSNorm scale of a row from its sum of squares over K elements (ss / K + eps >= eps > 0: never a denormal)
+__device__ __forceinline__ float rms_inv(float ss, int K, float eps) {
+  return __builtin_amdgcn_rsqf(ss * fast_rcp(float(K)) + eps);
 }
 
 static inline int cdiv(int a, int b) { return (a + b - 1) / b; }

@@ -111,7 +111,7 @@ __device__ void gemv_finish(const GemmArgs& a, int tile, const f32x4& acc, float
         float ss = 0.f;
 #pragma unroll
         for (int w = 0; w < W; ++w) ss += red_ss[w * 16 + (u & 15)];
-        v *= rsqrtf(ss / float(a.K) + a.eps);
+        v *= rms_inv(ss, a.K, a.eps);
       }
       return v;
     });

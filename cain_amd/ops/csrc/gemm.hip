@@ -294,7 +294,7 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_gemm_kernel(const GemmArgs 
     }
     red[0][lane] = v;
     if constexpr (NORM) {
-      if (lane < 16) s_inv[lane] = rsqrtf(ss / float(a.K) + a.eps);
+      if (lane < 16) s_inv[lane] = rms_inv(ss, a.K, a.eps);
     }
     if (lane == 0) sk.counters[tg] = 0u;  // ready for the next launch (launch-ordered)
     const int m = mo + (lane & 15);
@@ -316,7 +316,7 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_gemm_kernel(const GemmArgs 
       float ss = 0.f;
 #pragma unroll
       for (int w = 0; w < WAVES; ++w) ss += red_ss[w][m16];
-      v *= rsqrtf(ss / float(a.K) + a.eps);
+      v *= rms_inv(ss, a.K, a.eps);
     }
     return v;
   };
@@ -774,7 +774,7 @@ __global__ __launch_bounds__(W * 64, LB) void bgemm_kernel(const GemmArgs a, con
       for (int b = 0; b < NBW; ++b) red[unit(t, b) * 64 + lane] = acc[t][b];
     __syncthreads();
     if constexpr (NORM) {
-      if (threadIdx.x < NB * 16) s_inv[threadIdx.x] = rsqrtf(s_ss[threadIdx.x] / float(a.K) + a.eps);
+      if (threadIdx.x < NB * 16) s_inv[threadIdx.x] = rms_inv(s_ss[threadIdx.x], a.K, a.eps);
       __syncthreads();
     }
   } else {
@@ -836,7 +836,7 @@ __global__ __launch_bounds__(W * 64, LB) void bgemm_kernel(const GemmArgs a, con
         for (int k = 0; k < bg.ksplit; ++k)
           x += __hip_atomic_load(bg.part_ss + (pb + k) * (NB * 16) + threadIdx.x, __ATOMIC_RELAXED,
                                  __HIP_MEMORY_SCOPE_AGENT);
-        s_inv[threadIdx.x] = rsqrtf(x / float(a.K) + a.eps);
+        s_inv[threadIdx.x] = rms_inv(x, a.K, a.eps);
       }
     }
     if (threadIdx.x == 0) bg.counters[blk] = 0u;  // ready for the next launch (launch-ordered)

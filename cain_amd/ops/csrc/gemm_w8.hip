@@ -176,7 +176,7 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_w8_kernel(const GemmArgs a,
         float ss = 0.f;
 #pragma unroll
         for (int w = 0; w < WAVES; ++w) ss += red_ss[w][b][l & 15];
-        v *= rsqrtf(ss / float(a.K) + a.eps);
+        v *= rms_inv(ss, a.K, a.eps);
       }
       return v;
     };

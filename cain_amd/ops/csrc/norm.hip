@@ -43,7 +43,7 @@ __global__ __launch_bounds__(THREADS) void rmsnorm_kernel(const __bf16* __restri
     }
   }
   float tot = block_sum<THREADS>(ss, sh);
-  float inv = rsqrtf(tot / float(d) + eps);
+  float inv = rms_inv(tot, d, eps);
   const bf16x8* gr = reinterpret_cast<const bf16x8*>(g);
   bf16x8* yr = reinterpret_cast<bf16x8*>(y + (size_t)m * ldy);
 #pragma unroll

@@ -37,12 +37,13 @@
 //     fragment, split between the WN waves that read the same rows.
 //
 // Split-K: narrow outputs (QKV, O, down: 32-48 column tiles) split K over ks workgroups so ~256 workgroups
-// stream; each writes its fp32 tile to a workspace slab (plain stores) and `wgemm_reduce_kernel` -- the next
-// launch on the stream, so the kernel boundary orders the hand-off -- sums the slabs and runs the fused
-// epilogue.  With ks = 1 (gate/up, LM head) the GEMM kernel runs the epilogue itself.  The epilogues are
+// stream; each writes its tile to a workspace slab (plain stores, fp16: OPT bit 32 below; the sums stay fp32) and
+// `wgemm_reduce_kernel` -- the next launch on the stream, so the kernel boundary orders the hand-off -- sums the
+// slabs in fp32 and runs the fused epilogue.  With ks = 1 (gate/up, LM head) the GEMM kernel runs the epilogue itself.  The epilogues are
 // gemm_epi.h's (residual, bias, SiLU/GeLU x up, RoPE + KV-cache append, fp32 logits).
 #include <algorithm>
 #include <cstdlib>
+#include <type_traits>
 
 #include "common.h"
 #include "gemm_epi.h"
@@ -77,7 +78,12 @@ constexpr int WG_CTR_BYTES = 16 * 1024;  // the workspace region before the slab
 //     its L2-served X never queues behind HBM-served W (vmcnt retires in issue order per wave);
 //   4 ROT: workgroup b walks its stages starting at ((b >> 3) * 7) mod nst, so the workgroups of one XCD do not
 //     all read the same X lines at the same time (any stage order gives the same sums up to fp32 rounding);
-//   8 XNT: X pieces non-temporal as well (no L1 allocation for lines a CU reads once per stage).
+//   8 XNT: X pieces non-temporal as well (no L1 allocation for lines a CU reads once per stage);
+//   16 PRO: the prologue issues stage by stage (W0 X0 W1 X1 W2) instead of W0 W1 X0 W2 X1, so stage 0 -- the one
+//     every workgroup waits for while the whole grid's prologue burst is in flight -- is not queued behind W1;
+//   32 H16: split-K slabs in fp16 instead of fp32 (wgemm_reduce_kernel H16 = true reads them): half the slab bytes
+//     stored, written back at the kernel boundary (MI355X_MICROARCH.md 'boundary': + dirty bytes / 6 TB/s) and read
+//     by the reduce.  A partial's fp16 rounding (2^-11 relative) is ~8x below the bf16 rounding of the output.
 template <int BM, int DX, int DW, int EPI, bool NORM, int NDMA, int ABL = 0, int OPT = 0>
 __global__ __launch_bounds__(64 * (8 + NDMA), (8 + NDMA) / 4) void wgemm_kernel(const GemmArgs a, const WgArgs w) {
   using G = WgGeo<BM>;
@@ -86,6 +92,8 @@ __global__ __launch_bounds__(64 * (8 + NDMA), (8 + NDMA) / 4) void wgemm_kernel(
   constexpr bool LSPLIT = (OPT & 2) && NDMA == 4;
   constexpr bool ROT = (OPT & 4) != 0;
   constexpr int XAUX = (OPT & 8) ? 1 : 0;
+  constexpr bool PRO = (OPT & 16) && !LSPLIT;
+  constexpr bool H16 = (OPT & 32) != 0;
   constexpr int NX = DX + 1, NW = DW + 1;
   constexpr int NLOAD = NDMA ? NDMA : 8;            // waves issuing LDS-DMA
   constexpr int NWL = LSPLIT ? 2 : NLOAD;           // waves issuing W pieces
@@ -184,6 +192,12 @@ __global__ __launch_bounds__(64 * (8 + NDMA), (8 + NDMA) / 4) void wgemm_kernel(
 #pragma unroll
         for (int s = 1; s < DX; ++s) n += XPW * (t + s < nst);
       }
+    } else if (PRO && t < DX) {
+      // X(t) went out in the stage-ordered prologue: younger are the prologue's later stages and steps 0 .. t-1
+#pragma unroll
+      for (int s = t + 1; s < DW; ++s) n += WPW * (s < nst) + XPW * (s < DX && s < nst);
+#pragma unroll
+      for (int u = 0; u < DX - 1; ++u) n += (u < t) ? WPW * (u + DW < nst) + XPW * (u + DX < nst) : 0;
     } else {
 #pragma unroll
       for (int u = t - DX + 1; u < t; ++u) n += WPW * (u + DW < nst) + XPW * (u + DX < nst);
@@ -273,10 +287,18 @@ __global__ __launch_bounds__(64 * (8 + NDMA), (8 + NDMA) / 4) void wgemm_kernel(
 
   // ---- prologue: steps -DW .. -1
   if (loader) {
+    if constexpr (PRO) {
 #pragma unroll
-    for (int u = -DW; u < 0; ++u) {
-      if (u + DW < nst) issue_w(u + DW);
-      if (u + DX >= 0 && u + DX < nst) issue_x(u + DX);
+      for (int s = 0; s < DW; ++s) {
+        if (s < nst) issue_w(s);
+        if (s < DX && s < nst) issue_x(s);
+      }
+    } else {
+#pragma unroll
+      for (int u = -DW; u < 0; ++u) {
+        if (u + DW < nst) issue_w(u + DW);
+        if (u + DX >= 0 && u + DX < nst) issue_x(u + DX);
+      }
     }
   }
 
@@ -356,7 +378,15 @@ __global__ __launch_bounds__(64 * (8 + NDMA), (8 + NDMA) / 4) void wgemm_kernel(
 #pragma unroll
           for (int mb = 0; mb < G::MB; ++mb) {
             const int unit = (tile0 + wn * G::TN + tn) * G::RB + wm * G::MB + mb;
-            *reinterpret_cast<f32x4*>(w.part + (((size_t)kc * n_units + unit) * 64 + lane) * 4) = acc[tn][mb];
+            const size_t e = ((size_t)kc * n_units + unit) * 64 + lane;
+            if constexpr (H16) {
+              f16x4 h;  // saturated: a partial past the fp16 range stays finite
+#pragma unroll
+              for (int i = 0; i < 4; ++i) h[i] = (_Float16)fminf(fmaxf(acc[tn][mb][i], -65504.f), 65504.f);
+              reinterpret_cast<f16x4*>(w.part)[e] = h;
+            } else {
+              reinterpret_cast<f32x4*>(w.part)[e] = acc[tn][mb];
+            }
           }
       }
       if constexpr (NORM) {
@@ -435,7 +465,7 @@ __global__ __launch_bounds__(64 * (8 + NDMA), (8 + NDMA) / 4) void wgemm_kernel(
           ss += wj * q[j];
         }
       }
-      if constexpr (NORM) v *= rsqrtf(ss / float(a.K) + a.eps);
+      if constexpr (NORM) v *= rms_inv(ss, a.K, a.eps);
       f32x4 pv;
 #pragma unroll
       for (int i = 0; i < 4; ++i) pv[i] = __shfl_xor(v[i], 32, 64);
@@ -445,7 +475,13 @@ __global__ __launch_bounds__(64 * (8 + NDMA), (8 + NDMA) / 4) void wgemm_kernel(
   }
   if (!compute) return;
 
-  // ---- fused epilogue (ks = 1)
+  // ---- fused epilogue (ks = 1); the RMSNorm scale once per row block
+  float rn[G::MB];
+#pragma unroll
+  for (int mb = 0; mb < G::MB; ++mb) {
+    const int m = (wm * G::MB + mb) * 16 + c;
+    rn[mb] = NORM ? rms_inv(s_ss[m] + s_ss[BM + m], a.K, a.eps) : 1.f;
+  }
 #pragma unroll
   for (int tn = 0; tn < G::TN; ++tn) {
     const int gt = tile0 + wn * G::TN + tn;
@@ -454,7 +490,7 @@ __global__ __launch_bounds__(64 * (8 + NDMA), (8 + NDMA) / 4) void wgemm_kernel(
       const int rb = wm * G::MB + mb;
       const int m = rb * 16 + c;
       f32x4 v = acc[tn][mb];
-      if constexpr (NORM) v *= rsqrtf((s_ss[m] + s_ss[BM + m]) / float(a.K) + a.eps);
+      if constexpr (NORM) v *= rn[mb];
       // the pair epilogues read the partner rows (+8 of the tile) from lane + 32: exchanged by every lane
       f32x4 pv;
 #pragma unroll
@@ -478,7 +514,7 @@ __global__ __launch_bounds__(64 * (8 + NDMA), (8 + NDMA) / 4) void wgemm_kernel(
 // and then its cos / sin) first, then all KS slab pieces and row sums (KS a compile-time split count; KS = 0 is
 // the runtime-count fallback).  Issued after the sum, as before, the epilogue loads were one more round trip
 // (two for QKV: position, then the tables).
-template <int BM, int EPI, bool NORM, int KS>
+template <int BM, int EPI, bool NORM, int KS, bool H16 = false>
 __global__ __launch_bounds__(256) void wgemm_reduce_kernel(const GemmArgs a, const WgArgs w, int n_units) {
   constexpr int RB = BM / 16;
   const int lane = threadIdx.x & 63;
@@ -491,12 +527,17 @@ __global__ __launch_bounds__(256) void wgemm_reduce_kernel(const GemmArgs a, con
   const bool live = gt < ntiles;
   const EpiIn e = live ? epi_load_at<EPI>(a, gt, m, lane) : EpiIn{};
   const int ks = KS ? KS : w.ks;
-  const f32x4* src = reinterpret_cast<const f32x4*>(w.part) + (size_t)unit * 64 + lane;
+  using slab_t = std::conditional_t<H16, f16x4, f32x4>;
+  const slab_t* src = reinterpret_cast<const slab_t*>(w.part) + (size_t)unit * 64 + lane;
+  auto widen = [](const slab_t& x) -> f32x4 {
+    if constexpr (H16) return f32x4{(float)x[0], (float)x[1], (float)x[2], (float)x[3]};
+    else return x;
+  };
   const float* ssrc = w.part_ss + (size_t)(gt / WG_NT) * ks * BM + m;
   f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
   float ss = 0.f;
   if constexpr (KS > 0) {
-    f32x4 p[KS];
+    slab_t p[KS];
     float q[KS];
 #pragma unroll
     for (int k = 0; k < KS; ++k) p[k] = src[(size_t)k * n_units * 64];
@@ -506,16 +547,16 @@ __global__ __launch_bounds__(256) void wgemm_reduce_kernel(const GemmArgs a, con
     }
 #pragma unroll
     for (int k = 0; k < KS; ++k) {
-      v += p[k];
+      v += widen(p[k]);
       if constexpr (NORM) ss += q[k];
     }
   } else {
-    for (int k = 0; k < ks; ++k) v += src[(size_t)k * n_units * 64];
+    for (int k = 0; k < ks; ++k) v += widen(src[(size_t)k * n_units * 64]);
     if constexpr (NORM) {
       for (int k = 0; k < ks; ++k) ss += ssrc[k * BM];
     }
   }
-  if constexpr (NORM) v *= rsqrtf(ss / float(a.K) + a.eps);
+  if constexpr (NORM) v *= rms_inv(ss, a.K, a.eps);
   f32x4 pv;
 #pragma unroll
   for (int i = 0; i < 4; ++i) pv[i] = __shfl_xor(v[i], 32, 64);
@@ -523,15 +564,15 @@ __global__ __launch_bounds__(256) void wgemm_reduce_kernel(const GemmArgs a, con
   epi_store<EPI>(a, gt, m, lane, e, [&](int off) { return off ? pv : v; });
 }
 
-template <int BM, int EPI, bool NORM>
+template <int BM, int EPI, bool NORM, bool H16 = false>
 void wg_reduce_launch(const GemmArgs& a, const WgArgs& w, int n_units, hipStream_t st) {
   const dim3 grid((n_units + 3) / 4), blk(256);
   switch (w.ks) {
 #define CAIN_WG_RED(K) \
-  case K: hipLaunchKernelGGL((wgemm_reduce_kernel<BM, EPI, NORM, K>), grid, blk, 0, st, a, w, n_units); return;
+  case K: hipLaunchKernelGGL((wgemm_reduce_kernel<BM, EPI, NORM, K, H16>), grid, blk, 0, st, a, w, n_units); return;
     CAIN_WG_RED(2) CAIN_WG_RED(3) CAIN_WG_RED(4) CAIN_WG_RED(5) CAIN_WG_RED(6) CAIN_WG_RED(7) CAIN_WG_RED(8)
 #undef CAIN_WG_RED
-    default: hipLaunchKernelGGL((wgemm_reduce_kernel<BM, EPI, NORM, 0>), grid, blk, 0, st, a, w, n_units);
+    default: hipLaunchKernelGGL((wgemm_reduce_kernel<BM, EPI, NORM, 0, H16>), grid, blk, 0, st, a, w, n_units);
   }
 }
 
@@ -605,7 +646,7 @@ hipError_t wg_launch(const GemmArgs& a, const WgArgs& w, const WgPlan& p, hipStr
                      lds, st, a, w);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || p.ks == 1 || w.combine) return e;
-  wg_reduce_launch<BM, EPI, NORM>(a, w, p.nblk * WG_NT * G::RB, st);
+  wg_reduce_launch<BM, EPI, NORM, (OPT & 32) != 0>(a, w, p.nblk * WG_NT * G::RB, st);
   return hipGetLastError();
 }
 
@@ -620,38 +661,32 @@ hipError_t wg_launch_v(const GemmArgs& a, const WgArgs& w, const WgPlan& p, hipS
   if (const WgShape* o = wg_shape(a.N, a.K, BM)) {
     if (o->variant >= 0) variant = o->variant;
   }
+  // Every default carries fp16 split-K slabs (OPT 32, H = 32 below): in the graph-replayed headline 26.33 / 26.17k
+  // -> 27.34 / 27.17k tok/s against fp32 slabs (same box, interleaved; profiles/r3/README.md).  Variant 4 keeps
+  // fp32 slabs for A/B runs; 5, 12, 14 and 17 are the loader alternatives that measured within box-to-box noise.
+  constexpr int H = 32;
   if constexpr (BM == 256) {  // X stage 32 KiB, W stage 16 KiB
     switch (variant) {
-      case 1: return wg_launch<BM, 2, 3, EPI, NORM, 0>(a, w, p, st);     // MFMA waves load
-      case 2: return wg_launch<BM, 2, 2, EPI, NORM, 4>(a, w, p, st);     // 144 KiB
-      case 3: return wg_launch<BM, 1, 5, EPI, NORM, 4>(a, w, p, st);     // 160 KiB
-      case 5: return wg_launch<BM, 2, 3, EPI, NORM, 4, 0, 1>(a, w, p, st);  // loader-wave sums of squares
-      case 6: return wg_launch<BM, 2, 3, EPI, NORM, 4, 3, 1>(a, w, p, st);  // 5 + timestamps
-      case 10: return wg_launch<BM, 2, 3, EPI, NORM, 4, 0, 2>(a, w, p, st);  // W / X loader roles
-      case 11: return wg_launch<BM, 1, 5, EPI, NORM, 4, 0, 2>(a, w, p, st);  // roles, deep W ring
-      case 12: return wg_launch<BM, 2, 3, EPI, NORM, 4, 0, 4>(a, w, p, st);  // rotated k start
-      case 13: return wg_launch<BM, 1, 5, EPI, NORM, 4, 0, 6>(a, w, p, st);  // roles + deep W + rotation
-      case 21: return wg_launch<BM, 1, 5, EPI, NORM, 4, 3, 2>(a, w, p, st);  // 11 + timestamps
-      case 22: return wg_launch<BM, 2, 3, EPI, NORM, 4, 3, 4>(a, w, p, st);  // 12 + timestamps
-      case 23: return wg_launch<BM, 1, 5, EPI, NORM, 4, 3, 6>(a, w, p, st);  // 13 + timestamps
-      case 20: return wg_launch<BM, 2, 3, EPI, NORM, 4, 3, 2>(a, w, p, st);  // 10 + timestamps
-      case 14: return wg_launch<BM, 2, 3, EPI, NORM, 4, 0, 6>(a, w, p, st);   // roles + rotation
-      case 15: return wg_launch<BM, 2, 3, EPI, NORM, 4, 0, 14>(a, w, p, st);  // roles + rotation + X nt
-      case 16: return wg_launch<BM, 2, 3, EPI, NORM, 4, 0, 8>(a, w, p, st);   // X nt
-      case 24: return wg_launch<BM, 2, 3, EPI, NORM, 4, 3, 6>(a, w, p, st);   // 14 + timestamps
-      case 25: return wg_launch<BM, 2, 3, EPI, NORM, 4, 3, 14>(a, w, p, st);  // 15 + timestamps
-      case 26: return wg_launch<BM, 2, 3, EPI, NORM, 4, 3, 8>(a, w, p, st);   // 16 + timestamps
-      case 7: return wg_launch<BM, 2, 3, EPI, NORM, 4, 3>(a, w, p, st);  // default + timestamps
-      case 8: return wg_launch<BM, 2, 3, EPI, NORM, 4, 1>(a, w, p, st);  // DMA only
-      case 9: return wg_launch<BM, 2, 3, EPI, NORM, 4, 2>(a, w, p, st);  // compute only
-      default: return wg_launch<BM, 2, 3, EPI, NORM, 4>(a, w, p, st);    // 160 KiB
+      case 1: return wg_launch<BM, 2, 3, EPI, NORM, 0, 0, H>(a, w, p, st);   // MFMA waves load
+      case 2: return wg_launch<BM, 2, 2, EPI, NORM, 4, 0, H>(a, w, p, st);   // 144 KiB
+      case 3: return wg_launch<BM, 1, 5, EPI, NORM, 4, 0, H>(a, w, p, st);   // 160 KiB
+      case 4: return wg_launch<BM, 2, 3, EPI, NORM, 4>(a, w, p, st);         // fp32 slabs
+      case 5: return wg_launch<BM, 2, 3, EPI, NORM, 4, 0, H | 1>(a, w, p, st);   // loader-wave sums of squares
+      case 12: return wg_launch<BM, 2, 3, EPI, NORM, 4, 0, H | 4>(a, w, p, st);  // rotated k start
+      case 14: return wg_launch<BM, 2, 3, EPI, NORM, 4, 0, H | 6>(a, w, p, st);  // W / X loader roles + rotation
+      case 17: return wg_launch<BM, 2, 3, EPI, NORM, 4, 0, H | 16>(a, w, p, st);  // stage-ordered prologue
+      case 7: return wg_launch<BM, 2, 3, EPI, NORM, 4, 3, H>(a, w, p, st);   // default + timestamps
+      case 8: return wg_launch<BM, 2, 3, EPI, NORM, 4, 1, H>(a, w, p, st);   // DMA only
+      case 9: return wg_launch<BM, 2, 3, EPI, NORM, 4, 2, H>(a, w, p, st);   // compute only
+      default: return wg_launch<BM, 2, 3, EPI, NORM, 4, 0, H>(a, w, p, st);  // 160 KiB
     }
   } else {  // X stage 16 KiB, W stage 16 KiB
     switch (variant) {
-      case 1: return wg_launch<BM, 3, 5, EPI, NORM, 0>(a, w, p, st);
-      case 2: return wg_launch<BM, 3, 3, EPI, NORM, 4>(a, w, p, st);     // 128 KiB
-      case 3: return wg_launch<BM, 2, 6, EPI, NORM, 4>(a, w, p, st);     // 160 KiB
-      default: return wg_launch<BM, 3, 5, EPI, NORM, 4>(a, w, p, st);    // 160 KiB
+      case 1: return wg_launch<BM, 3, 5, EPI, NORM, 0, 0, H>(a, w, p, st);
+      case 2: return wg_launch<BM, 3, 3, EPI, NORM, 4, 0, H>(a, w, p, st);   // 128 KiB
+      case 3: return wg_launch<BM, 2, 6, EPI, NORM, 4, 0, H>(a, w, p, st);   // 160 KiB
+      case 4: return wg_launch<BM, 3, 5, EPI, NORM, 4>(a, w, p, st);         // fp32 slabs
+      default: return wg_launch<BM, 3, 5, EPI, NORM, 4, 0, H>(a, w, p, st);  // 160 KiB
     }
   }
 }
@@ -700,13 +735,13 @@ CAIN_API void cain_wgemm_clear_shapes() { g_wg_nshapes = 0; }
 static unsigned long long* g_wg_stamps = nullptr;
 CAIN_API void cain_wgemm_set_stamps(void* p) { g_wg_stamps = static_cast<unsigned long long*>(p); }
 CAIN_API int cain_wgemm_eligible(int N, int K, int M);
-// The plan the next launch of this shape would use: ks * 16 + variant (tests, tools).
+// The plan the next launch of this shape would use: ks * 64 + variant (tests, tools).
 CAIN_API int cain_wgemm_plan(int N, int K, int M) {
   if (!cain_wgemm_eligible(N, K, M)) return -1;
   const WgPlan p = wg_plan(N, K, M);
   if (g_wgemm_variant < 0) g_wgemm_variant = wg_env("CAIN_WGEMM_VARIANT", 0);
   const WgShape* o = wg_shape(N, K, p.bm);
-  return p.ks * 16 + (o && o->variant >= 0 ? o->variant : g_wgemm_variant);
+  return p.ks * 64 + (o && o->variant >= 0 ? o->variant : g_wgemm_variant);
 }
 
 CAIN_API int cain_wgemm_eligible(int N, int K, int M) {

@@ -291,7 +291,7 @@ __global__ __launch_bounds__(QR_THREADS) void quant_rows_kernel(const __bf16* __
       *reinterpret_cast<u32x2_t*>(orow + k) = o;
     }
   }
-  if (threadIdx.x == 0) xs[m] = scale * (norm ? rsqrtf(ss / float(K) + eps) : 1.f);
+  if (threadIdx.x == 0) xs[m] = scale * (norm ? rms_inv(ss, K, eps) : 1.f);
 }
 
 namespace {

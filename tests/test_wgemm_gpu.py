@@ -118,7 +118,8 @@ def test_wide_splitk_repeatable_after_batched_path(N, K, norm, epi):
 
 @pytest.mark.parametrize("ks,variant", [(3, 2), (6, 0), (16, 2), (1, 0)])
 def test_shape_plan_override(ks, variant):
-    """A per-shape plan (split count, ring variant) from the autotune table changes the launch, not the result."""
+    """A per-shape plan (split count, ring variant) changes the launch, not the result (up to the fp16 rounding of the
+    split-K slabs, which differs with the split count: ~1e-4 relative, 8x below the bf16 output rounding)."""
     torch.manual_seed(ks)
     N, K, M = 4096, 4096, 256
     W = (torch.randn(N, K, device=DEV) * 0.02).bfloat16()
@@ -131,4 +132,4 @@ def test_shape_plan_override(ks, variant):
         y = ops.skinny_gemm(wp, x, N, ops.EPI_F32, norm=True)
     finally:
         ops.clear_wide_gemm_plans()
-    assert rel_err(y, ref) < 1e-5
+    assert rel_err(y, ref) < 1e-3
