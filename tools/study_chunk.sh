@@ -16,4 +16,7 @@ export CAIN_STUDY_RESULTS_DIR="$PWD/$OUT" CAIN_STUDY_NAME=full_factorial_r3 CAIN
 timeout -k 30 1140 python -u -m cain_amd experiments/study.py --gpus 1 --yes > "$OUT/session_$(date +%s).log" 2>&1
 rc=$?
 grep -c ",DONE," "$OUT/full_factorial_r3/run_table.csv" || true
+# one archive instead of ~5k per-run files: gpurun merges back at most 2,000 files, and a partial merge once lost
+# the run table of two sessions (unpack with: tar xzf gpurun_out/study_r3/full_factorial_r3.tgz -C gpurun_out/study_r3)
+tar czf "$OUT/full_factorial_r3.tgz" -C "$OUT" full_factorial_r3 && rm -rf "$OUT/full_factorial_r3"
 exit $rc
