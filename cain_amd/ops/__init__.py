@@ -93,6 +93,7 @@ def load() -> ctypes.CDLL:
         lib.cain_attention_ex.argtypes = ([vp, vp, vp, vp, vp, vp, vp, vp, vp, ci, ci, ci, ci, ci, ci, ci, cf, ci, cf, cf]
                                           + [vp])
         lib.cain_front_eligible.argtypes = [ci] * 8
+        lib.cain_attention_set_ring.argtypes = [ci]
         lib.cain_front.argtypes = ([vp] * 12 + [ci] * 6 + [cf, ci, vp, vp, vp, ci, cf, vp, vp, vp])
         lib.cain_sample.argtypes = [vp, ci, ci, vp, vp, vp, ci, vp, vp, vp, vp, vp, ci, ci, vp, vp]
         lib.cain_sample_ex.argtypes = [vp, ci, ci, vp, vp, vp, ci, vp, vp, vp, vp, vp, ci, ci, vp, vp,
@@ -415,6 +416,13 @@ def attention(q, kc, vtc, slot, pos, H, Hkv, hd, nsplit, scale, out=None, part_o
                                  vscale, _stream()),
            "attention")
     return out
+
+
+def set_attention_ring(variant: int) -> None:
+    """LDS-DMA ring body of the wide decode attention (csrc/attention.hip attn_ring_kernel; hd 128, bf16 cache,
+    one split, >= 2 (row, kv head) pairs per CU): 0 off (the register kernel), 1 = 4 compute waves x 2 slots (the
+    default), 2 = 2 x 4, 3 = 3 x 3.  A/B switch (CAIN_ATTN_RING), read at every launch and graph capture."""
+    load().cain_attention_set_ring(int(variant))
 
 
 def front_eligible(M: int, d: int, H: int, Hkv: int, hd: int, nsplit: int, kv8: bool = False) -> bool:

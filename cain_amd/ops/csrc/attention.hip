@@ -41,6 +41,7 @@
 #include <type_traits>
 
 #include "common.h"
+#include "wgemm_ring.h"
 
 constexpr float LOG2E = 1.4426950408889634f;
 // AW: waves per workgroup (4; 8 for few (row, kv head) pairs: single-stream decode, where one workgroup per
@@ -356,6 +357,242 @@ static hipError_t launch_attn(const void* q, const void* kc, const void* vtc, co
   return hipGetLastError();
 }
 
+
+// =====================================================================================================
+// Wide decode attention on an LDS-DMA ring (LDS-staged KV tiles; the default wide body, CAIN_ATTN_RING).
+//
+// One workgroup per CU, persistent over the (row, kv head) pairs: 4 compute waves, each owning whole pairs (pair
+// blockIdx.x + (c + 4 i) * gridDim.x for compute wave c), so no cross-wave merge; and 4 loader waves, loader c
+// streaming compute wave c's next 32-position block (K 2*hd/32 + V hd/16 fragments of 1 KiB = 16 KiB at hd 128,
+// the fragment-major cache layout, so every piece is one lane-linear `global_load_lds_dwordx4 ... nt` and every
+// fragment read a conflict-free `ds_read_b128`) into that wave's R-slot sub-ring.  One barrier per ring step for
+// all 8 waves; the loader keeps R - 1 blocks per compute wave in flight across it (counted vmcnt), and a slot is
+// refilled only after the barrier that follows its reads.  Both roles walk the same per-wave block schedule.
+// Compute per block is the register kernel's (QK^T and PV on v_mfma_f32_16x16x32_bf16, online softmax).
+// Why it might pay: the per-CU DMA stream reaches ~7 TB/s chip-wide with ~32-64 KiB in flight
+// (tools/ingest_bench.hip), against ~6.0-6.5 TB/s for the register kernel's 16 waves of loads.
+// =====================================================================================================
+namespace ring {
+struct Cursor {
+  int i;    // pair index within this wave's list
+  int p;    // pair id (m * Hkv + kh), or >= P when done
+  int b;    // block within the pair
+  int nb;   // blocks of the pair
+};
+
+__device__ __forceinline__ int pair_blocks(const int* slot, const int* pos, int p, int Hkv) {
+  const int m = p / Hkv;
+  return slot[m] >= 0 ? (pos[m] + 1 + 31) >> 5 : 0;
+}
+// pair i of compute wave w's list: blockIdx.x + (w + NC i) * gridDim.x
+template <int NC>
+__device__ __forceinline__ int pair_of(int w, int i) {
+  return blockIdx.x + (w + NC * i) * gridDim.x;
+}
+// first pair with blocks from c.i on (pairs with none get zero outputs from the compute wave)
+template <int NC>
+__device__ __forceinline__ void seek(Cursor& c, int w, int P, int Hkv, const int* slot, const int* pos) {
+  for (;;) {
+    c.p = pair_of<NC>(w, c.i);
+    if (c.p >= P) return;
+    c.nb = pair_blocks(slot, pos, c.p, Hkv);
+    c.b = 0;
+    if (c.nb > 0) return;
+    ++c.i;
+  }
+}
+template <int NC>
+__device__ __forceinline__ void advance(Cursor& c, int w, int P, int Hkv, const int* slot, const int* pos) {
+  if (++c.b == c.nb) {
+    ++c.i;
+    seek<NC>(c, w, P, Hkv, slot, pos);
+  }
+}
+}  // namespace ring
+
+// NC compute waves + NC loader waves; R ring slots per compute wave (R - 1 blocks in flight per compute wave)
+template <int HD, int NC, int R>
+__global__ __launch_bounds__(64 * 2 * NC, 1) void attn_ring_kernel(
+    const __bf16* __restrict__ q, const __bf16* __restrict__ kc, const __bf16* __restrict__ vtc,
+    const int* __restrict__ slot, const int* __restrict__ pos, __bf16* __restrict__ out, int ldo, int M, int H,
+    int Hkv, int T_max, float scale) {
+  using namespace ring;
+  constexpr int NKS = HD / 32, NDT = HD / 16;
+  constexpr int PIECES = 2 * NKS + NDT;
+  constexpr int BLK = PIECES * 1024;  // bytes of one 32-position block (K then V fragments)
+  static_assert(R >= 2 && R <= 5, "ring depth");
+  extern __shared__ __attribute__((aligned(16))) char smem[];  // [NC][R][BLK]
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const bool loader = wave >= NC;
+  const int c = loader ? wave - NC : wave;  // the compute wave this wave is, or feeds
+  const int P = M * Hkv;
+  const int G = H / Hkv;
+  char* sub = smem + c * R * BLK;
+
+  // ring steps of this workgroup: the longest block schedule of its NC compute waves (every wave computes it)
+  int steps = 0;
+  for (int w = 0; w < NC; ++w) {
+    int tot = 0;
+    for (int i = 0;; ++i) {
+      const int p = pair_of<NC>(w, i);
+      if (p >= P) break;
+      tot += pair_blocks(slot, pos, p, Hkv);
+    }
+    steps = max(steps, tot);
+  }
+
+  Cursor cur{0, 0, 0, 0};
+  seek<NC>(cur, c, P, Hkv, slot, pos);
+
+  if (loader) {
+    auto issue = [&](const Cursor& k, int n) {  // the block under cursor k into slot n % R
+      const int m = k.p / Hkv, kh = k.p - m * Hkv, s = slot[m];
+      const char* kb = reinterpret_cast<const char*>(kc) + ((size_t)s * Hkv + kh) * T_max * HD * 2 +
+                       (size_t)k.b * (2 * NKS * 1024) + lane * 16;
+      const char* vb = reinterpret_cast<const char*>(vtc) + ((size_t)s * Hkv + kh) * HD * T_max * 2 +
+                       (size_t)k.b * (NDT * 1024) + lane * 16;
+      char* dst = sub + (n % R) * BLK;
+#pragma unroll
+      for (int j = 0; j < 2 * NKS; ++j) wg::glds16(kb + j * 1024, dst + j * 1024, 1);
+#pragma unroll
+      for (int j = 0; j < NDT; ++j) wg::glds16(vb + j * 1024, dst + (2 * NKS + j) * 1024, 1);
+    };
+    Cursor ahead = cur;
+    unsigned real = 0;  // bit n % R: block n was issued (not past the end of the schedule)
+    auto issue_next = [&](int n) {
+      const bool live = ahead.p < P;
+      if (live) {
+        issue(ahead, n);
+        advance<NC>(ahead, c, P, Hkv, slot, pos);
+      }
+      real = (real & ~(1u << (n % R))) | (unsigned(live) << (n % R));
+    };
+    for (int n = 0; n < R - 1; ++n) issue_next(n);
+    for (int st = 0; st < steps; ++st) {
+      // block st has landed once at most the pieces of the real blocks st+1 .. st+R-2 are outstanding
+      int younger = 0;
+#pragma unroll
+      for (int k = 1; k <= R - 2; ++k) younger += (real >> ((st + k) % R)) & 1;
+      switch (younger) {
+        case 0: wg::wait_vmcnt<0>(); break;
+        case 1: wg::wait_vmcnt<PIECES>(); break;
+        case 2: wg::wait_vmcnt<2 * PIECES>(); break;
+        default: wg::wait_vmcnt<3 * PIECES>(); break;
+      }
+      wg::ring_barrier();
+      issue_next(st + R - 1);
+    }
+    return;
+  }
+
+  // ---- compute wave c
+  const int g = lane & 15, hq = lane >> 4;
+  const float sl2 = scale * LOG2E;
+  bf16x8 qf[NKS];
+  float m_run = -INFINITY, l_run = 0.f;
+  f32x4 o[NDT];
+  int written = 0;  // pairs of this wave's list with their output written (empty ones as zeros)
+  auto zero_pairs_before = [&](int upto) {
+    for (; written < upto; ++written) {
+      const int p = pair_of<NC>(c, written);
+      if (p >= P) return;
+      const int m = p / Hkv, kh = p - m * Hkv;
+      for (int e = lane; e < G * HD; e += 64) out[(size_t)m * ldo + kh * G * HD + e] = f2bf(0.f);
+    }
+  };
+  for (int st = 0; st < steps; ++st) {
+    wg::ring_barrier();
+    if (cur.p >= P) continue;
+    const int m = cur.p / Hkv, kh = cur.p - m * Hkv;
+    const int L = pos[m] + 1;
+    if (cur.b == 0) {
+      zero_pairs_before(cur.i);
+      const bool gvalid = g < G;
+      const __bf16* qrow = q + ((size_t)m * H + kh * G + (gvalid ? g : 0)) * HD + hq * 8;
+#pragma unroll
+      for (int i = 0; i < NKS; ++i) {
+        bf16x8 v = *reinterpret_cast<const bf16x8*>(qrow + i * 32);
+        if (!gvalid) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] = f2bf(0.f);
+        }
+        qf[i] = v;
+      }
+      m_run = -INFINITY, l_run = 0.f;
+#pragma unroll
+      for (int i = 0; i < NDT; ++i) o[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    const char* blk = sub + (st % R) * BLK + lane * 16;
+    bf16x8 ka[NKS], kb[NKS];
+#pragma unroll
+    for (int i = 0; i < NKS; ++i) {
+      ka[i] = *reinterpret_cast<const bf16x8*>(blk + i * 1024);
+      kb[i] = *reinterpret_cast<const bf16x8*>(blk + (NKS + i) * 1024);
+    }
+    f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < NKS; ++i) {
+      s0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ka[i], qf[i], s0, 0, 0, 0);
+      s1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kb[i], qf[i], s1, 0, 0, 0);
+    }
+    bf16x8 va[NDT];
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt) va[dt] = *reinterpret_cast<const bf16x8*>(blk + (2 * NKS + dt) * 1024);
+    const int t0 = cur.b * 32;
+    float bmax = -INFINITY;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int ta = t0 + hq * 4 + r, tb = ta + 16;
+      s0[r] = (ta < L) ? s0[r] * sl2 : -INFINITY;
+      s1[r] = (tb < L) ? s1[r] * sl2 : -INFINITY;
+      bmax = fmaxf(bmax, fmaxf(s0[r], s1[r]));
+    }
+    bmax = fmaxf(bmax, __shfl_xor(bmax, 16, 64));
+    bmax = fmaxf(bmax, __shfl_xor(bmax, 32, 64));
+    const float m_new = fmaxf(m_run, bmax);
+    const float alpha = exp2f(m_run - m_new);
+    m_run = m_new;
+    bf16x8 pf;
+    float psum = 0.f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float pa = exp2f(s0[r] - m_new), pb = exp2f(s1[r] - m_new);
+      psum += pa + pb;
+      pf[r] = f2bf(pa);
+      pf[4 + r] = f2bf(pb);
+    }
+    l_run = l_run * alpha + psum;
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt) {
+      o[dt] *= alpha;
+      o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va[dt], pf, o[dt], 0, 0, 0);
+    }
+    if (cur.b == cur.nb - 1) {  // pair done: normalise and store O (lane (g, hq) holds d = 16 dt + 4 hq + r)
+      float l = l_run + __shfl_xor(l_run, 16, 64);
+      l += __shfl_xor(l, 32, 64);
+      const float inv = l > 0.f ? fast_rcp(l) : 0.f;
+      if (g < G) {
+        __bf16* dst = out + (size_t)m * ldo + (kh * G + g) * HD + hq * 4;
+#pragma unroll
+        for (int dt = 0; dt < NDT; ++dt) {
+          bf16x4 v;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = f2bf(o[dt][r] * inv);
+          *reinterpret_cast<bf16x4*>(dst + dt * 16) = v;
+        }
+      }
+      written = cur.i + 1;
+    }
+    advance<NC>(cur, c, P, Hkv, slot, pos);
+  }
+  zero_pairs_before(1 << 30);
+}
+
+static int g_attn_ring = -1;
+CAIN_API void cain_attention_set_ring(int on) { g_attn_ring = on; }
+
+
 // Workspace: part_o M*H*nsplit*hd floats, part_ml M*Hkv*align32(G*nsplit*2) floats, counters M*Hkv uints
 // (zeroed once; the reducer resets them).  kv8: the caches hold e4m3 elements (value = element * k/vscale).
 CAIN_API int cain_attention_ex(const void* q, const void* kc, const void* vtc, const int* slot, const int* pos,
@@ -363,6 +600,36 @@ CAIN_API int cain_attention_ex(const void* q, const void* kc, const void* vtc, c
                                int Hkv, int hd, int T_max, int nsplit, float scale, int kv8, float kscale,
                                float vscale, hipStream_t st) {
   if (H % Hkv || H / Hkv > 16 || T_max % 32 || nsplit < 1 || nsplit > 64 || M > 256) return -1;
+  // LDS-DMA ring body (default for hd 128, bf16 cache, no position split, >= 2 pairs per CU; CAIN_ATTN_RING=0 or
+  // cain_attention_set_ring(0) selects the register kernel).  Measured (profiles/r3/README.md, same box): 113.3 vs
+  // 113.7 us at 256 rows x 700 positions, 217.8 vs 221.5 at 1400 (6.74 TB/s), 60.3 vs 58.6 at 350; in the
+  // graph-replayed headline 27.44k vs 27.21-27.23k tok/s.  The 2 x 4 and 3 x 3 ring shapes measured slower.
+  if (g_attn_ring < 0) {
+    const char* e = getenv("CAIN_ATTN_RING");
+    g_attn_ring = e && *e ? atoi(e) : 1;
+  }
+  static const int n_cu = [] {
+    int dev = 0, n = 0;
+    (void)hipGetDevice(&dev);
+    return hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess ? n : 0;
+  }();
+  if (g_attn_ring && hd == 128 && !kv8 && nsplit == 1 && n_cu > 0 && M * Hkv >= 2 * n_cu) {
+    // ring shapes (CAIN_ATTN_RING): 1 = 4 compute waves x 2 slots, 2 = 2 x 4, 3 = 3 x 3 (16 KiB slots)
+    auto go = [&](auto kern, int nc, int r) {
+      const int lds = nc * r * 16 * 1024;
+      if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, lds) !=
+          hipSuccess)
+        return int(hipErrorInvalidConfiguration);
+      hipLaunchKernelGGL(kern, dim3(n_cu), dim3(64 * 2 * nc), lds, st, (const __bf16*)q, (const __bf16*)kc,
+                         (const __bf16*)vtc, slot, pos, (__bf16*)out, ldo, M, H, Hkv, T_max, scale);
+      return int(hipGetLastError());
+    };
+    switch (g_attn_ring) {
+      case 2: return go(attn_ring_kernel<128, 2, 4>, 2, 4);
+      case 3: return go(attn_ring_kernel<128, 3, 3>, 3, 3);
+      default: return go(attn_ring_kernel<128, 4, 2>, 4, 2);
+    }
+  }
   // 8-wave workgroups for few (row, kv head) pairs (hd <= 128: the hd-256 body needs one wave per SIMD)
   const bool wide = M * Hkv <= 64;
 #define CAIN_ATTN_CASE(HDV)                                                                                        \

@@ -314,6 +314,46 @@ def test_attention_many_rows(H, Hkv, hd, kv):
         assert rel_err(out[m].view(H, hd), ref) < 2e-2, (m, lengths[m])
 
 
+@pytest.mark.parametrize("H,Hkv", [(32, 8), (28, 4), (12, 2)])
+@pytest.mark.parametrize("ring", [1, 2, 3])
+def test_attention_ring(H, Hkv, ring):
+    """The LDS-DMA ring body (persistent workgroups, loader waves streaming whole 32-position blocks) against the
+    fp32 reference and the register kernel: 256 rows of different lengths (block-aligned and not), idle rows."""
+    torch.manual_seed(22 + ring)
+    hd, T_max, M = 128, 512, 256
+    lengths = torch.randint(1, T_max, (M,)).tolist()
+    lengths[3], lengths[4], lengths[5] = 32, 33, T_max
+    kc = torch.randn(M, Hkv, T_max, hd, device=DEV).bfloat16().float()
+    vt = torch.randn(M, Hkv, T_max, hd, device=DEV).bfloat16().float()
+    kp, vp = ops.pack_kcache(kc.bfloat16()), ops.pack_vcache(vt.bfloat16())
+    q = torch.randn(M, H * hd, device=DEV).bfloat16()
+    slot = torch.arange(M, device=DEV, dtype=torch.int32)
+    slot[7] = slot[200] = -1  # idle rows: zero output
+    pos = torch.tensor([L - 1 for L in lengths], device=DEV, dtype=torch.int32)
+    try:
+        ops.set_attention_ring(0)
+        base = ops.attention(q, kp, vp, slot, pos, H, Hkv, hd, 1, 1.0 / math.sqrt(hd))
+        ops.set_attention_ring(ring)
+        outs = []
+        for _ in range(2):
+            out = torch.full((M, H * hd), 7.0, device=DEV).bfloat16()
+            ops.attention(q, kp, vp, slot, pos, H, Hkv, hd, 1, 1.0 / math.sqrt(hd), out=out)
+            outs.append(out)
+    finally:
+        ops.set_attention_ring(1)  # the default
+    out = outs[0]
+    assert torch.equal(outs[0], outs[1])  # deterministic
+    assert not out.isnan().any()
+    assert float(out[7].float().abs().max()) == 0.0 and float(out[200].float().abs().max()) == 0.0
+    live = [m for m in range(M) if m not in (7, 200)]
+    assert rel_err(out[live].float(), base[live].float()) < 1e-2
+    for m in list(range(0, M, 17)) + [3, 4, 5]:
+        if m in (7, 200):
+            continue
+        ref = _attn_ref(q[m].view(H, hd), kc[m], vt[m], lengths[m], H // Hkv)
+        assert rel_err(out[m].view(H, hd), ref) < 2e-2, (m, lengths[m])
+
+
 @pytest.mark.parametrize("M", [1, 4, 16])
 @pytest.mark.parametrize("N,K,epi,norm", [(1536, 8960, ops.EPI_RESID, False),     # qwen2:1.5b down (96 tiles)
                                           (1536, 1536, ops.EPI_RESID, False),     # qwen2:1.5b O
