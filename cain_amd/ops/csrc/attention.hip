@@ -501,6 +501,17 @@ __global__ __launch_bounds__(64 * 2 * NC, 1) void attn_ring_kernel(
       for (int e = lane; e < G * HD; e += 64) out[(size_t)m * ldo + kh * G * HD + e] = f2bf(0.f);
     }
   };
+  // q of the wave's next pair, requested a block ahead (a pair's start no longer waits for a global load while the
+  // other waves wait at the next barrier); lanes of columns g >= G are zeroed when it is taken
+  const bool gvalid = g < G;
+  bf16x8 qn[NKS];
+  auto load_q = [&](int p) {
+    const int m = p / Hkv, kh = p - m * Hkv;
+    const __bf16* qrow = q + ((size_t)m * H + kh * G + (gvalid ? g : 0)) * HD + hq * 8;
+#pragma unroll
+    for (int i = 0; i < NKS; ++i) qn[i] = *reinterpret_cast<const bf16x8*>(qrow + i * 32);
+  };
+  if (cur.p < P) load_q(cur.p);
   for (int st = 0; st < steps; ++st) {
     wg::ring_barrier();
     if (cur.p >= P) continue;
@@ -508,11 +519,9 @@ __global__ __launch_bounds__(64 * 2 * NC, 1) void attn_ring_kernel(
     const int L = pos[m] + 1;
     if (cur.b == 0) {
       zero_pairs_before(cur.i);
-      const bool gvalid = g < G;
-      const __bf16* qrow = q + ((size_t)m * H + kh * G + (gvalid ? g : 0)) * HD + hq * 8;
 #pragma unroll
       for (int i = 0; i < NKS; ++i) {
-        bf16x8 v = *reinterpret_cast<const bf16x8*>(qrow + i * 32);
+        bf16x8 v = qn[i];
         if (!gvalid) {
 #pragma unroll
           for (int j = 0; j < 8; ++j) v[j] = f2bf(0.f);
@@ -522,6 +531,12 @@ __global__ __launch_bounds__(64 * 2 * NC, 1) void attn_ring_kernel(
       m_run = -INFINITY, l_run = 0.f;
 #pragma unroll
       for (int i = 0; i < NDT; ++i) o[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    if (cur.b == max(cur.nb - 2, 0)) {
+      Cursor nx = cur;
+      nx.b = nx.nb - 1;
+      advance<NC>(nx, c, P, Hkv, slot, pos);
+      if (nx.p < P) load_q(nx.p);
     }
     const char* blk = sub + (st % R) * BLK + lane * 16;
     bf16x8 ka[NKS], kb[NKS];

@@ -51,6 +51,7 @@ CAIN_API int cain_sample(float* logits, int ldl, int V, int* tok, int* pos, int*
                          const int* max_new, int* done, int* hist, const int* slot, int T_max, int M,
                          const void* params, hipStream_t st);
 CAIN_API long long cain_sample_ws_bytes(int M);
+CAIN_API int cain_sample_split_max();
 CAIN_API int cain_front_eligible(int M, int d, int q_dim, int hd, int H, int Hkv, int nsplit, int kv8);
 CAIN_API int cain_front(const void* wqkv, const float* bqkv, const void* wo, void* x, void* q, void* attn,
                         void* kc, void* vtc, const int* slot, const int* pos, const float* cos_t, const float* sin_t,
@@ -300,7 +301,7 @@ CAIN_API void* cain_plan_create(const CainPlanDesc* desc) {
   p->d = *desc;
   p->layers.assign(desc->layers, desc->layers + desc->n_layers);
   p->d.layers = p->layers.data();
-  const int ms = desc->Mpad < 64 ? desc->Mpad : 64;
+  const int ms = desc->Mpad < cain_sample_split_max() ? desc->Mpad : cain_sample_split_max();
   if (ms > 0) {
     const long long nb = cain_sample_ws_bytes(ms);
     if (hipMalloc(&p->sample_ws, nb) == hipSuccess && hipMemset(p->sample_ws, 0, nb) == hipSuccess) {

@@ -15,6 +15,8 @@
 //   pos[m]  += 1                 (position of that token)
 //   gen[m][n_gen[m]++] <- id     (output buffer, read back once at the end)
 //   hist ring of the last 64 ids (repeat penalty), done[m] on EOS / budget.
+#include <cstdlib>
+
 #include "common.h"
 
 struct SampleParams {
@@ -700,12 +702,23 @@ CAIN_API long long cain_sample_ws_bytes(int M) {
   return (long long)M * SS_P * SS_KMAX * 8 + (long long)M * SS_P * 4 + (long long)M * 4 + 256;
 }
 
-// Sampler with a workspace: the two-stage kernel (SS_P workgroups per row) for rows <= 64, else the
-// one-workgroup kernel.  ws must hold cain_sample_ws_bytes(M) zeroed bytes (null: one-workgroup kernel).
+// Rows up to which the two-stage kernel runs (CAIN_SAMPLE_SPLIT_MAX, default 64; the decode plan sizes its
+// workspace for min(rows, this)).  A/B switch for wide batches.
+static int g_split_max = -1;
+CAIN_API int cain_sample_split_max() {
+  if (g_split_max < 0) {
+    const char* e = getenv("CAIN_SAMPLE_SPLIT_MAX");
+    g_split_max = e && *e ? atoi(e) : 64;
+  }
+  return g_split_max;
+}
+
+// Sampler with a workspace: the two-stage kernel (SS_P workgroups per row) for rows <= cain_sample_split_max(),
+// else the one-workgroup kernel.  ws must hold cain_sample_ws_bytes(M) zeroed bytes (null: one-workgroup kernel).
 CAIN_API int cain_sample_ex(float* logits, int ldl, int V, int* tok, int* pos, int* gen, int ldg, int* n_gen,
                             const int* max_new, int* done, int* hist, const int* slot, int T_max, int M,
                             const void* params, void* ws, long long ws_bytes, hipStream_t st) {
-  if (!ws || M > 64 || ws_bytes < cain_sample_ws_bytes(M) || V < 4 * SS_P ||
+  if (!ws || M > cain_sample_split_max() || ws_bytes < cain_sample_ws_bytes(M) || V < 4 * SS_P ||
       (V + SS_P - 1) / SS_P + 3 > SS_NJ * 4 * SS_THREADS)
     return cain_sample(logits, ldl, V, tok, pos, gen, ldg, n_gen, max_new, done, hist, slot, T_max, M, params, st);
   SampleWs w{};

@@ -178,13 +178,21 @@ __global__ __launch_bounds__(64 * (8 + NDMA), (8 + NDMA) / 4) void wgemm8_kernel
   if (!compute) return;
 
   if (w.ks > 1) {
+    // slabs in fp16 as the bf16 kernel's (wgemm.hip OPT 32), already scaled (the scales are linear, so the reduce
+    // sums scaled partials): the raw e4m3 x e4m3 sums would overflow fp16
     const int n_units = nblk * WG_NT * G::RB;
 #pragma unroll
     for (int tn = 0; tn < G::TN; ++tn)
 #pragma unroll
       for (int mb = 0; mb < G::MB; ++mb) {
-        const int unit = (tile0 + wn * G::TN + tn) * G::RB + wm * G::MB + mb;
-        *reinterpret_cast<f32x4*>(w.part + (((size_t)kc * n_units + unit) * 64 + lane) * 4) = acc[tn][mb];
+        const int gt = tile0 + wn * G::TN + tn;
+        const int unit = gt * G::RB + wm * G::MB + mb;
+        const int m = (wm * G::MB + mb) * 16 + c;
+        const f32x4 v = gt < ntiles ? w8_scaled(acc[tn][mb], q, gt, m, lane, a.M) : acc[tn][mb];
+        f16x4 h;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) h[i] = (_Float16)fminf(fmaxf(v[i], -65504.f), 65504.f);
+        reinterpret_cast<f16x4*>(w.part)[((size_t)kc * n_units + unit) * 64 + lane] = h;
       }
     return;
   }
@@ -206,8 +214,9 @@ __global__ __launch_bounds__(64 * (8 + NDMA), (8 + NDMA) / 4) void wgemm8_kernel
   }
 }
 
-// Split-K combine + scales + fused epilogue: one wave per 16 x 16 output unit.  As wgemm.hip's reduce: the
-// epilogue inputs, the scales and all KS slab pieces are issued before the first add (KS = 0: runtime count).
+// Split-K combine + fused epilogue: one wave per 16 x 16 output unit (the slabs hold scaled fp16 partials).  As
+// wgemm.hip's reduce: the epilogue inputs and all KS slab pieces are issued before the first add (KS = 0: runtime
+// count).
 template <int BM, int EPI, int KS>
 __global__ __launch_bounds__(256) void wgemm8_reduce_kernel(const GemmArgs a, const WgArgs w, const W8Scales q,
                                                             int n_units) {
@@ -220,18 +229,18 @@ __global__ __launch_bounds__(256) void wgemm8_reduce_kernel(const GemmArgs a, co
   const int m = rb * 16 + (lane & 15);
   const bool live = gt < ntiles;
   const EpiIn e = live ? epi_load_at<EPI>(a, gt, m, lane) : EpiIn{};
-  const f32x4* src = reinterpret_cast<const f32x4*>(w.part) + (size_t)unit * 64 + lane;
+  const f16x4* src = reinterpret_cast<const f16x4*>(w.part) + (size_t)unit * 64 + lane;  // scaled fp16 partials
+  auto widen = [](const f16x4& x) { return f32x4{(float)x[0], (float)x[1], (float)x[2], (float)x[3]}; };
   f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
   if constexpr (KS > 0) {
-    f32x4 p[KS];
+    f16x4 p[KS];
 #pragma unroll
     for (int k = 0; k < KS; ++k) p[k] = src[(size_t)k * n_units * 64];
 #pragma unroll
-    for (int k = 0; k < KS; ++k) v += p[k];
+    for (int k = 0; k < KS; ++k) v += widen(p[k]);
   } else {
-    for (int k = 0; k < w.ks; ++k) v += src[(size_t)k * n_units * 64];
+    for (int k = 0; k < w.ks; ++k) v += widen(src[(size_t)k * n_units * 64]);
   }
-  if (live) v = w8_scaled(v, q, gt, m, lane, a.M);
   f32x4 pv;
 #pragma unroll
   for (int i = 0; i < 4; ++i) pv[i] = __shfl_xor(v[i], 32, 64);
