@@ -420,8 +420,8 @@ def attention(q, kc, vtc, slot, pos, H, Hkv, hd, nsplit, scale, out=None, part_o
 
 def set_attention_ring(variant: int) -> None:
     """LDS-DMA ring body of the wide decode attention (csrc/attention.hip attn_ring_kernel; hd 128, bf16 cache,
-    one split, >= 2 (row, kv head) pairs per CU): 0 off (the register kernel), 1 = 4 compute waves x 2 slots (the
-    default), 2 = 2 x 4, 3 = 3 x 3.  A/B switch (CAIN_ATTN_RING), read at every launch and graph capture."""
+    one split, 2 to 64 (row, kv head) pairs per CU): 0 off (the register kernel), 1 on (the default).  A/B switch
+    (CAIN_ATTN_RING), read at every launch and graph capture."""
     load().cain_attention_set_ring(int(variant))
 
 

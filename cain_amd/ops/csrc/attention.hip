@@ -373,46 +373,25 @@ static hipError_t launch_attn(const void* q, const void* kc, const void* vtc, co
 // (tools/ingest_bench.hip), against ~6.0-6.5 TB/s for the register kernel's 16 waves of loads.
 // =====================================================================================================
 namespace ring {
-struct Cursor {
-  int i;    // pair index within this wave's list
-  int p;    // pair id (m * Hkv + kh), or >= P when done
-  int b;    // block within the pair
-  int nb;   // blocks of the pair
-};
+constexpr int NC = 4;  // compute waves (= loader waves); the schedule's lane layout needs a power of two
+constexpr int R = 2;   // ring slots per compute wave
+constexpr int LMAX = 64 / NC;  // pairs per compute wave the lane-held schedule covers
 
-__device__ __forceinline__ int pair_blocks(const int* slot, const int* pos, int p, int Hkv) {
-  const int m = p / Hkv;
-  return slot[m] >= 0 ? (pos[m] + 1 + 31) >> 5 : 0;
-}
-// pair i of compute wave w's list: blockIdx.x + (w + NC i) * gridDim.x
-template <int NC>
-__device__ __forceinline__ int pair_of(int w, int i) {
-  return blockIdx.x + (w + NC * i) * gridDim.x;
-}
-// first pair with blocks from c.i on (pairs with none get zero outputs from the compute wave)
-template <int NC>
-__device__ __forceinline__ void seek(Cursor& c, int w, int P, int Hkv, const int* slot, const int* pos) {
-  for (;;) {
-    c.p = pair_of<NC>(w, c.i);
-    if (c.p >= P) return;
-    c.nb = pair_blocks(slot, pos, c.p, Hkv);
-    c.b = 0;
-    if (c.nb > 0) return;
-    ++c.i;
-  }
-}
-template <int NC>
-__device__ __forceinline__ void advance(Cursor& c, int w, int P, int Hkv, const int* slot, const int* pos) {
-  if (++c.b == c.nb) {
-    ++c.i;
-    seek<NC>(c, w, P, Hkv, slot, pos);
-  }
-}
+// The workgroup's schedule, one list entry per lane, the same in every wave: lane l describes pair i = l / NC of
+// compute wave w = l % NC, i.e. pair blockIdx.x + (w + NC i) * gridDim.x -- its cache slot, length (positions) and
+// 32-position blocks.  Built by one parallel load of slot / pos per lane at the start; afterwards the cursors
+// read it by lane index (readlane), so no global load sits in the loops.
+struct Sched {
+  int s, L, nb;
+};
+struct Cursor {
+  int i;  // pair index within the wave's list (LMAX: done)
+  int b;  // block within the pair
+};
 }  // namespace ring
 
-// NC compute waves + NC loader waves; R ring slots per compute wave (R - 1 blocks in flight per compute wave)
-template <int HD, int NC, int R>
-__global__ __launch_bounds__(64 * 2 * NC, 1) void attn_ring_kernel(
+template <int HD>
+__global__ __launch_bounds__(64 * 2 * ring::NC, 1) void attn_ring_kernel(
     const __bf16* __restrict__ q, const __bf16* __restrict__ kc, const __bf16* __restrict__ vtc,
     const int* __restrict__ slot, const int* __restrict__ pos, __bf16* __restrict__ out, int ldo, int M, int H,
     int Hkv, int T_max, float scale) {
@@ -420,7 +399,6 @@ __global__ __launch_bounds__(64 * 2 * NC, 1) void attn_ring_kernel(
   constexpr int NKS = HD / 32, NDT = HD / 16;
   constexpr int PIECES = 2 * NKS + NDT;
   constexpr int BLK = PIECES * 1024;  // bytes of one 32-position block (K then V fragments)
-  static_assert(R >= 2 && R <= 5, "ring depth");
   extern __shared__ __attribute__((aligned(16))) char smem[];  // [NC][R][BLK]
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -430,24 +408,46 @@ __global__ __launch_bounds__(64 * 2 * NC, 1) void attn_ring_kernel(
   const int G = H / Hkv;
   char* sub = smem + c * R * BLK;
 
-  // ring steps of this workgroup: the longest block schedule of its NC compute waves (every wave computes it)
-  int steps = 0;
-  for (int w = 0; w < NC; ++w) {
-    int tot = 0;
-    for (int i = 0;; ++i) {
-      const int p = pair_of<NC>(w, i);
-      if (p >= P) break;
-      tot += pair_blocks(slot, pos, p, Hkv);
+  // ---- the lane-held schedule (host check: P <= 64 * gridDim.x, so LMAX entries per wave cover every pair)
+  Sched me{-1, 0, 0};
+  {
+    const int pl = blockIdx.x + ((lane % NC) + NC * (lane / NC)) * gridDim.x;
+    if (pl < P) {
+      const int m = pl / Hkv;
+      me.s = slot[m];
+      me.L = pos[m] + 1;
+      me.nb = me.s >= 0 ? (me.L + 31) >> 5 : 0;
     }
-    steps = max(steps, tot);
   }
-
-  Cursor cur{0, 0, 0, 0};
-  seek<NC>(cur, c, P, Hkv, slot, pos);
+  // steps = the longest of the NC compute waves' block totals
+  int tot = me.nb;
+#pragma unroll
+  for (int o = NC; o < 64; o <<= 1) tot += __shfl_xor(tot, o, 64);
+#pragma unroll
+  for (int o = 1; o < NC; o <<= 1) tot = max(tot, __shfl_xor(tot, o, 64));
+  const int steps = __builtin_amdgcn_readfirstlane(tot);
+  auto pair_id = [&](int i) { return blockIdx.x + (c + NC * i) * gridDim.x; };
+  auto entry_nb = [&](int i) { return __builtin_amdgcn_readlane(me.nb, c + NC * i); };
+  auto live = [&](int i) { return i < LMAX && pair_id(i) < P; };
+  // first pair with blocks at or after list index i (pairs with none get zero outputs from the compute wave)
+  auto seek = [&](Cursor& k) {
+    while (live(k.i) && entry_nb(k.i) == 0) ++k.i;
+    if (!live(k.i)) k.i = LMAX;
+    k.b = 0;
+  };
+  auto advance = [&](Cursor& k) {
+    if (++k.b == entry_nb(k.i)) {
+      ++k.i;
+      seek(k);
+    }
+  };
+  Cursor cur{0, 0};
+  seek(cur);
 
   if (loader) {
     auto issue = [&](const Cursor& k, int n) {  // the block under cursor k into slot n % R
-      const int m = k.p / Hkv, kh = k.p - m * Hkv, s = slot[m];
+      const int p = pair_id(k.i), m = p / Hkv, kh = p - m * Hkv;
+      const int s = __builtin_amdgcn_readlane(me.s, c + NC * k.i);
       const char* kb = reinterpret_cast<const char*>(kc) + ((size_t)s * Hkv + kh) * T_max * HD * 2 +
                        (size_t)k.b * (2 * NKS * 1024) + lane * 16;
       const char* vb = reinterpret_cast<const char*>(vtc) + ((size_t)s * Hkv + kh) * HD * T_max * 2 +
@@ -459,29 +459,17 @@ __global__ __launch_bounds__(64 * 2 * NC, 1) void attn_ring_kernel(
       for (int j = 0; j < NDT; ++j) wg::glds16(vb + j * 1024, dst + (2 * NKS + j) * 1024, 1);
     };
     Cursor ahead = cur;
-    unsigned real = 0;  // bit n % R: block n was issued (not past the end of the schedule)
     auto issue_next = [&](int n) {
-      const bool live = ahead.p < P;
-      if (live) {
+      if (ahead.i < LMAX) {
         issue(ahead, n);
-        advance<NC>(ahead, c, P, Hkv, slot, pos);
+        advance(ahead);
       }
-      real = (real & ~(1u << (n % R))) | (unsigned(live) << (n % R));
     };
-    for (int n = 0; n < R - 1; ++n) issue_next(n);
+    issue_next(0);
     for (int st = 0; st < steps; ++st) {
-      // block st has landed once at most the pieces of the real blocks st+1 .. st+R-2 are outstanding
-      int younger = 0;
-#pragma unroll
-      for (int k = 1; k <= R - 2; ++k) younger += (real >> ((st + k) % R)) & 1;
-      switch (younger) {
-        case 0: wg::wait_vmcnt<0>(); break;
-        case 1: wg::wait_vmcnt<PIECES>(); break;
-        case 2: wg::wait_vmcnt<2 * PIECES>(); break;
-        default: wg::wait_vmcnt<3 * PIECES>(); break;
-      }
+      wg::wait_vmcnt<0>();  // R = 2: block st is the only one outstanding
       wg::ring_barrier();
-      issue_next(st + R - 1);
+      issue_next(st + 1);
     }
     return;
   }
@@ -494,10 +482,8 @@ __global__ __launch_bounds__(64 * 2 * NC, 1) void attn_ring_kernel(
   f32x4 o[NDT];
   int written = 0;  // pairs of this wave's list with their output written (empty ones as zeros)
   auto zero_pairs_before = [&](int upto) {
-    for (; written < upto; ++written) {
-      const int p = pair_of<NC>(c, written);
-      if (p >= P) return;
-      const int m = p / Hkv, kh = p - m * Hkv;
+    for (; written < upto && live(written); ++written) {
+      const int p = pair_id(written), m = p / Hkv, kh = p - m * Hkv;
       for (int e = lane; e < G * HD; e += 64) out[(size_t)m * ldo + kh * G * HD + e] = f2bf(0.f);
     }
   };
@@ -505,18 +491,19 @@ __global__ __launch_bounds__(64 * 2 * NC, 1) void attn_ring_kernel(
   // other waves wait at the next barrier); lanes of columns g >= G are zeroed when it is taken
   const bool gvalid = g < G;
   bf16x8 qn[NKS];
-  auto load_q = [&](int p) {
-    const int m = p / Hkv, kh = p - m * Hkv;
+  auto load_q = [&](int i) {
+    const int p = pair_id(i), m = p / Hkv, kh = p - m * Hkv;
     const __bf16* qrow = q + ((size_t)m * H + kh * G + (gvalid ? g : 0)) * HD + hq * 8;
 #pragma unroll
-    for (int i = 0; i < NKS; ++i) qn[i] = *reinterpret_cast<const bf16x8*>(qrow + i * 32);
+    for (int k = 0; k < NKS; ++k) qn[k] = *reinterpret_cast<const bf16x8*>(qrow + k * 32);
   };
-  if (cur.p < P) load_q(cur.p);
+  if (cur.i < LMAX) load_q(cur.i);
   for (int st = 0; st < steps; ++st) {
     wg::ring_barrier();
-    if (cur.p >= P) continue;
-    const int m = cur.p / Hkv, kh = cur.p - m * Hkv;
-    const int L = pos[m] + 1;
+    if (cur.i >= LMAX) continue;
+    const int p = pair_id(cur.i), m = p / Hkv, kh = p - m * Hkv;
+    const int L = __builtin_amdgcn_readlane(me.L, c + NC * cur.i);
+    const int nb = entry_nb(cur.i);
     if (cur.b == 0) {
       zero_pairs_before(cur.i);
 #pragma unroll
@@ -532,11 +519,11 @@ __global__ __launch_bounds__(64 * 2 * NC, 1) void attn_ring_kernel(
 #pragma unroll
       for (int i = 0; i < NDT; ++i) o[i] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
-    if (cur.b == max(cur.nb - 2, 0)) {
+    if (cur.b == max(nb - 2, 0)) {
       Cursor nx = cur;
-      nx.b = nx.nb - 1;
-      advance<NC>(nx, c, P, Hkv, slot, pos);
-      if (nx.p < P) load_q(nx.p);
+      nx.b = nb - 1;
+      advance(nx);
+      if (nx.i < LMAX) load_q(nx.i);
     }
     const char* blk = sub + (st % R) * BLK + lane * 16;
     bf16x8 ka[NKS], kb[NKS];
@@ -583,7 +570,7 @@ __global__ __launch_bounds__(64 * 2 * NC, 1) void attn_ring_kernel(
       o[dt] *= alpha;
       o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va[dt], pf, o[dt], 0, 0, 0);
     }
-    if (cur.b == cur.nb - 1) {  // pair done: normalise and store O (lane (g, hq) holds d = 16 dt + 4 hq + r)
+    if (cur.b == nb - 1) {  // pair done: normalise and store O (lane (g, hq) holds d = 16 dt + 4 hq + r)
       float l = l_run + __shfl_xor(l_run, 16, 64);
       l += __shfl_xor(l, 32, 64);
       const float inv = l > 0.f ? fast_rcp(l) : 0.f;
@@ -599,9 +586,9 @@ __global__ __launch_bounds__(64 * 2 * NC, 1) void attn_ring_kernel(
       }
       written = cur.i + 1;
     }
-    advance<NC>(cur, c, P, Hkv, slot, pos);
+    advance(cur);
   }
-  zero_pairs_before(1 << 30);
+  zero_pairs_before(LMAX);
 }
 
 static int g_attn_ring = -1;
@@ -618,7 +605,8 @@ CAIN_API int cain_attention_ex(const void* q, const void* kc, const void* vtc, c
   // LDS-DMA ring body (default for hd 128, bf16 cache, no position split, >= 2 pairs per CU; CAIN_ATTN_RING=0 or
   // cain_attention_set_ring(0) selects the register kernel).  Measured (profiles/r3/README.md, same box): 113.3 vs
   // 113.7 us at 256 rows x 700 positions, 217.8 vs 221.5 at 1400 (6.74 TB/s), 60.3 vs 58.6 at 350; in the
-  // graph-replayed headline 27.44k vs 27.21-27.23k tok/s.  The 2 x 4 and 3 x 3 ring shapes measured slower.
+  // graph-replayed headline 27.44k vs 27.21-27.23k tok/s.  The 2 x 4 and 3 x 3 ring shapes measured slower and
+  // were removed (profiles/r3/attn_ring_isolated.log).
   if (g_attn_ring < 0) {
     const char* e = getenv("CAIN_ATTN_RING");
     g_attn_ring = e && *e ? atoi(e) : 1;
@@ -628,22 +616,15 @@ CAIN_API int cain_attention_ex(const void* q, const void* kc, const void* vtc, c
     (void)hipGetDevice(&dev);
     return hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess ? n : 0;
   }();
-  if (g_attn_ring && hd == 128 && !kv8 && nsplit == 1 && n_cu > 0 && M * Hkv >= 2 * n_cu) {
-    // ring shapes (CAIN_ATTN_RING): 1 = 4 compute waves x 2 slots, 2 = 2 x 4, 3 = 3 x 3 (16 KiB slots)
-    auto go = [&](auto kern, int nc, int r) {
-      const int lds = nc * r * 16 * 1024;
-      if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, lds) !=
-          hipSuccess)
-        return int(hipErrorInvalidConfiguration);
-      hipLaunchKernelGGL(kern, dim3(n_cu), dim3(64 * 2 * nc), lds, st, (const __bf16*)q, (const __bf16*)kc,
-                         (const __bf16*)vtc, slot, pos, (__bf16*)out, ldo, M, H, Hkv, T_max, scale);
-      return int(hipGetLastError());
-    };
-    switch (g_attn_ring) {
-      case 2: return go(attn_ring_kernel<128, 2, 4>, 2, 4);
-      case 3: return go(attn_ring_kernel<128, 3, 3>, 3, 3);
-      default: return go(attn_ring_kernel<128, 4, 2>, 4, 2);
-    }
+  if (g_attn_ring && hd == 128 && !kv8 && nsplit == 1 && n_cu > 0 && M * Hkv >= 2 * n_cu &&
+      M * Hkv <= ring::LMAX * ring::NC * n_cu) {
+    constexpr int lds = ring::NC * ring::R * 16 * 1024;
+    static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_ring_kernel<128>),
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, lds) == hipSuccess;
+    if (!attr) return int(hipErrorInvalidConfiguration);
+    hipLaunchKernelGGL((attn_ring_kernel<128>), dim3(n_cu), dim3(64 * 2 * ring::NC), lds, st, (const __bf16*)q,
+                       (const __bf16*)kc, (const __bf16*)vtc, slot, pos, (__bf16*)out, ldo, M, H, Hkv, T_max, scale);
+    return int(hipGetLastError());
   }
   // 8-wave workgroups for few (row, kv head) pairs (hd <= 128: the hd-256 body needs one wave per SIMD)
   const bool wide = M * Hkv <= 64;
