@@ -96,6 +96,8 @@ def load() -> ctypes.CDLL:
         lib.cain_attention_set_ring.argtypes = [ci]
         lib.cain_front.argtypes = ([vp] * 12 + [ci] * 6 + [cf, ci, vp, vp, vp, ci, cf, vp, vp, vp])
         lib.cain_sample.argtypes = [vp, ci, ci, vp, vp, vp, ci, vp, vp, vp, vp, vp, ci, ci, vp, vp]
+        lib.cain_sample_cm.argtypes = [vp, ci, ci, vp, vp, vp, vp, ci, vp, vp, vp, vp, vp, ci, ci, vp, vp]
+        lib.cain_sample_set_cm.argtypes = [ci]
         lib.cain_sample_ex.argtypes = [vp, ci, ci, vp, vp, vp, ci, vp, vp, vp, vp, vp, ci, ci, vp, vp,
                                        ctypes.c_longlong, vp]
         lib.cain_sample_set_trace.argtypes = [vp]
@@ -418,6 +420,13 @@ def attention(q, kc, vtc, slot, pos, H, Hkv, hd, nsplit, scale, out=None, part_o
     return out
 
 
+def set_sample_cm(on: bool) -> None:
+    """Chunk-maximum sampler for decode forwards of <= 16 rows (the LM head writes 16-column chunk maxima; opt-in,
+    CAIN_SAMPLE_CM=1: same tokens, slower than the two-stage kernel at batch 1).  A/B switch, read at every forward
+    / graph capture."""
+    load().cain_sample_set_cm(int(bool(on)))
+
+
 def set_attention_ring(variant: int) -> None:
     """LDS-DMA ring body of the wide decode attention (csrc/attention.hip attn_ring_kernel; hd 128, bf16 cache,
     one split, 2 to 64 (row, kv head) pairs per CU): 0 off (the register kernel), 1 on (the default).  A/B switch
@@ -473,12 +482,19 @@ def sample_params_tensor(rows, device) -> torch.Tensor:
     return torch.from_numpy(arr.view(np.uint8).copy()).to(device)
 
 
-def sample(logits, tok, pos, gen, n_gen, max_new, done, hist, slot, params, T_max, split: bool = False) -> None:
+def sample(logits, tok, pos, gen, n_gen, max_new, done, hist, slot, params, T_max, split: bool = False,
+           cmax=None) -> None:
     """On-device sampling + decode-state update (csrc/sample.hip).  ``split``: the two-stage kernel (vocabulary
-    slices on 16 workgroups per row, last-arriver merge) that decode forwards of <= 64 rows use; otherwise the
-    one-workgroup-per-row kernel."""
+    slices on 16 workgroups per row, last-arriver merge) that decode forwards of <= 64 rows use; ``cmax`` ([M][V/16]
+    fp32 maxima of the logits' 16-column chunks, as the few-row LM head writes them): the chunk-maximum kernel that
+    single-stream decode uses; otherwise the one-workgroup-per-row kernel."""
     lib = load()
     M, V = logits.shape[0], logits.shape[1]
+    if cmax is not None:
+        _check(lib.cain_sample_cm(_p(logits), logits.stride(0), V, _p(cmax), _p(tok), _p(pos), _p(gen), gen.stride(0),
+                                  _p(n_gen), _p(max_new), _p(done), _p(hist), _p(slot), T_max, M, _p(params),
+                                  _stream()), "sample_cm")
+        return
     if split:
         nb = int(lib.cain_sample_ws_bytes(M))
         ws = _sample_ws(logits.device, nb)

@@ -330,6 +330,16 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_gemm_kernel(const GemmArgs 
     const int m = mo + b * 16 + (lane & 15);
     const EpiIn e = (PRE && ub == wave * 64) ? pre : epi_load<NT, NB, EPI>(a, tile0, mo, u);
     epi_store<EPI>(a, tile0 + t, m, lane, e, [&](int off) { return unit_sum(u + off); });
+    if constexpr (EPI == EPI_F32) {
+      // the LM head's per-row maximum of this 16-column chunk (lanes c, c + 16, c + 32, c + 48 hold row c's 16)
+      if (a.cmax) {
+        const f32x4 v = unit_sum(u);
+        float mx = fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3]));
+        mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+        if ((lane >> 4) == 0 && m < a.M) a.cmax[(size_t)m * a.ld_cm + tile0 + t] = mx;
+      }
+    }
   }
 }
 
@@ -1063,6 +1073,19 @@ CAIN_API long long cain_gemm_ws_bytes(int N, int K, int M) {
   return (long long)bgemm_ws_bytes(bgemm_plan(N, K, M, bgemm_ntw()));
 }
 
+// Chunk maxima of the next few-row fp32-logits GEMM (the LM head at <= 16 rows): set by the runtime right before
+// that call, consumed (and cleared) by it when it runs on the plain skinny kernel; cain_gemm_cmax_take() then
+// reports that the buffer was written, so the runtime can hand it to the chunk-max sampler.
+// (thread-local: engines of different models may run forwards on different threads of one process)
+static thread_local float* g_next_cmax = nullptr;
+static thread_local int g_cmax_used = 0;
+CAIN_API void cain_gemm_set_cmax(float* cmax) { g_next_cmax = cmax, g_cmax_used = 0; }
+CAIN_API int cain_gemm_cmax_take() {
+  const int u = g_cmax_used;
+  g_next_cmax = nullptr, g_cmax_used = 0;
+  return u;
+}
+
 // Entry used by the runtime and the bindings.  norm != 0 selects the fused RMSNorm (gain pre-folded into Wp).
 CAIN_API int cain_skinny_gemm_ex(const void* Wp, const void* X, int ldx, int K, int N, int M, void* Y, int ldy,
                                  const float* bias, int norm, float eps, const int* slot, const int* pos,
@@ -1079,6 +1102,10 @@ CAIN_API int cain_skinny_gemm_ex(const void* Wp, const void* X, int ldx, int K, 
   a.kc = reinterpret_cast<__bf16*>(kc), a.vtc = reinterpret_cast<__bf16*>(vtc);
   a.H = H, a.Hkv = Hkv, a.hd = hd, a.T_max = T_max, a.kv8 = kv8;
   if (epi == EPI_QKV_ROPE && (hd % 16 || (hd / 2) % 8)) return -1;
+  if (epi == EPI_F32 && g_next_cmax && M <= 16 && N % 16 == 0) {
+    a.cmax = g_next_cmax, a.ld_cm = N / 16;
+    g_next_cmax = nullptr, g_cmax_used = 1;
+  }
   return gemm_dispatch(a, epi, norm != 0, waves, st);
 }
 

@@ -35,6 +35,10 @@ struct GemmArgs {
   __bf16* vtc;
   int H, Hkv, hd, T_max;
   int kv8;
+  // EPI_F32 on the skinny kernel (the few-row LM head): also the max of every 16-column chunk of each row,
+  // cmax[m * ld_cm + n / 16] (null: not written) -- the sampler's first stage (sample.hip sample_cm_kernel)
+  float* cmax;
+  int ld_cm;
 };
 
 // Epilogue inputs of one (tile, column-tile, lane) unit, loaded BEFORE the main loop

@@ -52,6 +52,12 @@ CAIN_API int cain_sample(float* logits, int ldl, int V, int* tok, int* pos, int*
                          const void* params, hipStream_t st);
 CAIN_API long long cain_sample_ws_bytes(int M);
 CAIN_API int cain_sample_split_max();
+CAIN_API int cain_sample_cm_enabled();
+CAIN_API int cain_sample_cm(float* logits, int ldl, int V, const float* cmax, int* tok, int* pos, int* gen, int ldg,
+                            int* n_gen, const int* max_new, int* done, int* hist, const int* slot, int T_max, int M,
+                            const void* params, hipStream_t st);
+CAIN_API void cain_gemm_set_cmax(float* cmax);
+CAIN_API int cain_gemm_cmax_take();
 CAIN_API int cain_front_eligible(int M, int d, int q_dim, int hd, int H, int Hkv, int nsplit, int kv8);
 CAIN_API int cain_front(const void* wqkv, const float* bqkv, const void* wo, void* x, void* q, void* attn,
                         void* kc, void* vtc, const int* slot, const int* pos, const float* cos_t, const float* sin_t,
@@ -172,9 +178,12 @@ struct Plan {
   long long sample_ws_bytes = 0;
   // layer-front launch (front.hip) hand-off counters for forwards of <= 4 rows, zeroed once (null: never used)
   unsigned* front_flags = nullptr;
+  // LM-head chunk maxima for forwards of <= 16 rows ([16][V / 16] floats; sample.hip sample_cm_kernel)
+  float* cmax = nullptr;
   ~Plan() {
     if (sample_ws) (void)hipFree(sample_ws);
     if (front_flags) (void)hipFree(front_flags);
+    if (cmax) (void)hipFree(cmax);
   }
 };
 
@@ -282,12 +291,19 @@ int forward(const Plan& p, int M, const CainRows& r, int want_logits, int want_s
       e = g_lt.gemm_f32(d.lm_head_lt, d.xn, d.d, d.d, d.V, M, d.logits, d.V, d.lt_ws, d.lt_ws_bytes, st);
       if (e > 0) CK(e);  // a library failure; no plan / unsupported shape (< 0) falls back
     }
+    // few rows: the skinny LM head also writes the chunk maxima the chunk-max sampler starts from
+    if (e != 0 && p.cmax && M <= 16 && cain_sample_cm_enabled()) cain_gemm_set_cmax(p.cmax);
     if (e != 0) CK(gemm(d.lm_head, d.lm_head8, d.lm_head_scale, d.x, d.d, d.d, d.V, d.logits, d.V, nullptr, 1, nullptr,
                         nullptr, /*EPI_F32*/ 2));
   }
+  const bool cm = want_logits && cain_gemm_cmax_take();
   if (want_sample) {
-    CK(cain_sample_ex(d.logits, d.V, d.V, r.tok, r.pos, r.gen, r.ldg, r.n_gen, r.max_new, r.done, r.hist, r.slot,
-                      d.T_max, M, r.sample_params, p.sample_ws, p.sample_ws_bytes, st));
+    if (cm)
+      CK(cain_sample_cm(d.logits, d.V, d.V, p.cmax, r.tok, r.pos, r.gen, r.ldg, r.n_gen, r.max_new, r.done, r.hist,
+                        r.slot, d.T_max, M, r.sample_params, st));
+    else
+      CK(cain_sample_ex(d.logits, d.V, d.V, r.tok, r.pos, r.gen, r.ldg, r.n_gen, r.max_new, r.done, r.hist, r.slot,
+                        d.T_max, M, r.sample_params, p.sample_ws, p.sample_ws_bytes, st));
   }
   return 0;
 }
@@ -310,6 +326,10 @@ CAIN_API void* cain_plan_create(const CainPlanDesc* desc) {
       if (p->sample_ws) (void)hipFree(p->sample_ws);
       p->sample_ws = nullptr;  // the one-workgroup sampler needs no workspace
     }
+  }
+  if (!desc->w8 && desc->V % 64 == 0 && desc->Mpad > 0) {  // LM-head chunk maxima (<= 16 rows)
+    const int rows = desc->Mpad < 16 ? desc->Mpad : 16;
+    if (hipMalloc(&p->cmax, (size_t)rows * (desc->V / 16) * sizeof(float)) != hipSuccess) p->cmax = nullptr;
   }
   if (!desc->w8 && hipMalloc(&p->front_flags, 4096 * 4) == hipSuccess) {  // front.hip: 4096 flag words
     if (hipMemset(p->front_flags, 0, 4096 * 4) != hipSuccess) {

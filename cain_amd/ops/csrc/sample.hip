@@ -736,4 +736,198 @@ CAIN_API int cain_sample_ex(float* logits, int ldl, int V, int* tok, int* pos, i
   return int(hipGetLastError());
 }
 
+// =====================================================================================================
+// Chunk-maximum sampler for few rows (the single-stream decode): the LM head's skinny kernel also writes every
+// row's maximum over each 16-column chunk of the vocabulary (gemm.hip, GemmArgs::cmax), so the sampler's first
+// stage reads V / 16 chunk maxima instead of V logits.  One 256-thread workgroup per row:
+//   1. repeat penalty in place on the logits (as sample_kernel: once per distinct recent id);
+//   2. tau_c = the (K + R)-th largest of the 256 thread maxima of the chunk maxima (R = the penalised ids): at
+//      least K + R distinct logits are >= tau_c, at least K of them unpenalised, so the penalised row's K-th largest
+//      is >= tau_c, and every top-K logit lies in a chunk whose (unpenalised) maximum is >= tau_c -- for a penalty
+//      >= 1, which only lowers logits; the penalised ids whose chunks were not gathered are added as candidates
+//      themselves, which covers a penalty < 1;
+//   3. the logits of the gathered chunks (typically ~K + R chunks of 16) are the candidate set, reduced with the
+//      same threshold argument to the elements >= the K-th largest thread maximum, ranked (value desc, index asc)
+//      and drawn by draw_topk_wave -- the same candidates in the same order as the other two kernels, so the same
+//      token for the same seed.  Greedy (temperature 0): K = 1, the lowest index on ties, as sample_kernel.
+// Overflows of the candidate buffers (more than MAXC chunks or elements above a threshold) tighten it
+// (tighten_tau), as in the other kernels.
+// =====================================================================================================
+constexpr int CM_NJ = 64;  // chunk maxima (then candidate logits) per thread: V / 16 <= 64 * 256 chunks
+constexpr int CM_MAPW = CM_NJ * SS_THREADS / 32;  // words of the gathered-chunk bitmap
+
+__global__ __launch_bounds__(SS_THREADS) void sample_cm_kernel(
+    float* __restrict__ logits, int ldl, int V, const float* __restrict__ cmax, int* __restrict__ tok,
+    int* __restrict__ pos, int* __restrict__ gen, int ldg, int* __restrict__ n_gen, const int* __restrict__ max_new,
+    int* __restrict__ done, int* __restrict__ hist, const int* __restrict__ slot, int T_max,
+    const SampleParams* __restrict__ params) {
+  const int m = blockIdx.x;
+  if (slot[m] < 0 || done[m]) return;
+  const SampleParams P = params[m];
+  float* lg = logits + (size_t)m * ldl;
+  const int C = V >> 4;
+  const float* cm = cmax + (size_t)m * C;
+  const int tid = threadIdx.x;
+  __shared__ int s_hist[HIST];
+  __shared__ float ws_v[SS_NW][64];
+  __shared__ int ws_i[SS_NW][64];
+  __shared__ float s_tau;
+  __shared__ float sv[SS_KMAX];
+  __shared__ int si[SS_KMAX];
+  __shared__ __attribute__((aligned(16))) float cval[MAXC + 68];
+  __shared__ __attribute__((aligned(16))) int cidx[MAXC + 68];
+  __shared__ int s_ch[MAXC];
+  __shared__ unsigned s_map[CM_MAPW];
+  __shared__ int s_nc;
+  __shared__ int s_choice;
+
+  // ---- 1. repeat penalty, in place
+  const int* hr = hist + (size_t)m * HIST;
+  const int ng = n_gen[m];
+  const int nrep = (P.repeat_penalty != 1.0f && P.repeat_last_n > 0) ? min(min(P.repeat_last_n, HIST), ng) : 0;
+  if (tid < HIST) s_hist[tid] = (tid < nrep) ? hr[(ng - 1 - tid) & (HIST - 1)] : -1;
+  __syncthreads();
+  bool first = false;  // this thread's history id is the first occurrence of a valid id
+  if (tid < nrep) {
+    const int id = s_hist[tid];
+    first = id >= 0 && id < V;
+    for (int j = 0; j < tid; ++j) first &= (s_hist[j] != id);
+    if (first) {
+      const float v = lg[id];
+      lg[id] = v > 0.f ? v / P.repeat_penalty : v * P.repeat_penalty;
+    }
+  }
+  __syncthreads();
+
+  int K = P.top_k;
+  if (K <= 0 || K > SS_KMAX) K = SS_KMAX;
+  if (K > V) K = V;
+  if (P.temperature <= 0.f) K = 1;
+  const int R = nrep;
+
+  // ---- 2. chunk maxima: thread tid holds chunks 4 (tid + 256 j) .. + 3 (16-byte loads); threshold tau_c, then the
+  // chunks >= tau_c
+  float cv[CM_NJ];
+  float bv = -INFINITY;
+  int bi = 0x7fffffff - tid;  // distinct keys for threads without chunks
+  auto cid = [&](int k) { return 4 * (tid + (k >> 2) * SS_THREADS) + (k & 3); };
+  const f32x4* cm4 = reinterpret_cast<const f32x4*>(cm);
+#pragma unroll
+  for (int j = 0; j < CM_NJ / 4; ++j) {
+    const int c4 = tid + j * SS_THREADS;
+    const f32x4 v = 4 * c4 < C ? cm4[c4] : f32x4{-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      cv[4 * j + i] = v[i];
+      if (v[i] > bv) bv = v[i], bi = 4 * c4 + i;
+    }
+  }
+  const int Kc = K + R;
+  if (Kc <= SS_THREADS) {
+    ss_kth(bv, bi, Kc, ws_v, ws_i, &s_tau);
+  } else {
+    if (tid == 0) s_tau = -INFINITY;
+    __syncthreads();
+  }
+  int n_ch = 0;
+#pragma unroll 1
+  for (int attempt = 0; attempt < 4; ++attempt) {
+    if (tid == 0) s_nc = 0;
+    __syncthreads();
+    const float tau = s_tau;
+    gather_candidates(
+        cv, [&](int k) { return cid(k) < C && cv[k] >= tau; }, cid, cval, cidx, &s_nc);
+    n_ch = min(s_nc, MAXC);
+    if (s_nc <= MAXC) break;
+    tighten_tau(cval, cidx, Kc, SS_THREADS, &s_tau);
+  }
+  // the gathered chunk ids, and a bitmap of them (the penalised ids' membership test)
+  for (int w = tid; w < CM_MAPW; w += SS_THREADS) s_map[w] = 0u;
+  __syncthreads();
+  for (int k = tid; k < n_ch; k += SS_THREADS) {
+    const int ch = cidx[k];
+    s_ch[k] = ch;
+    atomicOr(&s_map[ch >> 5], 1u << (ch & 31));
+  }
+  __syncthreads();
+
+  // ---- 3. candidate logits: the gathered chunks' 16 each (chunk slot tid + 256 j: four 16-byte loads), plus the
+  // penalised ids outside them
+  float ev[CM_NJ + 1];
+  int eidv[CM_NJ + 1];  // vocabulary ids (distinct placeholders past the candidates)
+#pragma unroll
+  for (int j = 0; j < CM_NJ / 16; ++j) {
+    const int k = tid + j * SS_THREADS;
+    const int ch = k < n_ch ? s_ch[k] : 0;
+    const f32x4* src = reinterpret_cast<const f32x4*>(lg + (size_t)ch * 16);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const f32x4 v = src[q];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int e = 16 * j + 4 * q + i;
+        ev[e] = k < n_ch ? v[i] : -INFINITY;
+        eidv[e] = k < n_ch ? ch * 16 + 4 * q + i : 0x7ffff000 - (k * 16 + 4 * q + i);
+      }
+    }
+  }
+  int xid = -1;
+  if (first) {
+    const int id = s_hist[tid], ch = id >> 4;
+    if (!((s_map[ch >> 5] >> (ch & 31)) & 1u)) xid = id;
+  }
+  ev[CM_NJ] = xid >= 0 ? lg[xid] : -INFINITY;
+  eidv[CM_NJ] = xid >= 0 ? xid : 0x7fffffff - tid;
+  float bv2 = -INFINITY;
+  int bi2 = 0x7fffffff - tid;
+#pragma unroll
+  for (int k = 0; k <= CM_NJ; ++k) {
+    if (ev[k] > bv2 || (ev[k] == bv2 && eidv[k] < bi2)) bv2 = ev[k], bi2 = eidv[k];
+  }
+  ss_kth(bv2, bi2, K, ws_v, ws_i, &s_tau);
+  int nc = 0;
+#pragma unroll 1
+  for (int attempt = 0; attempt < 4; ++attempt) {
+    if (tid == 0) s_nc = 0;
+    __syncthreads();
+    const float tau = s_tau;
+    gather_candidates(
+        ev, [&](int k) { return ev[k] >= tau && ev[k] > -INFINITY; }, [&](int k) { return eidv[k]; }, cval, cidx,
+        &s_nc);
+    nc = min(s_nc, MAXC);
+    if (s_nc <= MAXC) break;
+    tighten_tau(cval, cidx, K, SS_THREADS, &s_tau);
+  }
+  const int nk = rank_candidates(cval, cidx, nc, K, sv, si, SS_THREADS);
+  if (tid < 64) {
+    const int pick = (P.temperature <= 0.f) ? si[0] : draw_topk_wave(sv, si, nk, P, ng);
+    if (tid == 0) s_choice = pick;
+  }
+  __syncthreads();
+  if (tid == 0) advance_row(m, s_choice, ng, P, tok, pos, gen, ldg, n_gen, max_new, done, hist, T_max);
+}
+
+// The chunk-maximum sampler (rows <= 16, V % 64 == 0, V / 16 <= 64 * 256); cmax as the LM head wrote it
+// (cain_gemm_set_cmax).  Opt-in (CAIN_SAMPLE_CM=1 / cain_sample_set_cm): it draws the same tokens, but one
+// workgroup's chain of phases (37.4 us per token on qwen2:1.5b, profiles/r3/README.md) is longer than the two-stage
+// kernel's 16-way split (29 us), so cain_sample_ex stays the default.
+static int g_sample_cm = -1;
+CAIN_API int cain_sample_cm_enabled() {
+  if (g_sample_cm < 0) {
+    const char* e = getenv("CAIN_SAMPLE_CM");
+    g_sample_cm = e && *e ? atoi(e) : 0;
+  }
+  return g_sample_cm;
+}
+// A/B switch for tests and tools (takes effect at the next forward / graph capture).
+CAIN_API void cain_sample_set_cm(int on) { g_sample_cm = on; }
+CAIN_API int cain_sample_cm(float* logits, int ldl, int V, const float* cmax, int* tok, int* pos, int* gen, int ldg,
+                            int* n_gen, const int* max_new, int* done, int* hist, const int* slot, int T_max, int M,
+                            const void* params, hipStream_t st) {
+  if (!cmax || M > 16 || V % 64 || V / 16 > CM_NJ * SS_THREADS) return -1;  // whole 16-byte chunk-max loads
+  hipLaunchKernelGGL(sample_cm_kernel, dim3(M), dim3(SS_THREADS), 0, st, logits, ldl, V, cmax, tok, pos, gen, ldg,
+                     n_gen, max_new, done, hist, slot, T_max, reinterpret_cast<const SampleParams*>(params));
+  return int(hipGetLastError());
+}
+
 CAIN_API int cain_sample_params_size() { return int(sizeof(SampleParams)); }

@@ -44,6 +44,22 @@ def test_graph_replay_equals_eager_steps(name):
     eng.close()
 
 
+@pytest.mark.parametrize("name", ["tiny-llama3.1:8b", "tiny-qwen2:1.5b", "tiny-gemma:2b"])
+def test_chunk_max_sampler_same_tokens(name):
+    """Few-row decode with the chunk-maximum sampler (the LM head writes 16-column maxima) generates exactly the
+    tokens of the two-stage sampler: sampled (Ollama defaults, repeat penalty) and greedy rows."""
+    from cain_amd import ops
+    opts = [dict(seed=21, eos_id=-1), dict(temperature=0.0, eos_id=-1), dict(repeat_penalty=0.9, seed=5, eos_id=-1)]
+    out = []
+    for cm in (True, False):
+        ops.set_sample_cm(cm)
+        eng = DecodeEngine(name, device="cuda", max_batch=4, max_context=256, seed=7, steps_per_graph=4)
+        out.append([r.tokens for r in eng.generate(PROMPTS, 24, opts)])
+        eng.close()
+    ops.set_sample_cm(False)  # the default
+    assert out[0] == out[1]
+
+
 def test_greedy_first_token_matches_oracle():
     eng = DecodeEngine("tiny-mistral:7b", device="cuda", max_batch=4, max_context=256, keep_natural=True, seed=9)
     ref = ReferenceModel(eng.weights)

@@ -259,6 +259,52 @@ def test_sample_greedy_and_topk():
     assert gen[:, 0].cpu().tolist() == t
 
 
+@pytest.mark.parametrize("V", [128256, 151936, 32064, 256000])
+def test_sample_chunk_max_matches(V):
+    """The chunk-maximum sampler draws the same token as the one-workgroup and two-stage kernels for the same
+    logits, seeds and decode state: greedy, Ollama defaults with a repeat history (penalty > 1), a penalty < 1 (which
+    raises history logits above their chunk maxima), top_k 256, top_p off, and a row with a planted history max."""
+    torch.manual_seed(V % 97)
+    M = 12
+    base = torch.randn(M, V, device=DEV) * 3
+    base[5, 777] = 40.0   # a dominant logit that is also in row 5's history (penalised)
+    rows = []
+    for i in range(M):
+        kind = i % 6
+        rows.append([dict(temperature=0.0, top_p=1.0, repeat_penalty=1.1, top_k=40, repeat_last_n=64),
+                     dict(temperature=0.8, top_p=0.9, repeat_penalty=1.1, top_k=40, repeat_last_n=64),
+                     dict(temperature=0.8, top_p=0.9, repeat_penalty=0.8, top_k=40, repeat_last_n=64),
+                     dict(temperature=1.0, top_p=1.0, repeat_penalty=1.0, top_k=256, repeat_last_n=0),
+                     dict(temperature=1.2, top_p=0.5, repeat_penalty=1.3, top_k=10, repeat_last_n=32),
+                     dict(temperature=0.8, top_p=0.9, repeat_penalty=1.1, top_k=40, repeat_last_n=64)][kind])
+        rows[-1].update(eos_id=-1, seed=1000 + i)
+    params = ops.sample_params_tensor(rows, DEV)
+    # a history of 20 generated ids per row, including the row's top logits (so the penalty matters)
+    hist = torch.zeros(M, 64, device=DEV, dtype=torch.int32)
+    top = base.topk(10, dim=-1).indices
+    for i in range(M):
+        ids = torch.cat([top[i, :6], torch.randint(0, V, (14,), device=DEV)]).to(torch.int32)
+        hist[i, :20] = ids
+    hist[5, 3] = 777
+    results = []
+    for mode in ("cm", "one", "split"):
+        lg = base.clone()
+        tok = torch.zeros(M, device=DEV, dtype=torch.int32)
+        pos = torch.full((M,), 50, device=DEV, dtype=torch.int32)
+        gen = torch.zeros(M, 32, device=DEV, dtype=torch.int32)
+        n_gen = torch.full((M,), 20, device=DEV, dtype=torch.int32)
+        max_new = torch.full((M,), 30, device=DEV, dtype=torch.int32)
+        done = torch.zeros(M, device=DEV, dtype=torch.int32)
+        h = hist.clone().view(-1)
+        slot = torch.arange(M, device=DEV, dtype=torch.int32)
+        cmax = base.view(M, V // 16, 16).amax(-1).contiguous() if mode == "cm" else None
+        ops.sample(lg, tok, pos, gen, n_gen, max_new, done, h, slot, params, 2048, split=(mode == "split"), cmax=cmax)
+        results.append((tok.cpu(), pos.cpu(), n_gen.cpu(), h.cpu()))
+    for r in results[1:]:
+        for a, b in zip(results[0], r):
+            assert torch.equal(a, b)
+
+
 def test_sample_distribution_matches_topk_softmax():
     """Sampling frequencies over many seeds follow softmax over the top-k (top_p off)."""
     torch.manual_seed(6)
