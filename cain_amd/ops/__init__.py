@@ -420,11 +420,17 @@ def attention(q, kc, vtc, slot, pos, H, Hkv, hd, nsplit, scale, out=None, part_o
     return out
 
 
-def set_sample_cm(on: bool) -> None:
-    """Chunk-maximum sampler for decode forwards of <= 16 rows (the LM head writes 16-column chunk maxima; opt-in,
-    CAIN_SAMPLE_CM=1: same tokens, slower than the two-stage kernel at batch 1).  A/B switch, read at every forward
-    / graph capture."""
-    load().cain_sample_set_cm(int(bool(on)))
+def set_sample_cm(mode: int) -> None:
+    """Chunk-maximum sampler (the LM head writes 16-column chunk maxima, the sampler reads only the chunks above a
+    provable threshold; same tokens).  mode 0 off, 1 every decode forward, 2 forwards of more than 64 rows (the
+    default, CAIN_SAMPLE_CM=2: 42 vs 62 us at 256 rows; at batch 1 the two-stage kernel is faster).  A/B switch,
+    read at every forward / graph capture."""
+    load().cain_sample_set_cm(int(mode))
+
+
+def sample_cm_mode() -> int:
+    """The chunk-maximum sampler mode in effect (see set_sample_cm)."""
+    return int(load().cain_sample_cm_enabled())
 
 
 def set_attention_ring(variant: int) -> None:

@@ -1077,6 +1077,7 @@ CAIN_API long long cain_gemm_ws_bytes(int N, int K, int M) {
 // that call, consumed (and cleared) by it when it runs on the plain skinny kernel; cain_gemm_cmax_take() then
 // reports that the buffer was written, so the runtime can hand it to the chunk-max sampler.
 // (thread-local: engines of different models may run forwards on different threads of one process)
+CAIN_API int cain_wgemm_plan(int N, int K, int M);
 static thread_local float* g_next_cmax = nullptr;
 static thread_local int g_cmax_used = 0;
 CAIN_API void cain_gemm_set_cmax(float* cmax) { g_next_cmax = cmax, g_cmax_used = 0; }
@@ -1126,10 +1127,16 @@ CAIN_API int cain_gemm(const void* Wp, const void* X, int ldx, int K, int N, int
     a.slot = slot, a.pos = pos, a.cos_t = cos_t, a.sin_t = sin_t;
     a.kc = reinterpret_cast<__bf16*>(kc), a.vtc = reinterpret_cast<__bf16*>(vtc);
     a.H = H, a.Hkv = Hkv, a.hd = hd, a.T_max = T_max, a.kv8 = kv8;
+    // the wide LM head writes the chunk maxima in its unsplit epilogue (the plan's split count is 1 there)
+    const bool cm = epi == EPI_F32 && g_next_cmax && N % 16 == 0 && cain_wgemm_plan(N, K, M) / 64 == 1;
+    if (cm) a.cmax = g_next_cmax, a.ld_cm = N / 16;
     // the batched path's counters (first BG_COUNTER_BYTES) must stay zero: the slabs go after them
     const int rc = wgemm_dispatch(a, epi, norm != 0, static_cast<char*>(ws) + BG_COUNTER_BYTES,
                                   ws_bytes - (long long)BG_COUNTER_BYTES, st);
-    if (rc >= 0) return rc;
+    if (rc >= 0) {
+      if (cm) g_next_cmax = nullptr, g_cmax_used = 1;
+      return rc;
+    }
   }
   if (ws && bgemm_eligible(N, K, M) && K % 32 == 0 && N % 16 == 0) {
     const BgPlan p = bgemm_plan(N, K, M, bgemm_ntw());

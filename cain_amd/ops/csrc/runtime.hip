@@ -178,7 +178,7 @@ struct Plan {
   long long sample_ws_bytes = 0;
   // layer-front launch (front.hip) hand-off counters for forwards of <= 4 rows, zeroed once (null: never used)
   unsigned* front_flags = nullptr;
-  // LM-head chunk maxima for forwards of <= 16 rows ([16][V / 16] floats; sample.hip sample_cm_kernel)
+  // LM-head chunk maxima ([Mpad][V / 16] floats; sample.hip sample_cm_kernel)
   float* cmax = nullptr;
   ~Plan() {
     if (sample_ws) (void)hipFree(sample_ws);
@@ -291,8 +291,9 @@ int forward(const Plan& p, int M, const CainRows& r, int want_logits, int want_s
       e = g_lt.gemm_f32(d.lm_head_lt, d.xn, d.d, d.d, d.V, M, d.logits, d.V, d.lt_ws, d.lt_ws_bytes, st);
       if (e > 0) CK(e);  // a library failure; no plan / unsupported shape (< 0) falls back
     }
-    // few rows: the skinny LM head also writes the chunk maxima the chunk-max sampler starts from
-    if (e != 0 && p.cmax && M <= 16 && cain_sample_cm_enabled()) cain_gemm_set_cmax(p.cmax);
+    // the LM head also writes the chunk maxima the chunk-max sampler starts from (skinny or wide kernel)
+    const int cm_mode = cain_sample_cm_enabled();
+    if (e != 0 && p.cmax && (cm_mode == 1 || (cm_mode == 2 && M > 64))) cain_gemm_set_cmax(p.cmax);
     if (e != 0) CK(gemm(d.lm_head, d.lm_head8, d.lm_head_scale, d.x, d.d, d.d, d.V, d.logits, d.V, nullptr, 1, nullptr,
                         nullptr, /*EPI_F32*/ 2));
   }
@@ -327,8 +328,8 @@ CAIN_API void* cain_plan_create(const CainPlanDesc* desc) {
       p->sample_ws = nullptr;  // the one-workgroup sampler needs no workspace
     }
   }
-  if (!desc->w8 && desc->V % 64 == 0 && desc->Mpad > 0) {  // LM-head chunk maxima (<= 16 rows)
-    const int rows = desc->Mpad < 16 ? desc->Mpad : 16;
+  if (!desc->w8 && desc->V % 64 == 0 && desc->Mpad > 0) {  // LM-head chunk maxima ([Mpad][V / 16])
+    const int rows = desc->Mpad;
     if (hipMalloc(&p->cmax, (size_t)rows * (desc->V / 16) * sizeof(float)) != hipSuccess) p->cmax = nullptr;
   }
   if (!desc->w8 && hipMalloc(&p->front_flags, 4096 * 4) == hipSuccess) {  // front.hip: 4096 flag words

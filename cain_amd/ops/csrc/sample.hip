@@ -907,15 +907,16 @@ __global__ __launch_bounds__(SS_THREADS) void sample_cm_kernel(
   if (tid == 0) advance_row(m, s_choice, ng, P, tok, pos, gen, ldg, n_gen, max_new, done, hist, T_max);
 }
 
-// The chunk-maximum sampler (rows <= 16, V % 64 == 0, V / 16 <= 64 * 256); cmax as the LM head wrote it
-// (cain_gemm_set_cmax).  Opt-in (CAIN_SAMPLE_CM=1 / cain_sample_set_cm): it draws the same tokens, but one
-// workgroup's chain of phases (37.4 us per token on qwen2:1.5b, profiles/r3/README.md) is longer than the two-stage
-// kernel's 16-way split (29 us), so cain_sample_ex stays the default.
+// The chunk-maximum sampler (V % 64 == 0, V / 16 <= 64 * 256); cmax as the LM head wrote it (cain_gemm_set_cmax).
+// CAIN_SAMPLE_CM / cain_sample_set_cm: 0 off, 1 every forward whose LM head wrote the maxima, 2 only forwards of
+// more than 64 rows (the default).  It draws the same tokens; at one row its one-workgroup chain of phases (37.4 us
+// on qwen2:1.5b, profiles/r3/README.md) is longer than the two-stage kernel's 16-way split (29 us); at 256 rows it
+// takes 42 us against the one-workgroup-per-row kernel's 62 us (+0.2-0.3 % in-graph on the headline).
 static int g_sample_cm = -1;
 CAIN_API int cain_sample_cm_enabled() {
   if (g_sample_cm < 0) {
     const char* e = getenv("CAIN_SAMPLE_CM");
-    g_sample_cm = e && *e ? atoi(e) : 0;
+    g_sample_cm = e && *e ? atoi(e) : 2;
   }
   return g_sample_cm;
 }
@@ -924,7 +925,7 @@ CAIN_API void cain_sample_set_cm(int on) { g_sample_cm = on; }
 CAIN_API int cain_sample_cm(float* logits, int ldl, int V, const float* cmax, int* tok, int* pos, int* gen, int ldg,
                             int* n_gen, const int* max_new, int* done, int* hist, const int* slot, int T_max, int M,
                             const void* params, hipStream_t st) {
-  if (!cmax || M > 16 || V % 64 || V / 16 > CM_NJ * SS_THREADS) return -1;  // whole 16-byte chunk-max loads
+  if (!cmax || V % 64 || V / 16 > CM_NJ * SS_THREADS) return -1;  // whole 16-byte chunk-max loads
   hipLaunchKernelGGL(sample_cm_kernel, dim3(M), dim3(SS_THREADS), 0, st, logits, ldl, V, cmax, tok, pos, gen, ldg,
                      n_gen, max_new, done, hist, slot, T_max, reinterpret_cast<const SampleParams*>(params));
   return int(hipGetLastError());

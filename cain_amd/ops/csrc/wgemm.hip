@@ -499,6 +499,16 @@ __global__ __launch_bounds__(64 * (8 + NDMA), (8 + NDMA) / 4) void wgemm_kernel(
         const EpiIn e = epi_load_at<EPI>(a, gt, m, lane);
         epi_store<EPI>(a, gt, m, lane, e, [&](int off) { return off ? pv : v; });
       }
+      if constexpr (EPI == EPI_F32) {
+        // LM head: this 16-column chunk's maximum of row m (lanes c, c + 16, c + 32, c + 48), as gemm.hip's skinny
+        // kernel writes it for the chunk-maximum sampler
+        if (a.cmax) {
+          float mx = fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3]));
+          mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+          mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+          if ((lane >> 4) == 0 && gt < ntiles && m < a.M) a.cmax[(size_t)m * a.ld_cm + gt] = mx;
+        }
+      }
     }
   }
   if constexpr (ABL == 3) {

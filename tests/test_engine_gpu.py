@@ -51,12 +51,30 @@ def test_chunk_max_sampler_same_tokens(name):
     from cain_amd import ops
     opts = [dict(seed=21, eos_id=-1), dict(temperature=0.0, eos_id=-1), dict(repeat_penalty=0.9, seed=5, eos_id=-1)]
     out = []
-    for cm in (True, False):
+    saved = ops.sample_cm_mode()
+    for cm in (1, 0):
         ops.set_sample_cm(cm)
         eng = DecodeEngine(name, device="cuda", max_batch=4, max_context=256, seed=7, steps_per_graph=4)
         out.append([r.tokens for r in eng.generate(PROMPTS, 24, opts)])
         eng.close()
-    ops.set_sample_cm(False)  # the default
+    ops.set_sample_cm(saved)
+    assert out[0] == out[1]
+
+
+def test_chunk_max_sampler_wide_batch_same_tokens():
+    """80 rows (the wide GEMM path: its unsplit LM-head epilogue writes the chunk maxima): the chunk-maximum sampler
+    generates exactly the tokens of the one-workgroup-per-row sampler."""
+    from cain_amd import ops
+    prompts = [f"In {50 + i} words, please give me information about topic {i}" for i in range(80)]
+    opts = [dict(seed=100 + i, eos_id=-1) if i % 3 else dict(temperature=0.0, eos_id=-1) for i in range(80)]
+    out = []
+    saved = ops.sample_cm_mode()
+    for cm in (1, 0):
+        ops.set_sample_cm(cm)
+        eng = DecodeEngine("tiny-llama3.1:8b", device="cuda", max_batch=80, max_context=256, seed=7, steps_per_graph=4)
+        out.append([r.tokens for r in eng.generate(prompts, 12, opts)])
+        eng.close()
+    ops.set_sample_cm(saved)
     assert out[0] == out[1]
 
 
