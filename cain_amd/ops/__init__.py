@@ -98,6 +98,7 @@ def load() -> ctypes.CDLL:
         lib.cain_sample.argtypes = [vp, ci, ci, vp, vp, vp, ci, vp, vp, vp, vp, vp, ci, ci, vp, vp]
         lib.cain_sample_cm.argtypes = [vp, ci, ci, vp, vp, vp, vp, ci, vp, vp, vp, vp, vp, ci, ci, vp, vp]
         lib.cain_sample_set_cm.argtypes = [ci]
+        lib.cain_gemm_set_skinny_split.argtypes = [ci]
         lib.cain_sample_ex.argtypes = [vp, ci, ci, vp, vp, vp, ci, vp, vp, vp, vp, vp, ci, ci, vp, vp,
                                        ctypes.c_longlong, vp]
         lib.cain_sample_set_trace.argtypes = [vp]
@@ -426,6 +427,13 @@ def set_sample_cm(mode: int) -> None:
     default, CAIN_SAMPLE_CM=2: 42 vs 62 us at 256 rows; at batch 1 the two-stage kernel is faster).  A/B switch,
     read at every forward / graph capture."""
     load().cain_sample_set_cm(int(mode))
+
+
+def set_skinny_split(mode: int) -> None:
+    """Split-K rule of the few-row (<= 16) skinny GEMM (gemm.hip skinny_split): 0 never, 1 narrow long-K grids
+    (default), 2 also grids between one and two tiles per CU (k halved).  Takes effect at the next launch; an
+    engine's workspace is sized at construction, so switch before building one."""
+    load().cain_gemm_set_skinny_split(int(mode))
 
 
 def sample_cm_mode() -> int:

@@ -399,13 +399,25 @@ static hipError_t launch_e(int epi, int waves, const GemmArgs& a, const SkArgs& 
 // qwen2:1.5b's QKV) costs more than it spreads.  (Also measured and not kept: "one-shot" waves that load all of
 // their <= 16 slices in one burst before any MFMA -- the 128 staging VGPRs halve the resident waves, and with
 // them the bytes in flight: qwen2:1.5b gate/up 11.9 -> 12.5 us, split down 9.0 -> 10.4 us, gpurun_out/r3d.)
-// CAIN_SKINNY_SPLIT=0 disables it.
+// CAIN_SKINNY_SPLIT=0 disables it.  CAIN_SKINNY_SPLIT=2 (A/B) also halves the k-range of grids between one and
+// two tiles per CU (llama3.1:8b QKV at one row: 384 tiles on 256 CUs): measured slower -- QKV 12.3 -> 15.4 us,
+// 338 -> 328 tok/s single stream (profiles/r3/b1_skinny_split2_ab.txt): the uneven rounds overlap anyway (several
+// workgroups per CU), and the combine round trip is pure added latency.
+static int g_skinny_split = -1;
+CAIN_API void cain_gemm_set_skinny_split(int mode) { g_skinny_split = mode; }
 static int skinny_split(int N, int K, int M) {
-  static const int on = [] {
+  if (g_skinny_split < 0) {
     const char* e = getenv("CAIN_SKINNY_SPLIT");
-    return e ? atoi(e) : 1;
+    g_skinny_split = e ? atoi(e) : 1;
+  }
+  const int on = g_skinny_split;
+  static const int n_cu = [] {
+    int dev = 0, n = 0;
+    (void)hipGetDevice(&dev);
+    return hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess ? n : 0;
   }();
   const int nt = N / 16, KS = K / 32;
+  if (on == 2 && M <= 16 && n_cu > 0 && nt > n_cu && nt < 2 * n_cu && KS >= 64) return 2;
   if (!on || M > 16 || nt >= 192 || nt < 1 || KS <= 128) return 1;
   // ~80 slices per workgroup, at most ~512 workgroups (qwen2:1.5b down: ks 4 = 9.0 us vs ks 3 = 10.4 us)
   return std::max(1, std::min(std::min(8, (KS + 79) / 80), 512 / nt));

@@ -444,6 +444,33 @@ def test_skinny_split_k_matches_fp32_and_unsplit(M, N, K, epi, norm):
     assert rel_err(outs[0], outs[1]) < 5e-3
 
 
+@pytest.mark.parametrize("M", [1, 16])
+@pytest.mark.parametrize("N,K,epi", [(6144, 4096, ops.EPI_F32), (4608, 3584, ops.EPI_F32)])
+def test_skinny_split_one_to_two_rounds(M, N, K, epi):
+    """CAIN_SKINNY_SPLIT=2: a grid between one and two tiles per CU (llama3.1:8b / qwen2:7b QKV widths at
+    <= 16 rows) halves its k-range; the result matches the fp32 reference and the unsplit kernel."""
+    torch.manual_seed(N + M)
+    W = (torch.randn(N, K, device=DEV) / K ** 0.5).bfloat16()
+    x = (2 * torch.randn(M, K, device=DEV)).bfloat16()
+    g = (1 + 0.2 * torch.randn(K, device=DEV)).bfloat16()
+    Wp = pack_mfma_a(fold_gain(W, g))
+    xr = x.float()
+    xr = xr * torch.rsqrt(xr.pow(2).mean(-1, keepdim=True) + 1e-6) * g.float()
+    ref = xr @ W.float().t()
+    outs = []
+    try:
+        for mode in (2, 1):
+            ops.set_skinny_split(mode)
+            if mode == 2 and torch.cuda.get_device_properties(0).multi_processor_count < N // 16:
+                assert ops.gemm_ws_bytes(N, K, M) > 0  # the split grid is taken
+            out = ops.skinny_gemm(Wp, x, N, epi, norm=True, eps=1e-6, batched=True)
+            assert rel_err(out, ref) < 1e-2, (mode, rel_err(out, ref))
+            outs.append(out.float())
+    finally:
+        ops.set_skinny_split(1)
+    assert rel_err(outs[0], outs[1]) < 5e-3
+
+
 @pytest.mark.parametrize("V", [151936, 32064, 600, 257])
 @pytest.mark.parametrize("M", [1, 3, 64])
 def test_split_sampler_draws_the_same_tokens(V, M):
