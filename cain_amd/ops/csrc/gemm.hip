@@ -53,8 +53,18 @@ struct SkArgs {
   float* part_ss;      // [ntiles][ks][16]
 };
 
-template <int NT, int NB, int WAVES, int U, int EPI, bool NORM, bool PP, bool SPLIT = false>
+// XL (one row block, M <= 16, M * K * 2 <= 64 KiB, unsplit, copy pipeline): the activation rows are staged once
+// into LDS by LDS-DMA and every k-slice reads its fragment from LDS -- one vector-memory load instruction per
+// KiB of weights instead of two.  The fp8 kernel (gemm_w8.hip) gains from it; this bf16 one does not (single
+// stream llama3.1:8b 340.8 -> 339.5 tok/s, qwen2:1.5b 852.9 -> 845.3; 8 slices in flight 316.9 / 768.1:
+// profiles/r3/b1_xlds_ab.txt), so it stays an A/B option (CAIN_SKINNY_XLDS).
+typedef __attribute__((address_space(3))) void sk_lds_t;
+typedef __attribute__((address_space(1))) const void sk_gbl_t;
+
+template <int NT, int NB, int WAVES, int U, int EPI, bool NORM, bool PP, bool SPLIT = false, bool XL0 = false>
 __global__ __launch_bounds__(WAVES * 64) void skinny_gemm_kernel(const GemmArgs a, const SkArgs sk) {
+  constexpr bool XL = XL0 && NB == 1 && !PP && !SPLIT;
+  extern __shared__ __attribute__((aligned(16))) char sk_xs[];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int K = a.K;
@@ -117,7 +127,28 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_gemm_kernel(const GemmArgs 
   // (always non-temporal: a runtime choice of the cache policy put a branch around every load, which
   // defeats the counted waits of the pipeline below; with msplit > 1 the tile-mates still hit L2/MALL)
   auto load_w = [&](int s, int t) -> bf16x8 { return __builtin_nontemporal_load(wbase[t] + (size_t)s * 64); };
-  auto load_x = [&](int s, int b) -> bf16x8 { return *reinterpret_cast<const bf16x8*>(xbase[b] + s * 32); };
+  // XL: this lane's row in the LDS copy (rows past M re-read row M-1) at its k-group
+  const __bf16* xl_row =
+      reinterpret_cast<const __bf16*>(sk_xs) + (size_t)min(lane & 15, a.M - 1) * K + ((lane >> 4) << 3);
+  auto load_x = [&](int s, int b) -> bf16x8 {
+    if constexpr (XL) return *reinterpret_cast<const bf16x8*>(xl_row + s * 32);
+    else return *reinterpret_cast<const bf16x8*>(xbase[b] + s * 32);
+  };
+  // XL: rows [0, M) x K into LDS by LDS-DMA (16-byte chunk c <- row c / (K / 8), column chunk c % (K / 8); wave
+  // instruction j covers chunks 64 j .. 64 j + 63), then every wave's copy has landed
+  auto stage_x = [&]() {
+    const int cpr = K >> 3, nch = a.M * cpr;
+    for (int j = wave; j * 64 < nch; j += WAVES) {
+      const int c = j * 64 + lane;
+      if (c < nch) {
+        const int r = c / cpr, col = c - r * cpr;
+        __builtin_amdgcn_global_load_lds((sk_gbl_t*)(a.X + (size_t)r * a.ldx + col * 8), (sk_lds_t*)(sk_xs + j * 1024),
+                                         16, 0, 0);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  };
   // RMSNorm factorisation: (W diag(g)) (x * inv) = inv * ((W diag(g)) x); the per-row inv is applied in
   // the epilogue and the sum of squares is accumulated from the x fragments this WG streams anyway
   // (its waves cover all of K), so no separate norm kernel and no cross-kernel sum-of-squares buffer.
@@ -189,6 +220,10 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_gemm_kernel(const GemmArgs 
     for (int u = 0; u < U; ++u) {
 #pragma unroll
       for (int t = 0; t < NT; ++t) wa[u][t] = load_w(s + u, t);
+    }
+    if constexpr (XL) stage_x();  // under the weight prologue's latency
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
 #pragma unroll
       for (int b = 0; b < NB; ++b) xa[u][b] = load_x(s + u, b);
     }
@@ -217,6 +252,8 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_gemm_kernel(const GemmArgs 
       }
       s = sn;
     }
+  } else if constexpr (XL) {
+    stage_x();
   }
   for (; s < s_end; ++s) {
 #pragma unroll
@@ -357,6 +394,22 @@ static hipError_t launch_t(const GemmArgs& a, const SkArgs& sk, hipStream_t st) 
       return hipGetLastError();
     }
     return hipErrorInvalidValue;
+  }
+  // activations staged in LDS (XL): CAIN_SKINNY_XLDS=0 off, 1 on, 8 on with 8 slices in flight (A/B)
+  static const int xlds = [] {
+    const char* e = getenv("CAIN_SKINNY_XLDS");
+    return e ? atoi(e) : 0;
+  }();
+  if constexpr (NB == 1) {
+    if (xlds && !pp && a.msplit == 1 && (long long)a.M * a.K * 2 <= 65536) {
+      if (xlds >= 8)  // 8 slices in flight per wave (the LDS copy frees the activation registers)
+        hipLaunchKernelGGL((skinny_gemm_kernel<NT, NB, WAVES, 8, EPI, NORM, false, false, true>),
+                           dim3(a.N / (16 * NT) * a.msplit), dim3(WAVES * 64), (size_t)a.M * a.K * 2, st, a, sk);
+      else
+        hipLaunchKernelGGL((skinny_gemm_kernel<NT, NB, WAVES, U, EPI, NORM, false, false, true>),
+                           dim3(a.N / (16 * NT) * a.msplit), dim3(WAVES * 64), (size_t)a.M * a.K * 2, st, a, sk);
+      return hipGetLastError();
+    }
   }
   if (pp)
     hipLaunchKernelGGL((skinny_gemm_kernel<NT, NB, WAVES, U, EPI, NORM, true>), dim3(a.N / (16 * NT) * a.msplit),

@@ -17,6 +17,8 @@
 // Structure: one workgroup per (16-row tile, 16-row M split); WAVES waves split the k-pairs and
 // keep U pairs of loads in flight in two register sets (copy pipeline), then reduce through LDS;
 // wave 0 runs the epilogue.  Fused RMSNorm as in gemm.hip (gain folded into W before quantisation).
+#include <algorithm>
+
 #include "common.h"
 #include "gemm_epi.h"
 
@@ -31,8 +33,16 @@ __device__ __forceinline__ bf16x8 w8_frag(const u32x4& w, int h) {
   return bf16x8{c0[0], c0[1], c1[0], c1[1], c2[0], c2[1], c3[0], c3[1]};
 }
 
-template <int WAVES, int U, int NT, int NB, int EPI, bool NORM>
+// XL (NB = 1, M <= 16, M * K * 2 <= 64 KiB): the workgroup's activation rows are staged once into LDS by
+// LDS-DMA (global_load_lds_dwordx4) and every k pair reads its two fragments from LDS, so the vector-memory
+// path carries one load instruction per KiB of weights instead of three.
+typedef __attribute__((address_space(3))) void w8_lds_t;
+typedef __attribute__((address_space(1))) const void w8_gbl_t;
+
+template <int WAVES, int U, int NT, int NB, int EPI, bool NORM, bool XL0 = false>
 __global__ __launch_bounds__(WAVES * 64) void skinny_w8_kernel(const GemmArgs a, const float* __restrict__ wscale) {
+  constexpr bool XL = XL0 && NB == 1;
+  extern __shared__ __attribute__((aligned(16))) char w8_xs[];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int KP = a.K >> 6;  // 64-wide k pairs
@@ -81,26 +91,40 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_w8_kernel(const GemmArgs a,
   // (each activation fragment feeds NT tiles: fewer load instructions per weight byte)
   struct Pair {
     u32x4 w[NT];
-    bf16x8 x[NB][2];
+    bf16x8 x[XL ? 1 : NB][2];
+    int p;
   };
+  // XL: this lane's activation row in LDS (rows past M re-read row M-1) at its k-group
+  const __bf16* xl_row =
+      reinterpret_cast<const __bf16*>(w8_xs) + (size_t)min(lane & 15, a.M - 1) * a.K + ((lane >> 4) << 3);
   auto load = [&](Pair& q, int p) {
+    q.p = p;
 #pragma unroll
     for (int t = 0; t < NT; ++t) q.w[t] = __builtin_nontemporal_load(wb + ((size_t)t * KP + p) * 64);
+    if constexpr (!XL) {
 #pragma unroll
-    for (int b = 0; b < NB; ++b) {
-      q.x[b][0] = *reinterpret_cast<const bf16x8*>(xb[b] + p * 64);
-      q.x[b][1] = *reinterpret_cast<const bf16x8*>(xb[b] + p * 64 + 32);
+      for (int b = 0; b < NB; ++b) {
+        q.x[b][0] = *reinterpret_cast<const bf16x8*>(xb[b] + p * 64);
+        q.x[b][1] = *reinterpret_cast<const bf16x8*>(xb[b] + p * 64 + 32);
+      }
     }
+  };
+  auto xfrag = [&](const Pair& q, int b, int h) -> bf16x8 {
+    if constexpr (XL) return *reinterpret_cast<const bf16x8*>(xl_row + q.p * 64 + h * 32);
+    else return q.x[b][h];
   };
   auto step = [&](const Pair& q) {
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
+      bf16x8 xv[NB];
+#pragma unroll
+      for (int b = 0; b < NB; ++b) xv[b] = xfrag(q, b, h);
       if constexpr (NORM) {
 #pragma unroll
         for (int b = 0; b < NB; ++b)
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
-            const float f = bf2f(q.x[b][h][j]);
+            const float f = bf2f(xv[b][j]);
             ssq[b] += f * f;
           }
       }
@@ -109,7 +133,7 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_w8_kernel(const GemmArgs a,
         const bf16x8 wf = w8_frag(q.w[t], h);
 #pragma unroll
         for (int b = 0; b < NB; ++b)
-          acc[t][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, q.x[b][h], acc[t][b], 0, 0, 0);
+          acc[t][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, xv[b], acc[t][b], 0, 0, 0);
       }
     }
   };
@@ -117,10 +141,28 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_w8_kernel(const GemmArgs a,
   // copy pipeline: U pairs in flight while the previous U are multiplied
   int p = p_beg;
   const int nfull = (p_end - p_beg) / U;
+  Pair cur[U];
   if (nfull > 0) {
-    Pair cur[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) load(cur[u], p + u);
+  }
+  if constexpr (XL) {
+    // stage rows [0, M) x K of X by LDS-DMA (the weight prologue above is already in flight): 16-byte chunk c of
+    // the row-contiguous LDS copy <- row c / (K / 8), column chunk c % (K / 8); wave instruction j covers chunks
+    // 64 j .. 64 j + 63 (lane l -> LDS byte 1024 j + 16 l)
+    const int cpr = a.K >> 3, nch = a.M * cpr;
+    for (int j = wave; j * 64 < nch; j += WAVES) {
+      const int c = j * 64 + lane;
+      if (c < nch) {
+        const int r = c / cpr, col = c - r * cpr;
+        __builtin_amdgcn_global_load_lds((w8_gbl_t*)(a.X + (size_t)r * a.ldx + col * 8), (w8_lds_t*)(w8_xs + j * 1024),
+                                         16, 0, 0);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  if (nfull > 0) {
     for (int c = 0; c < nfull; ++c) {
       Pair nxt[U];
       const int pn = p + U;
@@ -186,28 +228,40 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_w8_kernel(const GemmArgs a,
 }
 
 template <int WAVES, int U, int NT, int NB, int EPI, bool NORM>
-static hipError_t w8_launch(const GemmArgs& a, const float* wscale, hipStream_t st) {
+static hipError_t w8_launch(const GemmArgs& a, const float* wscale, bool xl, hipStream_t st) {
+  if constexpr (NB == 1) {
+    if (xl) {
+      hipLaunchKernelGGL((skinny_w8_kernel<WAVES, U, NT, NB, EPI, NORM, true>), dim3(a.N / 16 / NT * a.msplit),
+                         dim3(WAVES * 64), (size_t)a.M * a.K * 2, st, a, wscale);
+      return hipGetLastError();
+    }
+  }
   hipLaunchKernelGGL((skinny_w8_kernel<WAVES, U, NT, NB, EPI, NORM>), dim3(a.N / 16 / NT * a.msplit),
                      dim3(WAVES * 64), 0, st, a, wscale);
   return hipGetLastError();
 }
 
 // kernel variants: (waves, pairs in flight, 16-row tiles of N, 16-row blocks of M) per workgroup
-enum W8Var { W8_4_2_1_1, W8_8_2_1_1, W8_4_4_1_1, W8_8_4_1_1, W8_4_2_2_1, W8_8_2_2_1, W8_4_2_4_1, W8_4_2_1_2, W8_8_2_1_2 };
+enum W8Var { W8_4_2_1_1, W8_8_2_1_1, W8_4_4_1_1, W8_8_4_1_1, W8_4_2_2_1, W8_8_2_2_1, W8_4_2_4_1, W8_4_2_1_2, W8_8_2_1_2,
+              W8_4_8_1_1, W8_8_8_1_1, W8_4_4_2_1, W8_8_4_2_1 };
 
 template <bool NORM>
-static hipError_t w8_launch_e(int epi, int var, const GemmArgs& a, const float* wscale, hipStream_t st) {
+static hipError_t w8_launch_e(int epi, int var, const GemmArgs& a, const float* wscale, bool xl, hipStream_t st) {
 #define CAIN_W8_VAR(E)                                                       \
   switch (var) {                                                             \
-    case W8_4_2_1_1: return w8_launch<4, 2, 1, 1, E, NORM>(a, wscale, st);   \
-    case W8_8_2_1_1: return w8_launch<8, 2, 1, 1, E, NORM>(a, wscale, st);   \
-    case W8_4_4_1_1: return w8_launch<4, 4, 1, 1, E, NORM>(a, wscale, st);   \
-    case W8_8_4_1_1: return w8_launch<8, 4, 1, 1, E, NORM>(a, wscale, st);   \
-    case W8_4_2_2_1: return w8_launch<4, 2, 2, 1, E, NORM>(a, wscale, st);   \
-    case W8_8_2_2_1: return w8_launch<8, 2, 2, 1, E, NORM>(a, wscale, st);   \
-    case W8_4_2_4_1: return w8_launch<4, 2, 4, 1, E, NORM>(a, wscale, st);   \
-    case W8_4_2_1_2: return w8_launch<4, 2, 1, 2, E, NORM>(a, wscale, st);   \
-    default: return w8_launch<8, 2, 1, 2, E, NORM>(a, wscale, st);           \
+    case W8_4_2_1_1: return w8_launch<4, 2, 1, 1, E, NORM>(a, wscale, xl, st);   \
+    case W8_8_2_1_1: return w8_launch<8, 2, 1, 1, E, NORM>(a, wscale, xl, st);   \
+    case W8_4_4_1_1: return w8_launch<4, 4, 1, 1, E, NORM>(a, wscale, xl, st);   \
+    case W8_8_4_1_1: return w8_launch<8, 4, 1, 1, E, NORM>(a, wscale, xl, st);   \
+    case W8_4_2_2_1: return w8_launch<4, 2, 2, 1, E, NORM>(a, wscale, xl, st);   \
+    case W8_8_2_2_1: return w8_launch<8, 2, 2, 1, E, NORM>(a, wscale, xl, st);   \
+    case W8_4_2_4_1: return w8_launch<4, 2, 4, 1, E, NORM>(a, wscale, xl, st);   \
+    case W8_4_2_1_2: return w8_launch<4, 2, 1, 2, E, NORM>(a, wscale, xl, st);   \
+    case W8_4_8_1_1: return w8_launch<4, 8, 1, 1, E, NORM>(a, wscale, xl, st);   \
+    case W8_8_8_1_1: return w8_launch<8, 8, 1, 1, E, NORM>(a, wscale, xl, st);   \
+    case W8_4_4_2_1: return w8_launch<4, 4, 2, 1, E, NORM>(a, wscale, xl, st);   \
+    case W8_8_4_2_1: return w8_launch<8, 4, 2, 1, E, NORM>(a, wscale, xl, st);   \
+    default: return w8_launch<8, 2, 1, 2, E, NORM>(a, wscale, xl, st);           \
   }
   switch (epi) {
     case EPI_BF16: CAIN_W8_VAR(EPI_BF16)
@@ -253,16 +307,28 @@ CAIN_API int cain_gemm_w8(const void* Wp, const float* wscale, const void* X, in
   // 8 waves when there are few workgroups to spread over the CUs and enough k-pairs per wave, else 4
   int waves = (N / 16 / nt * a.msplit < 512 && K / 64 >= 64) ? 8 : 4;
   if (f_w) waves = f_w >= 8 ? 8 : 4;
-  const int u = (nb == 1 && nt == 1 && f_u >= 4) ? 4 : 2;
+  // activations staged in LDS (XL above): one row block, at most 64 KiB of rows.  CAIN_W8_XLDS=0 for A/B runs;
+  // measured single stream (same box, interleaved): llama3.1:8b 471.9 / 472.4 -> 478.5 / 479.9 tok/s, qwen2:1.5b
+  // 970.2 -> 982.1; gate/up 25.2 -> 23.9 us, QKV 9.5 -> 9.2 (profiles/r3/README.md).
+  static const int f_xl = env_int("CAIN_W8_XLDS", 1);
+  const bool xl = f_xl && nb == 1 && a.msplit == 1 && (long long)M * K * 2 <= 65536;
+  // pairs in flight per wave: with the activations in LDS the registers of the deeper weight prologue are free
+  // (U = 4: llama3.1:8b 480.7 -> 514.1 tok/s single stream); without, U = 4 measured no gain (w8_decode.md)
+  int u = (nb == 1 && f_u >= 4) ? (f_u >= 8 ? 8 : 4) : 2;
+  if (!f_u && xl) u = 4;
+  if (nt == 4 || (nt == 2 && u == 8)) u = std::min(u, nt == 4 ? 2 : 4);
   int var;
   if (nb == 2)
     var = waves == 8 ? W8_8_2_1_2 : W8_4_2_1_2;
   else if (nt == 4)
     var = W8_4_2_4_1;
   else if (nt == 2)
-    var = waves == 8 ? W8_8_2_2_1 : W8_4_2_2_1;
+    var = u == 4 ? (waves == 8 ? W8_8_4_2_1 : W8_4_4_2_1) : (waves == 8 ? W8_8_2_2_1 : W8_4_2_2_1);
+  else if (u == 8)
+    var = waves == 8 ? W8_8_8_1_1 : W8_4_8_1_1;
   else
     var = u == 4 ? (waves == 8 ? W8_8_4_1_1 : W8_4_4_1_1) : (waves == 8 ? W8_8_2_1_1 : W8_4_2_1_1);
-  const hipError_t e = norm ? w8_launch_e<true>(epi, var, a, wscale, st) : w8_launch_e<false>(epi, var, a, wscale, st);
+  const hipError_t e = norm ? w8_launch_e<true>(epi, var, a, wscale, xl, st)
+                            : w8_launch_e<false>(epi, var, a, wscale, xl, st);
   return int(e);
 }
