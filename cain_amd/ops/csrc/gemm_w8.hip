@@ -304,14 +304,22 @@ CAIN_API int cain_gemm_w8(const void* Wp, const float* wscale, const void* X, in
   int nt = nb == 2 ? 1 : (f_nt ? (f_nt >= 4 ? 4 : f_nt) : (N >= 65536 ? 2 : 1));
   if ((N / 16) % nt) nt = 1;
   a.msplit = (M + 16 * nb - 1) / (16 * nb);
-  // 8 waves when there are few workgroups to spread over the CUs and enough k-pairs per wave, else 4
-  int waves = (N / 16 / nt * a.msplit < 512 && K / 64 >= 64) ? 8 : 4;
-  if (f_w) waves = f_w >= 8 ? 8 : 4;
   // activations staged in LDS (XL above): one row block, at most 64 KiB of rows.  CAIN_W8_XLDS=0 for A/B runs;
   // measured single stream (same box, interleaved): llama3.1:8b 471.9 / 472.4 -> 478.5 / 479.9 tok/s, qwen2:1.5b
   // 970.2 -> 982.1; gate/up 25.2 -> 23.9 us, QKV 9.5 -> 9.2 (profiles/r3/README.md).
   static const int f_xl = env_int("CAIN_W8_XLDS", 1);
   const bool xl = f_xl && nb == 1 && a.msplit == 1 && (long long)M * K * 2 <= 65536;
+  // 8 waves when the grid is at most one workgroup per CU and there are enough k-pairs per wave, else 4.  (The
+  // bound was 512 workgroups; with XL + U = 4, llama3.1:8b's 384-workgroup QKV runs 8.9 -> 8.2 us on 4 waves
+  // while the 256-workgroup O / down stay faster on 8: 8.7 vs 9.9 us, profiles/r3/README.md.)
+  static const int n_cu = [] {
+    int dev = 0, n = 0;
+    (void)hipGetDevice(&dev);
+    return hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess ? n : 256;
+  }();
+  static const int f_wb = env_int("CAIN_W8_WAVE_BOUND", 0);  // A/B: the workgroup bound of the 8-wave rule
+  int waves = (N / 16 / nt * a.msplit <= (f_wb ? f_wb : xl ? n_cu : 511) && K / 64 >= 64) ? 8 : 4;
+  if (f_w) waves = f_w >= 8 ? 8 : 4;
   // pairs in flight per wave: with the activations in LDS the registers of the deeper weight prologue are free
   // (U = 4: llama3.1:8b 480.7 -> 514.1 tok/s single stream); without, U = 4 measured no gain (w8_decode.md)
   int u = (nb == 1 && f_u >= 4) ? (f_u >= 8 ? 8 : 4) : 2;
