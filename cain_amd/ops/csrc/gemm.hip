@@ -479,7 +479,18 @@ static int skinny_split(int N, int K, int M) {
 // Waves per workgroup: 8 (the tuned choice on every llama3.1:8b decode shape, profiles/gemm_tune.md)
 // unless the grid is small (then 16, to keep >= ~2k waves streaming) or K is too short to give each
 // wave two pipelined chunks.
-static int pick_waves(int n_wg, int ks) {
+static int pick_waves(int n_wg, int ks, bool split = false) {
+  // grids of (b, 2b] workgroups, b = the CU count, on 4 waves (CAIN_SKINNY_W4 = b overrides, 0 disables):
+  // llama3.1:8b's 384-workgroup QKV at one row 12.3 -> 11.9 us, single stream 340.7 -> 341.8 tok/s (same box,
+  // interleaved; qwen2:7b 356.2 -> 356.9; profiles/r3/b1_skinny_w4_ab.txt).  The fp8 kernel showed it first.
+  static const int w4 = [] {
+    const char* e = getenv("CAIN_SKINNY_W4");
+    if (e) return atoi(e);
+    int dev = 0, n = 0;
+    (void)hipGetDevice(&dev);
+    return hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess ? n : 0;
+  }();
+  if (!split && w4 > 0 && n_wg > w4 && n_wg <= 2 * w4 && ks / 4 >= 8) return 4;  // unsplit grids (measured)
   int w = 8;
   if (n_wg * w < 1024 && ks / 16 >= 8) w = 16;
   while (w > 4 && ks / w < 8) w /= 2;
@@ -500,7 +511,7 @@ static int gemm_dispatch(GemmArgs a, int epi, int norm, int waves, hipStream_t s
   const int nt = 1;
   a.msplit = (a.M + 15) / 16;
   const int n_wg = a.N / 16 * a.msplit * sk.ks;
-  if (waves <= 0) waves = pick_waves(n_wg, a.K / 32 / sk.ks);
+  if (waves <= 0) waves = pick_waves(n_wg, a.K / 32 / sk.ks, sk.ks > 1);
   while (waves > 4 && waves * nt * nb > 64) waves /= 2;  // LDS reduction buffer <= 64 KiB
   // 16-wave groups cap registers at 128/lane: the RoPE / norm-prologue / NB=4 bodies would spill
   if (waves > 8 && (epi == EPI_QKV_ROPE || norm || nb >= 4)) waves = 8;
