@@ -491,6 +491,12 @@ static int pick_waves(int n_wg, int ks, bool split = false) {
     return hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess ? n : 0;
   }();
   if (!split && w4 > 0 && n_wg > w4 && n_wg <= 2 * w4 && ks / 4 >= 8) return 4;  // unsplit grids (measured)
+  // A/B (CAIN_SKINNY_W16 = b): unsplit grids of <= b workgroups on 16 waves when every wave keeps >= 8 slices
+  static const int w16 = [] {
+    const char* e = getenv("CAIN_SKINNY_W16");
+    return e ? atoi(e) : 0;
+  }();
+  if (!split && w16 > 0 && n_wg <= w16 && ks / 16 >= 8) return 16;
   int w = 8;
   if (n_wg * w < 1024 && ks / 16 >= 8) w = 16;
   while (w > 4 && ks / w < 8) w /= 2;
