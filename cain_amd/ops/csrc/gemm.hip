@@ -490,7 +490,11 @@ static int pick_waves(int n_wg, int ks, bool split = false) {
     (void)hipGetDevice(&dev);
     return hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess ? n : 0;
   }();
-  if (!split && w4 > 0 && n_wg > w4 && n_wg <= 2 * w4 && ks / 4 >= 8) return 4;  // unsplit grids (measured)
+  static const int w4x = [] {  // upper bound, in multiples of b (CAIN_SKINNY_W4X; A/B)
+    const char* e = getenv("CAIN_SKINNY_W4X");
+    return e ? atoi(e) : 2;
+  }();
+  if (!split && w4 > 0 && n_wg > w4 && n_wg <= w4x * w4 && ks / 4 >= 8) return 4;  // unsplit grids (measured)
   // A/B (CAIN_SKINNY_W16 = b): unsplit grids of <= b workgroups on 16 waves when every wave keeps >= 8 slices
   static const int w16 = [] {
     const char* e = getenv("CAIN_SKINNY_W16");
