@@ -21,10 +21,12 @@ Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--model M] [--words 
        (multi-GPU: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ..., or plain
        ``python bench.py --gpus N``, which spawns the N ranks itself before anything touches a GPU)
 
-After the timed steps every rank also runs ONE trial alone (batch 1, the reference's one-request-at-a-time
-protocol) and the JSON reports it beside the batched number: ``single_stream_tok_per_s`` and
-``single_stream_J_per_token``, then the same trial on fp8 (e4m3 per-row) weights, the
-analogue of the reference's 4-bit Ollama models: ``single_stream_fp8_tok_per_s`` / ``_J_per_token``.
+After the timed steps and a ``--settle`` every rank also runs the reference's one-request-at-a-time protocol
+(batch 1; reference experiment/RunnerConfig.py:120-131): the median of ``--single-trials`` full-length
+generations, each in its own energy window, for the bench model on bf16 (``single_stream_tok_per_s`` /
+``single_stream_J_per_token``), fp8 e4m3 (``single_stream_fp8_*``) and MXFP4 weights (``single_stream_fp4_*``,
+the reference's 4-bit precision class: Ollama serves 4-bit builds), and for ``--single-models`` (default
+qwen2:1.5b, gemma:2b) on bf16 and MXFP4: ``single_stream_by_model`` with each cell's BASELINE.md numbers.
 """
 from __future__ import annotations
 
@@ -34,6 +36,7 @@ import json
 import math
 import os
 import socket
+import statistics
 import subprocess
 import sys
 import time
@@ -93,16 +96,19 @@ def main() -> int:
     ap.add_argument("--context", type=int, default=1536)
     ap.add_argument("--steps-per-graph", type=int, default=16)
     ap.add_argument("--no-energy", action="store_true")
-    ap.add_argument("--weights", choices=("bf16", "fp8"), default="bf16",
-                    help="GEMM weight storage: bf16 (headline) or fp8 e4m3 per-row scaled (W8A8 above 16 rows, W8A16 below)")
+    ap.add_argument("--weights", choices=("bf16", "fp8", "fp4"), default="bf16",
+                    help="GEMM weight storage: bf16 (headline), fp8 e4m3 per-row scaled (W8A8 above 16 rows, W8A16 "
+                         "below) or MXFP4 (W4A16, <= 64 rows)")
     ap.add_argument("--kv", choices=("bf16", "fp8"), default="bf16",
                     help="KV-cache storage: bf16 (headline) or fp8 e4m3 (half the attention bytes; separate config)")
     ap.add_argument("--device", choices=("cuda", "cpu"), default="cuda",
                     help="cpu: the torch oracle backend over gloo (tests of the multi-rank plumbing; tiny models)")
     ap.add_argument("--settle", type=float, default=8.0, help="seconds of rest before the idle-power baseline")
     ap.add_argument("--no-single", action="store_true", help="skip the batch-1 (single-stream) measurement")
-    ap.add_argument("--no-single-fp8", action="store_true",
-                    help="skip the fp8-weight batch-1 trial (the analogue of the reference's 4-bit Ollama models)")
+    ap.add_argument("--single-trials", type=int, default=3, help="batch-1 generations per (model, dtype); median")
+    ap.add_argument("--single-settle", type=float, default=1.0, help="seconds of rest before each batch-1 trial")
+    ap.add_argument("--single-models", default="qwen2:1.5b,gemma:2b",
+                    help="other models measured at batch 1 (bf16 and MXFP4 weights), comma-separated")
     ns = ap.parse_args()
 
     world_env = os.environ.get("WORLD_SIZE")
@@ -195,48 +201,59 @@ def main() -> int:
     dt = time.perf_counter() - t0
     reading = meter.stop() if meter else None
 
-    # batch-1 trial (outside the timed region): the reference's one-request-at-a-time protocol
-    ss_tps, ss_j = float("nan"), float("nan")
-    if not ns.no_single:
-        eng.generate(prompts(-7)[:1], min(n_tok, 32), [dict(opts, seed=7)])  # warm the batch-1 graphs
-        barrier()
-        if meter:
-            meter.start()
-        t1 = time.perf_counter()
-        r1 = eng.generate(prompts(-8)[:1], n_tok, [dict(opts, seed=8)])[0]
-        sync()
-        dt1 = time.perf_counter() - t1
-        rd1 = meter.stop() if meter else None
-        ss_tps = r1.eval_count / dt1
-        if rd1 is not None:
-            ss_j = rd1.gpu_energy_j / max(1, r1.eval_count)
+    # ---- batch 1, the reference's one-request-at-a-time protocol (outside the timed region): after a settle, the
+    # median of --single-trials generations of the full request length per (model, weight dtype), each with its
+    # own energy window; the bench model on bf16 / fp8 / MXFP4 weights (fp4: the reference's 4-bit precision class)
+    # and the --single-models on bf16 / fp4.
+    single = {}  # (model, dtype) -> (median tok/s, median J/token)
 
-    # the same batch-1 trial on fp8 (e4m3, per-row scaled) weights: the closest analogue of the reference's
-    # 4-bit quantised Ollama models (outside the timed region; a second engine of the same architecture)
-    f8_tps, f8_j = float("nan"), float("nan")
-    if not ns.no_single and not ns.no_single_fp8 and not cpu and ns.weights == "bf16":
-        try:
-            e8 = DecodeEngine(ns.model, device=dev, max_batch=1, max_context=ns.context, seed=1234 + rank,
-                              steps_per_graph=ns.steps_per_graph, weight_dtype="fp8", kv_dtype=ns.kv)
-            e8.generate(prompts(-7)[:1], min(n_tok, 32), [dict(opts, seed=7)])
+    def single_stream(model: str, dtype: str, engine=None):
+        own = engine is None
+        e1 = engine or DecodeEngine(model, device=dev, max_batch=1, max_context=ns.context, seed=1234 + rank,
+                                    steps_per_graph=ns.steps_per_graph, weight_dtype=dtype, kv_dtype=ns.kv)
+        e1.generate(prompts(-7)[:1], min(n_tok, 32), [dict(opts, seed=7)])  # warm the batch-1 graphs
+        rates, jpt = [], []
+        for t in range(ns.single_trials):
             barrier()
+            time.sleep(ns.single_settle)
             if meter:
                 meter.start()
-            t2 = time.perf_counter()
-            r2 = e8.generate(prompts(-8)[:1], n_tok, [dict(opts, seed=8)])[0]
+            t1 = time.perf_counter()
+            r1 = e1.generate(prompts(-8 - t)[:1], n_tok, [dict(opts, seed=8 + t)])[0]
             sync()
-            dt2 = time.perf_counter() - t2
-            rd2 = meter.stop() if meter else None
-            f8_tps = r2.eval_count / dt2
-            if rd2 is not None:
-                f8_j = rd2.gpu_energy_j / max(1, r2.eval_count)
-            e8.close()
-        except Exception as exc:  # auxiliary measurement
-            print(f"[bench] fp8 single stream unavailable: {exc}", file=sys.stderr)
+            dt1 = time.perf_counter() - t1
+            rd1 = meter.stop() if meter else None
+            rates.append(r1.eval_count / dt1)
+            jpt.append(rd1.gpu_energy_j / max(1, r1.eval_count) if rd1 is not None else float("nan"))
+        if own:
+            e1.close()
+            del e1
+            if not cpu:
+                torch.cuda.empty_cache()
+        progress(f"single stream {model} {dtype}: {statistics.median(rates):.1f} tok/s")
+        return statistics.median(rates), statistics.median(jpt)
 
+    cases = []
+    if not ns.no_single:
+        cases = [(ns.model, "bf16")]
+        if not cpu and ns.weights == "bf16":
+            cases += [(ns.model, "fp8"), (ns.model, "fp4")]
+            cases += [(m, dt) for m in filter(None, ns.single_models.split(",")) if m != ns.model
+                      for dt in ("bf16", "fp4")]
+        sync()
+        time.sleep(max(0.0, ns.settle))  # the board returns toward idle after the batched steps
+    for model, dtype in cases:
+        try:
+            single[(model, dtype)] = single_stream(model, dtype, eng if (model, dtype) == (ns.model, ns.weights) else None)
+        except Exception as exc:  # auxiliary measurement
+            print(f"[bench] single stream {model} {dtype} unavailable: {exc}", file=sys.stderr)
+            single[(model, dtype)] = (float("nan"), float("nan"))
+
+    flat = [v for c in cases for v in single[c]]
     vals = torch.tensor([dt, float(toks), reading.gpu_energy_j if reading else float("nan"),
                          reading.idle_subtracted_j if reading else float("nan"),
-                         reading.total_energy_j if reading else float("nan"), ss_tps, ss_j, f8_tps, f8_j],
+                         reading.total_energy_j if reading else float("nan"),
+                         meter.idle_power_w if meter and getattr(meter, "idle_power_w", None) else float("nan")] + flat,
                         dtype=torch.float64, device=dev)
     if world > 1:
         allv = [torch.zeros_like(vals) for _ in range(world)]
@@ -249,10 +266,14 @@ def main() -> int:
     energy = float(allv[:, 2].sum())
     energy_idle_sub = float(allv[:, 3].sum())
     energy_total = float(allv[:, 4].sum())
-    ss_tps_mean = float(allv[:, 5].mean())
-    ss_j_mean = float(allv[:, 6].mean())
-    f8_tps_mean = float(allv[:, 7].mean())
-    f8_j_mean = float(allv[:, 8].mean())
+    idle_w = float(allv[:, 5].mean())
+    ss = {c: (float(allv[:, 6 + 2 * i].mean()), float(allv[:, 7 + 2 * i].mean())) for i, c in enumerate(cases)}
+
+    def rnd(v, nd):
+        return None if math.isnan(v) else round(v, nd)
+
+    def ss_get(model, dtype, j):
+        return rnd(ss.get((model, dtype), (float("nan"), float("nan")))[j], 4 if j else 2)
     value = tokens / t_max
     base_tps, base_jpt = BASELINE.get((ns.model, ns.words), (None, None))
     if rank == 0:
@@ -268,6 +289,7 @@ def main() -> int:
             "scaling": "weak",
             "vs_baseline": round(value / base_tps, 2) if base_tps else None,
             "dtype": ("bf16" if ns.weights == "bf16" else
+                      "bf16 activations, MXFP4 (e2m1 + e8m0 block-32) weights" if ns.weights == "fp4" else
                       "fp8-e4m3 weights and per-row e4m3 GEMM activations (W8A8), bf16 elsewhere"
                       if getattr(eng, "w8a8", False) else "bf16 activations, fp8-e4m3 weights")
                      + (", fp8-e4m3 KV cache" if ns.kv == "fp8" else ""),
@@ -283,15 +305,26 @@ def main() -> int:
             "J_per_token_incl_host": (round(energy_total / tokens, 5) if not math.isnan(energy_total) else None),
             "host_energy_source": reading.cpu_energy_source if reading else None,
             "avg_gpu_power_W": round(energy / t_max / world, 1) if not math.isnan(energy) else None,
-            "single_stream_tok_per_s": round(ss_tps_mean, 2) if not math.isnan(ss_tps_mean) else None,
-            "single_stream_J_per_token": round(ss_j_mean, 4) if not math.isnan(ss_j_mean) else None,
-            "single_stream_fp8_tok_per_s": round(f8_tps_mean, 2) if not math.isnan(f8_tps_mean) else None,
-            "single_stream_fp8_J_per_token": round(f8_j_mean, 4) if not math.isnan(f8_j_mean) else None,
+            "idle_power_W": rnd(idle_w, 1),
+            "single_stream_trials": ns.single_trials,
+            "single_stream_tok_per_s": ss_get(ns.model, "bf16", 0),
+            "single_stream_J_per_token": ss_get(ns.model, "bf16", 1),
+            "single_stream_fp8_tok_per_s": ss_get(ns.model, "fp8", 0),
+            "single_stream_fp8_J_per_token": ss_get(ns.model, "fp8", 1),
+            "single_stream_fp4_tok_per_s": ss_get(ns.model, "fp4", 0),
+            "single_stream_fp4_J_per_token": ss_get(ns.model, "fp4", 1),
+            "single_stream_by_model": {
+                m: {dt: {"tok_per_s": ss_get(m, dt, 0), "J_per_token": ss_get(m, dt, 1)}
+                    for dt in ("bf16", "fp8", "fp4") if (m, dt) in ss}
+                | {"baseline": dict(zip(("tok_per_s", "J_per_token"), BASELINE.get((m, ns.words), (None, None))))}
+                for m in dict.fromkeys(c[0] for c in cases)},
             "baseline": {"tok_per_s": base_tps, "J_per_token": base_jpt, "hardware": "MacBook Pro M2 (est.)"},
             "vs_baseline_J_per_token": (round(base_jpt / (energy / tokens), 2)
                                         if base_jpt and not math.isnan(energy) and energy > 0 else None),
-            "single_stream_vs_baseline_J_per_token": (round(base_jpt / ss_j_mean, 3)
-                                                      if base_jpt and not math.isnan(ss_j_mean) else None),
+            "single_stream_vs_baseline_J_per_token": (round(base_jpt / ss_get(ns.model, "bf16", 1), 3)
+                                                      if base_jpt and ss_get(ns.model, "bf16", 1) else None),
+            "single_stream_fp4_vs_baseline_J_per_token": (round(base_jpt / ss_get(ns.model, "fp4", 1), 3)
+                                                          if base_jpt and ss_get(ns.model, "fp4", 1) else None),
             # wide-batch GEMM plans in use: N x K @ rows -> k-splits x ring variant (csrc/wgemm.hip)
             "wgemm_plans": {f"{t['n']}x{t['k']}@{t['m']}": f"{t['ks']}x{t['variant']}"
                             for t in getattr(eng, "wgemm_plans", [])},

@@ -3,13 +3,11 @@
 * ``cain_amd/ops/libcain_kernels.so`` — every HIP kernel + the decode runtime,
   compiled by ``hipcc --offload-arch=gfx950`` (cross-compiles without a GPU); no vendor
   GEMM library is linked;
-* ``cain_amd/ops/libcain_blas.so`` — OPT-IN (``--blas`` / ``CAIN_BUILD_BLAS=1``): the hipBLASLt
-  A/B path (``ops/csrc_blas/blas.hip``), registered with the runtime by ``ops.enable_lt()``;
 * ``cain_amd/energy/libcain_energy.so`` — the amd-smi sampler (g++).
 
 Both are plain C ABIs loaded with ctypes, so the build needs no torch headers
 (fast, seconds per file) and the same ``.so`` is what tests and the bench load.
-Usage: ``python -m cain_amd.build [--force] [--blas] [-v]``.
+Usage: ``python -m cain_amd.build [--force] [-v]``.
 """
 from __future__ import annotations
 
@@ -26,8 +24,6 @@ ROOT = Path(__file__).resolve().parent
 OPS = ROOT / "ops"
 CSRC = OPS / "csrc"
 KLIB = OPS / "libcain_kernels.so"
-BLAS_SRC = OPS / "csrc_blas" / "blas.hip"
-BLAS_LIB = OPS / "libcain_blas.so"
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 
@@ -89,29 +85,11 @@ def build_kernels(force: bool = False, verbose: bool = False, jobs: int = 0) -> 
     return KLIB
 
 
-def build_blas(force: bool = False, verbose: bool = False) -> Path:
-    """The opt-in hipBLASLt A/B library (not part of the default build or the headline path)."""
-    if not (force or _stale(BLAS_LIB, [BLAS_SRC] + _headers())):
-        return BLAS_LIB
-    tmp = str(BLAS_LIB) + ".tmp"
-    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", "-shared", f"-I{CSRC}", str(BLAS_SRC),
-           "-o", tmp, f"-L{ROCM}/lib", f"-Wl,-rpath,{ROCM}/lib", "-lhipblaslt"]
-    if verbose:
-        print(" ".join(cmd), flush=True)
-    r = subprocess.run(cmd, capture_output=True, text=True)
-    if r.returncode != 0:
-        raise RuntimeError(f"hipcc failed for {BLAS_SRC.name}:\n{r.stderr[-6000:]}")
-    os.replace(tmp, BLAS_LIB)
-    return BLAS_LIB
-
-
-def build_all(force: bool = False, verbose: bool = False, blas: bool = False) -> None:
+def build_all(force: bool = False, verbose: bool = False) -> None:
     from .energy import native as energy_native
 
     energy_native.build(force=force, verbose=verbose)
     build_kernels(force=force, verbose=verbose)
-    if blas or os.environ.get("CAIN_BUILD_BLAS", "0") == "1":
-        build_blas(force=force, verbose=verbose)
     if verbose:
         print(f"built {KLIB} and {energy_native.LIB}")
 
@@ -120,9 +98,8 @@ def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--force", action="store_true")
     ap.add_argument("-v", "--verbose", action="store_true")
-    ap.add_argument("--blas", action="store_true", help="also build the opt-in hipBLASLt A/B library")
     ns = ap.parse_args(argv)
-    build_all(force=ns.force, verbose=ns.verbose, blas=ns.blas)
+    build_all(force=ns.force, verbose=ns.verbose)
     return 0
 
 

@@ -37,14 +37,14 @@ import torch
 
 from ..models.config import ModelConfig, get_config, rope_inv_freq
 from ..models.tokenizer import SyntheticTokenizer, get_tokenizer
-from ..models.weights import ModelWeights, fp8_roundtrip_weights, pack_for_engine, random_weights
+from ..models.weights import WEIGHT_DTYPES, ModelWeights, pack_for_engine, random_weights, roundtrip_weights
 
 #: Ollama's default sampling options (SURVEY §2.4 "Sampling" row)
 OLLAMA_DEFAULTS = dict(temperature=0.8, top_k=40, top_p=0.9, repeat_penalty=1.1, repeat_last_n=64, seed=None)
 
 MAX_ROWS = 256  # rows per forward: decode batch (runtime.hip CAIN_MAX_ROWS)
 PREFILL_ROWS = 128  # prompt tokens per prefill forward
-W8_MAX_ROWS = 64  # W8A16 fp8-weight kernels (gemm_w8.hip): rows per forward when W8A8 is off
+W8_MAX_ROWS = 64  # few-row fp8 / MXFP4 weight kernels (gemm_w8.hip / gemm_w4.hip): rows per forward without W8A8
 W8A8_MIN_ROWS = 16  # fp8 engines run forwards of more rows on the W8A8 wide kernel (csrc/wgemm8.hip)
 
 
@@ -101,26 +101,13 @@ def _row_options(opts: Optional[Dict], cfg: ModelConfig, index: int, base_seed: 
                 seed=int(seed) & 0xFFFFFFFFFFFFFFFF)
 
 
-LT_WS_BYTES = 64 << 20  # hipBLASLt workspace of the wide-batch path
-
-
-def lt_min_rows(max_batch: int, weight_dtype: str = "bf16") -> int:
-    """Row count from which a forward runs its O and gate/up projections on hipBLASLt (0: never, the default).
-
-    Off by default since the hand-written wide-batch kernel (csrc/wgemm.hip) took over 64 < M <= 256
-    (profiles/wgemm_r2.md); ``CAIN_LT_MIN_ROWS=128`` brings the library path back for A/B runs, which loads the
-    opt-in ``libcain_blas.so`` (``python -m cain_amd.build --blas``; the default library links no vendor GEMM).
-    The fp8 weight path has no library equivalent."""
-    v = int(os.environ.get("CAIN_LT_MIN_ROWS", "0"))
-    if v <= 0 or weight_dtype != "bf16" or max_batch < v:
-        return 0
-    return v
-
-
 # ============================================================== ctypes structs
+LAYER_FIELDS = ("wqkv", "bqkv", "wo", "wgu", "wdown", "sqkv", "so", "sgu", "sdown", "wqkv8", "wo8", "wgu8", "wdown8")
+WFMT = {"bf16": 0, "fp8": 1, "fp4": 2}  # runtime.hip WFMT_*
+
+
 class _CainLayer(ctypes.Structure):
-    _fields_ = [(n, ctypes.c_void_p) for n in ("wqkv", "bqkv", "wo", "wgu", "wdown", "sqkv", "so", "sgu", "sdown",
-                                                  "wo_lt", "wgu_lt", "wqkv8", "wo8", "wgu8", "wdown8")]
+    _fields_ = [(n, ctypes.c_void_p) for n in LAYER_FIELDS]
 
 
 class _CainPlanDesc(ctypes.Structure):
@@ -131,9 +118,7 @@ class _CainPlanDesc(ctypes.Structure):
                 + [("kv_layer_elems", ctypes.c_longlong)]
                 + [(n, ctypes.c_void_p) for n in ("cos_t", "sin_t", "x", "q", "attn", "act", "logits",
                                                  "part_o", "part_ml", "counters", "gemm_ws")]
-                + [("gemm_ws_bytes", ctypes.c_longlong), ("w8", ctypes.c_int), ("lm_head_scale", ctypes.c_void_p)]
-                + [("lt_min_rows", ctypes.c_int), ("gu", ctypes.c_void_p), ("lt_ws", ctypes.c_void_p),
-                   ("lt_ws_bytes", ctypes.c_longlong), ("lm_head_lt", ctypes.c_void_p), ("xn", ctypes.c_void_p)]
+                + [("gemm_ws_bytes", ctypes.c_longlong), ("wfmt", ctypes.c_int), ("lm_head_scale", ctypes.c_void_p)]
                 + [("kv8", ctypes.c_int), ("lm_head8", ctypes.c_void_p), ("x8", ctypes.c_void_p),
                    ("xs", ctypes.c_void_p), ("x8_ld", ctypes.c_int)])
 
@@ -181,11 +166,16 @@ class DecodeEngine:
         forwards of up to 16 rows run W8A16 (gemm_w8.hip, bf16 activations), wider ones W8A8 (wgemm8.hip: the
         activations quantised per row to e4m3, fp8 MFMA) up to 256 rows; CAIN_W8A8=0 keeps W8A16 only (<= 64
         rows).
+        ``weight_dtype="fp4"``: OCP MXFP4 GEMM weights (e2m1, one e8m0 scale per 32 k; 0.53 bytes per parameter),
+        the reference's 4-bit precision class: W4A16 few-row kernels (gemm_w4.hip), up to 64 rows per forward;
+        every GEMM K (d_model, q_dim, ffn) must be a multiple of 128.
         ``kv_dtype="fp8"``: the KV cache holds e4m3 elements (half the attention bytes per decode step and half
         the cache memory; csrc/attention.hip KV8)."""
         self.cfg = get_config(model) if isinstance(model, str) else model
-        if weight_dtype not in ("bf16", "fp8"):
-            raise ValueError(f"weight_dtype must be 'bf16' or 'fp8', got {weight_dtype!r}")
+        if weight_dtype not in WEIGHT_DTYPES:
+            raise ValueError(f"weight_dtype must be one of {WEIGHT_DTYPES}, got {weight_dtype!r}")
+        if weight_dtype == "fp4" and any(k % 128 for k in (self.cfg.d_model, self.cfg.q_dim, self.cfg.ffn)):
+            raise ValueError(f"weight_dtype='fp4' needs d_model, q_dim and ffn to be multiples of 128 ({self.cfg.name})")
         if kv_dtype not in ("bf16", "fp8"):
             raise ValueError(f"kv_dtype must be 'bf16' or 'fp8', got {kv_dtype!r}")
         self.weight_dtype = weight_dtype
@@ -193,7 +183,7 @@ class DecodeEngine:
         # W8A8 needs whole 128-deep stages, >= 4 of them, on every GEMM's K (all real configs; not the tiny ones)
         self.w8a8 = (weight_dtype == "fp8" and os.environ.get("CAIN_W8A8", "1") != "0"
                      and all(k % 128 == 0 and k >= 512 for k in (self.cfg.d_model, self.cfg.q_dim, self.cfg.ffn)))
-        row_cap = W8_MAX_ROWS if weight_dtype == "fp8" and not self.w8a8 else MAX_ROWS
+        row_cap = W8_MAX_ROWS if weight_dtype == "fp4" or (weight_dtype == "fp8" and not self.w8a8) else MAX_ROWS
         self.device = torch.device(device)
         if backend is None:
             backend = "hip" if self.device.type == "cuda" else "torch"
@@ -216,8 +206,8 @@ class DecodeEngine:
             self._init_hip()
         elif backend == "torch":
             from ..models.reference import ReferenceModel
-            # fp8: the oracle runs on the dequantised weights the fp8 kernels multiply by
-            ref_w = fp8_roundtrip_weights(weights) if weight_dtype == "fp8" else weights
+            # fp8 / fp4: the oracle runs on the dequantised weights the kernels multiply by
+            ref_w = roundtrip_weights(weights, weight_dtype)
             self.ref = ReferenceModel(ref_w, memo_weights=self.device.type == "cpu", kv_dtype=kv_dtype)
         else:
             raise ValueError(f"unknown backend {backend!r}")
@@ -235,16 +225,9 @@ class DecodeEngine:
         cfg, dev = self.cfg, self.device
         if self.device.type != "cuda":
             raise ValueError("hip backend needs a GPU device")
-        # O and gate/up projections of forwards with >= lt_rows rows go through hipBLASLt (ops/csrc/blas.hip:
-        # 23 vs 39 us and 66 vs 103 us at 256 rows on llama3.1:8b, profiles/lt_gemm.md); it needs plain
-        # row-major copies of those two weights beside the MFMA packing
-        lt_rows = lt_min_rows(self.max_batch, self.weight_dtype)
-        if lt_rows > 0:
-            ops.enable_lt()  # the opt-in hipBLASLt library (A/B runs only; csrc_blas/blas.hip)
         w8a8 = self.w8a8 and max(self.max_batch, self.prefill_chunk) > W8A8_MIN_ROWS
         packed = pack_for_engine(self.weights, free_natural=not self.keep_natural, weight_dtype=self.weight_dtype,
-                                 plain_lt=lt_rows > 0, w8a8=w8a8,
-                                 plain_lm_head=lt_rows > 0 and os.environ.get("CAIN_LT_LM_HEAD", "1") != "0")
+                                 w8a8=w8a8)
         torch.cuda.synchronize(dev)
         S, T, L = self.max_batch, self.T_max, cfg.n_layers
         bf = torch.bfloat16
@@ -277,9 +260,7 @@ class DecodeEngine:
             dev)
         self._layers = (_CainLayer * L)()
         for i, lp in enumerate(packed["layers"]):
-            self._layers[i] = _CainLayer(*(_ptr(lp.get(k)) for k in ("wqkv", "bqkv", "wo", "wgu", "wdown",
-                                                                     "sqkv", "so", "sgu", "sdown", "wo_lt",
-                                                                     "wgu_lt", "wqkv8", "wo8", "wgu8", "wdown8")))
+            self._layers[i] = _CainLayer(*(_ptr(lp.get(k)) for k in LAYER_FIELDS))
         self._packed = packed
         d = _CainPlanDesc()
         d.n_layers, d.d, d.H, d.Hkv, d.hd = L, cfg.d_model, cfg.n_heads, cfg.n_kv_heads, cfg.head_dim
@@ -311,16 +292,7 @@ class DecodeEngine:
             d.lm_head8, d.x8, d.xs, d.x8_ld = _ptr(packed.get("lm_head8")), _ptr(self.x8), _ptr(self.xs), kmax
         self.gemm_ws = torch.zeros(max(ws, 16) // 4 + 1, device=dev, dtype=torch.int32)
         d.gemm_ws, d.gemm_ws_bytes = _ptr(self.gemm_ws), ws
-        d.w8, d.lm_head_scale = int(self.weight_dtype == "fp8"), _ptr(packed.get("lm_head_scale"))
-        d.lt_min_rows = lt_rows
-        if lt_rows > 0:
-            self.gu = z(R, 2 * cfg.ffn)
-            self.lt_ws = torch.zeros(LT_WS_BYTES // 4, device=dev, dtype=torch.int32)
-            d.gu, d.lt_ws, d.lt_ws_bytes = _ptr(self.gu), _ptr(self.lt_ws), LT_WS_BYTES
-            if packed.get("lm_head_lt") is not None:
-                # LM head on hipBLASLt too (~300 vs ~400 us at 256 rows on llama3.1:8b, profiles/lt_gemm.md)
-                self.xn = z(R, cfg.d_model)
-                d.lm_head_lt, d.xn = _ptr(packed["lm_head_lt"]), _ptr(self.xn)
+        d.wfmt, d.lm_head_scale = WFMT[self.weight_dtype], _ptr(packed.get("lm_head_scale"))
         self._desc = d
         self._plans: Dict[int, int] = {}
         self._graphs: Dict[tuple, int] = {}

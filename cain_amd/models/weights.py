@@ -24,6 +24,11 @@ Two layouts:
   ``ops/csrc/gemm_w8.hip`` (``pack_mfma_a_fp8``).  The reference's models are
   4-bit GGUF quantisations served by Ollama; fp8 is the gfx950
   native narrow weight type.
+* **packed MXFP4** (``weight_dtype="fp4"``, the reference's 4-bit precision
+  class) — e2m1 elements with one e8m0 scale per 32 k of a row
+  (``quantize_mxfp4``), bytes laid out ``[N/16][K/128][64 lanes][16]`` plus
+  scale bytes ``[N/16][K/128][64]`` for ``ops/csrc/gemm_w4.hip``
+  (``pack_mxfp4``).
 """
 from __future__ import annotations
 
@@ -99,6 +104,82 @@ def unpack_mfma_a_fp8(p: torch.Tensor) -> torch.Tensor:
     nt, kp = p.shape[0], p.shape[1]
     t = p.reshape(nt, kp, 4, 16, 2, 8).permute(0, 3, 1, 4, 2, 5)   # [t, r, p, h, g, j]
     return t.contiguous().reshape(nt * 16, kp * 64).view(torch.float8_e4m3fn)
+
+
+#: e2m1 magnitudes by 3-bit code (OCP MX: sign bit 3, 2 exponent bits, 1 mantissa bit)
+E2M1_VALUES = (0.0, 0.5, 1.0, 1.5, 2.0, 3.0, 4.0, 6.0)
+_E2M1_BOUNDS = (0.25, 0.75, 1.25, 1.75, 2.5, 3.5, 5.0)  # round-to-nearest decision points between the magnitudes
+MX_BLOCK = 32
+
+
+def quantize_mxfp4(w: torch.Tensor):
+    """OCP MXFP4 quantisation along K: (codes uint8 [N, K] in 0..15, e8m0 scale bytes uint8 [N, K/32]).
+
+    Each 32-element block of a row shares a power-of-two scale 2^e, stored biased (e + 127, clamped to e >= -126
+    so the decoded scale is a normal fp32).  Per block the scale is the better (smaller squared error) of
+    e0 = ceil(log2(amax / 6)) -- the block's largest magnitude lands in (3, 6], nothing saturates -- and e0 - 1,
+    which resolves the small elements twice as finely and saturates the largest at 6 (chosen for ~1/3 of Gaussian
+    blocks: 11.8 -> 11.1 % relative error).  Elements round to the nearest e2m1 value of w / 2^e."""
+    n, k = w.shape
+    if k % MX_BLOCK:
+        raise ValueError(f"quantize_mxfp4 needs K % {MX_BLOCK} == 0, got {tuple(w.shape)}")
+    wf = w.float().reshape(n, k // MX_BLOCK, MX_BLOCK)
+    amax = wf.abs().amax(dim=2)
+    e0 = torch.ceil(torch.log2(amax / 6.0))
+    e0 = torch.where(amax > 0, e0, torch.full_like(e0, -126.0)).clamp(-126, 127)
+    bounds = torch.tensor(_E2M1_BOUNDS, device=w.device, dtype=torch.float32)
+    vals = torch.tensor(E2M1_VALUES, device=w.device, dtype=torch.float32)
+
+    def rnd(e):
+        sc = torch.exp2(e)[..., None]
+        y = wf / sc
+        mag = torch.bucketize(y.abs().clamp(max=6.0), bounds)
+        err = ((vals[mag] * sc - y.abs() * sc) ** 2).sum(dim=2)
+        return mag.to(torch.uint8) | ((y < 0).to(torch.uint8) << 3), err
+
+    c0, err0 = rnd(e0)
+    e1 = (e0 - 1).clamp(-126, 127)
+    c1, err1 = rnd(e1)
+    pick = err1 < err0
+    codes = torch.where(pick[..., None], c1, c0)
+    e = torch.where(pick, e1, e0)
+    return codes.reshape(n, k).contiguous(), (e + 127).to(torch.uint8).contiguous()
+
+
+def dequantize_mxfp4(codes: torch.Tensor, scales: torch.Tensor) -> torch.Tensor:
+    """fp32 [N, K] values of ``quantize_mxfp4``'s output (exactly representable in bf16)."""
+    n, k = codes.shape
+    vals = torch.tensor(E2M1_VALUES, device=codes.device, dtype=torch.float32)
+    c = codes.long()
+    v = vals[c & 7] * torch.where((c & 8) != 0, -1.0, 1.0)
+    sc = torch.exp2(scales.float() - 127.0)
+    return (v.reshape(n, k // MX_BLOCK, MX_BLOCK) * sc[..., None]).reshape(n, k)
+
+
+def pack_mxfp4(codes: torch.Tensor, scales: torch.Tensor):
+    """MXFP4 codes [N, K] + e8m0 scales [N, K/32] -> the few-row kernel's layout (ops/csrc/gemm_w4.hip):
+    (wq uint8 [N/16, K/128, 64, 16], ws uint8 [N/16, K/128, 64]).  Lane l = 16g + r of quad p holds row 16t + r,
+    k = 128p + 32g + 8s + 2b + h at byte 4s + b, nibble h (0 low) -- one whole scale block per lane -- and
+    ws[t, p, l] is that block's scale byte."""
+    n, k = codes.shape
+    if n % 16 or k % 128:
+        raise ValueError(f"pack_mxfp4 needs N%16==0 and K%128==0, got {tuple(codes.shape)}")
+    t = codes.reshape(n // 16, 16, k // 128, 4, 4, 4, 2)              # [t, r, p, g, s, b, h]
+    t = t.permute(0, 2, 3, 1, 4, 5, 6)                                  # [t, p, g, r, s, b, h]
+    byte = t[..., 0] | (t[..., 1] << 4)
+    wq = byte.contiguous().reshape(n // 16, k // 128, 64, 16)
+    s = scales.reshape(n // 16, 16, k // 128, 4).permute(0, 2, 3, 1)  # [t, p, g, r]
+    return wq, s.contiguous().reshape(n // 16, k // 128, 64)
+
+
+def unpack_mxfp4(wq: torch.Tensor, ws: torch.Tensor):
+    """Inverse of ``pack_mxfp4``: (codes [N, K], scales [N, K/32])."""
+    nt, kq = wq.shape[0], wq.shape[1]
+    lo, hi = wq & 15, wq >> 4
+    t = torch.stack([lo, hi], dim=-1).reshape(nt, kq, 4, 16, 4, 4, 2)  # [t, p, g, r, s, b, h]
+    codes = t.permute(0, 3, 1, 2, 4, 5, 6).contiguous().reshape(nt * 16, kq * 128)
+    s = ws.reshape(nt, kq, 4, 16).permute(0, 3, 1, 2).contiguous().reshape(nt * 16, kq * 4)
+    return codes, s
 
 
 def rope_pair_order(hd: int) -> torch.Tensor:
@@ -205,22 +286,52 @@ def fp8_roundtrip_weights(mw: ModelWeights) -> ModelWeights:
     return ModelWeights(mw.cfg, mw.embed, mw.final_norm, rt(mw.lm_head), layers)
 
 
+def mxfp4_roundtrip_weights(mw: ModelWeights) -> ModelWeights:
+    """Copy of ``mw`` whose GEMM weights are dequant(quant_mxfp4(W)) in bf16 (LM head untied from the embedding
+    table, which the engine keeps in bf16): the torch oracle of a ``weight_dtype="fp4"`` engine.  The RMSNorm
+    gains stay separate here while the engine quantises W diag(g); with the unit gains of random init the two
+    are the same matrix."""
+    def rt(w):
+        return dequantize_mxfp4(*quantize_mxfp4(w)).to(w.dtype)
+
+    layers = [LayerWeights(attn_norm=lw.attn_norm, wqkv=rt(lw.wqkv), bqkv=lw.bqkv, wo=rt(lw.wo), mlp_norm=lw.mlp_norm,
+                           w_gate=rt(lw.w_gate), w_up=rt(lw.w_up), w_down=rt(lw.w_down)) for lw in mw.layers]
+    return ModelWeights(mw.cfg, mw.embed, mw.final_norm, rt(mw.lm_head), layers)
+
+
+def roundtrip_weights(mw: ModelWeights, weight_dtype: str) -> ModelWeights:
+    """The weights a ``weight_dtype`` engine multiplies by, for the torch oracle."""
+    if weight_dtype == "fp8":
+        return fp8_roundtrip_weights(mw)
+    if weight_dtype == "fp4":
+        return mxfp4_roundtrip_weights(mw)
+    return mw
+
+
+WEIGHT_DTYPES = ("bf16", "fp8", "fp4")
+
+
 def pack_for_engine(mw: ModelWeights, free_natural: bool = False, weight_dtype: str = "bf16",
-                    plain_lt: bool = False, plain_lm_head: bool = False, w8a8: bool = False) -> Dict[str, object]:
+                    w8a8: bool = False) -> Dict[str, object]:
     """Build the decode engine's packed tensors (see module doc); norm gains are folded into the GEMM
     weights they feed (attn_norm -> wqkv, mlp_norm -> gate/up, final_norm -> lm_head).
 
     ``weight_dtype="fp8"``: every GEMM weight (LM head included) is quantised per row after the gain
     fold; each matrix entry becomes the fp8 packing and its scales are stored under ``s<name>``.  With
-    ``w8a8`` the same e4m3 bytes are also stored in the W8A8 wide kernel's packing under ``<name>8``."""
-    if weight_dtype not in ("bf16", "fp8"):
-        raise ValueError(f"weight_dtype must be 'bf16' or 'fp8', got {weight_dtype!r}")
+    ``w8a8`` the same e4m3 bytes are also stored in the W8A8 wide kernel's packing under ``<name>8``.
+    ``weight_dtype="fp4"``: MXFP4 (``quantize_mxfp4``), the ``pack_mxfp4`` bytes under ``<name>`` and the e8m0
+    scale bytes under ``s<name>``."""
+    if weight_dtype not in WEIGHT_DTYPES:
+        raise ValueError(f"weight_dtype must be one of {WEIGHT_DTYPES}, got {weight_dtype!r}")
     cfg = mw.cfg
     fp8 = weight_dtype == "fp8"
+    fp4 = weight_dtype == "fp4"
     perm = qkv_row_permutation(cfg).to(mw.device)
 
     def put(dst: Dict[str, object], name: str, w: torch.Tensor) -> None:
-        if fp8:
+        if fp4:
+            dst[name], dst["s" + name[1:]] = pack_mxfp4(*quantize_mxfp4(w))
+        elif fp8:
             q, sc = quantize_fp8_rows(w)
             dst[name], dst["s" + name[1:]] = pack_mfma_a_fp8(q), sc
             if w8a8:
@@ -237,8 +348,6 @@ def pack_for_engine(mw: ModelWeights, free_natural: bool = False, weight_dtype: 
         put(lp, "wo", lw.wo)
         wgu = interleave_tiles(fold_gain(lw.w_gate, gm), fold_gain(lw.w_up, gm), tile=8)
         put(lp, "wgu", wgu)
-        if plain_lt and not fp8:
-            lp["wo_lt"], lp["wgu_lt"] = lw.wo.contiguous(), wgu.contiguous()
         put(lp, "wdown", lw.w_down)
         layers.append(lp)
         if free_natural:
@@ -246,11 +355,9 @@ def pack_for_engine(mw: ModelWeights, free_natural: bool = False, weight_dtype: 
     packed: Dict[str, object] = {"layers": layers, "weight_dtype": weight_dtype}
     lm = fold_gain(mw.lm_head, effective_gain(cfg, mw.final_norm))
     put(packed, "wlm_head", lm)
-    if plain_lm_head and not fp8:
-        packed["lm_head_lt"] = lm.contiguous()  # plain row-major copy for the hipBLASLt LM head (blas.hip)
     del lm
     packed["lm_head"] = packed.pop("wlm_head")
-    if fp8:
+    if fp8 or fp4:
         packed["lm_head_scale"] = packed.pop("slm_head")
         if w8a8:
             packed["lm_head8"] = packed.pop("wlm_head8")

@@ -14,8 +14,9 @@ op                     source                      replaces (Ollama/llama.cpp)
                        csrc/wgemm.hip              fused RMSNorm, residual epilogue (wgemm: the
                                                    LDS-DMA ring kernel for 64 < M <= 256 rows)
 ``qkv_rope``           csrc/gemm.hip               QKV GEMV + bias + RoPE + KV-cache append
-``lt_gemm``            csrc_blas/blas.hip          hipBLASLt GEMM (opt-in libcain_blas.so, A/B runs only)
-``rownorm_act``        csrc_blas/blas.hip          RMSNorm scale + SiLU/GeLU*up after lt_gemm (opt-in)
+``gemm_w8``            csrc/gemm_w8.hip            the same GEMMs on fp8 (e4m3) weights, <= 64 rows
+``gemm_w8a8``          csrc/wgemm8.hip             fp8 weights x per-row fp8 activations, 16 < M <= 256
+``gemm_w4``            csrc/gemm_w4.hip            the same GEMMs on MXFP4 (e2m1 + e8m0) weights, <= 64 rows
 ``rmsnorm``            csrc/norm.hip               RMSNorm (standalone; the engine fuses it)
 ``embed``              csrc/norm.hip               embedding gather (+Gemma scale)
 ``attention``          csrc/attention.hip          decode / prefill attention (split-K, in-kernel combine)
@@ -74,6 +75,10 @@ def load() -> ctypes.CDLL:
                                   + [ci] * 4 + [vp, ctypes.c_longlong, ci, ci, vp])
         lib.cain_gemm_w8.argtypes = ([vp, vp, vp, ci, ci, ci, ci, vp, ci, vp, ci, cf, vp, vp, vp, vp, vp, vp]
                                      + [ci] * 5 + [vp])
+        lib.cain_gemm_w4.argtypes = ([vp, vp, vp, ci, ci, ci, ci, vp, ci, vp, ci, cf, vp, vp, vp, vp, vp, vp]
+                                     + [ci] * 5 + [vp])
+        lib.cain_gemm_w4_set_variant.argtypes = [ci]
+        lib.cain_gemm_w4_variant.argtypes = [ci, ci, ci]
         lib.cain_gemm_w8a8.argtypes = ([vp, vp, vp, ci, vp, ci, ci, ci, vp, ci, vp, vp, vp, vp, vp, vp, vp]
                                        + [ci] * 4 + [vp, ctypes.c_longlong, ci, vp])
         lib.cain_quant_rows.argtypes = [vp, ci, ci, ci, vp, ci, vp, ci, cf, vp]
@@ -86,15 +91,12 @@ def load() -> ctypes.CDLL:
         lib.cain_wgemm_eligible.argtypes = [ci, ci, ci]
         lib.cain_wgemm_set_shape.argtypes = [ci, ci, ci, ci, ci]
         lib.cain_wgemm_plan.argtypes = [ci, ci, ci]
-        lib.cain_set_lt_api.argtypes = [vp]
         lib.cain_rmsnorm.argtypes = [vp, ci, vp, vp, ci, ci, ci, cf, vp]
         lib.cain_embed.argtypes = [vp, vp, vp, ci, ci, ci, cf, vp]
         lib.cain_attention.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp, ci, ci, ci, ci, ci, ci, ci, cf, vp]
         lib.cain_attention_ex.argtypes = ([vp, vp, vp, vp, vp, vp, vp, vp, vp, ci, ci, ci, ci, ci, ci, ci, cf, ci, cf, cf]
                                           + [vp])
-        lib.cain_front_eligible.argtypes = [ci] * 8
         lib.cain_attention_set_ring.argtypes = [ci]
-        lib.cain_front.argtypes = ([vp] * 12 + [ci] * 6 + [cf, ci, vp, vp, vp, ci, cf, vp, vp, vp])
         lib.cain_sample.argtypes = [vp, ci, ci, vp, vp, vp, ci, vp, vp, vp, vp, vp, ci, ci, vp, vp]
         lib.cain_sample_cm.argtypes = [vp, ci, ci, vp, vp, vp, vp, ci, vp, vp, vp, vp, vp, ci, ci, vp, vp]
         lib.cain_sample_set_cm.argtypes = [ci]
@@ -276,6 +278,46 @@ def gemm_w8(wq: torch.Tensor, scale: torch.Tensor, x: torch.Tensor, n: int, epi:
     return out
 
 
+def gemm_w4(wq: torch.Tensor, wsc: torch.Tensor, x: torch.Tensor, n: int, epi: int = EPI_BF16, bias=None,
+            out: Optional[torch.Tensor] = None, norm: bool = False, eps: float = 1e-6, rope=None) -> torch.Tensor:
+    """MXFP4-weight GEMM (``csrc/gemm_w4.hip``, M <= 64): y = epi(B(x) @ dequant(codes, scales)^T) with
+    (``wq``, ``wsc``) = ``models.weights.pack_mxfp4(...)``.  Same epilogues, RMSNorm fusion and ``rope`` arguments
+    as ``gemm_w8``."""
+    lib = load()
+    _gpu(wq, wsc, x)
+    M, K = x.shape
+    assert x.dtype == torch.bfloat16 and x.stride(1) == 1 and 1 <= M <= 64
+    assert wq.dtype == torch.uint8 and wq.shape[0] * 16 == n and wq.shape[1] * 128 == K, (tuple(wq.shape), K, n)
+    assert wsc.dtype == torch.uint8 and wsc.numel() * 32 == n * K
+    n_out = n // 2 if epi in (EPI_SILU, EPI_GELU) else n
+    if epi == EPI_RESID:
+        assert out is not None and out.shape == (M, n_out), "EPI_RESID updates `out` (the residual) in place"
+    if out is None:
+        out = torch.empty(M, n_out, device=x.device, dtype=torch.float32 if epi == EPI_F32 else torch.bfloat16)
+    r = rope or {}
+    if epi == EPI_QKV_ROPE:
+        assert rope is not None, "EPI_QKV_ROPE needs the rope/cache arguments"
+    T_max = r["kc"].shape[-2] if rope else 0
+    if rope and is_fp8_cache(r["kc"]):
+        epi |= EPI_KV_FP8
+    rc = lib.cain_gemm_w4(_p(wq), _p(wsc), _p(x), x.stride(0), K, n, M, _p(out), out.stride(0), _p(bias),
+                          int(bool(norm)), eps, _p(r.get("slot")), _p(r.get("pos")), _p(r.get("cos_t")),
+                          _p(r.get("sin_t")), _p(r.get("kc")), _p(r.get("vtc")), r.get("H", 0), r.get("Hkv", 0),
+                          r.get("hd", 0), T_max, epi, _stream())
+    _check(rc, "gemm_w4")
+    return out
+
+
+def set_w4_variant(v: int) -> None:
+    """Force the few-row MXFP4 kernel shape (gemm_w4.hip W4Var index; -1: the shape rule).  Tests / tuning."""
+    load().cain_gemm_w4_set_variant(int(v))
+
+
+def w4_variant(n: int, k: int, m: int) -> int:
+    """The W4Var index the shape rule picks for an (N, K, M) problem."""
+    return int(load().cain_gemm_w4_variant(int(n), int(k), int(m)))
+
+
 def quant_rows(x: torch.Tensor, norm: bool = False, eps: float = 1e-6):
     """Per-row e4m3 quantisation of bf16 activations (csrc/wgemm8.hip quant_rows_kernel): returns (x8 uint8
     [M, K], xs fp32 [M]) with x ~= e4m3(x8) * amax/448 and xs = amax/448 * (rsqrt(mean(x^2) + eps) if norm)."""
@@ -448,38 +490,6 @@ def set_attention_ring(variant: int) -> None:
     load().cain_attention_set_ring(int(variant))
 
 
-def front_eligible(M: int, d: int, H: int, Hkv: int, hd: int, nsplit: int, kv8: bool = False) -> bool:
-    return bool(load().cain_front_eligible(M, d, H * hd, hd, H, Hkv, nsplit, int(kv8)))
-
-
-def layer_front(wqkv, bqkv, wo, x, q, attn, kc, vtc, slot, pos, cos_t, sin_t, H, Hkv, hd, nsplit, scale,
-                eps: float = 1e-6, norm: bool = True, part_o=None, part_ml=None, counters=None, flags=None,
-                trace=None) -> None:
-    """QKV (+RMSNorm, bias, RoPE, KV append) -> attention -> O (+residual) of one layer in ONE launch
-    (csrc/front.hip; <= 4 rows, bf16 caches, ``front_eligible``).  Same operands as ``qkv_rope`` ->
-    ``attention`` -> ``skinny_gemm(EPI_RESID)``: ``x`` [M, d] is the residual stream (updated in place), ``q`` /
-    ``attn`` [M, H*hd] the intermediate buffers.  ``counters`` / ``flags`` must be zero (they are again after).
-    ``trace``: optional int64 [grid, 4] per-workgroup timestamps (10 ns ticks: start, wait begin, wait end, end;
-    workgroups [0, n_qkv) QKV, then M*Hkv*nsplit attention, then d/16 O)."""
-    lib = load()
-    _gpu(wqkv, wo, x, q, attn, kc, vtc)
-    M, d = x.shape
-    T_max = kc.shape[-2]
-    assert not is_fp8_cache(kc) and x.dtype == torch.bfloat16 and x.stride(0) == d and q.stride(0) == H * hd
-    assert attn.stride(0) == H * hd and front_eligible(M, d, H, Hkv, hd, nsplit), (M, d, H, Hkv, hd, nsplit)
-    if part_o is None:
-        part_o = torch.empty(M * H * nsplit * hd, device=x.device, dtype=torch.float32)
-        part_ml = torch.empty(attention_ml_floats(M, H, Hkv, nsplit), device=x.device, dtype=torch.float32)
-    if counters is None:
-        counters = torch.zeros(M * Hkv, device=x.device, dtype=torch.int32)
-    if flags is None:
-        flags = torch.zeros(4096, device=x.device, dtype=torch.int32)
-    _check(lib.cain_front(_p(wqkv), _p(bqkv), _p(wo), _p(x), _p(q), _p(attn), _p(kc), _p(vtc), _p(slot), _p(pos),
-                          _p(cos_t), _p(sin_t), M, d, H, Hkv, hd, T_max, eps, int(bool(norm)), _p(part_o),
-                          _p(part_ml), _p(counters), nsplit, scale, _p(flags), _p(trace), _stream()),
-           "layer_front")
-
-
 SAMPLE_DTYPE = [("temperature", "f4"), ("top_p", "f4"), ("repeat_penalty", "f4"), ("top_k", "i4"),
                 ("repeat_last_n", "i4"), ("eos_id", "i4"), ("seed", "u8")]
 
@@ -529,76 +539,3 @@ def _sample_ws(device, nbytes: int) -> torch.Tensor:
     if t is None or t.numel() * 4 < nbytes:
         t = _SAMPLE_WS[device] = torch.zeros((nbytes + 3) // 4, device=device, dtype=torch.int32)
     return t
-
-
-_LT_WS: dict = {}
-BLAS_LIB_PATH = HERE / "libcain_blas.so"
-_blas: Optional[ctypes.CDLL] = None
-
-
-def load_blas() -> ctypes.CDLL:
-    """The opt-in hipBLASLt A/B library (``python -m cain_amd.build --blas``); the default build has none."""
-    global _blas
-    with _lock:
-        if _blas is not None:
-            return _blas
-        if not BLAS_LIB_PATH.exists():
-            if os.environ.get("CAIN_AUTOBUILD", "1") != "0":
-                from .. import build
-                build.build_blas()
-            if not BLAS_LIB_PATH.exists():
-                raise NativeOpsUnavailable(f"{BLAS_LIB_PATH} missing: `python -m cain_amd.build --blas` (opt-in)")
-        lib = ctypes.CDLL(str(BLAS_LIB_PATH))
-        lib.cain_lt_gemm.argtypes = [vp, vp, ci, ci, ci, ci, vp, ci, ci, vp, ctypes.c_longlong, vp]
-        lib.cain_lt_prepare.argtypes = [ci, ci, ci, ci, ci, ci, ctypes.c_longlong]
-        lib.cain_rownorm_act.argtypes = [vp, ci, ci, cf, ci, vp, ci, vp, ci, ci, ci, ci, vp]
-        _blas = lib
-        return lib
-
-
-class _LtApi(ctypes.Structure):
-    _fields_ = [(n, ctypes.c_void_p) for n in ("gemm", "prepare", "gemm_f32", "prepare_f32", "rownorm",
-                                                "rownorm_act")]
-
-
-def enable_lt() -> None:
-    """Register the hipBLASLt entries with the decode runtime (runtime.hip cain_set_lt_api): forwards with
-    >= CAIN_LT_MIN_ROWS rows then run O and gate/up on the library (A/B runs against the hand kernels)."""
-    blas = load_blas()
-    fp = lambda f: ctypes.cast(f, ctypes.c_void_p).value  # noqa: E731
-    api = _LtApi(fp(blas.cain_lt_gemm), fp(blas.cain_lt_prepare), fp(blas.cain_lt_gemm_f32),
-                 fp(blas.cain_lt_prepare_f32), fp(blas.cain_rownorm), fp(blas.cain_rownorm_act))
-    load().cain_set_lt_api(ctypes.byref(api))
-
-
-def lt_gemm(w: torch.Tensor, x: torch.Tensor, out: Optional[torch.Tensor] = None,
-            accumulate: bool = False) -> torch.Tensor:
-    """``out = x @ w.T`` (``out += x @ w.T`` with ``accumulate``) on hipBLASLt: w [N, K], x [M, K] bf16
-    row-major, on the opt-in library (csrc_blas/blas.hip, ``load_blas``)."""
-    _gpu(w, x, out)
-    N, K = w.shape
-    M = x.shape[0]
-    if out is None:
-        out = torch.empty(M, N, device=x.device, dtype=torch.bfloat16)
-    assert w.is_contiguous() and x.stride(1) == 1 and out.stride(1) == 1 and x.shape[1] == K
-    ws = _LT_WS.get(x.device)
-    if ws is None:
-        ws = _LT_WS[x.device] = torch.zeros((64 << 20) // 4, device=x.device, dtype=torch.int32)
-    _check(load_blas().cain_lt_gemm(_p(w), _p(x), x.stride(0), K, N, M, _p(out), out.stride(0), int(accumulate), _p(ws),
-                               ws.numel() * 4, _stream()), "cain_lt_gemm")
-    return out
-
-
-def rownorm_act(x: torch.Tensor, gu: torch.Tensor, eps: float, kind: int = 0, norm: bool = True,
-                out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """``act = f(s*gate) * (s*up)`` from an 8-row-interleaved gate/up GEMM output ``gu`` [M, 2 ffn]
-    (s = rsqrt(mean(x^2) + eps) per row when ``norm``; kind 0 SiLU, 1 tanh-GeLU)."""
-    _gpu(x, gu, out)
-    M, d = x.shape
-    ffn = gu.shape[1] // 2
-    if out is None:
-        out = torch.empty(M, ffn, device=x.device, dtype=torch.bfloat16)
-    assert x.stride(1) == 1 and gu.stride(1) == 1 and out.stride(1) == 1 and gu.shape[0] == M
-    _check(load_blas().cain_rownorm_act(_p(x), x.stride(0), d, eps, int(norm), _p(gu), gu.stride(0), _p(out),
-                                   out.stride(0), M, ffn, kind, _stream()), "cain_rownorm_act")
-    return out

@@ -7,7 +7,7 @@
 // prompt token, each with its own cache slot and position):
 //
 //   embed -> L x [QKV GEMM(+RMSNorm, +bias, RoPE, KV append)
-//                 -> attention(+split combine) -> O GEMM(+residual)      (CAIN_FRONT=1, <= 4 bf16 rows: ONE launch)
+//                 -> attention(+split combine) -> O GEMM(+residual)
 //                 -> gate/up GEMM(+RMSNorm, act*mul) -> down GEMM(+residual)]
 //                 -> LM-head GEMM(+RMSNorm) -> sample
 //
@@ -32,6 +32,10 @@ CAIN_API int cain_gemm_w8(const void* Wp, const float* wscale, const void* X, in
                           int ldy, const float* bias, int norm, float eps, const int* slot, const int* pos,
                           const float* cos_t, const float* sin_t, void* kc, void* vtc, int H, int Hkv, int hd,
                           int T_max, int epi, hipStream_t st);
+CAIN_API int cain_gemm_w4(const void* Wp, const void* wsc, const void* X, int ldx, int K, int N, int M, void* Y, int ldy,
+                          const float* bias, int norm, float eps, const int* slot, const int* pos, const float* cos_t,
+                          const float* sin_t, void* kc, void* vtc, int H, int Hkv, int hd, int T_max, int epi_flags,
+                          hipStream_t st);
 CAIN_API int cain_gemm_w8a8(const void* Wp8, const float* wscale, const void* X8, int ld8, const float* xs, int K,
                             int N, int M, void* Y, int ldy, const float* bias, const int* slot, const int* pos,
                             const float* cos_t, const float* sin_t, void* kc, void* vtc, int H, int Hkv, int hd,
@@ -58,31 +62,14 @@ CAIN_API int cain_sample_cm(float* logits, int ldl, int V, const float* cmax, in
                             const void* params, hipStream_t st);
 CAIN_API void cain_gemm_set_cmax(float* cmax);
 CAIN_API int cain_gemm_cmax_take();
-CAIN_API int cain_front_eligible(int M, int d, int q_dim, int hd, int H, int Hkv, int nsplit, int kv8);
-CAIN_API int cain_front(const void* wqkv, const float* bqkv, const void* wo, void* x, void* q, void* attn,
-                        void* kc, void* vtc, const int* slot, const int* pos, const float* cos_t, const float* sin_t,
-                        int M, int d, int H, int Hkv, int hd, int T_max, float eps, int norm, float* part_o,
-                        float* part_ml, unsigned* att_ctr, int nsplit, float scale, unsigned* flags,
-                        unsigned long long* trace, hipStream_t st);
 CAIN_API int cain_sample_ex(float* logits, int ldl, int V, int* tok, int* pos, int* gen, int ldg, int* n_gen,
                             const int* max_new, int* done, int* hist, const int* slot, int T_max, int M,
                             const void* params, void* ws, long long ws_bytes, hipStream_t st);
 
-// hipBLASLt A/B path (opt-in library libcain_blas.so, csrc_blas/blas.hip): not linked into this library; its
-// entry points are registered at run time by cain_amd.ops.enable_lt().  Unregistered (the default), every
-// forward runs the hand-written kernels.
-struct CainLtApi {
-  int (*gemm)(const void*, const void*, int, int, int, int, void*, int, int, void*, long long, hipStream_t);
-  int (*prepare)(int, int, int, int, int, int, long long);
-  int (*gemm_f32)(const void*, const void*, int, int, int, int, float*, int, void*, long long, hipStream_t);
-  int (*prepare_f32)(int, int, int, int, int, long long);
-  int (*rownorm)(const void*, int, int, float, void*, int, int, hipStream_t);
-  int (*rownorm_act)(const void*, int, int, float, int, const void*, int, void*, int, int, int, int, hipStream_t);
-};
-static CainLtApi g_lt{};
-CAIN_API void cain_set_lt_api(const CainLtApi* a) { g_lt = a ? *a : CainLtApi{}; }
-
 extern "C" {
+
+// weight storage of a plan (CainPlanDesc::wfmt)
+enum { WFMT_BF16 = 0, WFMT_FP8 = 1, WFMT_FP4 = 2 };
 
 // RMSNorm gains are folded into the weight columns of the GEMM each norm feeds (attn_norm -> wqkv,
 // mlp_norm -> wgu, final_norm -> lm_head; models/weights.py fold_gain), so a norm is just a flag here.
@@ -92,15 +79,12 @@ struct CainLayer {
   const void* wo;
   const void* wgu;
   const void* wdown;
-  // fp8 weights (CainPlanDesc::w8): per-output-row scales of each packed matrix (null for bf16)
-  const float* sqkv;
-  const float* so;
-  const float* sgu;
-  const float* sdown;
-  // plain row-major bf16 copies for the hipBLASLt path (blas.hip; null: fused kernels only): Wo [d, q_dim] and
-  // the 8-row-interleaved gate/up [2 ffn, d]
-  const void* wo_lt;
-  const void* wgu_lt;
+  // scales of each packed matrix (null for bf16): fp8 -- fp32 per output row; fp4 -- e8m0 bytes per 32-k block in
+  // the kernel's lane order (models/weights.py pack_mxfp4)
+  const void* sqkv;
+  const void* so;
+  const void* sgu;
+  const void* sdown;
   // fp8 weights in the W8A8 wide kernel's packing (wgemm8.hip; null: W8A16 only), same scales as above
   const void* wqkv8;
   const void* wo8;
@@ -129,22 +113,14 @@ struct CainPlanDesc {
   unsigned* counters;
   void* gemm_ws;  // batched-GEMM workspace (counters zeroed once + split-K partials), see gemm.hip
   long long gemm_ws_bytes;
-  int w8;                      // 1: fp8 (e4m3) weights with per-row scales, W8A16 kernels (gemm_w8.hip), M <= 64
-  const float* lm_head_scale;  // w8: scales of the packed LM head
-  // forwards with >= lt_min_rows rows (0: never) run the O and gate/up projections through hipBLASLt
-  // (blas.hip); gu: [Mpad, 2 ffn] bf16 gate/up output, lt_ws: the library's workspace
-  int lt_min_rows;
-  void* gu;
-  void* lt_ws;
-  long long lt_ws_bytes;
-  // wide forwards with lm_head_lt set run the final RMSNorm (rownorm into xn [Mpad, d] bf16) and the LM head
-  // (plain row-major [V, d] bf16, gain folded, fp32 logits) through hipBLASLt; the hand GEMM is the fallback
-  const void* lm_head_lt;
-  void* xn;
+  // WFMT_FP8: e4m3 weights with per-row scales, W8A16 kernels (gemm_w8.hip) up to 64 rows (W8A8 above 16 rows
+  // when the <name>8 packings are present); WFMT_FP4: MXFP4 weights, W4A16 kernels (gemm_w4.hip), up to 64 rows
+  int wfmt;
+  const void* lm_head_scale;  // fp8 / fp4: scales of the packed LM head
   // 1: the KV caches hold fp8 e4m3 elements (same fragment-major offsets, one byte each, unscaled and
   // saturated at +-448): the QKV epilogue writes them (gemm_epi.h EPI_KV_FP8), attention widens them
   int kv8;
-  // W8A8 (w8 with the <name>8 packings): forwards of more than 16 rows quantise each GEMM input per row into
+  // W8A8 (fp8 with the <name>8 packings): forwards of more than 16 rows quantise each GEMM input per row into
   // x8 [Mpad][x8_ld] e4m3 + xs [Mpad] (wgemm8.hip quant_rows_kernel) and run the fp8-MFMA wide kernel
   const void* lm_head8;
   void* x8;
@@ -176,13 +152,10 @@ struct Plan {
   // two-stage sampler workspace (sample.hip cain_sample_ex) for decode forwards of <= 64 rows, zeroed once
   void* sample_ws = nullptr;
   long long sample_ws_bytes = 0;
-  // layer-front launch (front.hip) hand-off counters for forwards of <= 4 rows, zeroed once (null: never used)
-  unsigned* front_flags = nullptr;
   // LM-head chunk maxima ([Mpad][V / 16] floats; sample.hip sample_cm_kernel)
   float* cmax = nullptr;
   ~Plan() {
     if (sample_ws) (void)hipFree(sample_ws);
-    if (front_flags) (void)hipFree(front_flags);
     if (cmax) (void)hipFree(cmax);
   }
 };
@@ -199,30 +172,10 @@ thread_local char g_fail[160] = {0};
     }                                                                            \
   } while (0)
 
-// CAIN_FRONT=1: the fused layer front (front.hip) instead of the three launches QKV / attention / O.  Off by
-// default: in the graph-replayed batch-1 decode it measured 16.9 vs 14.9 us per layer (qwen2:1.5b) and 28.7 vs
-// 25.8 (llama3.1:8b) -- its in-launch hand-offs cost more than the two kernel boundaries they remove
-// (profiles/r3/front_trace_*.log, profiles/r3/README.md).
-bool front_enabled() {
-  static const bool on = [] {
-    const char* e = getenv("CAIN_FRONT");
-    return e && e[0] == '1';
-  }();
-  return on;
-}
-
-bool lt_rows(const CainPlanDesc& d, int M) { return g_lt.gemm && d.lt_min_rows > 0 && M >= d.lt_min_rows && !d.w8 && d.gu; }
-
-// hipBLASLt heuristics allocate and synchronise: resolve them before a stream capture
-int lt_prepare(const Plan& p, int M) {
-  const CainPlanDesc& d = p.d;
-  if (!lt_rows(d, M) || p.layers.empty()) return 0;
-  const int q_dim = d.H * d.hd;
-  if (p.layers[0].wo_lt) CK(g_lt.prepare(d.d, q_dim, M, q_dim, d.d, 1, d.lt_ws_bytes));
-  if (p.layers[0].wgu_lt) CK(g_lt.prepare(2 * d.ffn, d.d, M, d.d, 2 * d.ffn, 0, d.lt_ws_bytes));
-  // no library algorithm for the fp32-output LM head is not an error: forward() falls back to the hand GEMM
-  if (d.lm_head_lt && d.xn) (void)g_lt.prepare_f32(d.V, d.d, M, d.d, d.V, d.lt_ws_bytes);
-  return 0;
+// rows a forward of this plan may have: 64 for the few-row-only weight formats
+int max_rows(const CainPlanDesc& d) {
+  if (d.wfmt == WFMT_FP4 || (d.wfmt == WFMT_FP8 && !d.x8)) return d.Mpad < 64 ? d.Mpad : 64;
+  return d.Mpad < CAIN_MAX_ROWS ? d.Mpad : CAIN_MAX_ROWS;
 }
 
 // 5 launches per layer: QKV(+RMSNorm, bias, RoPE, KV append) -> attention(+combine) ->
@@ -232,77 +185,58 @@ int forward(const Plan& p, int M, const CainRows& r, int want_logits, int want_s
   const int qkv_dim = (d.H + 2 * d.Hkv) * d.hd;
   const int q_dim = d.H * d.hd;
   const int epi_act = d.act_kind == 1 ? 4 : 3;
-  // one GEMM of the schedule: the bf16 kernels (gemm.hip) or the fp8-weight ones (gemm_w8.hip)
-  auto gemm = [&](const void* W, const void* W8, const float* ws, const void* X, int ldx, int K, int N, void* Y,
+  // one GEMM of the schedule: the bf16 kernels (gemm.hip / wgemm.hip), fp8 weights (gemm_w8.hip / wgemm8.hip) or
+  // MXFP4 weights (gemm_w4.hip)
+  auto gemm = [&](const void* W, const void* W8, const void* ws, const void* X, int ldx, int K, int N, void* Y,
                   int ldy, const float* bias, int norm, const void* kc, const void* vc, int epi) -> int {
-    if (d.w8 && W8 && d.x8 && cain_w8a8_eligible(N, K, M)) {  // W8A8: per-row fp8 activations, fp8 MFMA
+    void* kcm = const_cast<void*>(kc);
+    void* vcm = const_cast<void*>(vc);
+    if (d.wfmt == WFMT_FP4)
+      return cain_gemm_w4(W, ws, X, ldx, K, N, M, Y, ldy, bias, norm, d.eps, r.slot, r.pos, d.cos_t, d.sin_t, kcm, vcm,
+                          d.H, d.Hkv, d.hd, d.T_max, epi, st);
+    const float* wsf = static_cast<const float*>(ws);
+    if (d.wfmt == WFMT_FP8 && W8 && d.x8 && cain_w8a8_eligible(N, K, M)) {  // W8A8: per-row fp8 activations
       CK(cain_quant_rows(X, ldx, K, M, d.x8, d.x8_ld, d.xs, norm, d.eps, st));
-      return cain_gemm_w8a8(W8, ws, d.x8, d.x8_ld, d.xs, K, N, M, Y, ldy, bias, r.slot, r.pos, d.cos_t, d.sin_t,
-                            const_cast<void*>(kc), const_cast<void*>(vc), d.H, d.Hkv, d.hd, d.T_max, d.gemm_ws,
-                            d.gemm_ws_bytes, epi, st);
+      return cain_gemm_w8a8(W8, wsf, d.x8, d.x8_ld, d.xs, K, N, M, Y, ldy, bias, r.slot, r.pos, d.cos_t, d.sin_t, kcm,
+                            vcm, d.H, d.Hkv, d.hd, d.T_max, d.gemm_ws, d.gemm_ws_bytes, epi, st);
     }
-    if (d.w8)
-      return cain_gemm_w8(W, ws, X, ldx, K, N, M, Y, ldy, bias, norm, d.eps, r.slot, r.pos, d.cos_t, d.sin_t,
-                          const_cast<void*>(kc), const_cast<void*>(vc), d.H, d.Hkv, d.hd, d.T_max, epi, st);
-    return cain_gemm(W, X, ldx, K, N, M, Y, ldy, bias, norm, d.eps, r.slot, r.pos, d.cos_t, d.sin_t,
-                     const_cast<void*>(kc), const_cast<void*>(vc), d.H, d.Hkv, d.hd, d.T_max, d.gemm_ws,
-                     d.gemm_ws_bytes, epi, d.waves, st);
+    if (d.wfmt == WFMT_FP8)
+      return cain_gemm_w8(W, wsf, X, ldx, K, N, M, Y, ldy, bias, norm, d.eps, r.slot, r.pos, d.cos_t, d.sin_t, kcm, vcm,
+                          d.H, d.Hkv, d.hd, d.T_max, epi, st);
+    return cain_gemm(W, X, ldx, K, N, M, Y, ldy, bias, norm, d.eps, r.slot, r.pos, d.cos_t, d.sin_t, kcm, vcm, d.H,
+                     d.Hkv, d.hd, d.T_max, d.gemm_ws, d.gemm_ws_bytes, epi, d.waves, st);
   };
-  const bool lt = lt_rows(d, M);
-  // few-row bf16 forwards: QKV -> attention -> O of a layer as ONE launch (front.hip)
-  const bool front = p.front_flags && !d.w8 && !lt && front_enabled() &&
-                     cain_front_eligible(M, d.d, q_dim, d.hd, d.H, d.Hkv, d.nsplit, d.kv8);
   CK(cain_embed(r.tok, d.embed, d.x, d.d, M, d.d, d.embed_scale, st));
   for (int l = 0; l < d.n_layers; ++l) {
     const CainLayer& L = p.layers[l];
     const size_t kv_off = (size_t)l * d.kv_layer_elems * (d.kv8 ? 1 : 2);  // bytes
     char* kc = static_cast<char*>(d.kcache) + kv_off;
     char* vc = static_cast<char*>(d.vtcache) + kv_off;
-    if (front) {
-      CK(cain_front(L.wqkv, L.bqkv, L.wo, d.x, d.q, d.attn, kc, vc, r.slot, r.pos, d.cos_t, d.sin_t, M, d.d, d.H,
-                    d.Hkv, d.hd, d.T_max, d.eps, 1, d.part_o, d.part_ml, d.counters, d.nsplit, d.attn_scale,
-                    p.front_flags, nullptr, st));
-    } else {
-      CK(gemm(L.wqkv, L.wqkv8, L.sqkv, d.x, d.d, d.d, qkv_dim, d.q, q_dim, L.bqkv, 1, kc, vc,
-              /*EPI_QKV_ROPE*/ 5 | (d.kv8 ? /*EPI_KV_FP8*/ 0x100 : 0)));
-      CK(cain_attention_ex(d.q, kc, vc, r.slot, r.pos, d.part_o, d.part_ml, d.counters, d.attn, q_dim, M, d.H,
-                           d.Hkv, d.hd, d.T_max, d.nsplit, d.attn_scale, d.kv8, 1.f, 1.f, st));
-    }
-    if (!front) {  // (the front launch ran the O projection too)
-      if (lt && L.wo_lt)
-        CK(g_lt.gemm(L.wo_lt, d.attn, q_dim, q_dim, d.d, M, d.x, d.d, 1, d.lt_ws, d.lt_ws_bytes, st));
-      else
-        CK(gemm(L.wo, L.wo8, L.so, d.attn, q_dim, q_dim, d.d, d.x, d.d, nullptr, 0, nullptr, nullptr,
-                /*EPI_RESID*/ 1));
-    }
-    if (lt && L.wgu_lt) {
-      CK(g_lt.gemm(L.wgu_lt, d.x, d.d, d.d, 2 * d.ffn, M, d.gu, 2 * d.ffn, 0, d.lt_ws, d.lt_ws_bytes, st));
-      CK(g_lt.rownorm_act(d.x, d.d, d.d, d.eps, 1, d.gu, 2 * d.ffn, d.act, d.ffn, M, d.ffn, d.act_kind, st));
-    } else {
-      CK(gemm(L.wgu, L.wgu8, L.sgu, d.x, d.d, d.d, 2 * d.ffn, d.act, d.ffn, nullptr, 1, nullptr, nullptr, epi_act));
-    }
+    CK(gemm(L.wqkv, L.wqkv8, L.sqkv, d.x, d.d, d.d, qkv_dim, d.q, q_dim, L.bqkv, 1, kc, vc,
+            /*EPI_QKV_ROPE*/ 5 | (d.kv8 ? /*EPI_KV_FP8*/ 0x100 : 0)));
+    CK(cain_attention_ex(d.q, kc, vc, r.slot, r.pos, d.part_o, d.part_ml, d.counters, d.attn, q_dim, M, d.H, d.Hkv,
+                         d.hd, d.T_max, d.nsplit, d.attn_scale, d.kv8, 1.f, 1.f, st));
+    CK(gemm(L.wo, L.wo8, L.so, d.attn, q_dim, q_dim, d.d, d.x, d.d, nullptr, 0, nullptr, nullptr, /*EPI_RESID*/ 1));
+    CK(gemm(L.wgu, L.wgu8, L.sgu, d.x, d.d, d.d, 2 * d.ffn, d.act, d.ffn, nullptr, 1, nullptr, nullptr, epi_act));
     CK(gemm(L.wdown, L.wdown8, L.sdown, d.act, d.ffn, d.ffn, d.d, d.x, d.d, nullptr, 0, nullptr, nullptr,
             /*EPI_RESID*/ 1));
   }
   if (want_logits) {
-    int e = -2;
-    if (lt && d.lm_head_lt && d.xn) {
-      CK(g_lt.rownorm(d.x, d.d, d.d, d.eps, d.xn, d.d, M, st));
-      e = g_lt.gemm_f32(d.lm_head_lt, d.xn, d.d, d.d, d.V, M, d.logits, d.V, d.lt_ws, d.lt_ws_bytes, st);
-      if (e > 0) CK(e);  // a library failure; no plan / unsupported shape (< 0) falls back
-    }
-    // the LM head also writes the chunk maxima the chunk-max sampler starts from (skinny or wide kernel)
+    // the LM head also writes the chunk maxima the chunk-max sampler starts from (skinny or wide bf16 kernel)
     const int cm_mode = cain_sample_cm_enabled();
-    if (e != 0 && p.cmax && (cm_mode == 1 || (cm_mode == 2 && M > 64))) cain_gemm_set_cmax(p.cmax);
-    if (e != 0) CK(gemm(d.lm_head, d.lm_head8, d.lm_head_scale, d.x, d.d, d.d, d.V, d.logits, d.V, nullptr, 1, nullptr,
-                        nullptr, /*EPI_F32*/ 2));
+    if (p.cmax && (cm_mode == 1 || (cm_mode == 2 && M > 64))) cain_gemm_set_cmax(p.cmax);
+    CK(gemm(d.lm_head, d.lm_head8, d.lm_head_scale, d.x, d.d, d.d, d.V, d.logits, d.V, nullptr, 1, nullptr, nullptr,
+            /*EPI_F32*/ 2));
   }
   const bool cm = want_logits && cain_gemm_cmax_take();
   if (want_sample) {
-    if (cm)
-      CK(cain_sample_cm(d.logits, d.V, d.V, p.cmax, r.tok, r.pos, r.gen, r.ldg, r.n_gen, r.max_new, r.done, r.hist,
-                        r.slot, d.T_max, M, r.sample_params, st));
-    else
+    // the chunk-max sampler refuses (< 0) vocabularies beyond its chunk capacity: the two-stage / one-workgroup
+    // kernels take those
+    const int e = cm ? cain_sample_cm(d.logits, d.V, d.V, p.cmax, r.tok, r.pos, r.gen, r.ldg, r.n_gen, r.max_new,
+                                      r.done, r.hist, r.slot, d.T_max, M, r.sample_params, st)
+                     : -1;
+    if (e > 0) CK(e);
+    if (e < 0)
       CK(cain_sample_ex(d.logits, d.V, d.V, r.tok, r.pos, r.gen, r.ldg, r.n_gen, r.max_new, r.done, r.hist, r.slot,
                         d.T_max, M, r.sample_params, p.sample_ws, p.sample_ws_bytes, st));
   }
@@ -328,17 +262,9 @@ CAIN_API void* cain_plan_create(const CainPlanDesc* desc) {
       p->sample_ws = nullptr;  // the one-workgroup sampler needs no workspace
     }
   }
-  if (!desc->w8 && desc->V % 64 == 0 && desc->Mpad > 0) {  // LM-head chunk maxima ([Mpad][V / 16])
-    const int rows = desc->Mpad;
-    if (hipMalloc(&p->cmax, (size_t)rows * (desc->V / 16) * sizeof(float)) != hipSuccess) p->cmax = nullptr;
-  }
-  if (!desc->w8 && hipMalloc(&p->front_flags, 4096 * 4) == hipSuccess) {  // front.hip: 4096 flag words
-    if (hipMemset(p->front_flags, 0, 4096 * 4) != hipSuccess) {
-      (void)hipFree(p->front_flags);
-      p->front_flags = nullptr;
-    }
-  } else {
-    p->front_flags = nullptr;
+  // LM-head chunk maxima ([Mpad][V / 16]): bf16 weights only (the kernels that write them)
+  if (desc->wfmt == WFMT_BF16 && desc->V % 64 == 0 && desc->Mpad > 0) {
+    if (hipMalloc(&p->cmax, (size_t)desc->Mpad * (desc->V / 16) * sizeof(float)) != hipSuccess) p->cmax = nullptr;
   }
   return p;
 }
@@ -351,8 +277,7 @@ CAIN_API int cain_plan_forward(void* plan, int M, const CainRows* rows, int want
                                hipStream_t st) {
   auto* p = static_cast<Plan*>(plan);
   g_fail[0] = 0;
-  // W8A16 alone (no W8A8 buffers) takes at most 64 rows
-  if (M < 1 || M > CAIN_MAX_ROWS || M > p->d.Mpad || (p->d.w8 && !p->d.x8 && M > 64)) return -1;
+  if (M < 1 || M > max_rows(p->d)) return -1;
   return forward(*p, M, *rows, want_logits, want_sample, st);
 }
 
@@ -360,11 +285,10 @@ CAIN_API int cain_plan_forward(void* plan, int M, const CainRows* rows, int want
 CAIN_API void* cain_plan_capture(void* plan, int M, const CainRows* rows, int steps, hipStream_t st, int* err) {
   auto* p = static_cast<Plan*>(plan);
   *err = 0;
-  if (M < 1 || M > CAIN_MAX_ROWS || M > p->d.Mpad || (p->d.w8 && !p->d.x8 && M > 64) || steps < 1) {
+  if (M < 1 || M > max_rows(p->d) || steps < 1) {
     *err = -1;
     return nullptr;
   }
-  if ((*err = lt_prepare(*p, M)) != 0) return nullptr;
   hipGraph_t g = nullptr;
   hipError_t e = hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal);
   if (e != hipSuccess) {

@@ -575,7 +575,7 @@ def main(argv: Optional[List[str]] = None) -> None:
     ap.add_argument("--fake-tok-s", type=float, default=2000.0, help="fake backend: modelled decode rate")
     ap.add_argument("--fake-prefill-s", type=float, default=0.0, help="fake backend: modelled time to first token")
     ap.add_argument("--trace-dir", default=None, help="write a torch.profiler Chrome trace of every decode batch here")
-    ap.add_argument("--weights", choices=["bf16", "fp8"], default="bf16",
+    ap.add_argument("--weights", choices=["bf16", "fp8", "fp4"], default="bf16",
                     help="GEMM weight storage (fp8: e4m3 per-row scaled; W8A8 above 16 rows, W8A16 below)")
     ap.add_argument("--kv", choices=["bf16", "fp8"], default="bf16", help="KV-cache storage (fp8: e4m3)")
     ap.add_argument("--static-batching", action="store_true",
@@ -610,7 +610,7 @@ def generate_main(argv: Optional[List[str]] = None) -> None:
     ap.add_argument("--device", default="cuda:0")
     ap.add_argument("--temperature", type=float, default=None)
     ap.add_argument("--seed", type=int, default=None)
-    ap.add_argument("--weights", choices=["bf16", "fp8"], default="bf16")
+    ap.add_argument("--weights", choices=["bf16", "fp8", "fp4"], default="bf16")
     ap.add_argument("--kv", choices=["bf16", "fp8"], default="bf16")
     ns = ap.parse_args(argv)
     be = EngineBackend([ns.model], device=ns.device, max_batch=1, weight_dtype=ns.weights, kv_dtype=ns.kv)

@@ -20,7 +20,7 @@ if not torch.cuda.is_available():  # pragma: no cover
 from cain_amd.engine import DecodeEngine  # noqa: E402
 from cain_amd.models.config import MODELS  # noqa: E402
 from cain_amd.models.reference import ReferenceModel  # noqa: E402
-from cain_amd.models.weights import fp8_roundtrip_weights  # noqa: E402
+from cain_amd.models.weights import fp8_roundtrip_weights, mxfp4_roundtrip_weights  # noqa: E402
 from numerics import assert_within_eager, eager_bf16, rel  # noqa: E402
 
 TOPICS = ["India", "World War II", "Elizabeth II", "United States", "Cristiano Ronaldo", "The Beatles",
@@ -74,6 +74,22 @@ def test_fullsize_fp8_weights_match_dequantised_oracle(name, monkeypatch):
     eager = eager_bf16(wq)  # the torch path on the same fp8-rounded weights
     for m, rows in ((1, [0]), (64, [0, 40, 63])):
         _check(eng, ref, eager, _prompts(m), rows, f"{name} fp8 M={m}")
+    eng.close()
+    del ref, eager, wq
+    torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("name", sorted(MODELS))
+def test_fullsize_fp4_weights_match_dequantised_oracle(name):
+    """The MXFP4 W4A16 path (the reference's 4-bit precision class) for all seven models at 1 and 64 rows: the fp32
+    oracle and the bf16-eager baseline both run on the dequantised MXFP4 weights."""
+    eng = DecodeEngine(name, device="cuda", max_batch=64, max_context=128, keep_natural=True, seed=29,
+                       weight_dtype="fp4")
+    wq = mxfp4_roundtrip_weights(eng.weights)
+    ref = ReferenceModel(wq, memo_weights=True)
+    eager = eager_bf16(wq)
+    for m, rows in ((1, [0]), (64, [0, 40, 63])):
+        _check(eng, ref, eager, _prompts(m), rows, f"{name} fp4 M={m}")
     eng.close()
     del ref, eager, wq
     torch.cuda.empty_cache()

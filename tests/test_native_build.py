@@ -30,11 +30,12 @@ def test_energy_library_loads_without_gpu():
 
 
 def test_default_kernel_library_links_no_vendor_gemm():
-    """hipBLASLt is an opt-in A/B build (libcain_blas.so): the default library the engine and the headline load
-    needs no vendor GEMM library and exports no library-GEMM entry."""
+    """Every GEMM is a hand-written kernel: the library the engine and the headline load links no vendor GEMM
+    library and has no library-GEMM hook (the round-3 hipBLASLt A/B path is gone)."""
     import subprocess
 
     lib = ops.load()
-    assert not hasattr(lib, "cain_lt_gemm") and hasattr(lib, "cain_set_lt_api")
+    assert not hasattr(lib, "cain_lt_gemm") and not hasattr(lib, "cain_set_lt_api")
+    assert hasattr(lib, "cain_gemm_w4") and not hasattr(lib, "cain_front")
     needed = subprocess.run(["readelf", "-d", str(ops.LIB_PATH)], capture_output=True, text=True).stdout
     assert "hipblaslt" not in needed.lower() and "rocblas" not in needed.lower(), needed

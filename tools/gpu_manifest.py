@@ -1,0 +1,62 @@
+#!/usr/bin/env python3
+"""Named GPU run sets: every GPU call of the build is ``python3 tools/gpu_manifest.py <set>`` -- one manifest
+instead of one shell script per call (round 3 left 45 ``tools/r3*.sh``; their findings are in profiles/r3/README.md
+and the git history).  Each set is a list of steps ``(name, time limit s, command)`` run in order by
+tools/gpu_steps.sh, which logs each step to gpurun_out/<set>/<name>.log and stops the set after a crash or time
+limit.  ``python3 tools/gpu_manifest.py --list`` prints the sets.
+
+Conventions: kernel statistics come from ``rocprofv3 --kernel-trace --stats`` of graph-replayed bench runs
+(per-kernel averages include no host time); bench A/Bs run the variants interleaved on one box (DVFS and
+box-to-box spread are ~1-3 %)."""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+PY = "python3"
+TEST = f"{PY} -u -m pytest -x -q --timeout 300 --timeout-method thread"
+B1 = f"{PY} bench.py --batch 1 --steps 2 --warmup 1 --no-single --no-energy"
+
+
+def prof(tag: str, args: str, limit: int = 300):
+    """A rocprof kernel-stats step of bench.py (the trace CSV itself is dropped, the stats CSV kept)."""
+    return (f"prof_{tag}", limit,
+            f"rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_{tag} -o run -- "
+            f"{PY} bench.py {args} && find gpurun_out/prof_{tag} -name '*kernel_trace.csv' -delete")
+
+
+SETS = {
+    # round 4: MXFP4 weights (gemm_w4.hip) -- kernels vs fp32, engine vs oracle, then the single-stream rates
+    "r4_fp4": [
+        ("w4_tests", 600, f"{TEST} tests/test_w4_gpu.py"),
+        ("engine_tests", 600, f"{TEST} tests/test_engine_gpu.py tests/test_w8_gpu.py"),
+        ("b1_llama_fp4", 300, f"{B1} --weights fp4"),
+        ("b1_llama_bf16", 300, B1),
+        ("b1_qwen_fp4", 300, f"{B1} --weights fp4 --model qwen2:1.5b"),
+        ("b1_gemma_fp4", 300, f"{B1} --weights fp4 --model gemma:2b"),
+        prof("b1_llama_fp4", "--batch 1 --steps 1 --warmup 1 --no-energy --no-single --weights fp4"),
+    ],
+    # the whole GPU suite (what the driver runs at round end)
+    "suite": [("gpu_suite", 1500, f"{PY} -u -m pytest tests -m gpu -x -q --timeout 600 --timeout-method thread")],
+    # the driver's bench command
+    "bench": [("bench", 900, f"{PY} bench.py --gpus 1 --steps 20 --warmup 5")],
+}
+
+
+def main(argv) -> int:
+    if not argv or argv[0] in ("-h", "--help", "--list"):
+        for k, steps in SETS.items():
+            print(k, ":", ", ".join(s[0] for s in steps))
+        return 0
+    steps = [s for name in argv for s in SETS[name]]
+    specs = [f"{n}|{t}|{c}" for n, t, c in steps]
+    env = dict(os.environ, TMPDIR="/tmp")
+    return subprocess.call(["bash", str(ROOT / "tools" / "gpu_steps.sh"), "_".join(argv)] + specs, cwd=str(ROOT),
+                           env=env)
+
+
+if __name__ == "__main__":
+    sys.exit(main(sys.argv[1:]))
