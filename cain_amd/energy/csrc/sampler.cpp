@@ -27,6 +27,7 @@
 #include <amd_smi/amdsmi.h>
 #include <dlfcn.h>
 #include <pthread.h>
+#include <sys/syscall.h>
 #include <sched.h>
 #include <time.h>
 #include <unistd.h>
@@ -380,6 +381,7 @@ struct Sampler {
   int fast_us = 1000;
   int core = -1;
   std::thread th;
+  std::atomic<long> tid{0};  // kernel thread id of the sampling thread (its CPU time is not the client's)
   std::atomic<bool> running{false};
   std::mutex mu;  // guards traces and ring
   std::vector<es_sample_t> ring;
@@ -500,6 +502,7 @@ struct Sampler {
   }
 
   void loop() {
+    tid.store(long(syscall(SYS_gettid)), std::memory_order_release);
     pin();
     uint64_t next_slow = now_ns();
     while (running.load(std::memory_order_acquire)) {
@@ -694,6 +697,10 @@ int es_drain(void* h, es_sample_t* out, int max) {
 uint64_t es_dropped(void* h) { return h ? static_cast<Sampler*>(h)->dropped.load(std::memory_order_relaxed) : 0; }
 
 int es_sample_size(void) { return int(sizeof(es_sample_t)); }
+
+// Kernel thread id of the running sampler thread (0 before es_start): process-attributed CPU energy leaves the
+// measurement's own thread out of the client's CPU time (cain_amd/energy/meter.py).
+long es_sampler_tid(void* h) { return h ? static_cast<Sampler*>(h)->tid.load(std::memory_order_acquire) : 0; }
 
 // Host CPU energy source of a sampler: "amdsmi-cpu", "rapl", "hwmon" or "" (none readable).
 const char* es_host_energy_source(void* h) { return h ? static_cast<Sampler*>(h)->host.source.c_str() : ""; }

@@ -18,8 +18,16 @@ Energy sources, per window:
 * ``ram``  — codecarbon's 3 W per 8 GB rule applied to this process's resident
   memory (the client's share of the DIMMs, not the whole 3 TB host).
 
-The host is shared by every rank of a node: ``host_share`` (1 / ranks per node)
-scales the host-wide CPU energy charged to one window.  Idle subtraction is per
+The host is shared by every rank of a node.  ``cpu_attribution="system"`` charges a
+window ``host_share`` (1 / ranks per node) of the host-wide CPU energy;
+``cpu_attribution="process"`` (the study's default) charges only the client's own
+work: the CPU seconds the client process tree spent in the window (``cpu_roots``
+and their descendants, minus ``cpu_exclude`` subtrees and the meter's own sampling
+thread; from ``/proc/<pid>/stat`` utime + stime + the reaped children's cutime +
+cstime) times the per-CPU share of the socket TDP -- codecarbon's CPU-load model
+applied to the client's CPU time instead of the whole host's, so neither a
+co-located server nor another rank's work is charged to the window (the
+reference's client laptop ran none of the server, README.md:15-16).  Idle subtraction is per
 source: a window charged with GPU and CPU energy subtracts the idle GPU and the
 idle CPU power measured by ``measure_idle`` (never the GPU's idle power from a
 CPU-only window).  Reference: codecarbon measured CPU + GPU + RAM of the client
@@ -97,6 +105,7 @@ class EnergyReading:
     host_share: float = 1.0
     idle_cpu_power_w: float = float("nan")
     sampler_core: int = -1    # CPU core the native sampler thread was pinned to
+    client_cpu_s: float = float("nan")  # cpu_attribution="process": CPU seconds of the client process tree
     samples: List[dict] = field(default_factory=list)
 
     @property
@@ -129,6 +138,62 @@ def sampler_core(local_rank: Optional[int] = None, cpus: Optional[Sequence[int]]
     if not cpus:
         return -1
     return cpus[-1 - (max(0, int(local_rank)) % len(cpus))]
+
+
+_CLK_TCK = os.sysconf("SC_CLK_TCK") if hasattr(os, "sysconf") else 100
+
+
+def _stat_fields(path: str) -> Optional[List[str]]:
+    """Fields after the ``(comm)`` of a /proc stat file (index 0 = state, 1 = ppid, 11 = utime, 12 = stime,
+    13 = cutime, 14 = cstime), or None if it vanished."""
+    try:
+        with open(path, "rb") as fh:
+            raw = fh.read().decode(errors="replace")
+    except OSError:
+        return None
+    i = raw.rfind(")")
+    return raw[i + 2:].split() if i >= 0 else None
+
+
+def process_tree(roots: Sequence[int], exclude: Sequence[int] = ()) -> List[int]:
+    """``roots`` and all their live descendants (one /proc scan), without the ``exclude`` pids' subtrees."""
+    children: Dict[int, List[int]] = {}
+    try:
+        entries = os.listdir("/proc")
+    except OSError:  # pragma: no cover
+        return list(roots)
+    for e in entries:
+        if not e.isdigit():
+            continue
+        f = _stat_fields(f"/proc/{e}/stat")
+        if f is not None and len(f) > 1:
+            children.setdefault(int(f[1]), []).append(int(e))
+    skip, out, todo = set(int(x) for x in exclude), [], [int(r) for r in roots]
+    seen = set()
+    while todo:
+        p = todo.pop()
+        if p in skip or p in seen:
+            continue
+        seen.add(p)
+        out.append(p)
+        todo.extend(children.get(p, ()))
+    return out
+
+
+def tree_cpu_seconds(roots: Sequence[int], exclude: Sequence[int] = (), skip_threads: Sequence[tuple] = ()) -> float:
+    """CPU seconds (user + system, including reaped children) of the process tree of ``roots``, minus the
+    ``(pid, tid)`` threads in ``skip_threads`` (e.g. the measurement's own sampler thread)."""
+    ticks = 0
+    for p in process_tree(roots, exclude):
+        f = _stat_fields(f"/proc/{p}/stat")
+        if f is not None and len(f) > 14:
+            ticks += int(f[11]) + int(f[12]) + int(f[13]) + int(f[14])
+    for pid, tid in skip_threads:
+        if tid > 0:
+            f = _stat_fields(f"/proc/{pid}/task/{tid}/stat")
+            if f is not None and len(f) > 12:
+                ticks -= int(f[11]) + int(f[12])
+    return ticks / float(_CLK_TCK)
 
 
 def resolve_smi_indices(devices: Optional[Sequence[int]] = None) -> List[int]:
@@ -179,7 +244,9 @@ class EnergyMeter:
                  period_ms: float = 100.0, fast_period_ms: float = 1.0, cpu_core: int = -1,
                  cpu_tdp_w: Optional[float] = None, ram_w_per_gb: float = RAM_W_PER_GB,
                  sources: Sequence[str] = ("gpu", "cpu", "ram"), keep_samples: bool = True,
-                 host_share: float = 1.0):
+                 host_share: float = 1.0, cpu_attribution: str = "system"):
+        if cpu_attribution not in ("system", "process"):
+            raise ValueError(f"cpu_attribution must be 'system' or 'process', got {cpu_attribution!r}")
         self.smi = list(smi_indices) if smi_indices is not None else resolve_smi_indices(devices)
         self.sources = tuple(sources)
         tdp, desc = host_cpu_tdp_w()
@@ -190,6 +257,12 @@ class EnergyMeter:
         self.cpu_tdp_w, self.cpu_tdp_desc = tdp, desc
         self.ram_w_per_gb = ram_w_per_gb
         self.host_share = float(host_share)
+        self.cpu_attribution = cpu_attribution
+        # process attribution: the client's process tree (default: this process) and subtrees left out of it
+        self.cpu_roots: Optional[List[int]] = None
+        self.cpu_exclude: List[int] = []
+        self.n_cpus = max(1, os.cpu_count() or 1)
+        self._cpu0 = 0.0
         self.keep_samples = keep_samples
         if cpu_core is None or cpu_core < 0:
             cpu_core = sampler_core()
@@ -246,23 +319,30 @@ class EnergyMeter:
         # before the window for the interpolation at its left edge
         self.sampler.trim(max(0, self._t0 - 2_000_000_000))
         self._rss0 = _rss_gb()
+        if self.cpu_attribution == "process":
+            self._cpu0 = self._client_cpu_s()
         return self._t0
+
+    def _client_cpu_s(self) -> float:
+        roots = self.cpu_roots or [os.getpid()]
+        return tree_cpu_seconds(roots, self.cpu_exclude, [(os.getpid(), self.sampler.thread_id)])
 
     def stop(self, settle_ms: float = 25.0) -> EnergyReading:
         if self._t0 is None:
             raise RuntimeError("EnergyMeter.stop() without start()")
         t1 = native.now_ns()
+        cpu_s = self._client_cpu_s() - self._cpu0 if self.cpu_attribution == "process" else None
         t0 = self._t0
         self._t0 = None
         # the accumulator updates every ~10-20 ms: wait for the update that covers t1
         if settle_ms > 0 and self.n_gpus:
             time.sleep(settle_ms / 1000.0)
-        return self._reading(t0, t1)
+        return self._reading(t0, t1, cpu_s)
 
     def reading_between(self, t0_ns: int, t1_ns: int) -> EnergyReading:
         return self._reading(t0_ns, t1_ns)
 
-    def _reading(self, t0: int, t1: int) -> EnergyReading:
+    def _reading(self, t0: int, t1: int, client_cpu_s: Optional[float] = None) -> EnergyReading:
         dur = max(1e-9, (t1 - t0) * 1e-9)
         samples = [s for s in self._collect() if t0 <= s["t_ns"] <= t1 + 5_000_000]
         with self._lock:
@@ -284,7 +364,7 @@ class EnergyMeter:
         vram = mean("vram_pct", True)
         cpu_j, cpu_src = 0.0, "none"
         if "cpu" in self.sources:
-            cpu_j, cpu_src = self._cpu_energy(samples, dur, cpu_pct)
+            cpu_j, cpu_src = self._cpu_energy(samples, dur, cpu_pct, client_cpu_s)
         ram_j = 0.0
         if "ram" in self.sources and self.ram_w_per_gb > 0:
             ram_j = self.ram_w_per_gb * 0.5 * (self._rss0 + _rss_gb()) * dur
@@ -308,11 +388,16 @@ class EnergyMeter:
             gpu_power_w=gpu_j / dur if self.n_gpus else float("nan"), vram_usage=vram,
             idle_power_w=self.idle_power_w, idle_subtracted_j=idle_sub, gpu_counter_updates=updates,
             per_gpu_energy_j=per_gpu, host_share=self.host_share, idle_cpu_power_w=self.idle_cpu_power_w,
-            sampler_core=self.cpu_core, samples=samples if self.keep_samples else [])
+            sampler_core=self.cpu_core, client_cpu_s=float("nan") if client_cpu_s is None else client_cpu_s,
+            samples=samples if self.keep_samples else [])
 
-    def _cpu_energy(self, samples: List[dict], dur: float, cpu_pct: float):
-        """(joules, source) of host CPU energy charged to a window of ``dur`` s: the readable counter's increase
+    def _cpu_energy(self, samples: List[dict], dur: float, cpu_pct: float, client_cpu_s: Optional[float] = None):
+        """(joules, source) of CPU energy charged to a window of ``dur`` s.  Process attribution: the client tree's
+        CPU seconds x (socket TDP / logical CPUs).  System attribution: the readable host counter's increase
         (rescaled from the sample span to the window), else the CPU-load model; times ``host_share``."""
+        if client_cpu_s is not None:
+            return (self.cpu_tdp_w / self.n_cpus * max(0.0, client_cpu_s),
+                    f"process(client cpu-s x tdp {self.cpu_tdp_w:.0f} W / {self.n_cpus} cpus; {self.cpu_tdp_desc})")
         ctr = [s for s in samples if not math.isnan(s["cpu_energy_j"])]
         # one host sample per slow period (the per-GPU rows repeat it)
         seen, pts = set(), []

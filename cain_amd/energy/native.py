@@ -85,6 +85,8 @@ def load() -> ctypes.CDLL:
         lib.es_drain.argtypes = [ctypes.c_void_p, ctypes.POINTER(ESample), ctypes.c_int]
         lib.es_dropped.argtypes = [ctypes.c_void_p]
         lib.es_dropped.restype = ctypes.c_uint64
+        lib.es_sampler_tid.argtypes = [ctypes.c_void_p]
+        lib.es_sampler_tid.restype = ctypes.c_long
         lib.es_host_energy_source.argtypes = [ctypes.c_void_p]
         lib.es_host_energy_source.restype = ctypes.c_char_p
         lib.es_test_wrap_accumulate.argtypes = [ctypes.POINTER(ctypes.c_uint64), ctypes.c_int, ctypes.c_uint64]
@@ -157,6 +159,11 @@ class NativeSampler:
 
     def trim(self, before_ns: int) -> None:
         self.lib.es_trim(self.h, ctypes.c_uint64(before_ns))
+
+    @property
+    def thread_id(self) -> int:
+        """Kernel tid of the sampling thread (0 until it runs)."""
+        return int(self.lib.es_sampler_tid(self.h))
 
     @property
     def host_energy_source(self) -> str:

@@ -100,7 +100,8 @@ def emission_tracker(online: bool = False, *decargs, **deckwargs):
     """Class decorator (reference signature ``emission_tracker(online=False, *args, **kwargs)``)."""
     data_columns = list(deckwargs.pop("data_columns", [DataColumns.EMISSIONS]))
     meter_kwargs = {k: deckwargs.pop(k) for k in ("devices", "smi_indices", "period_ms", "fast_period_ms",
-                                                    "cpu_core", "cpu_tdp_w", "ram_w_per_gb", "sources", "host_share")
+                                                    "cpu_core", "cpu_tdp_w", "ram_w_per_gb", "sources", "host_share",
+                                                    "cpu_attribution")
                     if k in deckwargs}
     country = deckwargs.pop("country_iso_code", "WORLD")
     carbon = deckwargs.pop("carbon_intensity", None)
@@ -142,6 +143,7 @@ def _meter_for(self, meter_kwargs, idle_s) -> EnergyMeter:
         kw.setdefault("devices", getattr(self, "energy_devices", None))
         # the host's CPU energy is shared by the data-parallel ranks of the node
         kw.setdefault("host_share", 1.0 / max(1, int(getattr(self, "dp_world", 1) or 1)))
+        kw.setdefault("cpu_attribution", getattr(self, "cpu_attribution", "system"))
         meter = EnergyMeter(**kw)
         if getattr(self, "idle_power_w", None) is not None:
             meter.idle_power_w = float(self.idle_power_w)
@@ -167,6 +169,7 @@ def measure_idle_baseline(config, seconds: float = 2.0) -> float:
     kw = dict(getattr(config, "__energy_meter_kwargs__", None) or {})
     kw.setdefault("devices", getattr(config, "energy_devices", None))
     kw.setdefault("host_share", 1.0 / max(1, int(getattr(config, "dp_world", 1) or 1)))
+    kw.setdefault("cpu_attribution", getattr(config, "cpu_attribution", "system"))
     with EnergyMeter(**kw) as m:
         config.idle_power_w = m.measure_idle(seconds)
         config.idle_cpu_power_w = m.idle_cpu_power_w
@@ -181,6 +184,9 @@ def _start(meter_kwargs, idle_s):
             pick = getattr(self, "energy_sources_for", None)
             if callable(pick):  # per-run measured sources (e.g. the remote arm: client CPU only)
                 meter.sources = tuple(pick(context))
+            procs = getattr(self, "cpu_processes_for", None)
+            if callable(procs):  # process attribution: the client's process tree of this run
+                meter.cpu_roots, meter.cpu_exclude = (list(x) for x in procs(context))
             meter.start()
             return fn(self, context, *a, **kw)
         return wrapper

@@ -464,7 +464,8 @@ class DecodeEngine:
                 if nsteps % k:
                     g1 = self._graph(B, 1)
                     for _ in range(nsteps % k):
-                        self.lib.cain_graph_launch(ctypes.c_void_p(g1), stream_h)
+                        if self.lib.cain_graph_launch(ctypes.c_void_p(g1), stream_h) != 0:
+                            raise RuntimeError("hipGraphLaunch failed")
 
             # first token on its own so time-to-first-token is measured exactly
             launch(1)
@@ -667,7 +668,8 @@ class ContinuousBatch:
             if steps % k:
                 g1 = eng._graph(self.n, 1)
                 for _ in range(steps % k):
-                    eng.lib.cain_graph_launch(ctypes.c_void_p(g1), stream_h)
+                    if eng.lib.cain_graph_launch(ctypes.c_void_p(g1), stream_h) != 0:
+                        raise RuntimeError("hipGraphLaunch failed")
 
     def poll(self):
         """([new token ids per live row], [finished flag per live row])."""

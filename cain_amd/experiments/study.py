@@ -15,14 +15,19 @@ MI355X-native differences:
 
 * the on-device arm is this framework's own decode engine behind an Ollama-compatible server started per
   data-parallel rank on that rank's GPU (``python -m cain_amd serve``, port ``port_base + 1 + rank``);
-* a ``local:<device>`` remote arm is ONE engine server per node (port ``port_base + 101``): rank 0 starts it
-  after a memory-fit check and publishes its URL on the job's store, every other rank reuses it -- the
-  reference's one remote server (README.md:15-16); ``gpu_usage`` stays the client's own GPU residency and a
-  server sharing the client's GPU reports its activity in ``server_gpu_usage``;
-* energy is the amd-smi hardware accumulator of the measured GPU plus host CPU (HSMP / RAPL counters or the
-  CPU-load TDP model, this rank's share of the host) and the client's RAM, on a native sampler thread
-  (``cain_amd.energy``); the remote arm measures the client only (the rank's GPU when the server lives on
-  another device, otherwise host CPU + RAM only);
+* a ``local:<device>`` remote arm is ONE engine server per node (port ``port_base + 101``), as the reference
+  has one server every trial talks to (README.md:15-16).  In a data-parallel job its GPU is a dedicated
+  server GPU: when ``<device>`` is also a client GPU, the rank that owns it hosts the server and measures
+  nothing (N ranks -> N-1 clients), so no on-device window ever integrates the board energy of remote
+  decodes; otherwise rank 0 starts it on the spare GPU.  The host publishes the URL on the job's store and
+  every client rank reuses it.  A single-rank study may share its one GPU with the server (runs are strictly
+  sequential); the remote arm's ``gpu_usage`` then stays the client's own residency (0) and the board's
+  activity goes to ``server_gpu_usage``;
+* energy is the amd-smi hardware accumulator of the measured GPU plus the client's CPU energy -- by default
+  attributed to the client process tree (the rank's run process, its curl child and, for the on-device arm,
+  its own local server: the reference's client laptop ran Ollama itself), CPU seconds x the per-CPU share of
+  the socket TDP, so neither the remote server nor another rank's work is charged (``cpu_attribution``) -- and
+  the client's RAM, on a native sampler thread (``cain_amd.energy``); the remote arm measures the client only;
 * the response JSON is captured (the reference's curl printed it and dropped it), so the run table gains
   ``tokens_generated``, ``J_per_token``, ``tok_per_s``, ``ttft_s`` ... after the reference's columns;
 * topics are drawn with a per-run seeded RNG (reproducible), prompts/lengths are the reference's.
@@ -63,7 +68,8 @@ DEFAULT_TOPICS = REPO_ROOT / "experiments" / "topics.csv"
 
 REFERENCE_COLUMNS = ["topic", "execution_time", "cpu_usage", "gpu_usage", "memory_usage"]
 EXTRA_COLUMNS = ["tokens_generated", "prompt_tokens", "J_per_token", "tok_per_s", "ttft_s", "gen_time_s",
-                 "server_total_s", "server_eval_s", "client_wall_s", "device", "server", "server_gpu_usage"]
+                 "server_total_s", "server_eval_s", "client_wall_s", "device", "server", "server_gpu_usage",
+                 "idle_power_W", "dp_rank"]
 
 #: c10d store key under which rank 0 publishes the node's one remote server URL ("error:<msg>" on failure)
 REMOTE_URL_KEY = "cain/remote_url/{name}"
@@ -153,6 +159,9 @@ class StudySettings:
     weights: str = "bf16"
     # on-device KV-cache storage: bf16, or fp8 (e4m3)
     kv: str = "bf16"
+    # client CPU energy: "process" (the client process tree's CPU seconds x TDP per CPU) or "system" (this
+    # rank's share of the whole host's CPU energy, the round-3 model)
+    cpu_attribution: str = "process"
 
     @classmethod
     def from_env(cls, base: Optional["StudySettings"] = None) -> "StudySettings":
@@ -207,7 +216,8 @@ def _wait_alive(url: str, timeout_s: float, proc: Optional[subprocess.Popen] = N
 class _ServerProc:
     """``python -m cain_amd serve ...`` as a child process in its own process group."""
 
-    def __init__(self, args: List[str], log_path: Path, env: Optional[Dict[str, str]] = None):
+    def __init__(self, args: List[str], log_path: Path, env: Optional[Dict[str, str]] = None, role: str = ""):
+        self.role = role
         log_path.parent.mkdir(parents=True, exist_ok=True)
         self.log = open(log_path, "ab")
         e = dict(os.environ)
@@ -282,6 +292,9 @@ class _StudyBase:
         self.operation_type = OperationType.AUTO
         self.time_between_runs_in_ms = int(s.cooldown_ms)
         self.idle_power_w = None
+        self.cpu_attribution = s.cpu_attribution
+        # False on a rank that only hosts the node's remote server (parallel/fanout.py: it claims no runs)
+        self.claims_runs = True
         EventSubscriptionController.subscribe_to_multiple_events([
             (RunnerEvents.BEFORE_EXPERIMENT, self.before_experiment),
             (RunnerEvents.BEFORE_RUN, self.before_run),
@@ -329,10 +342,40 @@ class _StudyBase:
         except Exception:  # pragma: no cover
             return None
 
+    def _device_ordinal(self) -> Optional[int]:
+        """This rank's GPU ordinal on the node: its measured device, else LOCAL_RANK in a data-parallel job
+        (also on CPU, where the ordinal is the rank's slot), else the GPU of a single-rank study."""
+        devs = getattr(self, "energy_devices", None)
+        if devs:
+            return int(devs[0])
+        if int(getattr(self, "dp_world", 1) or 1) > 1:
+            return int(os.environ.get("LOCAL_RANK", self.rank) or self.rank)
+        return self._gpu_index()
+
+    def _remote_host_dev(self) -> Optional[str]:
+        """The ``local:<dev>`` remote server's device, when it is a GPU ordinal (else None)."""
+        spec = self.settings.remote or ""
+        if spec.startswith("local:") and spec.split(":", 1)[1].isdigit() and "remote" in self.settings.methods:
+            return spec.split(":", 1)[1]
+        return None
+
+    def serves_remote_only(self) -> bool:
+        """True on the rank of a data-parallel job whose GPU is the remote server's: it hosts the server and
+        measures nothing, so no measured window shares a board with the server."""
+        dev = self._remote_host_dev()
+        world = int(getattr(self, "dp_world", 1) or 1)
+        return dev is not None and world > 1 and self._device_ordinal() == int(dev)
+
     def before_experiment(self) -> None:
         s = self.settings
         log_dir = self.results_output_path / s.name / "servers"
         gpu = self._gpu_index()
+        if self.serves_remote_only():
+            self.claims_runs = False
+            self.remote_url = self._node_remote_server(self._remote_host_dev(), log_dir)
+            output.console_log_OK(f"rank {self.rank} hosts the node's remote server {self.remote_url} on its GPU "
+                                  f"and claims no runs (dedicated server GPU)")
+            return
         if "on_device" in s.methods:
             port = s.port_base + 1 + self.rank
             backend = s.device_backend
@@ -355,7 +398,7 @@ class _StudyBase:
                 # the server sees only this rank's GPU; the rank keeps addressing it by its own ordinal
                 env = {"HIP_VISIBLE_DEVICES": str(gpu)}
                 args[args.index("--device") + 1] = "cuda:0"
-            srv = _ServerProc(args, log_dir / f"on_device_rank{self.rank}.log", env)
+            srv = _ServerProc(args, log_dir / f"on_device_rank{self.rank}.log", env, role="on_device")
             self._servers.append(srv)
             atexit.register(srv.stop)  # never leave a server behind, even if the experiment dies
             self.local_url = f"http://127.0.0.1:{port}"
@@ -393,15 +436,18 @@ class _StudyBase:
 
     def _node_remote_server(self, dev: str, log_dir: Path) -> str:
         """ONE remote server per node, as the reference has one server every trial talks to
-        (README.md:15-16, experiment/RunnerConfig.py:122-131): rank 0 starts it on device ``dev`` and publishes
-        its URL on the job's c10d store; the other ranks wait for that URL and reuse the server.  Before
-        preloading, the server's footprint (plus the co-located on-device server's, when ``dev`` is also a
-        client GPU) is checked against the card's HBM."""
+        (README.md:15-16, experiment/RunnerConfig.py:122-131): its host starts it on device ``dev`` and publishes
+        its URL on the job's c10d store; the other ranks wait for that URL and reuse the server.  The host is the
+        rank whose own GPU is ``dev`` (that rank then runs nothing else: ``serves_remote_only``), else rank 0
+        (``dev`` is a spare GPU or not a GPU).  Before preloading, the footprint is checked against the card's
+        HBM (plus the co-located on-device server's in a single-rank study sharing its GPU)."""
         s = self.settings
-        self.remote_shares_gpu = dev.isdigit() and self._gpu_index() == int(dev)
-        store = _dist_store() if int(getattr(self, "dp_world", 1) or 1) > 1 else None
+        world = int(getattr(self, "dp_world", 1) or 1)
+        self.remote_shares_gpu = world == 1 and dev.isdigit() and self._gpu_index() == int(dev)
+        store = _dist_store() if world > 1 else None
         key = REMOTE_URL_KEY.format(name=s.name)
-        if self.rank != 0:
+        host_rank = int(dev) if (world > 1 and dev.isdigit() and int(dev) < world) else 0
+        if self.rank != host_rank:
             if store is None:
                 raise RuntimeError("a data-parallel rank > 0 needs the job's store to find the remote server")
             val = store.get(key).decode()  # blocks until rank 0 publishes (bounded by the store timeout)
@@ -413,9 +459,8 @@ class _StudyBase:
             backend = s.remote_backend or ""
             if backend != "fake" and dev.isdigit():
                 need = server_footprint_bytes(list(s.models), s.max_batch, s.max_context)
-                world = int(getattr(self, "dp_world", 1) or 1)
-                # rank r's on-device server lives on GPU r (LOCAL_RANK) in a data-parallel job
-                co_located = "on_device" in s.methods and (int(dev) < world if world > 1 else self.remote_shares_gpu)
+                # a data-parallel job never co-locates (the GPU's rank serves only); a single-rank study may
+                co_located = "on_device" in s.methods and self.remote_shares_gpu
                 if co_located:
                     need += server_footprint_bytes(list(s.models), s.max_batch, s.max_context, s.weights, s.kv)
                 if need > GPU_MEM_BYTES:
@@ -433,7 +478,7 @@ class _StudyBase:
                 args += ["--fake-tok-s", str(s.remote_fake_tok_s), "--fake-prefill-s", str(s.remote_fake_prefill_s)]
             else:
                 args.append("--preload")
-            srv = _ServerProc(args, log_dir / "remote_node.log", env)
+            srv = _ServerProc(args, log_dir / "remote_node.log", env, role="remote")
             self._servers.append(srv)
             atexit.register(srv.stop)
             url = f"http://127.0.0.1:{port}"
@@ -446,6 +491,19 @@ class _StudyBase:
             store.set(key, url)
         output.console_log(f"remote server {url} on device {dev} (one per node, shared by {getattr(self, 'dp_world', 1)} ranks)")
         return url
+
+    def cpu_processes_for(self, context: RunnerContext):
+        """(roots, excluded) of the client process tree whose CPU time a window is charged with: this run's process
+        (curl / the in-process client are its descendants or threads) and, for the on-device arm, the rank's own
+        local server -- the device's LLM runtime, as Ollama ran on the reference's laptop; every remote server
+        subtree is excluded."""
+        roots = [os.getpid()]
+        local = [srv.proc.pid for srv in self._servers if getattr(srv, "role", "") == "on_device"]
+        others = [srv.proc.pid for srv in self._servers if getattr(srv, "role", "") != "on_device"]
+        if context.run_variation.get("method") == "on_device":
+            roots += local
+            return roots, others
+        return roots, others + local
 
     def teardown_rank(self) -> None:
         for srv in self._servers:
@@ -620,5 +678,7 @@ class StudyConfig(_MeasuredStudy):
             "device": str(getattr(self, "energy_devices", [""])[0]) if getattr(self, "energy_devices", None) else "",
             "server": self.url,
             "server_gpu_usage": getattr(self, "_server_gpu_usage", ""),
+            "idle_power_W": round(float(self.idle_power_w), 2) if self.idle_power_w is not None else "",
+            "dp_rank": self.rank,
         })
         return data

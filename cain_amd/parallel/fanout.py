@@ -47,6 +47,7 @@ from typing import Any, Dict, List, Optional
 
 
 _SESSION_T0 = [0.0]  # monotonic start of this rank (run_rank), for CAIN_RUN_BUDGET_S
+_SKIPPED = "__skipped__"  # published for a queue index claimed after the writer's budget stop (not run)
 
 
 def _free_port() -> int:
@@ -169,11 +170,17 @@ class _Heartbeat:
         self._t.start()
 
     def _run(self) -> None:
+        fails = 0
         while not self._stop.is_set():
             try:
                 self.store.add(self.key, 1)
-            except Exception:  # pragma: no cover - the store went away with the job
-                return
+                fails = 0
+            except Exception as exc:  # a transient store error must not make a live rank look dead: retry
+                fails += 1
+                if fails in (1, 10, 100):
+                    from ..runner.output import OutputProcedure as output
+
+                    output.console_log_WARNING(f"heartbeat: store error ({fails}x): {exc}")
             self._stop.wait(self.period)
 
     def close(self) -> None:
@@ -209,6 +216,8 @@ def _work_queue(store, prefix: str, todo_ids: List[str], by_id: Dict[str, Dict[s
         for i in keys:
             row = pickle.loads(store.get(f"{prefix}res/{i}"))
             pending.discard(i)
+            if row == _SKIPPED:  # claimed after the writer's stop: not run, stays TODO (not a failure)
+                continue
             if row is None:
                 failed.append(todo_ids[i])
             else:
@@ -223,14 +232,23 @@ def _work_queue(store, prefix: str, todo_ids: List[str], by_id: Dict[str, Dict[s
     # CAIN_RUN_BUDGET_S > 0: stop claiming runs that long after the rank started (chunked sessions of a long study:
     # the rest stays TODO and the next session resumes it)
     budget = float(os.environ.get("CAIN_RUN_BUDGET_S", "0") or 0)
-    while True:
+    # a rank that only hosts a shared server (the study's dedicated remote-server GPU) claims no runs; as the
+    # writer it still commits every published row below
+    claims = bool(getattr(config, "claims_runs", True))
+    while claims:
         if budget > 0 and time.monotonic() - _SESSION_T0[0] > budget:
             output.console_log_WARNING(f"run budget of {budget:.0f} s used: the remaining runs stay TODO (resume)")
+            if writer:  # every rank stops claiming too, so the writer's count of claimed runs below is final
+                store.set(f"{prefix}stop", "1")
             break
         i = int(store.add(f"{prefix}next", 1)) - 1
         if i >= n:
             break
         store.set(f"{prefix}claim/{i}", str(rank))
+        if budget > 0 and store.check([f"{prefix}stop"]):
+            # the writer stopped (and may already have counted this index as claimed): hand it back untouched
+            store.set(f"{prefix}res/{i}", pickle.dumps(_SKIPPED))
+            break
         if ran:
             ctrl.cooldown()  # per rank: overlaps with the other ranks' runs
         rid = todo_ids[i]
@@ -243,7 +261,9 @@ def _work_queue(store, prefix: str, todo_ids: List[str], by_id: Dict[str, Dict[s
             EventSubscriptionController.raise_event(RunnerEvents.CONTINUE)
     if writer:
         if budget > 0:
-            # indices nobody claimed (every rank stopped at its budget) stay TODO: wait for the claimed ones only
+            # indices nobody claimed stay TODO: wait for the claimed ones only.  Set the stop key (also when the
+            # queue simply ran out) before counting, so an index claimed after the count is handed back
+            store.set(f"{prefix}stop", "1")
             claimed = min(n, int(store.add(f"{prefix}next", 0)))
             pending.difference_update(range(claimed, n))
         last_progress = time.monotonic()

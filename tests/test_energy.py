@@ -168,3 +168,67 @@ def test_wattsup_parsing_and_integration():
     s = w.log(timeout=0.05)
     assert len(s) == 2 and w.energy_j() >= 0.0
     assert w.s.written[0].startswith(b"#L,W,3,E")
+
+
+def _burn(seconds: float) -> None:
+    t = time.process_time()
+    while time.process_time() - t < seconds:
+        pass
+
+
+def test_process_attribution_charges_the_client_tree_only():
+    """cpu_attribution="process": a busy process outside the client's tree (reparented away by a double fork, like
+    a co-located server or another rank) does not change the window's CPU energy; the client's own CPU time and
+    that of a child it reaps inside the window do, at TDP / logical CPUs per CPU second."""
+    import os
+    import subprocess
+    import sys
+
+    tdp = 640.0
+    m = EnergyMeter(smi_indices=[], sources=("cpu",), cpu_attribution="process", keep_samples=False, cpu_tdp_w=tdp)
+    per_cpu_s = tdp / m.n_cpus
+    try:
+        m.start()
+        time.sleep(0.6)
+        quiet = m.stop()
+        out = subprocess.run(["sh", "-c", f"{sys.executable} -c 'import time\nt=time.time()\n"
+                                          f"while time.time()-t<4: pass' >/dev/null 2>&1 & echo $!"],
+                             capture_output=True, text=True, check=True)
+        busy_pid = int(out.stdout.strip())
+        try:
+            time.sleep(0.2)
+            m.start()
+            time.sleep(0.6)
+            unrelated = m.stop()
+        finally:
+            os.kill(busy_pid, 9)
+        assert quiet.cpu_energy_source.startswith("process(")
+        assert quiet.client_cpu_s < 0.1 and unrelated.client_cpu_s < 0.1, (quiet.client_cpu_s, unrelated.client_cpu_s)
+        assert unrelated.cpu_energy_j < 0.1 * per_cpu_s
+        # the client's own work and a reaped child's
+        m.start()
+        _burn(0.4)
+        subprocess.run([sys.executable, "-c", "import time\nt=time.process_time()\n"
+                                              "while time.process_time()-t<0.4: pass"], check=True)
+        own = m.stop()
+        assert 0.7 < own.client_cpu_s < 2.5, own.client_cpu_s  # 0.8 s of work (+ the child's interpreter start)
+        assert abs(own.cpu_energy_j - own.client_cpu_s * per_cpu_s) < 1e-6
+    finally:
+        m.close()
+
+
+def test_process_attribution_excludes_subtrees():
+    from cain_amd.energy.meter import process_tree
+
+    import os
+    import subprocess
+    import sys
+
+    p = subprocess.Popen([sys.executable, "-c", "import time; time.sleep(5)"])
+    try:
+        tree = process_tree([os.getpid()])
+        assert os.getpid() in tree and p.pid in tree
+        assert p.pid not in process_tree([os.getpid()], exclude=[p.pid])
+    finally:
+        p.kill()
+        p.wait()

@@ -268,3 +268,22 @@ def test_run_budget_leaves_unclaimed_runs_todo(monkeypatch):
     t0 = time.monotonic()
     failed, committed = _writer_pass(monkeypatch, store, ["a", "b", "c"], rank=0, hb_timeout_s=30, deadline_s=30)
     assert failed == [] and committed == [] and time.monotonic() - t0 < 5
+
+
+def test_budget_stop_hands_back_a_late_claim(monkeypatch):
+    """another rank that claims an index after the writer's budget stop publishes it back untouched
+    (the writer may already have counted it as claimed): the writer neither waits for it nor records a failure,
+    and the row stays TODO for the next session."""
+    import pickle
+    import time
+
+    from cain_amd.parallel import fanout
+
+    monkeypatch.setenv("CAIN_RUN_BUDGET_S", "5")
+    store = _DictStore()
+    store.add("cain/0/next", 1)  # rank 1 claimed index 0 before the stop ...
+    store.set("cain/0/claim/0", "1")
+    store.set("cain/0/res/0", pickle.dumps(fanout._SKIPPED))  # ... saw the stop key and handed it back
+    monkeypatch.setattr(fanout, "_SESSION_T0", [time.monotonic() - 10])  # the writer's budget is spent
+    failed, committed = _writer_pass(monkeypatch, store, ["a", "b"], rank=0, hb_timeout_s=30, deadline_s=5)
+    assert failed == [] and committed == [] and store.check(["cain/0/stop"])

@@ -96,6 +96,34 @@ def test_study_eight_ranks_share_one_remote_server(tmp_path):
         assert len(set(flat)) == len(flat), cores
 
 
+def test_study_dedicated_remote_server_gpu_at_eight_ranks(tmp_path):
+    """``remote=local:3`` in an 8-rank job: GPU 3 is a client GPU, so its rank hosts the node's remote server and
+    claims no runs (8 ranks -> 7 clients): no on-device window is ever measured on the server's board, and the
+    rank starts no on-device server of its own.  Client CPU energy is process-attributed (the default)."""
+    base = 25000 + os.getpid() % 1000
+    r = subprocess.run([sys.executable, "-m", "cain_amd", str(ROOT / "experiments" / "study.py"), "--gpus", "8"],
+                       capture_output=True, text=True, timeout=900, cwd=ROOT,
+                       env=_env(tmp_path, CAIN_STUDY_PORT_BASE=str(base), CAIN_STUDY_REPETITIONS="8",
+                                CAIN_STUDY_DEVICE_BACKEND="fake", CAIN_STUDY_REMOTE="local:3",
+                                CAIN_STUDY_REMOTE_BACKEND="fake", CAIN_STUDY_REMOTE_FAKE_TOK_S="2000",
+                                CAIN_STUDY_REMOTE_FAKE_PREFILL_S="0", CAIN_STUDY_IDLE_BASELINE_S="0"))
+    assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-4000:]
+    out = tmp_path / "full_factorial"
+    rows = list(csv.DictReader(open(out / "run_table.csv")))
+    assert len(rows) == 16 and all(x["__done"] == "DONE" for x in rows)
+    ranks = {int(x["dp_rank"]) for x in rows}
+    assert 3 not in ranks and ranks <= set(range(8)) - {3}, ranks
+    # no on-device row was served by a server on GPU 3 (rank r's on-device server listens on port_base + 1 + r)
+    assert all(int(x["server"].rsplit(":", 1)[1]) != base + 1 + 3 for x in rows if x["method"] == "on_device")
+    remote = [x for x in rows if x["method"] == "remote"]
+    assert len({x["server"] for x in remote}) == 1 and remote[0]["server"].endswith(f":{base + 101}")
+    logs = sorted(p.name for p in (out / "servers").iterdir())
+    assert "remote_node.log" in logs and "on_device_rank3.log" not in logs, logs
+    assert sum(n.startswith("on_device_rank") for n in logs) == 7
+    assert "rank 3 hosts the node's remote server" in r.stdout
+    assert all(x["cpu_energy_source"].startswith("process(") for x in rows), {x["cpu_energy_source"] for x in rows}
+
+
 @pytest.mark.gpu
 def test_study_on_device_arm_on_gpu_measures_energy(tmp_path):
     """On the GPU box: the per-rank server runs the HIP engine, the window reads the amd-smi accumulator."""
