@@ -78,7 +78,8 @@ def load() -> ctypes.CDLL:
         lib.cain_gemm_w4.argtypes = ([vp, vp, vp, ci, ci, ci, ci, vp, ci, vp, ci, cf, vp, vp, vp, vp, vp, vp]
                                      + [ci] * 5 + [vp])
         lib.cain_gemm_w4_set_variant.argtypes = [ci]
-        lib.cain_gemm_w4_variant.argtypes = [ci, ci, ci]
+        lib.cain_gemm_w4_variant.argtypes = [ci, ci, ci, ci]
+        lib.cain_gemm_w4_set_occupancy.argtypes = [ci]
         lib.cain_gemm_w8a8.argtypes = ([vp, vp, vp, ci, vp, ci, ci, ci, vp, ci, vp, vp, vp, vp, vp, vp, vp]
                                        + [ci] * 4 + [vp, ctypes.c_longlong, ci, vp])
         lib.cain_quant_rows.argtypes = [vp, ci, ci, ci, vp, ci, vp, ci, cf, vp]
@@ -309,13 +310,19 @@ def gemm_w4(wq: torch.Tensor, wsc: torch.Tensor, x: torch.Tensor, n: int, epi: i
 
 
 def set_w4_variant(v: int) -> None:
-    """Force the few-row MXFP4 kernel shape (gemm_w4.hip W4Var index; -1: the shape rule).  Tests / tuning."""
+    """Force the few-row MXFP4 kernel shape (gemm_w4.hip W4Var index; -1: the shape rule; a stream shape whose LDS
+    copy cannot hold the rows falls back to the rule).  Tests / tuning."""
     load().cain_gemm_w4_set_variant(int(v))
 
 
-def w4_variant(n: int, k: int, m: int) -> int:
-    """The W4Var index the shape rule picks for an (N, K, M) problem."""
-    return int(load().cain_gemm_w4_variant(int(n), int(k), int(m)))
+def set_w4_occupancy(wgs_per_cu: int) -> None:
+    """Workgroups per CU of the persistent single-stream MXFP4 grid (0: 2 of 8 waves / 4 of 4 waves).  Tuning."""
+    load().cain_gemm_w4_set_occupancy(int(wgs_per_cu))
+
+
+def w4_variant(n: int, k: int, m: int, epi: int = EPI_BF16) -> int:
+    """The W4Var index the shape rule picks for an (N, K, M) problem with epilogue ``epi``."""
+    return int(load().cain_gemm_w4_variant(int(n), int(k), int(m), int(epi)))
 
 
 def quant_rows(x: torch.Tensor, norm: bool = False, eps: float = 1e-6):

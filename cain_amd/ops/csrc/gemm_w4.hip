@@ -18,15 +18,27 @@
 // accumulation.  The fused RMSNorm, the epilogues and the activations-in-LDS (XL) staging are the fp8 kernel's
 // (gemm_w8.hip, gemm_epi.h).
 //
-// Structure: one workgroup per (NT 16-row tiles, 16*NB-row M block); WAVES waves split the k quads, keep U quads of
-// loads in flight (copy pipeline), reduce through LDS; wave 0 runs the epilogue.
+// Two kernels.  The single-stream one (w4_stream_kernel, rows <= 16 whose activations fit the LDS copy) is a
+// persistent stream: a grid of G <= (CUs x workgroups per CU) workgroups; workgroup b takes the
+// (16-row tile, 16*NB-row M block) pairs b, b + G, b + 2G, ...  Its WAVES waves deal every tile's k quads among
+// themselves (wave w: quads w, w + WAVES, ...) and walk ONE flattened sequence of (pair, quad) items with U items
+// of weight loads in flight in a register ring, across tile boundaries: while a tile's last quads are multiplied
+// the next tile's weights are already streaming, so a workgroup never drains its loads at a tile edge (a one-tile
+// workgroup did: the few-row fp4 tiles are only 32 KiB at K = 4096).  At each tile edge the waves drop their
+// 16x16 partials into a double-buffered LDS slab, one raw barrier, and wave 0 runs the fused epilogue while the
+// others go on.  The activation rows (XL: M x K <= 32 KiB) are staged into LDS once per workgroup by plain loads
+// issued ahead of the weight prologue (the compiler counts both load streams, so nothing drains early); the
+// RMSNorm sums of squares are taken once per workgroup from those staged chunks (8 VALU ops per MFMA when taken
+// from every activation fragment: +2-4 us per GEMM, profiles/r4/).
+// Wider problems (w4_tile_kernel: up to 64 rows, or activation rows beyond the LDS copy) run one workgroup per
+// (tile, 16*NB-row block) with the activation fragments loaded beside each weight quad.
+#include <algorithm>
+
 #include "common.h"
 #include "gemm_epi.h"
 
 typedef uint32_t w4u32x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 w4bf16x2 __attribute__((ext_vector_type(2)));
-typedef __attribute__((address_space(3))) void w4_lds_t;
-typedef __attribute__((address_space(1))) const void w4_gbl_t;
 
 // 8 e2m1 codes (one dword) -> the 8 bf16 of an MFMA A fragment, times the block scale
 __device__ __forceinline__ bf16x8 w4_frag(uint32_t w, float sc) {
@@ -40,112 +52,222 @@ __device__ __forceinline__ bf16x8 w4_frag(uint32_t w, float sc) {
 // e8m0 byte -> fp32 2^(e - 127) (the packer keeps e >= 1: never a zero / denormal scale)
 __device__ __forceinline__ float e8m0_f32(uint32_t e) { return __builtin_bit_cast(float, (e & 0xffu) << 23); }
 
-template <int WAVES, int U, int NT, int NB, int EPI, bool NORM, bool XL0>
-__global__ __launch_bounds__(WAVES * 64) void skinny_w4_kernel(const GemmArgs a, const uint8_t* __restrict__ wsc) {
-  constexpr bool XL = XL0 && NB == 1;
-  extern __shared__ __attribute__((aligned(16))) char w4_xs[];
+__device__ __forceinline__ void w4_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// pair j -> (16-row tile, M block): the M blocks of one tile get ids 8 apart (the same XCD's L2 under round-robin
+// dispatch when the grid is a multiple of 8; any placement is correct)
+__device__ __forceinline__ void w4_pair_tile(int j, int msp, int ntg, int& t, int& ms) {
+  if (msp == 1) {
+    t = j, ms = 0;
+  } else if ((ntg & 7) == 0) {
+    const int r = j >> 3;
+    ms = r % msp;
+    t = (r / msp) * 8 + (j & 7);
+  } else {
+    t = j / msp, ms = j - (j / msp) * msp;
+  }
+}
+
+// ================================================================ single stream: persistent, activations in LDS
+// LDS copy of the activation rows: 48 KiB for 8-wave workgroups (2 per CU), 28 KiB for 4-wave ones (4 per CU) --
+// every real model's down projection (K <= 24576) fits at one row
+template <int WAVES>
+constexpr int w4_xl_bytes() { return WAVES == 8 ? 49152 : 28672; }
+
+// 4 waves per SIMD (<= 128 VGPRs): the grid below assumes 16 resident waves per CU
+template <int WAVES, int U, int EPI, bool NORM>
+__global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(4, 4))) void w4_stream_kernel(
+    const GemmArgs a, const uint8_t* __restrict__ wsc, int npairs) {
+  constexpr int XLB = w4_xl_bytes<WAVES>();
+  constexpr int XCH = XLB / (WAVES * 64 * 16);  // 16-byte activation chunks staged per thread
+  __shared__ __attribute__((aligned(16))) char w4_xs[XLB];
+  __shared__ __attribute__((aligned(16))) f32x4 red[2][WAVES][64];
+  __shared__ float row_ss[16];  // NORM: the sum of squares of each activation row
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int KQ = a.K >> 7;                    // 128-wide k quads per tile
+  const int qmax = (KQ + WAVES - 1) / WAVES;  // items per tile (every wave walks the same sequence length)
+  if (NORM && threadIdx.x < 16) row_ss[threadIdx.x] = 0.f;
+  const int G = gridDim.x;
+  const int my_tiles = (npairs - (int)blockIdx.x + G - 1) / G;
+  const int n_items = my_tiles * qmax;
+  constexpr int R = U + 1;                      // ring slots: U items in flight + the one being multiplied
+  const int n_pad = (n_items + R - 1) / R * R;  // whole ring rounds; the padding items load clamped, compute nothing
+
+  // ---- this thread's activation chunks first (row-contiguous copy of rows [0, M) x K), then the weight prologue:
+  // the compiler counts both streams of plain loads, so staging X waits for X alone
+  bf16x8 xst[XCH];
+  const int cpr = a.K >> 3, nch = a.M * cpr;
+#pragma unroll
+  for (int i = 0; i < XCH; ++i) {
+    const int c = min((int)threadIdx.x + i * WAVES * 64, nch - 1);
+    const int r = c / cpr, col = c - r * cpr;
+    xst[i] = *reinterpret_cast<const bf16x8*>(a.X + (size_t)r * a.ldx + col * 8);
+  }
+
+  struct Quad {
+    w4u32x4 w;
+    uint32_t s;
+  };
+  const w4u32x4* wbase = reinterpret_cast<const w4u32x4*>(a.Wp) + lane;
+  const uint8_t* sbase = wsc + lane;
+  int ld_t = blockIdx.x, ld_e = 0, ld_i = 0;
+  const int last_t = (int)blockIdx.x + (my_tiles - 1) * G;
+  auto load_next = [&](Quad& q) {
+    // past the end of the sequence: re-load this wave's last item (a cache hit).  Not a branch around the load:
+    // hipcc then loses its counted waits and drains the ring (vmcnt(0)) at every item
+    const bool in = ld_i < n_items;
+    const int p = min(wave + (in ? ld_e : qmax - 1) * WAVES, KQ - 1);
+    const size_t off = ((size_t)(in ? ld_t : last_t) * KQ + p) * 64;
+    q.w = __builtin_nontemporal_load(wbase + off);
+    q.s = __builtin_nontemporal_load(sbase + off);
+    ++ld_i;
+    if (++ld_e == qmax) ld_e = 0, ld_t += G;
+  };
+  Quad ring[R];
+#pragma unroll
+  for (int u = 0; u < U; ++u) load_next(ring[u]);
+
+  int cp_t = blockIdx.x;
+  EpiIn pre{};
+  if (wave == 0 && my_tiles > 0) pre = epi_load_at<EPI>(a, cp_t, lane & 15, lane);
+#pragma unroll
+  for (int i = 0; i < XCH; ++i) {
+    const int c = (int)threadIdx.x + i * WAVES * 64;
+    if (c < nch) *reinterpret_cast<bf16x8*>(w4_xs + (size_t)c * 16) = xst[i];
+  }
+  w4_barrier();
+  if constexpr (NORM) {
+    // RMSNorm sums of squares once per workgroup, from the staged chunks still in registers (every element of X
+    // once: 8 squares per chunk) -- not per weight fragment, where they cost 8 VALU ops per MFMA (+2-4 us per GEMM)
+#pragma unroll
+    for (int i = 0; i < XCH; ++i) {
+      const int c = (int)threadIdx.x + i * WAVES * 64;
+      if (c < nch) {
+        float v = 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v += bf2f(xst[i][j]) * bf2f(xst[i][j]);
+        atomicAdd(&row_ss[c / cpr], v);
+      }
+    }
+  }
+  // this lane's activation row in LDS and its k group: fragment s of quad p starts at 128p + 32g + 8s.  Lanes of
+  // output columns >= M (padding rows) read nothing and multiply zeros: at one row 1/16 of the LDS traffic.
+  const bool xrow = (lane & 15) < a.M;
+  const __bf16* xl_row = reinterpret_cast<const __bf16*>(w4_xs) + (size_t)min(lane & 15, a.M - 1) * a.K + ((lane >> 4) << 5);
+
+  f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+  int cp_e = 0, cp_n = 0, buf = 0;
+
+  auto step = [&](const Quad& q, int p) {
+    const float sc = e8m0_f32(q.s);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const bf16x8 wf = w4_frag(q.w[s], sc);
+      bf16x8 xv = {};
+      if (xrow) xv = *reinterpret_cast<const bf16x8*>(xl_row + p * 128 + s * 8);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, xv, acc, 0, 0, 0);
+    }
+  };
+
+  // end of a tile: partials -> LDS slab `buf`, one barrier, wave 0 finishes the 16x16 block
+  auto tile_end = [&]() {
+    red[buf][wave][lane] = acc;
+    acc = f32x4{0.f, 0.f, 0.f, 0.f};
+    w4_barrier();
+    if (wave == 0) {
+      if (cp_n > 0) pre = epi_load_at<EPI>(a, cp_t, lane & 15, lane);  // later tiles (none for fp32 / act epis)
+      auto unit_sum = [&](int l) -> f32x4 {
+        f32x4 v = red[buf][0][l];
+#pragma unroll
+        for (int w = 1; w < WAVES; ++w) v += red[buf][w][l];
+        if constexpr (NORM) v *= rms_inv(row_ss[min(l & 15, a.M - 1)], a.K, a.eps);
+        return v;
+      };
+      epi_store<EPI>(a, cp_t, lane & 15, lane, pre, [&](int off) { return unit_sum(lane + off); });
+    }
+    buf ^= 1;
+  };
+
+  for (int i0 = 0; i0 < n_pad; i0 += R) {
+#pragma unroll
+    for (int u = 0; u < R; ++u) {
+      const int p = wave + cp_e * WAVES;
+      const bool live = i0 + u < n_items;
+      // item i0 + u + U goes into the spare slot (the one consumed by the previous item) BEFORE this item's math: a
+      // ring of U + 1 slots walked in whole rounds keeps every slot index a constant (a register copy of an
+      // in-flight load would force the compiler to drain the ring: vmcnt(0) at every round)
+      load_next(ring[(u + U) % (U + 1)]);
+      if (live && p < KQ) step(ring[u], p);
+      if (live && cp_e == qmax - 1) tile_end();
+      if (++cp_e == qmax) cp_e = 0, ++cp_n, cp_t += G;
+    }
+  }
+}
+
+// ================================================================ wide / fallback: one workgroup per (tile, M block)
+template <int WAVES, int U, int NB, int EPI, bool NORM>
+__global__ __launch_bounds__(WAVES * 64) void w4_tile_kernel(const GemmArgs a, const uint8_t* __restrict__ wsc) {
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int KQ = a.K >> 7;  // 128-wide k quads
-  // XCD-aware (tile, M block) mapping as gemm.hip: the M blocks of one tile get ids 8 apart (same L2)
   int tg, ms;
-  {
-    const int bid = blockIdx.x, msp = a.msplit;
-    const int ntg = gridDim.x / msp;
-    if (msp == 1) {
-      tg = bid, ms = 0;
-    } else if ((ntg & 7) == 0) {
-      const int r = bid >> 3;
-      ms = r % msp;
-      tg = (r / msp) * 8 + (bid & 7);
-    } else {
-      tg = bid / msp, ms = bid - (bid / msp) * msp;
-    }
-  }
+  w4_pair_tile(blockIdx.x, a.msplit, gridDim.x / a.msplit, tg, ms);
   const int mo = ms * 16 * NB;
   const int p_beg = (wave * KQ) / WAVES, p_end = ((wave + 1) * KQ) / WAVES;
-  const int t0 = tg * NT;
 
-  EpiIn pre[NT][NB];
+  EpiIn pre[NB];
   if (wave == 0) {
 #pragma unroll
-    for (int t = 0; t < NT; ++t)
-#pragma unroll
-      for (int b = 0; b < NB; ++b) pre[t][b] = epi_load_at<EPI>(a, t0 + t, mo + 16 * b + (lane & 15), lane);
+    for (int b = 0; b < NB; ++b) pre[b] = epi_load_at<EPI>(a, tg, mo + 16 * b + (lane & 15), lane);
   }
-
-  const w4u32x4* wb = reinterpret_cast<const w4u32x4*>(a.Wp) + (size_t)t0 * KQ * 64 + lane;
-  const uint8_t* sb = wsc + (size_t)t0 * KQ * 64 + lane;
+  const w4u32x4* wb = reinterpret_cast<const w4u32x4*>(a.Wp) + (size_t)tg * KQ * 64 + lane;
+  const uint8_t* sb = wsc + (size_t)tg * KQ * 64 + lane;
   // this lane's activation row and its k group: fragment s of quad p starts at element 128p + 32g + 8s
   const int kg = (lane >> 4) << 5;
   const __bf16* xb[NB];
 #pragma unroll
   for (int b = 0; b < NB; ++b) xb[b] = a.X + (size_t)min(mo + 16 * b + (lane & 15), a.M - 1) * a.ldx + kg;
-  const __bf16* xl_row = reinterpret_cast<const __bf16*>(w4_xs) + (size_t)min(lane & 15, a.M - 1) * a.K + kg;
 
-  f32x4 acc[NT][NB];
+  f32x4 acc[NB];
   float ssq[NB];
 #pragma unroll
-  for (int b = 0; b < NB; ++b) {
-    ssq[b] = 0.f;
-#pragma unroll
-    for (int t = 0; t < NT; ++t) acc[t][b] = f32x4{0.f, 0.f, 0.f, 0.f};
-  }
+  for (int b = 0; b < NB; ++b) acc[b] = f32x4{0.f, 0.f, 0.f, 0.f}, ssq[b] = 0.f;
 
   struct Quad {
-    w4u32x4 w[NT];
-    uint32_t s[NT];
-    bf16x8 x[XL ? 1 : NB][4];
-    int p;
+    w4u32x4 w;
+    uint32_t s;
+    bf16x8 x[NB][4];
   };
   auto load = [&](Quad& q, int p) {
-    q.p = p;
+    q.w = __builtin_nontemporal_load(wb + (size_t)p * 64);
+    q.s = __builtin_nontemporal_load(sb + (size_t)p * 64);
 #pragma unroll
-    for (int t = 0; t < NT; ++t) {
-      q.w[t] = __builtin_nontemporal_load(wb + ((size_t)t * KQ + p) * 64);
-      q.s[t] = __builtin_nontemporal_load(sb + ((size_t)t * KQ + p) * 64);
-    }
-    if constexpr (!XL) {
+    for (int b = 0; b < NB; ++b)
 #pragma unroll
-      for (int b = 0; b < NB; ++b)
-#pragma unroll
-        for (int s = 0; s < 4; ++s) q.x[b][s] = *reinterpret_cast<const bf16x8*>(xb[b] + p * 128 + s * 8);
-    }
+      for (int s = 0; s < 4; ++s) q.x[b][s] = *reinterpret_cast<const bf16x8*>(xb[b] + p * 128 + s * 8);
   };
   auto step = [&](const Quad& q) {
-    float sc[NT];
-#pragma unroll
-    for (int t = 0; t < NT; ++t) sc[t] = e8m0_f32(q.s[t]);
+    const float sc = e8m0_f32(q.s);
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-      bf16x8 xv[NB];
+      const bf16x8 wf = w4_frag(q.w[s], sc);
 #pragma unroll
       for (int b = 0; b < NB; ++b) {
-        if constexpr (XL) xv[b] = *reinterpret_cast<const bf16x8*>(xl_row + q.p * 128 + s * 8);
-        else xv[b] = q.x[b][s];
-      }
-      if constexpr (NORM) {
-#pragma unroll
-        for (int b = 0; b < NB; ++b)
+        if constexpr (NORM) {
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
-            const float f = bf2f(xv[b][j]);
+            const float f = bf2f(q.x[b][s][j]);
             ssq[b] += f * f;
           }
-      }
-#pragma unroll
-      for (int t = 0; t < NT; ++t) {
-        const bf16x8 wf = w4_frag(q.w[t][s], sc[t]);
-#pragma unroll
-        for (int b = 0; b < NB; ++b)
-          acc[t][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, xv[b], acc[t][b], 0, 0, 0);
+        }
+        acc[b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, q.x[b][s], acc[b], 0, 0, 0);
       }
     }
   };
 
-  // copy pipeline: chunks of U quads, the next chunk's loads in flight while the current one is multiplied.  A
-  // partial last chunk re-loads its last quad (clamped index, cache hit) instead of branching around loads, and
-  // multiplies only its valid quads.
+  // copy pipeline: chunks of U quads, the next chunk's loads in flight while the current one is multiplied; a
+  // partial last chunk re-loads its last quad (clamped, a cache hit) and multiplies only its valid quads
   const int nq = p_end - p_beg;
   const int nchunk = (nq + U - 1) / U;
   auto load_chunk = [&](Quad* q, int pc) {
@@ -154,27 +276,12 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_w4_kernel(const GemmArgs a,
   };
   Quad cur[U];
   if (nchunk > 0) load_chunk(cur, p_beg);
-  if constexpr (XL) {
-    // stage rows [0, M) x K of X by LDS-DMA under the weight prologue: 16-byte chunk c of the row-contiguous LDS copy
-    // <- row c / (K / 8), column chunk c % (K / 8); wave instruction j covers chunks 64 j .. 64 j + 63
-    const int cpr = a.K >> 3, nch = a.M * cpr;
-    for (int j = wave; j * 64 < nch; j += WAVES) {
-      const int c = j * 64 + lane;
-      if (c < nch) {
-        const int r = c / cpr, col = c - r * cpr;
-        __builtin_amdgcn_global_load_lds((w4_gbl_t*)(a.X + (size_t)r * a.ldx + col * 8), (w4_lds_t*)(w4_xs + j * 1024),
-                                         16, 0, 0);
-      }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-  }
   for (int c = 0; c < nchunk; ++c) {
     Quad nxt[U];
     const int pc = p_beg + c * U;
     const bool more = c + 1 < nchunk;
     if (more) load_chunk(nxt, pc + U);
-    const int nv = p_end - pc;  // valid quads of this chunk (>= U except in the last one)
+    const int nv = p_end - pc;
 #pragma unroll
     for (int u = 0; u < U; ++u)
       if (u < nv) step(cur[u]);
@@ -185,17 +292,15 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_w4_kernel(const GemmArgs a,
   }
 
   // ---- cross-wave reduction through LDS, epilogue by wave 0
-  __shared__ __attribute__((aligned(16))) f32x4 red[WAVES][NT][NB][64];
+  __shared__ __attribute__((aligned(16))) f32x4 red[WAVES][NB][64];
   __shared__ float red_ss[NORM ? WAVES : 1][NB][16];
 #pragma unroll
-  for (int t = 0; t < NT; ++t)
-#pragma unroll
-    for (int b = 0; b < NB; ++b) red[wave][t][b][lane] = acc[t][b];
+  for (int b = 0; b < NB; ++b) red[wave][b][lane] = acc[b];
   if constexpr (NORM) {
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
       float v = ssq[b];
-      v += __shfl_xor(v, 16, 64);  // the 4 k groups of row m
+      v += __shfl_xor(v, 16, 64);
       v += __shfl_xor(v, 32, 64);
       if (lane < 16) red_ss[wave][b][lane] = v;
     }
@@ -203,12 +308,11 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_w4_kernel(const GemmArgs a,
   __syncthreads();
   if (wave != 0) return;
 #pragma unroll
-  for (int tb = 0; tb < NT * NB; ++tb) {
-    const int t = tb / NB, b = tb % NB;
+  for (int b = 0; b < NB; ++b) {
     auto unit_sum = [&](int l) -> f32x4 {
-      f32x4 v = red[0][t][b][l];
+      f32x4 v = red[0][b][l];
 #pragma unroll
-      for (int w = 1; w < WAVES; ++w) v += red[w][t][b][l];
+      for (int w = 1; w < WAVES; ++w) v += red[w][b][l];
       if constexpr (NORM) {
         float ss = 0.f;
 #pragma unroll
@@ -217,72 +321,83 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_w4_kernel(const GemmArgs a,
       }
       return v;
     };
-    epi_store<EPI>(a, t0 + t, mo + 16 * b + (lane & 15), lane, pre[t][b],
-                   [&](int off) { return unit_sum(lane + off); });
+    epi_store<EPI>(a, tg, mo + 16 * b + (lane & 15), lane, pre[b], [&](int off) { return unit_sum(lane + off); });
   }
 }
 
-template <int WAVES, int U, int NT, int NB, int EPI, bool NORM>
-static hipError_t w4_launch(const GemmArgs& a, const uint8_t* wsc, bool xl, hipStream_t st) {
-  const dim3 grid(a.N / 16 / NT * a.msplit), block(WAVES * 64);
-  if constexpr (NB == 1) {
-    if (xl) {
-      hipLaunchKernelGGL((skinny_w4_kernel<WAVES, U, NT, NB, EPI, NORM, true>), grid, block, (size_t)a.M * a.K * 2, st,
-                         a, wsc);
-      return hipGetLastError();
-    }
+// ================================================================ launch
+// kernel shapes (W4Var): stream kernels (waves, items in flight) and tile kernels (waves, quads in flight, row blocks)
+enum W4Var { W4S_8_4, W4S_4_4, W4T_8_2_1, W4T_4_4_1, W4T_8_2_2, W4T_4_2_2, W4_N_VARS };
+static const int W4_WAVES[W4_N_VARS] = {8, 4, 8, 4, 8, 4};
+static const int W4_NB[W4_N_VARS] = {1, 1, 1, 1, 2, 2};
+static bool w4_is_stream(int v) { return v <= W4S_4_4; }
+
+template <bool NORM, int EPI>
+static hipError_t w4_launch_var(int var, const GemmArgs& a, const uint8_t* wsc, int grid, int npairs, hipStream_t st) {
+  const dim3 g(grid), b8(512), b4(256);
+  switch (var) {
+    case W4S_8_4: hipLaunchKernelGGL((w4_stream_kernel<8, 4, EPI, NORM>), g, b8, 0, st, a, wsc, npairs); break;
+    case W4S_4_4: hipLaunchKernelGGL((w4_stream_kernel<4, 4, EPI, NORM>), g, b4, 0, st, a, wsc, npairs); break;
+    case W4T_8_2_1: hipLaunchKernelGGL((w4_tile_kernel<8, 2, 1, EPI, NORM>), g, b8, 0, st, a, wsc); break;
+    case W4T_4_4_1: hipLaunchKernelGGL((w4_tile_kernel<4, 4, 1, EPI, NORM>), g, b4, 0, st, a, wsc); break;
+    case W4T_8_2_2: hipLaunchKernelGGL((w4_tile_kernel<8, 2, 2, EPI, NORM>), g, b8, 0, st, a, wsc); break;
+    default: hipLaunchKernelGGL((w4_tile_kernel<4, 2, 2, EPI, NORM>), g, b4, 0, st, a, wsc); break;
   }
-  hipLaunchKernelGGL((skinny_w4_kernel<WAVES, U, NT, NB, EPI, NORM, false>), grid, block, 0, st, a, wsc);
   return hipGetLastError();
 }
 
-// kernel shapes: (waves, quads in flight, 16-row tiles of N, 16-row blocks of M) per workgroup
-enum W4Var { W4_4_8_1_1, W4_8_4_1_1, W4_4_4_2_1, W4_8_2_2_1, W4_4_2_1_2, W4_8_2_1_2, W4_N_VARS };
-
 template <bool NORM>
-static hipError_t w4_launch_e(int epi, int var, const GemmArgs& a, const uint8_t* wsc, bool xl, hipStream_t st) {
-#define CAIN_W4_VAR(E)                                                      \
-  switch (var) {                                                            \
-    case W4_4_8_1_1: return w4_launch<4, 8, 1, 1, E, NORM>(a, wsc, xl, st); \
-    case W4_8_4_1_1: return w4_launch<8, 4, 1, 1, E, NORM>(a, wsc, xl, st); \
-    case W4_4_4_2_1: return w4_launch<4, 4, 2, 1, E, NORM>(a, wsc, xl, st); \
-    case W4_8_2_2_1: return w4_launch<8, 2, 2, 1, E, NORM>(a, wsc, xl, st); \
-    case W4_4_2_1_2: return w4_launch<4, 2, 1, 2, E, NORM>(a, wsc, xl, st); \
-    default: return w4_launch<8, 2, 1, 2, E, NORM>(a, wsc, xl, st);         \
-  }
+static hipError_t w4_launch(int epi, int var, const GemmArgs& a, const uint8_t* wsc, int grid, int npairs,
+                            hipStream_t st) {
   switch (epi) {
-    case EPI_BF16: CAIN_W4_VAR(EPI_BF16)
-    case EPI_RESID: CAIN_W4_VAR(EPI_RESID)
-    case EPI_F32: CAIN_W4_VAR(EPI_F32)
-    case EPI_SILU: CAIN_W4_VAR(EPI_SILU)
-    case EPI_GELU: CAIN_W4_VAR(EPI_GELU)
-    case EPI_QKV_ROPE: CAIN_W4_VAR(EPI_QKV_ROPE)
+    case EPI_BF16: return w4_launch_var<NORM, EPI_BF16>(var, a, wsc, grid, npairs, st);
+    case EPI_RESID: return w4_launch_var<NORM, EPI_RESID>(var, a, wsc, grid, npairs, st);
+    case EPI_F32: return w4_launch_var<NORM, EPI_F32>(var, a, wsc, grid, npairs, st);
+    case EPI_SILU: return w4_launch_var<NORM, EPI_SILU>(var, a, wsc, grid, npairs, st);
+    case EPI_GELU: return w4_launch_var<NORM, EPI_GELU>(var, a, wsc, grid, npairs, st);
+    case EPI_QKV_ROPE: return w4_launch_var<NORM, EPI_QKV_ROPE>(var, a, wsc, grid, npairs, st);
     default: return hipErrorInvalidValue;
   }
-#undef CAIN_W4_VAR
 }
 
-// Tuning override (tools / tests; -1: the rule below): the kernel shape index of W4Var
-static int g_w4_var = -1;
+// Tuning / test overrides (-1 / 0: the rules below): the kernel shape (W4Var) and the stream grid's workgroups per CU
+static int g_w4_var = -1, g_w4_wgs_per_cu = 0;
 CAIN_API void cain_gemm_w4_set_variant(int v) { g_w4_var = v < W4_N_VARS ? v : -1; }
+CAIN_API void cain_gemm_w4_set_occupancy(int wgs_per_cu) { g_w4_wgs_per_cu = wgs_per_cu > 0 ? wgs_per_cu : 0; }
 
-// Few-row shape rule: the kernel variant for an (N, K, M) problem.
-static int w4_variant(int N, int K, int M, int n_cu) {
-  if (g_w4_var >= 0) return g_w4_var;
-  if (M > 16) return (N / 16) * ((M + 31) / 32) <= n_cu ? W4_8_2_1_2 : W4_4_2_1_2;
+static int w4_n_cu() {
+  static const int n = [] {
+    int dev = 0, c = 0;
+    (void)hipGetDevice(&dev);
+    return hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess ? c : 256;
+  }();
+  return n;
+}
+
+static bool w4_stream_fits(int waves, int K, int M) {
+  return M <= 16 && (long long)M * K * 2 <= (waves == 8 ? w4_xl_bytes<8>() : w4_xl_bytes<4>());
+}
+
+// Shape rule (tools/w4_bench.py, in-graph, llama3.1:8b shapes at one row: profiles/r4/README.md).  Up to 16 rows
+// whose activations fit the LDS copy: the stream kernel, 4 items in flight per wave (8 lost 1-4 us on every shape:
+// deeper queues, no faster stream), 8 waves (gate/up 14.9 vs 16.3 us on 4, LM head 46.6 vs 53.8, O 5.2 vs 5.8),
+// except the fused QKV epilogue, whose registers at 8 waves spill (9.1 vs 10.2 us on 4).  Otherwise the tile
+// kernel, two 16-row blocks per workgroup above 16 rows.
+static int w4_variant(int N, int K, int M, int epi, int n_cu) {
+  (void)N, (void)n_cu;
   const int kq = K / 128;
-  // two tiles per workgroup on LM-head-sized grids (fewer, longer workgroups); else one tile, its k quads
-  // dealt to 8 waves when the grid is at most one workgroup per CU and each wave still gets >= 4 quads
-  if (N >= 65536 && (N / 16) % 2 == 0) return kq >= 32 ? W4_8_2_2_1 : W4_4_4_2_1;
-  return (N / 16 <= n_cu && kq >= 32) ? W4_8_4_1_1 : W4_4_8_1_1;
+  if (g_w4_var >= 0) {
+    const int v = g_w4_var;
+    if (!w4_is_stream(v) || w4_stream_fits(W4_WAVES[v], K, M)) return v;  // a stream shape needs its LDS copy
+  }
+  const bool w4 = epi == EPI_QKV_ROPE && w4_stream_fits(4, K, M);
+  if (w4) return W4S_4_4;
+  if (w4_stream_fits(8, K, M)) return W4S_8_4;
+  if (M > 16) return kq >= 32 ? W4T_8_2_2 : W4T_4_2_2;
+  return kq >= 32 ? W4T_8_2_1 : W4T_4_4_1;
 }
 
-CAIN_API int cain_gemm_w4_variant(int N, int K, int M) {
-  int dev = 0, n = 0;
-  (void)hipGetDevice(&dev);
-  if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) n = 256;
-  return w4_variant(N, K, M, n);
-}
+CAIN_API int cain_gemm_w4_variant(int N, int K, int M, int epi) { return w4_variant(N, K, M, epi & EPI_MASK, w4_n_cu()); }
 
 // Same arguments as cain_gemm_w8 (gemm_w8.hip); Wp is the MXFP4 packing, wsc its e8m0 scale bytes.
 CAIN_API int cain_gemm_w4(const void* Wp, const void* wsc, const void* X, int ldx, int K, int N, int M, void* Y, int ldy,
@@ -300,19 +415,18 @@ CAIN_API int cain_gemm_w4(const void* Wp, const void* wsc, const void* X, int ld
   a.slot = slot, a.pos = pos, a.cos_t = cos_t, a.sin_t = sin_t;
   a.kc = reinterpret_cast<__bf16*>(kc), a.vtc = reinterpret_cast<__bf16*>(vtc);
   a.H = H, a.Hkv = Hkv, a.hd = hd, a.T_max = T_max, a.kv8 = (epi_flags & EPI_KV_FP8) ? 1 : 0;
-  static const int n_cu = [] {
-    int dev = 0, n = 0;
-    (void)hipGetDevice(&dev);
-    return hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess ? n : 256;
-  }();
-  const int var = w4_variant(N, K, M, n_cu);
-  const int nb = (var == W4_4_2_1_2 || var == W4_8_2_1_2) ? 2 : 1;
-  const int nt = (var == W4_4_4_2_1 || var == W4_8_2_2_1) ? 2 : 1;
-  if ((N / 16) % nt) return -1;
+  const int n_cu = w4_n_cu();
+  const int var = w4_variant(N, K, M, epi, n_cu);
+  const int nb = W4_NB[var], waves = W4_WAVES[var];
   a.msplit = (M + 16 * nb - 1) / (16 * nb);
-  // activations in LDS: one row block, at most 64 KiB of rows
-  const bool xl = nb == 1 && a.msplit == 1 && (long long)M * K * 2 <= 65536;
+  const int npairs = N / 16 * a.msplit;
+  int grid = npairs;
+  if (w4_is_stream(var)) {  // persistent: at most the resident workgroups (2 of 8 waves / 4 of 4 waves per CU)
+    a.msplit = 1;
+    grid = std::min(npairs, n_cu * (g_w4_wgs_per_cu ? g_w4_wgs_per_cu : (waves == 8 ? 2 : 4)));
+  }
   const uint8_t* sc = reinterpret_cast<const uint8_t*>(wsc);
-  const hipError_t e = norm ? w4_launch_e<true>(epi, var, a, sc, xl, st) : w4_launch_e<false>(epi, var, a, sc, xl, st);
+  const hipError_t e = norm ? w4_launch<true>(epi, var, a, sc, grid, npairs, st)
+                            : w4_launch<false>(epi, var, a, sc, grid, npairs, st);
   return int(e);
 }

@@ -17,7 +17,7 @@ from cain_amd.models.weights import (dequantize_mxfp4, fold_gain, interleave_til
                                      mxfp4_roundtrip_weights, pack_mxfp4, quantize_mxfp4, rope_pair_order)
 
 DEV = torch.device("cuda")
-N_VARS = 6  # gemm_w4.hip W4Var
+N_VARS = 6  # gemm_w4.hip W4Var: 2 persistent stream shapes, 4 tile shapes
 
 
 def rel_err(a, b):
@@ -72,16 +72,42 @@ def test_w4_gemm_f32_and_bias(M, N, K):
 
 @pytest.mark.parametrize("var", range(N_VARS))
 @pytest.mark.parametrize("M", [1, 5, 40])
-def test_w4_every_variant(var, M):
-    """Every kernel shape (waves, quads in flight, tiles, row blocks) on a K that leaves partial chunks."""
+@pytest.mark.parametrize("N", [1024, 2 * 16 * 1024 + 16])
+def test_w4_every_variant(var, M, N):
+    """Every kernel shape on a K that leaves partial chunks: 15 quads, uneven over 4 / 8 waves; the second N gives
+    the persistent stream grid several tiles per workgroup (tile edges inside the ring, the last tile alone)."""
     torch.manual_seed(2)
-    N, K = 1024, 1920  # 15 quads: uneven over 4 / 8 waves, partial copy-pipeline chunks
+    K = 1920
     W = (torch.randn(N, K, device=DEV) * 0.02).bfloat16()
     x = torch.randn(M, K, device=DEV).bfloat16()
     wq, ws, Wd = q4(W)
     ops.set_w4_variant(var)
     y = ops.gemm_w4(wq, ws, x, N, ops.EPI_F32)
     assert rel_err(y, x.float() @ Wd.t()) < 1e-3, var
+    # the fused RMSNorm (sums of squares from the first tile of each stream workgroup) and the residual epilogue
+    yn = ops.gemm_w4(wq, ws, x, N, ops.EPI_F32, norm=True, eps=1e-6)
+    xn = x.float() * torch.rsqrt(x.float().pow(2).mean(-1, keepdim=True) + 1e-6)
+    assert rel_err(yn, xn @ Wd.t()) < 2e-3, var
+    r = torch.randn(M, N, device=DEV).bfloat16()
+    ref = x.float() @ Wd.t() + r.float()
+    ops.gemm_w4(wq, ws, x, N, ops.EPI_RESID, out=r)
+    assert rel_err(r, ref) < 1e-2, var
+
+
+@pytest.mark.parametrize("occ", [1, 3])
+def test_w4_stream_grid_occupancy(occ):
+    """The persistent grid at other workgroup counts per CU (more tiles per workgroup)."""
+    torch.manual_seed(4)
+    N, K = 28672, 4096
+    W = (torch.randn(N, K, device=DEV) * 0.02).bfloat16()
+    x = torch.randn(1, K, device=DEV).bfloat16()
+    wq, ws, Wd = q4(W)
+    ops.set_w4_occupancy(occ)
+    try:
+        y = ops.gemm_w4(wq, ws, x, N, ops.EPI_F32)
+    finally:
+        ops.set_w4_occupancy(0)
+    assert rel_err(y, x.float() @ Wd.t()) < 1e-3
 
 
 @pytest.mark.parametrize("M", [1, 32])

@@ -39,6 +39,36 @@ SETS = {
         ("b1_gemma_fp4", 300, f"{B1} --weights fp4 --model gemma:2b"),
         prof("b1_llama_fp4", "--batch 1 --steps 1 --warmup 1 --no-energy --no-single --weights fp4"),
     ],
+    # round 4: the persistent stream MXFP4 kernel
+    "r4_fp4b": [
+        ("w4_tests", 600, f"{TEST} tests/test_w4_gpu.py"),
+        ("b1_llama_fp4", 300, f"{B1} --weights fp4"),
+        ("b1_qwen_fp4", 300, f"{B1} --weights fp4 --model qwen2:1.5b"),
+        ("b1_gemma_fp4", 300, f"{B1} --weights fp4 --model gemma:2b"),
+        prof("b1_llama_fp4b", "--batch 1 --steps 1 --warmup 1 --no-energy --no-single --weights fp4"),
+    ],
+    # in-graph few-row GEMM microbenchmarks (every MXFP4 kernel shape vs fp8 / bf16)
+    "r4_w4bench2": [
+        ("w4_tests", 600, f"{TEST} tests/test_w4_gpu.py"),
+        ("w4bench_llama", 400, f"{PY} tools/w4_bench.py --variants rule,0,1,2,3,4,5"),
+        ("b1_llama_fp4", 300, f"{B1} --weights fp4"),
+    ],
+    "r4_fp4c": [
+        ("w4_tests", 600, f"{TEST} tests/test_w4_gpu.py"),
+        ("w4bench_llama", 400, f"{PY} tools/w4_bench.py --variants rule,0,1,2 --dtypes fp4"),
+        ("b1_llama_fp4", 300, f"{B1} --weights fp4"),
+        ("b1_qwen_fp4", 300, f"{B1} --weights fp4 --model qwen2:1.5b"),
+        prof("b1_llama_fp4c", "--batch 1 --steps 1 --warmup 1 --no-energy --no-single --weights fp4"),
+    ],
+    "r4_norm": [
+        ("norm_on", 300, f"{PY} tools/w4_bench.py --variants 1,3,4 --norm on --dtypes fp4,fp8"),
+        ("norm_off", 300, f"{PY} tools/w4_bench.py --variants 1,3,4 --norm off --dtypes fp4,fp8"),
+    ],
+    "r4_w4bench": [
+        ("w4bench_llama", 400, f"{PY} tools/w4_bench.py --variants rule,0,1,2,3,4,5 --occ 0"),
+        ("w4bench_occ", 300, f"{PY} tools/w4_bench.py --variants 0,2 --occ 1,3,4 --dtypes fp4"),
+        ("w4bench_qwen", 300, f"{PY} tools/w4_bench.py --model qwen2:1.5b --variants rule,0,2,3,4,5"),
+    ],
     # the whole GPU suite (what the driver runs at round end)
     "suite": [("gpu_suite", 1500, f"{PY} -u -m pytest tests -m gpu -x -q --timeout 600 --timeout-method thread")],
     # the driver's bench command
