@@ -132,6 +132,11 @@ def _ptr(t: Optional[torch.Tensor]) -> Optional[int]:
     return None if t is None else t.data_ptr()
 
 
+def _set_cu_budget(lib, n: int) -> None:
+    if n or hasattr(lib, "cain_set_cu_budget"):  # (older A/B builds have no CU budget; they never run cu_limit)
+        lib.cain_set_cu_budget(n)
+
+
 def attention_splits(M: int, Hkv: int, T_max: int) -> int:
     """Position splits per (row, kv head): ~256 workgroups in flight, >= 4 blocks of 32 per split at
     full context, <= 64 splits (measured: 1024-WG targets lose more to the split combine than they
@@ -161,7 +166,7 @@ class DecodeEngine:
     def __init__(self, model: Union[str, ModelConfig], device: Union[str, torch.device] = "cuda",
                  max_batch: int = 16, max_context: int = 2048, seed: int = 0, backend: Optional[str] = None,
                  steps_per_graph: int = 8, weights: Optional[ModelWeights] = None, tokenizer=None,
-                 keep_natural: bool = False, weight_dtype: str = "bf16", kv_dtype: str = "bf16"):
+                 keep_natural: bool = False, weight_dtype: str = "bf16", kv_dtype: str = "bf16", cu_limit: int = 0):
         """``weight_dtype="fp8"``: GEMM weights quantised per row to e4m3 (half the weight bytes per decode step):
         forwards of up to 16 rows run W8A16 (gemm_w8.hip, bf16 activations), wider ones W8A8 (wgemm8.hip: the
         activations quantised per row to e4m3, fp8 MFMA) up to 256 rows; CAIN_W8A8=0 keeps W8A16 only (<= 64
@@ -170,7 +175,10 @@ class DecodeEngine:
         the reference's 4-bit precision class: W4A16 few-row kernels (gemm_w4.hip), up to 64 rows per forward;
         every GEMM K (d_model, q_dim, ffn) must be a multiple of 128.
         ``kv_dtype="fp8"``: the KV cache holds e4m3 elements (half the attention bytes per decode step and half
-        the cache memory; csrc/attention.hip KV8)."""
+        the cache memory; csrc/attention.hip KV8).
+        ``cu_limit``: run every kernel on a stream whose hardware queue may use only that many CUs (a multiple of
+        8; runtime.hip cain_stream_create_cu_limited) and size the grids for them -- the batch-1 energy lever
+        measured by tools/cu_sweep.py.  0: the whole device."""
         self.cfg = get_config(model) if isinstance(model, str) else model
         if weight_dtype not in WEIGHT_DTYPES:
             raise ValueError(f"weight_dtype must be one of {WEIGHT_DTYPES}, got {weight_dtype!r}")
@@ -180,6 +188,9 @@ class DecodeEngine:
             raise ValueError(f"kv_dtype must be 'bf16' or 'fp8', got {kv_dtype!r}")
         self.weight_dtype = weight_dtype
         self.kv_dtype = kv_dtype
+        self.cu_limit = int(cu_limit)
+        if self.cu_limit and (self.cu_limit < 0 or self.cu_limit % 8):
+            raise ValueError(f"cu_limit must be a positive multiple of 8 (or 0), got {cu_limit}")
         # W8A8 needs whole 128-deep stages, >= 4 of them, on every GEMM's K (all real configs; not the tiny ones)
         self.w8a8 = (weight_dtype == "fp8" and os.environ.get("CAIN_W8A8", "1") != "0"
                      and all(k % 128 == 0 and k >= 512 for k in (self.cfg.d_model, self.cfg.q_dim, self.cfg.ffn)))
@@ -296,7 +307,17 @@ class DecodeEngine:
         self._desc = d
         self._plans: Dict[int, int] = {}
         self._graphs: Dict[tuple, int] = {}
-        self.stream = torch.cuda.Stream(device=dev)
+        self._cu_stream = None
+        if self.cu_limit and self.cu_limit < torch.cuda.get_device_properties(dev).multi_processor_count:
+            with torch.cuda.device(dev):
+                h = self.lib.cain_stream_create_cu_limited(self.cu_limit)
+            if not h:
+                raise RuntimeError(f"hipExtStreamCreateWithCUMask failed for {self.cu_limit} CUs")
+            self._cu_stream = h
+            self.stream = torch.cuda.ExternalStream(h, device=dev)
+        else:
+            self.cu_limit = 0
+            self.stream = torch.cuda.Stream(device=dev)
 
     def _wide_gemm_plans(self, R: int) -> list:
         """Split plans of the wide-batch GEMM (csrc/wgemm.hip) this engine runs, per projection shape at its
@@ -337,8 +358,13 @@ class DecodeEngine:
 
     def _forward(self, M: int, rows, want_logits: bool, want_sample: bool) -> None:
         rs = self._rows_struct(rows, want_sample)
-        rc = self.lib.cain_plan_forward(ctypes.c_void_p(self._plan(M)), M, ctypes.byref(rs), int(want_logits),
-                                        int(want_sample), ctypes.c_void_p(self.stream.cuda_stream))
+        plan = self._plan(M)
+        _set_cu_budget(self.lib, self.cu_limit)  # launch sizing for this engine's stream (0: whole device)
+        try:
+            rc = self.lib.cain_plan_forward(ctypes.c_void_p(plan), M, ctypes.byref(rs), int(want_logits),
+                                            int(want_sample), ctypes.c_void_p(self.stream.cuda_stream))
+        finally:
+            _set_cu_budget(self.lib, 0)
         if rc != 0:
             where = self.lib.cain_plan_last_failure()
             raise RuntimeError(f"cain_plan_forward failed rc={rc}" + (f" at {where.decode()}" if where else ""))
@@ -349,8 +375,13 @@ class DecodeEngine:
         if g is None:
             rs = self._rows_struct(self.rows, True)
             err = ctypes.c_int(0)
-            g = self.lib.cain_plan_capture(ctypes.c_void_p(self._plan(M)), M, ctypes.byref(rs), steps,
-                                           ctypes.c_void_p(self.stream.cuda_stream), ctypes.byref(err))
+            plan = self._plan(M)
+            _set_cu_budget(self.lib, self.cu_limit)
+            try:
+                g = self.lib.cain_plan_capture(ctypes.c_void_p(plan), M, ctypes.byref(rs), steps,
+                                               ctypes.c_void_p(self.stream.cuda_stream), ctypes.byref(err))
+            finally:
+                _set_cu_budget(self.lib, 0)
             if not g:
                 raise RuntimeError(f"hipGraph capture failed (err={err.value})")
             self._graphs[key] = g
@@ -365,6 +396,10 @@ class DecodeEngine:
         for p in self._plans.values():
             lib.cain_plan_destroy(ctypes.c_void_p(p))
         self._graphs, self._plans = {}, {}
+        if getattr(self, "_cu_stream", None):
+            self.stream.synchronize()
+            lib.cain_stream_destroy(ctypes.c_void_p(self._cu_stream))
+            self._cu_stream = None
 
     def __del__(self):  # pragma: no cover
         try:

@@ -116,6 +116,12 @@ def load() -> ctypes.CDLL:
         lib.cain_plan_capture.argtypes = [vp, ci, vp, ci, vp, ctypes.POINTER(ci)]
         lib.cain_graph_launch.argtypes = [vp, vp]
         lib.cain_graph_destroy.argtypes = [vp]
+        if hasattr(lib, "cain_set_cu_budget"):  # (absent from older builds loaded by CAIN_KERNELS_LIB for A/B runs)
+            lib.cain_set_cu_budget.argtypes = [ci]
+            lib.cain_cu_mask.argtypes = [ci, ci, ctypes.POINTER(ctypes.c_uint32), ci]
+            lib.cain_stream_create_cu_limited.restype = vp
+            lib.cain_stream_create_cu_limited.argtypes = [ci]
+            lib.cain_stream_destroy.argtypes = [vp]
         _lib = lib
         return lib
 
@@ -473,16 +479,36 @@ def attention(q, kc, vtc, slot, pos, H, Hkv, hd, nsplit, scale, out=None, part_o
 def set_sample_cm(mode: int) -> None:
     """Chunk-maximum sampler (the LM head writes 16-column chunk maxima, the sampler reads only the chunks above a
     provable threshold; same tokens).  mode 0 off, 1 every decode forward, 2 forwards of more than 64 rows (the
-    default, CAIN_SAMPLE_CM=2: 42 vs 62 us at 256 rows; at batch 1 the two-stage kernel is faster).  A/B switch,
-    read at every forward / graph capture."""
+    default: 42 vs 62 us at 256 rows; at batch 1 the two-stage kernel is faster).  A/B switch for tests and
+    profiles, read at every forward / graph capture."""
     load().cain_sample_set_cm(int(mode))
 
 
 def set_skinny_split(mode: int) -> None:
     """Split-K rule of the few-row (<= 16) skinny GEMM (gemm.hip skinny_split): 0 never, 1 narrow long-K grids
-    (default), 2 also grids between one and two tiles per CU (k halved).  Takes effect at the next launch; an
+    (default).  Takes effect at the next launch; an
     engine's workspace is sized at construction, so switch before building one."""
     load().cain_gemm_set_skinny_split(int(mode))
+
+
+def cu_mask(n_cu: int, total: int = 256) -> list:
+    """The 32-bit words of the CU mask a CU-limited stream uses (runtime.hip cain_cu_mask): n_cu of ``total`` CUs
+    as evenly spaced whole groups of 8 consecutive bits (balanced over the XCDs under either CU numbering)."""
+    words = (total + 31) // 32
+    arr = (ctypes.c_uint32 * words)()
+    if load().cain_cu_mask(int(n_cu), int(total), arr, words) != 0:
+        raise ValueError(f"no CU mask of {n_cu} of {total} CUs (multiples of 8 only)")
+    return list(arr)
+
+
+def set_cu_budget(n_cu: int) -> None:
+    """CUs the launch sizing of persistent / CU-proportional grids assumes (0: the device's).  The engine sets it
+    around every forward and graph capture of a CU-limited engine (``DecodeEngine(cu_limit=...)``)."""
+    load().cain_set_cu_budget(int(n_cu))
+
+
+def cu_budget() -> int:
+    return int(load().cain_get_cu_budget())
 
 
 def sample_cm_mode() -> int:
@@ -493,7 +519,7 @@ def sample_cm_mode() -> int:
 def set_attention_ring(variant: int) -> None:
     """LDS-DMA ring body of the wide decode attention (csrc/attention.hip attn_ring_kernel; hd 128, bf16 cache,
     one split, 2 to 64 (row, kv head) pairs per CU): 0 off (the register kernel), 1 on (the default).  A/B switch
-    (CAIN_ATTN_RING), read at every launch and graph capture."""
+    for tests and profiles, read at every launch and graph capture."""
     load().cain_attention_set_ring(int(variant))
 
 

@@ -295,24 +295,14 @@ __global__ __launch_bounds__(AW * 64, OCC) void attn_decode_kernel(
   }
 }
 
-// CAIN_ATTN_NT=0: default-policy cache loads instead of non-temporal ones (A/B runs)
-static bool attn_nt() {
-  static const bool nt = [] {
-    const char* e = getenv("CAIN_ATTN_NT");
-    return !(e && e[0] == '0');
-  }();
-  return nt;
-}
-
-// Body for hd <= 128 (CAIN_ATTN_VARIANT, A/B runs): 2 = one register set held to 128 registers (4 waves per
-// SIMD; default), 1 = one set (3 waves per SIMD), 0 = two register sets (2 waves per SIMD; round 1's body).
-static int attn_variant() {
-  static const int v = [] {
-    const char* e = getenv("CAIN_ATTN_VARIANT");
-    return e && *e ? atoi(e) : 2;
-  }();
-  return v;
-}
+// Cache loads are non-temporal (default-policy loads measured slower); the hd <= 128 body holds one register set to
+// 128 registers (4 waves per SIMD; the two-set and 3-wave bodies of rounds 1-2 measured slower,
+// profiles/r2/attn_occupancy.md).  cain_attention_set_body selects them for A/B runs: 2 = default, 1 = one set at
+// 3 waves per SIMD, 0 = two register sets.
+static int g_attn_body = 2;
+CAIN_API void cain_attention_set_body(int v) { g_attn_body = v; }
+static bool attn_nt() { return true; }
+static int attn_variant() { return g_attn_body; }
 
 template <int HD, int AW, bool KV8, bool NT>
 static void launch_attn_t(const void* q, const void* kc, const void* vtc, const int* slot, const int* pos,
@@ -359,7 +349,7 @@ static hipError_t launch_attn(const void* q, const void* kc, const void* vtc, co
 
 
 // =====================================================================================================
-// Wide decode attention on an LDS-DMA ring (LDS-staged KV tiles; the default wide body, CAIN_ATTN_RING).
+// Wide decode attention on an LDS-DMA ring (LDS-staged KV tiles; the default wide body).
 //
 // One workgroup per CU, persistent over the (row, kv head) pairs: 4 compute waves, each owning whole pairs (pair
 // blockIdx.x + (c + 4 i) * gridDim.x for compute wave c), so no cross-wave merge; and 4 loader waves, loader c
@@ -602,20 +592,13 @@ CAIN_API int cain_attention_ex(const void* q, const void* kc, const void* vtc, c
                                int Hkv, int hd, int T_max, int nsplit, float scale, int kv8, float kscale,
                                float vscale, hipStream_t st) {
   if (H % Hkv || H / Hkv > 16 || T_max % 32 || nsplit < 1 || nsplit > 64 || M > 256) return -1;
-  // LDS-DMA ring body (default for hd 128, bf16 cache, no position split, >= 2 pairs per CU; CAIN_ATTN_RING=0 or
+  // LDS-DMA ring body (default for hd 128, bf16 cache, no position split, >= 2 pairs per CU;
   // cain_attention_set_ring(0) selects the register kernel).  Measured (profiles/r3/README.md, same box): 113.3 vs
   // 113.7 us at 256 rows x 700 positions, 217.8 vs 221.5 at 1400 (6.74 TB/s), 60.3 vs 58.6 at 350; in the
   // graph-replayed headline 27.44k vs 27.21-27.23k tok/s.  The 2 x 4 and 3 x 3 ring shapes measured slower and
   // were removed (profiles/r3/attn_ring_isolated.log).
-  if (g_attn_ring < 0) {
-    const char* e = getenv("CAIN_ATTN_RING");
-    g_attn_ring = e && *e ? atoi(e) : 1;
-  }
-  static const int n_cu = [] {
-    int dev = 0, n = 0;
-    (void)hipGetDevice(&dev);
-    return hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess ? n : 0;
-  }();
+  if (g_attn_ring < 0) g_attn_ring = 1;
+  const int n_cu = cain_cu_budget();
   if (g_attn_ring && hd == 128 && !kv8 && nsplit == 1 && n_cu > 0 && M * Hkv >= 2 * n_cu &&
       M * Hkv <= ring::LMAX * ring::NC * n_cu) {
     constexpr int lds = ring::NC * ring::R * 16 * 1024;

@@ -14,6 +14,10 @@ typedef uint16_t u16x4 __attribute__((ext_vector_type(4)));
 
 #define CAIN_API extern "C" __attribute__((visibility("default")))
 
+// CUs the launch sizing of the persistent / CU-proportional grids assumes: the device's, or the smaller budget of
+// cain_set_cu_budget (runtime.hip) while the work runs on a CU-masked stream (cain_stream_create_cu_limited).
+extern "C" int cain_cu_budget();
+
 __device__ __forceinline__ float bf2f(__bf16 v) { return static_cast<float>(v); }
 __device__ __forceinline__ __bf16 f2bf(float v) { return static_cast<__bf16>(v); }  // v_cvt_pk_bf16_f32 (RNE, NaN-safe)
 
@@ -26,6 +30,17 @@ __device__ __forceinline__ float wave_max(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
   return v;
+}
+
+// Maximum over each 16-lane row of the wave for NON-NEGATIVE floats (their bit patterns order as integers): four
+// DPP row rotations, VALU only -- no LDS round trip (wave_max's ds_bpermute chain costs ~6 waits per value).
+__device__ __forceinline__ float row16_max_nonneg(float v) {
+  int x = __float_as_int(v);
+  x = max(x, __builtin_amdgcn_update_dpp(x, x, 0x128, 0xf, 0xf, false));  // row_ror:8
+  x = max(x, __builtin_amdgcn_update_dpp(x, x, 0x124, 0xf, 0xf, false));  // row_ror:4
+  x = max(x, __builtin_amdgcn_update_dpp(x, x, 0x122, 0xf, 0xf, false));  // row_ror:2
+  x = max(x, __builtin_amdgcn_update_dpp(x, x, 0x121, 0xf, 0xf, false));  // row_ror:1
+  return __int_as_float(x);
 }
 
 // Epilogue math on the hardware reciprocal / reciprocal square root (v_rcp_f32 / v_rsq_f32, ~1 ulp): hipcc's IEEE

@@ -53,18 +53,12 @@ struct SkArgs {
   float* part_ss;      // [ntiles][ks][16]
 };
 
-// XL (one row block, M <= 16, M * K * 2 <= 64 KiB, unsplit, copy pipeline): the activation rows are staged once
-// into LDS by LDS-DMA and every k-slice reads its fragment from LDS -- one vector-memory load instruction per
-// KiB of weights instead of two.  The fp8 kernel (gemm_w8.hip) gains from it; this bf16 one does not (single
-// stream llama3.1:8b 340.8 -> 339.5 tok/s, qwen2:1.5b 852.9 -> 845.3; 8 slices in flight 316.9 / 768.1:
-// profiles/r3/b1_xlds_ab.txt), so it stays an A/B option (CAIN_SKINNY_XLDS).
-typedef __attribute__((address_space(3))) void sk_lds_t;
-typedef __attribute__((address_space(1))) const void sk_gbl_t;
-
-template <int NT, int NB, int WAVES, int U, int EPI, bool NORM, bool PP, bool SPLIT = false, bool XL0 = false>
+// (Round 3 also kept the activations staged in LDS (XL) and a two-register-set ping-pong loop (PP) as A/B
+// options of this kernel; both measured slower or level in the single-stream decode -- llama3.1:8b 340.8 -> 339.5
+// tok/s with XL, profiles/r3/b1_xlds_ab.txt -- and were removed.  The MXFP4 kernel (gemm_w4.hip) stages its
+// activations, where they replace four fragment loads per KiB of weights.)
+template <int NT, int NB, int WAVES, int U, int EPI, bool NORM, bool SPLIT = false>
 __global__ __launch_bounds__(WAVES * 64) void skinny_gemm_kernel(const GemmArgs a, const SkArgs sk) {
-  constexpr bool XL = XL0 && NB == 1 && !PP && !SPLIT;
-  extern __shared__ __attribute__((aligned(16))) char sk_xs[];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int K = a.K;
@@ -127,28 +121,7 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_gemm_kernel(const GemmArgs 
   // (always non-temporal: a runtime choice of the cache policy put a branch around every load, which
   // defeats the counted waits of the pipeline below; with msplit > 1 the tile-mates still hit L2/MALL)
   auto load_w = [&](int s, int t) -> bf16x8 { return __builtin_nontemporal_load(wbase[t] + (size_t)s * 64); };
-  // XL: this lane's row in the LDS copy (rows past M re-read row M-1) at its k-group
-  const __bf16* xl_row =
-      reinterpret_cast<const __bf16*>(sk_xs) + (size_t)min(lane & 15, a.M - 1) * K + ((lane >> 4) << 3);
-  auto load_x = [&](int s, int b) -> bf16x8 {
-    if constexpr (XL) return *reinterpret_cast<const bf16x8*>(xl_row + s * 32);
-    else return *reinterpret_cast<const bf16x8*>(xbase[b] + s * 32);
-  };
-  // XL: rows [0, M) x K into LDS by LDS-DMA (16-byte chunk c <- row c / (K / 8), column chunk c % (K / 8); wave
-  // instruction j covers chunks 64 j .. 64 j + 63), then every wave's copy has landed
-  auto stage_x = [&]() {
-    const int cpr = K >> 3, nch = a.M * cpr;
-    for (int j = wave; j * 64 < nch; j += WAVES) {
-      const int c = j * 64 + lane;
-      if (c < nch) {
-        const int r = c / cpr, col = c - r * cpr;
-        __builtin_amdgcn_global_load_lds((sk_gbl_t*)(a.X + (size_t)r * a.ldx + col * 8), (sk_lds_t*)(sk_xs + j * 1024),
-                                         16, 0, 0);
-      }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-  };
+  auto load_x = [&](int s, int b) -> bf16x8 { return *reinterpret_cast<const bf16x8*>(xbase[b] + s * 32); };
   // RMSNorm factorisation: (W diag(g)) (x * inv) = inv * ((W diag(g)) x); the per-row inv is applied in
   // the epilogue and the sum of squares is accumulated from the x fragments this WG streams anyway
   // (its waves cover all of K), so no separate norm kernel and no cross-kernel sum-of-squares buffer.
@@ -183,45 +156,17 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_gemm_kernel(const GemmArgs 
     }
   };
 
-  // ---- software-pipelined main loop, branch-free and copy-free: group g+1's loads (clamped to the
-  // last full group) are issued before group g computes, into the other of two register sets that
-  // ping-pong (the loop is unrolled by two; an odd group count runs one masked dummy group).  A
-  // register copy of an in-flight load, or loads under a branch, made the compiler wait vmcnt(0).
+  // ---- copy pipeline: the next U slices' loads are issued before the current U compute (the compiler schedules
+  // the loads and their counted waits itself)
   int s = s_beg;
   const int nfull = (s_end - s_beg) / U;
-  if constexpr (PP) {
-    if (nfull > 0) {
-      const int s_lastf = s_beg + nfull * U - 1;
-      bf16x8 wa[U][NT], xa[U][NB], wb2[U][NT], xb2[U][NB];
-      auto load_group = [&](int s0, bf16x8 (&w)[U][NT], bf16x8 (&x)[U][NB]) {
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          const int si = min(s0 + u, s_lastf);
-#pragma unroll
-          for (int t = 0; t < NT; ++t) w[u][t] = load_w(si, t);
-#pragma unroll
-          for (int b = 0; b < NB; ++b) x[u][b] = load_x(si, b);
-        }
-      };
-      load_group(s, wa, xa);
-      for (int g = 0; g < nfull; g += 2) {
-        load_group(s_beg + (g + 1) * U, wb2, xb2);
-        __builtin_amdgcn_sched_barrier(0);
-        compute(wa, xa, true);
-        load_group(s_beg + (g + 2) * U, wa, xa);
-        __builtin_amdgcn_sched_barrier(0);
-        compute(wb2, xb2, g + 1 < nfull);
-      }
-      s = s_beg + nfull * U;
-    }
-  } else if (nfull > 0) {  // register-copy pipeline (the compiler schedules the loads itself)
+  if (nfull > 0) {
     bf16x8 wa[U][NT], xa[U][NB];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
 #pragma unroll
       for (int t = 0; t < NT; ++t) wa[u][t] = load_w(s + u, t);
     }
-    if constexpr (XL) stage_x();  // under the weight prologue's latency
 #pragma unroll
     for (int u = 0; u < U; ++u) {
 #pragma unroll
@@ -252,8 +197,6 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_gemm_kernel(const GemmArgs 
       }
       s = sn;
     }
-  } else if constexpr (XL) {
-    stage_x();
   }
   for (; s < s_end; ++s) {
 #pragma unroll
@@ -382,41 +325,17 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_gemm_kernel(const GemmArgs 
 
 template <int NT, int NB, int WAVES, int EPI, bool NORM>
 static hipError_t launch_t(const GemmArgs& a, const SkArgs& sk, hipStream_t st) {
-  constexpr int U = (NB >= 2) ? 2 : 4;  // x2 register sets (pipelined)
-  static const int pp = [] {
-    const char* e = getenv("CAIN_SKINNY_PP");
-    return e ? atoi(e) : 0;
-  }();
+  constexpr int U = (NB >= 2) ? 2 : 4;  // slices in flight per wave
   if (sk.ks > 1) {
     if constexpr (NT == 1 && NB == 1) {
-      hipLaunchKernelGGL((skinny_gemm_kernel<NT, NB, WAVES, U, EPI, NORM, false, true>), dim3(a.N / 16 * sk.ks),
+      hipLaunchKernelGGL((skinny_gemm_kernel<NT, NB, WAVES, U, EPI, NORM, true>), dim3(a.N / 16 * sk.ks),
                          dim3(WAVES * 64), 0, st, a, sk);
       return hipGetLastError();
     }
     return hipErrorInvalidValue;
   }
-  // activations staged in LDS (XL): CAIN_SKINNY_XLDS=0 off, 1 on, 8 on with 8 slices in flight (A/B)
-  static const int xlds = [] {
-    const char* e = getenv("CAIN_SKINNY_XLDS");
-    return e ? atoi(e) : 0;
-  }();
-  if constexpr (NB == 1) {
-    if (xlds && !pp && a.msplit == 1 && (long long)a.M * a.K * 2 <= 65536) {
-      if (xlds >= 8)  // 8 slices in flight per wave (the LDS copy frees the activation registers)
-        hipLaunchKernelGGL((skinny_gemm_kernel<NT, NB, WAVES, 8, EPI, NORM, false, false, true>),
-                           dim3(a.N / (16 * NT) * a.msplit), dim3(WAVES * 64), (size_t)a.M * a.K * 2, st, a, sk);
-      else
-        hipLaunchKernelGGL((skinny_gemm_kernel<NT, NB, WAVES, U, EPI, NORM, false, false, true>),
-                           dim3(a.N / (16 * NT) * a.msplit), dim3(WAVES * 64), (size_t)a.M * a.K * 2, st, a, sk);
-      return hipGetLastError();
-    }
-  }
-  if (pp)
-    hipLaunchKernelGGL((skinny_gemm_kernel<NT, NB, WAVES, U, EPI, NORM, true>), dim3(a.N / (16 * NT) * a.msplit),
-                       dim3(WAVES * 64), 0, st, a, sk);
-  else
-    hipLaunchKernelGGL((skinny_gemm_kernel<NT, NB, WAVES, U, EPI, NORM, false>), dim3(a.N / (16 * NT) * a.msplit),
-                       dim3(WAVES * 64), 0, st, a, sk);
+  hipLaunchKernelGGL((skinny_gemm_kernel<NT, NB, WAVES, U, EPI, NORM>), dim3(a.N / (16 * NT) * a.msplit),
+                     dim3(WAVES * 64), 0, st, a, sk);
   return hipGetLastError();
 }
 
@@ -452,25 +371,14 @@ static hipError_t launch_e(int epi, int waves, const GemmArgs& a, const SkArgs& 
 // qwen2:1.5b's QKV) costs more than it spreads.  (Also measured and not kept: "one-shot" waves that load all of
 // their <= 16 slices in one burst before any MFMA -- the 128 staging VGPRs halve the resident waves, and with
 // them the bytes in flight: qwen2:1.5b gate/up 11.9 -> 12.5 us, split down 9.0 -> 10.4 us, gpurun_out/r3d.)
-// CAIN_SKINNY_SPLIT=0 disables it.  CAIN_SKINNY_SPLIT=2 (A/B) also halves the k-range of grids between one and
-// two tiles per CU (llama3.1:8b QKV at one row: 384 tiles on 256 CUs): measured slower -- QKV 12.3 -> 15.4 us,
-// 338 -> 328 tok/s single stream (profiles/r3/b1_skinny_split2_ab.txt): the uneven rounds overlap anyway (several
-// workgroups per CU), and the combine round trip is pure added latency.
-static int g_skinny_split = -1;
+// cain_gemm_set_skinny_split(0) disables it (tests).  (Halving the k-range of grids between one and two tiles
+// per CU -- llama3.1:8b QKV at one row -- measured slower, 338 -> 328 tok/s single stream, and was removed:
+// profiles/r3/b1_skinny_split2_ab.txt.)
+static int g_skinny_split = 1;
 CAIN_API void cain_gemm_set_skinny_split(int mode) { g_skinny_split = mode; }
 static int skinny_split(int N, int K, int M) {
-  if (g_skinny_split < 0) {
-    const char* e = getenv("CAIN_SKINNY_SPLIT");
-    g_skinny_split = e ? atoi(e) : 1;
-  }
   const int on = g_skinny_split;
-  static const int n_cu = [] {
-    int dev = 0, n = 0;
-    (void)hipGetDevice(&dev);
-    return hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess ? n : 0;
-  }();
   const int nt = N / 16, KS = K / 32;
-  if (on == 2 && M <= 16 && n_cu > 0 && nt > n_cu && nt < 2 * n_cu && KS >= 64) return 2;
   if (!on || M > 16 || nt >= 192 || nt < 1 || KS <= 128) return 1;
   // ~80 slices per workgroup, at most ~512 workgroups (qwen2:1.5b down: ks 4 = 9.0 us vs ks 3 = 10.4 us)
   return std::max(1, std::min(std::min(8, (KS + 79) / 80), 512 / nt));
@@ -480,27 +388,12 @@ static int skinny_split(int N, int K, int M) {
 // unless the grid is small (then 16, to keep >= ~2k waves streaming) or K is too short to give each
 // wave two pipelined chunks.
 static int pick_waves(int n_wg, int ks, bool split = false) {
-  // grids of (b, 2b] workgroups, b = the CU count, on 4 waves (CAIN_SKINNY_W4 = b overrides, 0 disables):
-  // llama3.1:8b's 384-workgroup QKV at one row 12.3 -> 11.9 us, single stream 340.7 -> 341.8 tok/s (same box,
-  // interleaved; qwen2:7b 356.2 -> 356.9; profiles/r3/b1_skinny_w4_ab.txt).  The fp8 kernel showed it first.
-  static const int w4 = [] {
-    const char* e = getenv("CAIN_SKINNY_W4");
-    if (e) return atoi(e);
-    int dev = 0, n = 0;
-    (void)hipGetDevice(&dev);
-    return hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess ? n : 0;
-  }();
-  static const int w4x = [] {  // upper bound, in multiples of b (CAIN_SKINNY_W4X; A/B)
-    const char* e = getenv("CAIN_SKINNY_W4X");
-    return e ? atoi(e) : 2;
-  }();
-  if (!split && w4 > 0 && n_wg > w4 && n_wg <= w4x * w4 && ks / 4 >= 8) return 4;  // unsplit grids (measured)
-  // A/B (CAIN_SKINNY_W16 = b): unsplit grids of <= b workgroups on 16 waves when every wave keeps >= 8 slices
-  static const int w16 = [] {
-    const char* e = getenv("CAIN_SKINNY_W16");
-    return e ? atoi(e) : 0;
-  }();
-  if (!split && w16 > 0 && n_wg <= w16 && ks / 16 >= 8) return 16;
+  // grids of (b, 2b] workgroups, b = the CU count, on 4 waves: llama3.1:8b's 384-workgroup QKV at one row 12.3 ->
+  // 11.9 us, single stream 340.7 -> 341.8 tok/s (same box, interleaved; qwen2:7b 356.2 -> 356.9;
+  // profiles/r3/b1_skinny_w4_ab.txt).  (A wider (b, 8b] range and 16-wave workgroups for grids of <= b measured
+  // mixed / level and were removed.)
+  const int w4 = cain_cu_budget();
+  if (!split && w4 > 0 && n_wg > w4 && n_wg <= 2 * w4 && ks / 4 >= 8) return 4;  // unsplit grids (measured)
   int w = 8;
   if (n_wg * w < 1024 && ks / 16 >= 8) w = 16;
   while (w > 4 && ks / w < 8) w /= 2;
@@ -970,19 +863,11 @@ struct BgPlan {
 //  * no k-split once >= 128 row blocks exist (gate/up, LM head): the fp32 partials + combine cost more
 //    than the idle CUs;
 //  * otherwise ceil(target / row blocks) k-ranges, target 128 workgroups for K <= 4096 and 256 for longer
-//    K (down projection), at most 8.  Env overrides: CAIN_BGEMM_NTW, CAIN_BGEMM_WG, CAIN_BGEMM_KSMAX.
-static int env_int(const char* name, int dflt) {
-  const char* e = getenv(name);
-  return e ? atoi(e) : dflt;
-}
-
+//    K (down projection), at most 8.
+// (Round 1-2's A/B knobs of this plan -- workgroup target, waves, chunk, ring depth, wave rows -- are fixed at the
+// measured defaults; the alternatives are in profiles/bgemm_sweep.md and profiles/bgemm_r1.md.)
 static BgPlan bgemm_plan(int N, int K, int M, int ntw_req) {
-  static const int target_env = env_int("CAIN_BGEMM_WG", 0);
-  static const int ksmax = env_int("CAIN_BGEMM_KSMAX", 8);
-  static const int w_env = env_int("CAIN_BGEMM_W", 0);
-  static const int ck_env = env_int("CAIN_BGEMM_CK", 0);
-  static const int d_env = env_int("CAIN_BGEMM_D", -1);
-  static const int wm_env = env_int("CAIN_BGEMM_WM", 1);
+  constexpr int ksmax = 8;
   BgPlan p{};
   p.wm = 1;
   p.nb = M <= 32 ? 2 : (M <= 64 ? 4 : (M <= 128 ? 8 : 16));
@@ -992,37 +877,30 @@ static BgPlan bgemm_plan(int N, int K, int M, int ntw_req) {
   // measured faster on N <= 6144 (O / QKV / down projections at M = 64: 23.1 vs 25.6, 27.0 vs 30.0,
   // 41.1 vs 46.5 us; profiles/bgemm_sweep.md)
   const bool narrow = N <= 6144 && p.ntw == 1;
-  p.w = (w_env == 4 || (w_env == 0 && narrow)) && p.ntw == 1 ? 4 : BG_WAVES;
+  p.w = narrow ? 4 : BG_WAVES;
   if (p.nb == 16) {
     // 256 rows: 8 waves x 1 tile, 4-slice chunks, 128 KiB of stages (4 waves x 2 tiles at one wave per SIMD
     // measured 10-20 % slower on every shape, profiles/bgemm_r1.md)
     p.w = 8;
     p.ck = 4;
-    if (wm_env == 2) p.wm = 2, p.ntw = 2;
-    // 16 waves as 8 columns x 2 rows, one tile each: 4 waves per SIMD (128 VGPRs) to hide the weight latency
-    if (wm_env == 3) p.wm = 2, p.ntw = 1, p.w = 16;
   } else if (p.nb == 8) {
-    // 128 rows: 4-slice chunks keep the double-buffered stage at 64 KiB (2 workgroups per CU)
-    p.ck = p.w == 8 && ck_env == 8 ? 8 : 4;
-    // activation + weight register rings, depth 4, on the 4-wave (narrow-output) bodies; CAIN_BGEMM_D = 4 also on
-    // the 8-wave ones, any other value: off (depths 6 and 8 measured slower, profiles/bgemm_r1.md)
-    if (p.ck == 4) p.d = d_env == 4 ? 4 : (d_env < 0 && p.w == 4 ? 4 : 0);
-    if (wm_env == 2 && p.w == 8 && p.ck == 4) p.wm = 2, p.ntw = 2, p.d = 0;
-  }
-  else
-  {
+    // 128 rows: 4-slice chunks keep the double-buffered stage at 64 KiB (2 workgroups per CU); activation + weight
+    // register rings, depth 4, on the 4-wave (narrow-output) bodies (depths 6 and 8, and the ring on the 8-wave
+    // bodies, measured slower, profiles/bgemm_r1.md)
+    p.ck = 4;
+    p.d = p.w == 4 ? 4 : 0;
+  } else {
     // 64 rows: the mid-width gate/up projection measured faster with 4-slice chunks too (43.8 vs 47.0 us)
     const int nblk8 = (N + 16 * BG_WAVES - 1) / (16 * BG_WAVES);
     const bool mid = p.nb == 4 && nblk8 >= 128 && nblk8 < 512;
     p.ck = p.w == 4 ? 4  // the 4-wave variants run the deep register ring: one prefetch group per chunk
-           : (ck_env == 16 && p.ntw == 1 && (K / 32) % 16 == 0) ? 16
-           : (p.ntw == 1 && (ck_env == 4 || (ck_env == 0 && mid))) ? 4 : BG_CK;
+           : (p.ntw == 1 && mid) ? 4 : BG_CK;
   }
   const int rows = 16 * (p.w / p.wm) * p.ntw;
   p.nblk = (N + rows - 1) / rows;
   const int nchunk = (K / 32) / p.ck;
-  const int target = target_env > 0 ? target_env : (K > 4096 ? 256 : 128);
-  int ks = p.nblk >= 128 && target_env <= 0 ? 1 : std::max(1, std::min(std::min(nchunk, ksmax), (target + p.nblk - 1) / p.nblk));
+  const int target = K > 4096 ? 256 : 128;
+  int ks = p.nblk >= 128 ? 1 : std::max(1, std::min(std::min(nchunk, ksmax), (target + p.nblk - 1) / p.nblk));
   const int cpw = (nchunk + ks - 1) / ks;
   ks = (nchunk + cpw - 1) / cpw;
   p.ksplit = ks;
@@ -1083,26 +961,18 @@ static hipError_t bg_launch_e(int epi, const GemmArgs& a, const BgArgs& b, int n
 template <int NB, bool NORM>
 static hipError_t bg_launch_shape(int epi, const BgPlan& p, const GemmArgs& a, const BgArgs& b, hipStream_t st) {
   if constexpr (NB == 16) {
-    if (p.wm == 2 && p.w == 16) return bg_launch_e<16, 1, 16, 4, NORM, 0, 2>(epi, a, b, p.nblk, st);
-    if (p.wm == 2) return bg_launch_e<16, 2, 8, 4, NORM, 0, 2>(epi, a, b, p.nblk, st);
     return bg_launch_e<16, 1, 8, 4, NORM>(epi, a, b, p.nblk, st);
   } else if constexpr (NB == 8) {
-    if (p.wm == 2) return bg_launch_e<8, 2, 8, 4, NORM, 0, 2>(epi, a, b, p.nblk, st);
     // register rings for activations AND weights (AR) of depth p.d; not for the fused-norm bodies, whose
     // staging sums of squares make the rings spill (profiles/bgemm_r1.md)
     if constexpr (!NORM) {
-      if (p.d == 4) {
-        if (p.w == 4) return bg_launch_e<8, 1, 4, 4, NORM, 4>(epi, a, b, p.nblk, st);
-        return bg_launch_e<8, 1, 8, 4, NORM, 4>(epi, a, b, p.nblk, st);
-      }
+      if (p.d == 4) return bg_launch_e<8, 1, 4, 4, NORM, 4>(epi, a, b, p.nblk, st);
     }
     if (p.w == 4) return bg_launch_e<8, 1, 4, 4, NORM>(epi, a, b, p.nblk, st);
-    if (p.ck == 8) return bg_launch_e<8, 1, 8, 8, NORM>(epi, a, b, p.nblk, st);
     return bg_launch_e<8, 1, 8, 4, NORM>(epi, a, b, p.nblk, st);
   } else {
     if (p.ntw == 2) return bg_launch_e<NB, 2, 8, 8, NORM>(epi, a, b, p.nblk, st);
     if (p.w == 4) return bg_launch_e<NB, 1, 4, 4, NORM>(epi, a, b, p.nblk, st);
-    if (p.ck == 16) return bg_launch_e<NB, 1, 8, 16, NORM>(epi, a, b, p.nblk, st);
     if (p.ck == 4) return bg_launch_e<NB, 1, 8, 4, NORM>(epi, a, b, p.nblk, st);
     return bg_launch_e<NB, 1, 8, 8, NORM>(epi, a, b, p.nblk, st);
   }
@@ -1123,15 +993,9 @@ static int bgemm_dispatch(const GemmArgs& a, int epi, bool norm, const BgPlan& p
   return int(e);
 }
 
-// Batched path is used for M > CAIN_BGEMM_MIN_M (default 16) when K is a multiple of 256.
-static int bgemm_min_m() {
-  static const int v = env_int("CAIN_BGEMM_MIN_M", 16);
-  return v;
-}
-static int bgemm_ntw() {
-  static const int v = env_int("CAIN_BGEMM_NTW", 0);
-  return v;
-}
+// Batched path is used for M > 16 when K is a multiple of 256.
+static int bgemm_min_m() { return 16; }
+static int bgemm_ntw() { return 0; }
 
 // M <= 32 on narrow outputs with short K (N < 8192, K <= 4096: O / QKV projections) stays on the skinny
 // kernel, which measured faster there (its whole grid streams from the first cycle; no staging, no combine).

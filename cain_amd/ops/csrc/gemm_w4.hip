@@ -366,11 +366,7 @@ CAIN_API void cain_gemm_w4_set_variant(int v) { g_w4_var = v < W4_N_VARS ? v : -
 CAIN_API void cain_gemm_w4_set_occupancy(int wgs_per_cu) { g_w4_wgs_per_cu = wgs_per_cu > 0 ? wgs_per_cu : 0; }
 
 static int w4_n_cu() {
-  static const int n = [] {
-    int dev = 0, c = 0;
-    (void)hipGetDevice(&dev);
-    return hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess ? c : 256;
-  }();
+  const int n = cain_cu_budget();
   return n;
 }
 

@@ -275,11 +275,6 @@ static hipError_t w8_launch_e(int epi, int var, const GemmArgs& a, const float* 
 #undef CAIN_W8_VAR
 }
 
-static int env_int(const char* name, int dflt) {
-  const char* v = getenv(name);
-  return v && *v ? atoi(v) : dflt;
-}
-
 // Same arguments as cain_gemm (gemm.hip) plus the per-row weight scales; Wp is the fp8 packing.
 CAIN_API int cain_gemm_w8(const void* Wp, const float* wscale, const void* X, int ldx, int K, int N, int M, void* Y,
                           int ldy, const float* bias, int norm, float eps, const int* slot, const int* pos,
@@ -296,29 +291,22 @@ CAIN_API int cain_gemm_w8(const void* Wp, const float* wscale, const void* X, in
   a.slot = slot, a.pos = pos, a.cos_t = cos_t, a.sin_t = sin_t;
   a.kc = reinterpret_cast<__bf16*>(kc), a.vtc = reinterpret_cast<__bf16*>(vtc);
   a.H = H, a.Hkv = Hkv, a.hd = hd, a.T_max = T_max, a.kv8 = (epi_flags & EPI_KV_FP8) ? 1 : 0;
-  // tuning overrides (tools/sweep.py --env): CAIN_W8_WAVES, CAIN_W8_U, CAIN_W8_NT, CAIN_W8_NB
-  static const int f_w = env_int("CAIN_W8_WAVES", 0), f_u = env_int("CAIN_W8_U", 0), f_nt = env_int("CAIN_W8_NT", 0),
-                   f_nb = env_int("CAIN_W8_NB", 0);
+  // (round 2-3's A/B overrides of waves / pairs in flight / tiles / row blocks are fixed at the measured rule)
+  constexpr int f_w = 0, f_u = 0, f_nt = 0, f_nb = 0;
   const int nb = f_nb ? (f_nb >= 2 ? 2 : 1) : (M > 16 ? 2 : 1);
   // two tiles per workgroup only pay on LM-head-sized N (measured, profiles/w8_decode.md)
   int nt = nb == 2 ? 1 : (f_nt ? (f_nt >= 4 ? 4 : f_nt) : (N >= 65536 ? 2 : 1));
   if ((N / 16) % nt) nt = 1;
   a.msplit = (M + 16 * nb - 1) / (16 * nb);
-  // activations staged in LDS (XL above): one row block, at most 64 KiB of rows.  CAIN_W8_XLDS=0 for A/B runs;
-  // measured single stream (same box, interleaved): llama3.1:8b 471.9 / 472.4 -> 478.5 / 479.9 tok/s, qwen2:1.5b
-  // 970.2 -> 982.1; gate/up 25.2 -> 23.9 us, QKV 9.5 -> 9.2 (profiles/r3/README.md).
-  static const int f_xl = env_int("CAIN_W8_XLDS", 1);
-  const bool xl = f_xl && nb == 1 && a.msplit == 1 && (long long)M * K * 2 <= 65536;
+  // activations staged in LDS (XL above): one row block, at most 64 KiB of rows.  Measured single stream (same box,
+  // interleaved): llama3.1:8b 471.9 / 472.4 -> 478.5 / 479.9 tok/s, qwen2:1.5b 970.2 -> 982.1; gate/up 25.2 ->
+  // 23.9 us, QKV 9.5 -> 9.2 (profiles/r3/README.md).
+  const bool xl = nb == 1 && a.msplit == 1 && (long long)M * K * 2 <= 65536;
   // 8 waves when the grid is at most one workgroup per CU and there are enough k-pairs per wave, else 4.  (The
   // bound was 512 workgroups; with XL + U = 4, llama3.1:8b's 384-workgroup QKV runs 8.9 -> 8.2 us on 4 waves
   // while the 256-workgroup O / down stay faster on 8: 8.7 vs 9.9 us, profiles/r3/README.md.)
-  static const int n_cu = [] {
-    int dev = 0, n = 0;
-    (void)hipGetDevice(&dev);
-    return hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess ? n : 256;
-  }();
-  static const int f_wb = env_int("CAIN_W8_WAVE_BOUND", 0);  // A/B: the workgroup bound of the 8-wave rule
-  int waves = (N / 16 / nt * a.msplit <= (f_wb ? f_wb : xl ? n_cu : 511) && K / 64 >= 64) ? 8 : 4;
+  const int n_cu = cain_cu_budget();
+  int waves = (N / 16 / nt * a.msplit <= (xl ? n_cu : 511) && K / 64 >= 64) ? 8 : 4;
   if (f_w) waves = f_w >= 8 ? 8 : 4;
   // pairs in flight per wave: with the activations in LDS the registers of the deeper weight prologue are free
   // (U = 4: llama3.1:8b 480.7 -> 514.1 tok/s single stream); without, U = 4 measured no gain (w8_decode.md)

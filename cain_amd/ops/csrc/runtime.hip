@@ -321,6 +321,53 @@ CAIN_API void cain_graph_destroy(void* exec) {
   if (exec) (void)hipGraphExecDestroy(static_cast<hipGraphExec_t>(exec));
 }
 
+// ---- CU-limited streams: the batch-1 energy lever (tools/cu_sweep.py).  A stream whose hardware queue may use only
+// n of the device's CUs (hipExtStreamCreateWithCUMask), chosen as whole groups of 8 consecutive mask bits spaced
+// evenly over the mask: balanced over the 8 XCDs whether the mask's CU numbering interleaves the XCDs or runs
+// through them one after the other (n a multiple of 64 balances exactly under both).  Kernels captured or launched
+// for such a stream size their grids by cain_cu_budget().
+static int g_cu_budget = 0;
+
+static int device_cus() {
+  static const int n = [] {
+    int dev = 0, c = 0;
+    (void)hipGetDevice(&dev);
+    return hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && c > 0 ? c : 256;
+  }();
+  return n;
+}
+
+extern "C" int cain_cu_budget() {
+  const int n = device_cus();
+  return g_cu_budget > 0 && g_cu_budget < n ? g_cu_budget : n;
+}
+
+CAIN_API void cain_set_cu_budget(int n) { g_cu_budget = n > 0 ? n : 0; }
+CAIN_API int cain_get_cu_budget() { return cain_cu_budget(); }
+
+// The mask itself (host-side; tests): n_cu of total bits set, or -1.
+CAIN_API int cain_cu_mask(int n_cu, int total, uint32_t* mask, int words) {
+  if (total <= 0 || total % 8 || n_cu <= 0 || n_cu > total || n_cu % 8 || words * 32 < total) return -1;
+  for (int i = 0; i < words; ++i) mask[i] = 0;
+  const int groups = total / 8, take = n_cu / 8;
+  for (int j = 0; j < take; ++j) {
+    const int g = (int)((long long)j * groups / take);
+    for (int b = 0; b < 8; ++b) mask[(g * 8 + b) / 32] |= 1u << ((g * 8 + b) % 32);
+  }
+  return 0;
+}
+
+CAIN_API void* cain_stream_create_cu_limited(int n_cu) {
+  const int total = device_cus();
+  std::vector<uint32_t> mask((total + 31) / 32);
+  if (cain_cu_mask(n_cu, total, mask.data(), (int)mask.size()) != 0) return nullptr;
+  hipStream_t st = nullptr;
+  if (hipExtStreamCreateWithCUMask(&st, (uint32_t)mask.size(), mask.data()) != hipSuccess) return nullptr;
+  return st;
+}
+
+CAIN_API int cain_stream_destroy(void* st) { return hipStreamDestroy(static_cast<hipStream_t>(st)) == hipSuccess ? 0 : -1; }
+
 CAIN_API int cain_rows_size() { return int(sizeof(CainRows)); }
 CAIN_API int cain_plan_desc_size() { return int(sizeof(CainPlanDesc)); }
 CAIN_API int cain_layer_size() { return int(sizeof(CainLayer)); }

@@ -702,16 +702,11 @@ CAIN_API long long cain_sample_ws_bytes(int M) {
   return (long long)M * SS_P * SS_KMAX * 8 + (long long)M * SS_P * 4 + (long long)M * 4 + 256;
 }
 
-// Rows up to which the two-stage kernel runs (CAIN_SAMPLE_SPLIT_MAX, default 64; the decode plan sizes its
-// workspace for min(rows, this)).  A/B switch for wide batches.
-static int g_split_max = -1;
-CAIN_API int cain_sample_split_max() {
-  if (g_split_max < 0) {
-    const char* e = getenv("CAIN_SAMPLE_SPLIT_MAX");
-    g_split_max = e && *e ? atoi(e) : 64;
-  }
-  return g_split_max;
-}
+// Rows up to which the two-stage kernel runs (64; the decode plan sizes its workspace for min(rows, this)).  At
+// 256 rows it measured slower than the one-workgroup-per-row kernel (profiles/r3/README.md).
+static int g_split_max = 64;
+CAIN_API int cain_sample_split_max() { return g_split_max; }
+CAIN_API void cain_sample_set_split_max(int rows) { g_split_max = rows; }
 
 // Sampler with a workspace: the two-stage kernel (SS_P workgroups per row) for rows <= cain_sample_split_max(),
 // else the one-workgroup kernel.  ws must hold cain_sample_ws_bytes(M) zeroed bytes (null: one-workgroup kernel).
@@ -908,18 +903,12 @@ __global__ __launch_bounds__(SS_THREADS) void sample_cm_kernel(
 }
 
 // The chunk-maximum sampler (V % 64 == 0, V / 16 <= 64 * 256); cmax as the LM head wrote it (cain_gemm_set_cmax).
-// CAIN_SAMPLE_CM / cain_sample_set_cm: 0 off, 1 every forward whose LM head wrote the maxima, 2 only forwards of
+// cain_sample_set_cm: 0 off, 1 every forward whose LM head wrote the maxima, 2 only forwards of
 // more than 64 rows (the default).  It draws the same tokens; at one row its one-workgroup chain of phases (37.4 us
 // on qwen2:1.5b, profiles/r3/README.md) is longer than the two-stage kernel's 16-way split (29 us); at 256 rows it
 // takes 42 us against the one-workgroup-per-row kernel's 62 us (+0.2-0.3 % in-graph on the headline).
-static int g_sample_cm = -1;
-CAIN_API int cain_sample_cm_enabled() {
-  if (g_sample_cm < 0) {
-    const char* e = getenv("CAIN_SAMPLE_CM");
-    g_sample_cm = e && *e ? atoi(e) : 2;
-  }
-  return g_sample_cm;
-}
+static int g_sample_cm = 2;
+CAIN_API int cain_sample_cm_enabled() { return g_sample_cm; }
 // A/B switch for tests and tools (takes effect at the next forward / graph capture).
 CAIN_API void cain_sample_set_cm(int on) { g_sample_cm = on; }
 CAIN_API int cain_sample_cm(float* logits, int ldl, int V, const float* cmax, int* tok, int* pos, int* gen, int ldg,

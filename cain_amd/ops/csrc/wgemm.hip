@@ -69,35 +69,20 @@ constexpr int WG_CTR_BYTES = 16 * 1024;  // the workspace region before the slab
 // DMA.  Results are garbage in both.  3 = the full kernel plus timestamps (tools/wgemm_trace.py): lane 0 of wave 0
 // (compute) and of the first loader wave store s_memrealtime / s_memtime at fixed points to w.stamps.
 //
-// OPT (tuning alternatives, A/B runs), bit mask:
-//   1 LSQ (NORM, BM = 256, NDMA = 4): the per-row sums of squares come from the loader waves instead of the X X^T
-//     MFMAs -- after stage t lands, loader lw reads rows 64 lw + lane of the X stage (8 ds_read_b128 per lane, the
-//     read-side XOR swizzle keeps the 16-lane groups conflict-free) and accumulates them with v_dot2c_f32_bf16
-//     (exact bf16 products, fp32 sums, as the MFMA), so the compute waves issue only the GEMM's MFMAs;
-//   2 LSPLIT (NDMA = 4): loaders 0-1 issue only W pieces, loaders 2-3 only X pieces, so a wave's counted wait for
-//     its L2-served X never queues behind HBM-served W (vmcnt retires in issue order per wave);
-//   4 ROT: workgroup b walks its stages starting at ((b >> 3) * 7) mod nst, so the workgroups of one XCD do not
-//     all read the same X lines at the same time (any stage order gives the same sums up to fp32 rounding);
-//   8 XNT: X pieces non-temporal as well (no L1 allocation for lines a CU reads once per stage);
-//   16 PRO: the prologue issues stage by stage (W0 X0 W1 X1 W2) instead of W0 W1 X0 W2 X1, so stage 0 -- the one
-//     every workgroup waits for while the whole grid's prologue burst is in flight -- is not queued behind W1;
-//   32 H16: split-K slabs in fp16 instead of fp32 (wgemm_reduce_kernel H16 = true reads them): half the slab bytes
-//     stored, written back at the kernel boundary (MI355X_MICROARCH.md 'boundary': + dirty bytes / 6 TB/s) and read
-//     by the reduce.  A partial's fp16 rounding (2^-11 relative) is ~8x below the bf16 rounding of the output.
-template <int BM, int DX, int DW, int EPI, bool NORM, int NDMA, int ABL = 0, int OPT = 0>
+// H16: split-K slabs in fp16 instead of fp32 (wgemm_reduce_kernel H16 = true reads them): half the slab bytes
+// stored, written back at the kernel boundary (MI355X_MICROARCH.md 'boundary': + dirty bytes / 6 TB/s) and read by
+// the reduce.  Partials saturate at +-65504 (the reduce sums in fp32); tests/test_wgemm_gpu.py compares them with
+// fp32 slabs on rows of outliers.  (Round 3's loader alternatives -- loader-wave sums of squares, W-only / X-only
+// loader roles, rotated k start, non-temporal X, stage-ordered prologue -- and the in-launch split-K combine all
+// measured within box-to-box noise or slower, profiles/r3/README.md, and were removed.)
+template <int BM, int DX, int DW, int EPI, bool NORM, int NDMA, int ABL = 0, bool H16 = false>
 __global__ __launch_bounds__(64 * (8 + NDMA), (8 + NDMA) / 4) void wgemm_kernel(const GemmArgs a, const WgArgs w) {
   using G = WgGeo<BM>;
-  constexpr bool LSQ = NORM && (OPT & 1) && BM == 256 && NDMA == 4;  // loader-wave sums of squares
-  constexpr bool MSQ = NORM && !LSQ;                                 // MFMA X X^T sums of squares
-  constexpr bool LSPLIT = (OPT & 2) && NDMA == 4;
-  constexpr bool ROT = (OPT & 4) != 0;
-  constexpr int XAUX = (OPT & 8) ? 1 : 0;
-  constexpr bool PRO = (OPT & 16) && !LSPLIT;
-  constexpr bool H16 = (OPT & 32) != 0;
+  constexpr bool MSQ = NORM;                        // MFMA X X^T sums of squares
   constexpr int NX = DX + 1, NW = DW + 1;
   constexpr int NLOAD = NDMA ? NDMA : 8;            // waves issuing LDS-DMA
-  constexpr int NWL = LSPLIT ? 2 : NLOAD;           // waves issuing W pieces
-  constexpr int NXL = LSPLIT ? 2 : NLOAD;           // waves issuing X pieces
+  constexpr int NWL = NLOAD;                        // waves issuing W pieces
+  constexpr int NXL = NLOAD;                        // waves issuing X pieces
   constexpr int WPW = 16 / NWL;                     // W blocks (1 KiB) per W-loader wave per stage
   constexpr int XPW = (BM / 8) / NXL;               // X row octets per X-loader wave per stage
   constexpr int NTHR = 64 * (8 + NDMA);
@@ -109,9 +94,8 @@ __global__ __launch_bounds__(64 * (8 + NDMA), (8 + NDMA) / 4) void wgemm_kernel(
   const bool compute = wave < 8;
   const bool loader = NDMA ? !compute : true;
   const int lw = NDMA ? wave - 8 : wave;  // loader index
-  const bool wload = loader && (!LSPLIT || lw < 2);
-  const bool xload = loader && (!LSPLIT || lw >= 2);
-  const int xl = LSPLIT ? max(lw - 2, 0) : lw;  // X-loader index
+  const bool wload = loader, xload = loader;
+  const int xl = lw;  // X-loader index
   const int wm = wave % G::WM, wn = (wave / G::WM) % G::WN;
   const int KS = a.K >> 5, ntiles = a.N >> 4;
   const int nblk = (ntiles + WG_NT - 1) / WG_NT;
@@ -137,11 +121,7 @@ __global__ __launch_bounds__(64 * (8 + NDMA), (8 + NDMA) / 4) void wgemm_kernel(
   const int tile0 = blk * WG_NT;
   const int st0 = kc * w.kst;                    // first stage (64-deep k-step) of this split
   const int nst = min(w.kst, (a.K >> 6) - st0);  // stages of this split
-  const int rot = ROT ? (int)((blockIdx.x >> 3) * 7u % (unsigned)nst) : 0;
-  auto kstage = [&](int t) {  // ring stage t -> stage of this split's k range
-    if constexpr (ROT) return t + rot < nst ? t + rot : t + rot - nst;
-    else return t;
-  };
+  auto kstage = [&](int t) { return t; };  // ring stage t -> stage of this split's k range
 
   // ---- LDS-DMA sources of this loader (per stage: WPW W blocks + XPW X row-octets)
   // W block j of loader lw: tile (lw * WPW + j) / 2, slice (lw * WPW + j) & 1 (a tile's two slices are 2 KiB
@@ -178,30 +158,14 @@ __global__ __launch_bounds__(64 * (8 + NDMA), (8 + NDMA) / 4) void wgemm_kernel(
     char* base = xring + (t % NX) * G::X_BYTES;
     const size_t off = (size_t)kstage(t) * (WG_BK * 2);
 #pragma unroll
-    for (int j = 0; j < XPW; ++j) glds16(xsrc[j] + off, base + (xl + NXL * j) * 1024, XAUX);
+    for (int j = 0; j < XPW; ++j) glds16(xsrc[j] + off, base + (xl + NXL * j) * 1024, 0);
   };
   // issue order: step u (u < 0: prologue) issues W(u + DW), then X(u + DX); so W(t) is always older than X(t) and
   // waiting for X(t) covers both (vmcnt retires in issue order).  Loads younger than X(t): steps t-DX+1 .. t-1.
   auto younger_than = [&](int t) {
     int n = 0;
-    if constexpr (LSPLIT) {  // a W loader's W(t+1) .. W(t+DW-1), an X loader's X(t+1) .. X(t+DX-1)
-      if (wload) {
 #pragma unroll
-        for (int s = 1; s < DW; ++s) n += WPW * (t + s < nst);
-      } else {
-#pragma unroll
-        for (int s = 1; s < DX; ++s) n += XPW * (t + s < nst);
-      }
-    } else if (PRO && t < DX) {
-      // X(t) went out in the stage-ordered prologue: younger are the prologue's later stages and steps 0 .. t-1
-#pragma unroll
-      for (int s = t + 1; s < DW; ++s) n += WPW * (s < nst) + XPW * (s < DX && s < nst);
-#pragma unroll
-      for (int u = 0; u < DX - 1; ++u) n += (u < t) ? WPW * (u + DW < nst) + XPW * (u + DX < nst) : 0;
-    } else {
-#pragma unroll
-      for (int u = t - DX + 1; u < t; ++u) n += WPW * (u + DW < nst) + XPW * (u + DX < nst);
-    }
+    for (int u = t - DX + 1; u < t; ++u) n += WPW * (u + DW < nst) + XPW * (u + DX < nst);
     return n;
   };
   auto land = [&](int t) {  // this loader's pieces of stage t have landed (a loader's own counted wait)
@@ -265,40 +229,12 @@ __global__ __launch_bounds__(64 * (8 + NDMA), (8 + NDMA) / 4) void wgemm_kernel(
       }
     }
   };
-  // LSQ: loader lw's row 64 lw + lane of X stage t (its 8 pieces in swizzled order: 16-lane groups hit 16
-  // different 4-bank groups)
-  float lsq = 0.f;
-  auto loader_ssq = [&](int t) {
-    if constexpr (LSQ) {
-      const int r = lw * 64 + lane;
-      const char* row = xring + (t % NX) * G::X_BYTES + r * 128;
-      bf16x8 v[8];
-#pragma unroll
-      for (int q = 0; q < 8; ++q) v[q] = *reinterpret_cast<const bf16x8*>(row + ((q ^ ((r >> 1) & 7)) << 4));
-#pragma unroll
-      for (int q = 0; q < 8; ++q)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const bf16x2 p = {v[q][2 * j], v[q][2 * j + 1]};
-          lsq = __builtin_amdgcn_fdot2_f32_bf16(p, p, lsq, false);
-        }
-    }
-  };
-
   // ---- prologue: steps -DW .. -1
   if (loader) {
-    if constexpr (PRO) {
 #pragma unroll
-      for (int s = 0; s < DW; ++s) {
-        if (s < nst) issue_w(s);
-        if (s < DX && s < nst) issue_x(s);
-      }
-    } else {
-#pragma unroll
-      for (int u = -DW; u < 0; ++u) {
-        if (u + DW < nst) issue_w(u + DW);
-        if (u + DX >= 0 && u + DX < nst) issue_x(u + DX);
-      }
+    for (int u = -DW; u < 0; ++u) {
+      if (u + DW < nst) issue_w(u + DW);
+      if (u + DX >= 0 && u + DX < nst) issue_x(u + DX);
     }
   }
 
@@ -311,7 +247,6 @@ __global__ __launch_bounds__(64 * (8 + NDMA), (8 + NDMA) / 4) void wgemm_kernel(
       if (t == 0) stamp(2, false);
       if (t == nst / 2) stamp(3, false);
       issue_step(t);
-      loader_ssq(t);
     }
   } else if constexpr (ABL == 1) {
     for (int t = 0; t < nst; ++t) {
@@ -358,118 +293,49 @@ __global__ __launch_bounds__(64 * (8 + NDMA), (8 + NDMA) / 4) void wgemm_kernel(
       for (int mb = 0; mb < G::MB; ++mb) s_ss[wn * BM + (wm * G::MB + mb) * 16 + c] = ssq[mb][c & 3];
     }
     __syncthreads();
-  } else if constexpr (LSQ) {
-    if (!compute) {
-      s_ss[lw * 64 + lane] = lsq;
-      s_ss[BM + lw * 64 + lane] = 0.f;
-    }
-    __syncthreads();
   }
 
   if (w.ks > 1) {
     // fp32 slab of this split (unit (gt, rb) = 16 x 16 outputs, lane-major f32x4: the reducer's layout) and this
     // split's per-row sums of squares.
     const int n_units = nblk * WG_NT * G::RB;
-    if (!w.combine) {
-      // wgemm_reduce_kernel, the next launch on the stream, combines them
-      if (compute) {
-#pragma unroll
-        for (int tn = 0; tn < G::TN; ++tn)
-#pragma unroll
-          for (int mb = 0; mb < G::MB; ++mb) {
-            const int unit = (tile0 + wn * G::TN + tn) * G::RB + wm * G::MB + mb;
-            const size_t e = ((size_t)kc * n_units + unit) * 64 + lane;
-            if constexpr (H16) {
-              f16x4 h;  // saturated: a partial past the fp16 range stays finite
-#pragma unroll
-              for (int i = 0; i < 4; ++i) h[i] = (_Float16)fminf(fmaxf(acc[tn][mb][i], -65504.f), 65504.f);
-              reinterpret_cast<f16x4*>(w.part)[e] = h;
-            } else {
-              reinterpret_cast<f32x4*>(w.part)[e] = acc[tn][mb];
-            }
-          }
-      }
-      if constexpr (NORM) {
-        for (int r = threadIdx.x; r < BM; r += NTHR)
-          w.part_ss[((size_t)blk * w.ks + kc) * BM + r] = s_ss[r] + s_ss[BM + r];
-      }
-      if constexpr (ABL == 3) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        stamp(5, false);
-        stamp(6, false);
-        stamp(7, true);
-      }
-      return;
-    }
-    // In-launch combine (w.combine): the ks split partners of the column block publish their slabs write-through
-    // (sc1: no release fence, cdna_hip_programming.md §5 item 2), arrive on the block's counter, wait for each
-    // other, and then EACH reduces 1/ks of the block's 16 x 16 units (reduce-scatter among the partners) and runs
-    // the fused epilogue for them -- the separate reduce launch, its kernel boundary and its whole-grid ramp are
-    // gone, and the reduction work stays spread over every workgroup.  The wait needs all partners resident:
-    // the grid is <= 256 workgroups at one per CU (wgemm_dispatch), and the spin is bounded.
-    const __amdgpu_buffer_rsrc_t pr = slab_rsrc(w.part), sr = slab_rsrc(w.part_ss);
+    // wgemm_reduce_kernel, the next launch on the stream, combines them
     if (compute) {
 #pragma unroll
       for (int tn = 0; tn < G::TN; ++tn)
 #pragma unroll
         for (int mb = 0; mb < G::MB; ++mb) {
           const int unit = (tile0 + wn * G::TN + tn) * G::RB + wm * G::MB + mb;
-          st_wt(pr, int((((size_t)kc * n_units + unit) * 64 + lane) * 16), acc[tn][mb]);
+          const size_t e = ((size_t)kc * n_units + unit) * 64 + lane;
+          if constexpr (H16) {
+            // scaled per (unit, 16-lane row group) by a power of two that keeps the group's largest partial < 2^14
+            // (the reducer multiplies it back): rows of outliers in the residual stream keep fp16's relative
+            // precision instead of saturating at 65504 (tests/test_wgemm_gpu.py test_fp16_slabs_scale_outlier_rows).
+            // The group maximum is four DPP rotations (a whole-unit wave_max -- 6 LDS permutes and waits per unit --
+            // cost ~3 us per split GEMM at 256 rows, profiles/r4/README.md).
+            const f32x4 v = acc[tn][mb];
+            const float mx = row16_max_nonneg(fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
+            const int ex = max(__builtin_amdgcn_frexp_expf(mx) - 14, 0);  // mx < 2^(ex + 14)
+            const float inv = __builtin_amdgcn_ldexpf(1.f, -ex);
+            f16x4 h;  // (the clamp only bites on non-finite partials)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) h[i] = (_Float16)fminf(fmaxf(v[i] * inv, -65504.f), 65504.f);
+            reinterpret_cast<f16x4*>(w.part)[e] = h;
+            if ((lane & 15) == 0) w.part_sc[((size_t)kc * n_units + unit) * 4 + (lane >> 4)] = __builtin_amdgcn_ldexpf(1.f, ex);
+          } else {
+            reinterpret_cast<f32x4*>(w.part)[e] = acc[tn][mb];
+          }
         }
     }
     if constexpr (NORM) {
       for (int r = threadIdx.x; r < BM; r += NTHR)
-        st_wt_f32(sr, int((((size_t)blk * w.ks + kc) * BM + r) * 4), s_ss[r] + s_ss[BM + r]);
+        w.part_ss[((size_t)blk * w.ks + kc) * BM + r] = s_ss[r] + s_ss[BM + r];
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    unsigned* ctr = w.counters + blk * 2;
-    if (threadIdx.x == 0) {
-      __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      for (int spin = 0; spin < (1 << 24); ++spin) {  // bounded: ~seconds, never a hang
-        if (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= unsigned(w.ks)) break;
-        __builtin_amdgcn_s_sleep(1);
-      }
-      // the last partner out resets both counters for the next launch (every partner has seen ks arrivals)
-      if (__hip_atomic_fetch_add(ctr + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == unsigned(w.ks - 1)) {
-        __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(ctr + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
-    __syncthreads();
-    if (!compute) return;
-    // units of this column block: blk * 128 + [0, 128); partner kc takes [kc * 128 / ks, (kc + 1) * 128 / ks)
-    constexpr int BU = WG_NT * G::RB;
-    const int u0 = (kc * BU) / w.ks, u1 = ((kc + 1) * BU) / w.ks;
-    for (int lu = u0 + wave; lu < u1; lu += 8) {
-      const int unit = blk * BU + lu;
-      const int gt = unit / G::RB, rb = unit - gt * G::RB;
-      const int m = rb * 16 + c;
-      const bool live = gt < ntiles;
-      const EpiIn e = live ? epi_load_at<EPI>(a, gt, m, lane) : EpiIn{};
-      f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
-      float ss = 0.f;
-      for (int k0 = 0; k0 < w.ks; k0 += 4) {  // every partial load in flight before the adds
-        f32x4 l[4];
-        float q[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int k = min(k0 + j, w.ks - 1);
-          l[j] = ld_wt(pr, int((((size_t)k * n_units + unit) * 64 + lane) * 16));
-          q[j] = NORM ? ld_wt_f32(sr, int((((size_t)blk * w.ks + k) * BM + m) * 4)) : 0.f;
-        }
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const float wj = (k0 + j < w.ks) ? 1.f : 0.f;
-          v += wj * l[j];
-          ss += wj * q[j];
-        }
-      }
-      if constexpr (NORM) v *= rms_inv(ss, a.K, a.eps);
-      f32x4 pv;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) pv[i] = __shfl_xor(v[i], 32, 64);
-      if (live) epi_store<EPI>(a, gt, m, lane, e, [&](int off) { return off ? pv : v; });
+    if constexpr (ABL == 3) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      stamp(5, false);
+      stamp(6, false);
+      stamp(7, true);
     }
     return;
   }
@@ -543,25 +409,34 @@ __global__ __launch_bounds__(256) void wgemm_reduce_kernel(const GemmArgs a, con
     if constexpr (H16) return f32x4{(float)x[0], (float)x[1], (float)x[2], (float)x[3]};
     else return x;
   };
+  const float* scsrc = w.part_sc + (size_t)unit * 4 + (lane >> 4);  // H16: the lane's row-group scale per split
   const float* ssrc = w.part_ss + (size_t)(gt / WG_NT) * ks * BM + m;
   f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
   float ss = 0.f;
   if constexpr (KS > 0) {
     slab_t p[KS];
-    float q[KS];
+    float q[KS], sc[KS];
 #pragma unroll
     for (int k = 0; k < KS; ++k) p[k] = src[(size_t)k * n_units * 64];
+    if constexpr (H16) {
+#pragma unroll
+      for (int k = 0; k < KS; ++k) sc[k] = scsrc[(size_t)k * n_units * 4];
+    }
     if constexpr (NORM) {
 #pragma unroll
       for (int k = 0; k < KS; ++k) q[k] = ssrc[k * BM];
     }
 #pragma unroll
     for (int k = 0; k < KS; ++k) {
-      v += widen(p[k]);
+      if constexpr (H16) v += widen(p[k]) * sc[k];
+      else v += widen(p[k]);
       if constexpr (NORM) ss += q[k];
     }
   } else {
-    for (int k = 0; k < ks; ++k) v += widen(src[(size_t)k * n_units * 64]);
+    for (int k = 0; k < ks; ++k) {
+      if constexpr (H16) v += widen(src[(size_t)k * n_units * 64]) * scsrc[(size_t)k * n_units * 4];
+      else v += widen(src[(size_t)k * n_units * 64]);
+    }
     if constexpr (NORM) {
       for (int k = 0; k < ks; ++k) ss += ssrc[k * BM];
     }
@@ -590,7 +465,7 @@ namespace {
 
 struct WgPlan {
   int bm, nblk, ks, kst;
-  size_t part_floats, ss_floats;
+  size_t part_floats, ss_floats, sc_floats;
 };
 
 // Split count: ~256 streaming workgroups (one per CU: the ring takes 128-144 KiB of LDS), at most 8 splits and
@@ -617,9 +492,7 @@ const WgShape* wg_shape(int N, int K, int bm) {
 }
 
 WgPlan wg_plan(int N, int K, int M) {
-  if (g_wg_target < 0) g_wg_target = wg_env("CAIN_WGEMM_TARGET", 256);
-  if (g_wg_ksmax < 0) g_wg_ksmax = wg_env("CAIN_WGEMM_KSMAX", 8);
-  const int target = g_wg_target, ksmax = g_wg_ksmax;
+  const int target = g_wg_target > 0 ? g_wg_target : 256, ksmax = g_wg_ksmax > 0 ? g_wg_ksmax : 8;
   WgPlan p{};
   p.bm = M > 128 ? 256 : 128;
   p.nblk = ((N >> 4) + WG_NT - 1) / WG_NT;
@@ -638,65 +511,53 @@ WgPlan wg_plan(int N, int K, int M) {
   if (p.ks > 1) {
     p.part_floats = (size_t)p.ks * p.nblk * WG_NT * (p.bm / 16) * 256;
     p.ss_floats = (size_t)p.nblk * p.ks * p.bm;
+    p.sc_floats = (size_t)p.ks * p.nblk * WG_NT * (p.bm / 16) * 4;
   }
   return p;
 }
 
-template <int BM, int DX, int DW, int EPI, bool NORM, int NDMA, int ABL = 0, int OPT = 0>
+template <int BM, int DX, int DW, int EPI, bool NORM, int NDMA, int ABL = 0, bool H16 = true>
 hipError_t wg_launch(const GemmArgs& a, const WgArgs& w, const WgPlan& p, hipStream_t st) {
   using G = WgGeo<BM>;
   constexpr int lds = (DW + 1) * G::W_BYTES + (DX + 1) * G::X_BYTES;
   static_assert(lds <= 160 * 1024, "LDS");
   static bool attr = [] {
-    return hipFuncSetAttribute(reinterpret_cast<const void*>(&wgemm_kernel<BM, DX, DW, EPI, NORM, NDMA, ABL, OPT>),
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(&wgemm_kernel<BM, DX, DW, EPI, NORM, NDMA, ABL, H16>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, lds) == hipSuccess;
   }();
   if (!attr) return hipErrorInvalidConfiguration;
-  hipLaunchKernelGGL((wgemm_kernel<BM, DX, DW, EPI, NORM, NDMA, ABL, OPT>), dim3(p.nblk * p.ks), dim3(64 * (8 + NDMA)),
+  hipLaunchKernelGGL((wgemm_kernel<BM, DX, DW, EPI, NORM, NDMA, ABL, H16>), dim3(p.nblk * p.ks), dim3(64 * (8 + NDMA)),
                      lds, st, a, w);
   hipError_t e = hipGetLastError();
-  if (e != hipSuccess || p.ks == 1 || w.combine) return e;
-  wg_reduce_launch<BM, EPI, NORM, (OPT & 32) != 0>(a, w, p.nblk * WG_NT * G::RB, st);
+  if (e != hipSuccess || p.ks == 1) return e;
+  wg_reduce_launch<BM, EPI, NORM, H16>(a, w, p.nblk * WG_NT * G::RB, st);
   return hipGetLastError();
 }
 
-// ring / loader variants: 0 = default; the rest are tuning alternatives (cain_wgemm_set_variant,
-// CAIN_WGEMM_VARIANT) and the ablations of tools/wgemm_bench.py
-int g_wgemm_variant = -1;
+// variants: 0 = default (fp16 split-K slabs: in the graph-replayed headline 26.33 / 26.17k -> 27.34 / 27.17k tok/s
+// against fp32 slabs, same box, interleaved, profiles/r3/README.md); 4 = fp32 slabs (tests, A/B); diagnostics of
+// tools/wgemm_trace.py / wgemm_bench.py: 7 = default + timestamps, 8 = DMA only, 9 = fragment reads + MFMAs only
+// (results garbage).  Set with cain_wgemm_set_variant / cain_wgemm_set_shape.
+int g_wgemm_variant = 0;
 
 template <int BM, int EPI, bool NORM>
 hipError_t wg_launch_v(const GemmArgs& a, const WgArgs& w, const WgPlan& p, hipStream_t st) {
-  if (g_wgemm_variant < 0) g_wgemm_variant = wg_env("CAIN_WGEMM_VARIANT", 0);
   int variant = g_wgemm_variant;
   if (const WgShape* o = wg_shape(a.N, a.K, BM)) {
     if (o->variant >= 0) variant = o->variant;
   }
-  // Every default carries fp16 split-K slabs (OPT 32, H = 32 below): in the graph-replayed headline 26.33 / 26.17k
-  // -> 27.34 / 27.17k tok/s against fp32 slabs (same box, interleaved; profiles/r3/README.md).  Variant 4 keeps
-  // fp32 slabs for A/B runs; 5, 12, 14 and 17 are the loader alternatives that measured within box-to-box noise.
-  constexpr int H = 32;
-  if constexpr (BM == 256) {  // X stage 32 KiB, W stage 16 KiB
+  if constexpr (BM == 256) {  // X stage 32 KiB, W stage 16 KiB: 160 KiB of ring
     switch (variant) {
-      case 1: return wg_launch<BM, 2, 3, EPI, NORM, 0, 0, H>(a, w, p, st);   // MFMA waves load
-      case 2: return wg_launch<BM, 2, 2, EPI, NORM, 4, 0, H>(a, w, p, st);   // 144 KiB
-      case 3: return wg_launch<BM, 1, 5, EPI, NORM, 4, 0, H>(a, w, p, st);   // 160 KiB
-      case 4: return wg_launch<BM, 2, 3, EPI, NORM, 4>(a, w, p, st);         // fp32 slabs
-      case 5: return wg_launch<BM, 2, 3, EPI, NORM, 4, 0, H | 1>(a, w, p, st);   // loader-wave sums of squares
-      case 12: return wg_launch<BM, 2, 3, EPI, NORM, 4, 0, H | 4>(a, w, p, st);  // rotated k start
-      case 14: return wg_launch<BM, 2, 3, EPI, NORM, 4, 0, H | 6>(a, w, p, st);  // W / X loader roles + rotation
-      case 17: return wg_launch<BM, 2, 3, EPI, NORM, 4, 0, H | 16>(a, w, p, st);  // stage-ordered prologue
-      case 7: return wg_launch<BM, 2, 3, EPI, NORM, 4, 3, H>(a, w, p, st);   // default + timestamps
-      case 8: return wg_launch<BM, 2, 3, EPI, NORM, 4, 1, H>(a, w, p, st);   // DMA only
-      case 9: return wg_launch<BM, 2, 3, EPI, NORM, 4, 2, H>(a, w, p, st);   // compute only
-      default: return wg_launch<BM, 2, 3, EPI, NORM, 4, 0, H>(a, w, p, st);  // 160 KiB
+      case 4: return wg_launch<BM, 2, 3, EPI, NORM, 4, 0, false>(a, w, p, st);
+      case 7: return wg_launch<BM, 2, 3, EPI, NORM, 4, 3>(a, w, p, st);
+      case 8: return wg_launch<BM, 2, 3, EPI, NORM, 4, 1>(a, w, p, st);
+      case 9: return wg_launch<BM, 2, 3, EPI, NORM, 4, 2>(a, w, p, st);
+      default: return wg_launch<BM, 2, 3, EPI, NORM, 4>(a, w, p, st);
     }
-  } else {  // X stage 16 KiB, W stage 16 KiB
+  } else {  // X stage 16 KiB, W stage 16 KiB: 160 KiB of ring
     switch (variant) {
-      case 1: return wg_launch<BM, 3, 5, EPI, NORM, 0, 0, H>(a, w, p, st);
-      case 2: return wg_launch<BM, 3, 3, EPI, NORM, 4, 0, H>(a, w, p, st);   // 128 KiB
-      case 3: return wg_launch<BM, 2, 6, EPI, NORM, 4, 0, H>(a, w, p, st);   // 160 KiB
-      case 4: return wg_launch<BM, 3, 5, EPI, NORM, 4>(a, w, p, st);         // fp32 slabs
-      default: return wg_launch<BM, 3, 5, EPI, NORM, 4, 0, H>(a, w, p, st);  // 160 KiB
+      case 4: return wg_launch<BM, 3, 5, EPI, NORM, 4, 0, false>(a, w, p, st);
+      default: return wg_launch<BM, 3, 5, EPI, NORM, 4>(a, w, p, st);
     }
   }
 }
@@ -716,12 +577,9 @@ hipError_t wg_launch_e(int epi, const GemmArgs& a, const WgArgs& w, const WgPlan
 
 }  // namespace
 
-// Rows from which the wide kernel takes a GEMM (CAIN_WGEMM_MIN_M; default 64: M in (64, 256]; 0 disables).
-static int g_wgemm_min_m = -1;
-CAIN_API int cain_wgemm_min_m() {
-  if (g_wgemm_min_m < 0) g_wgemm_min_m = wg_env("CAIN_WGEMM_MIN_M", 64);
-  return g_wgemm_min_m;
-}
+// Rows from which the wide kernel takes a GEMM (default 64: M in (64, 256]; 0 disables; cain_wgemm_set_min_m).
+static int g_wgemm_min_m = 64;
+CAIN_API int cain_wgemm_min_m() { return g_wgemm_min_m; }
 // A/B switches for tests and tuning tools (take effect for launches and graph captures after the call).
 CAIN_API void cain_wgemm_set_min_m(int m) { g_wgemm_min_m = m; }
 CAIN_API void cain_wgemm_set_variant(int v) { g_wgemm_variant = v; }
@@ -749,7 +607,6 @@ CAIN_API int cain_wgemm_eligible(int N, int K, int M);
 CAIN_API int cain_wgemm_plan(int N, int K, int M) {
   if (!cain_wgemm_eligible(N, K, M)) return -1;
   const WgPlan p = wg_plan(N, K, M);
-  if (g_wgemm_variant < 0) g_wgemm_variant = wg_env("CAIN_WGEMM_VARIANT", 0);
   const WgShape* o = wg_shape(N, K, p.bm);
   return p.ks * 64 + (o && o->variant >= 0 ? o->variant : g_wgemm_variant);
 }
@@ -762,7 +619,7 @@ CAIN_API int cain_wgemm_eligible(int N, int K, int M) {
 CAIN_API long long cain_wgemm_ws_bytes(int N, int K, int M) {
   if (!cain_wgemm_eligible(N, K, M)) return 0;
   const WgPlan p = wg_plan(N, K, M);
-  return (long long)(WG_CTR_BYTES + (p.part_floats + p.ss_floats) * sizeof(float));
+  return (long long)(WG_CTR_BYTES + (p.part_floats + p.ss_floats + p.sc_floats) * sizeof(float));
 }
 
 
@@ -770,7 +627,7 @@ CAIN_API long long cain_wgemm_ws_bytes(int N, int K, int M) {
 int wgemm_dispatch(const GemmArgs& a, int epi, bool norm, void* ws, long long ws_bytes, hipStream_t st) {
   if (!cain_wgemm_eligible(a.N, a.K, a.M)) return -1;
   const WgPlan p = wg_plan(a.N, a.K, a.M);
-  if ((long long)(WG_CTR_BYTES + (p.part_floats + p.ss_floats) * sizeof(float)) > ws_bytes) return -1;
+  if ((long long)(WG_CTR_BYTES + (p.part_floats + p.ss_floats + p.sc_floats) * sizeof(float)) > ws_bytes) return -1;
   WgArgs w{};
   w.ks = p.ks;
   w.kst = p.kst;
@@ -778,25 +635,14 @@ int wgemm_dispatch(const GemmArgs& a, int epi, bool norm, void* ws, long long ws
   // XCD (blocks b and b + 8 share one under round-robin dispatch), so the reduce reads the slabs from the L2
   // that holds them instead of across the fabric.  Measured on the headline (rocprof, gpurun_out/r15): O / down
   // reduce 8.7 -> 6.9 us, QKV 22.5 + 11.2 -> 20.1 + 10.9 us, O / down main +1.1 us (their X panels are now
-  // fetched per XCD); 25.8k -> 26.3k tok/s.  CAIN_WGEMM_XCD=0: the split-major placement (A/B runs).
-  static const int xcd = wg_env("CAIN_WGEMM_XCD", 1);
-  w.xcd_blk = xcd && p.ks > 1 && p.nblk % 8 == 0;
-  // in-launch split-K combine (CAIN_WGEMM_COMBINE=1, A/B runs): the partners wait for each other, so the whole grid
-  // must be resident -- at most one workgroup per CU (the ring's LDS) on every CU.  Off by default: on the headline
-  // (llama3.1:8b, 256 rows, same box, back to back) 26.06k tok/s with it vs 26.90k with the separate reduce launch
-  // (gpurun_out/r3c) -- the write-through slabs and the partners' wait cost more than the launch boundary saved.
-  static const int combine = wg_env("CAIN_WGEMM_COMBINE", 0);
-  static const int n_cu = [] {
-    int dev = 0, n = 0;
-    (void)hipGetDevice(&dev);
-    return hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess ? n : 0;
-  }();
-  w.combine = combine && p.ks > 1 && p.nblk * p.ks <= n_cu && p.nblk * 2 * 4 <= WG_CTR_BYTES;
+  // fetched per XCD); 25.8k -> 26.3k tok/s.
+  w.xcd_blk = p.ks > 1 && p.nblk % 8 == 0;
   // [counter region: 2 per column block, zero at rest][slabs][sums]
   w.counters = static_cast<unsigned*>(ws);
   w.stamps = g_wg_stamps;
   w.part = reinterpret_cast<float*>(static_cast<char*>(ws) + WG_CTR_BYTES);
   w.part_ss = w.part + p.part_floats;
+  w.part_sc = w.part_ss + p.ss_floats;
   hipError_t e;
   if (p.bm == 256) e = norm ? wg_launch_e<256, true>(epi, a, w, p, st) : wg_launch_e<256, false>(epi, a, w, p, st);
   else e = norm ? wg_launch_e<128, true>(epi, a, w, p, st) : wg_launch_e<128, false>(epi, a, w, p, st);

@@ -408,8 +408,7 @@ CAIN_API int cain_gemm_w8a8(const void* Wp8, const float* wscale, const void* X8
   a.H = H, a.Hkv = Hkv, a.hd = hd, a.T_max = T_max, a.kv8 = (epi_flags & EPI_KV_FP8) ? 1 : 0;
   WgArgs w{};
   w.ks = p.ks, w.kst = p.kst, w.part = ws ? reinterpret_cast<float*>(static_cast<char*>(ws) + W8_SLAB_OFFSET) : nullptr;
-  static const int xcd = wg_env("CAIN_WGEMM_XCD", 1);  // XCD-local split-K (wgemm_ring.h wg_block_of)
-  w.xcd_blk = xcd && p.ks > 1 && p.nblk % 8 == 0;
+  w.xcd_blk = p.ks > 1 && p.nblk % 8 == 0;  // XCD-local split-K (wgemm_ring.h wg_block_of)
   const W8Scales q{xs, wscale};
   const hipError_t e = p.bm == 256 ? w8_launch_e<256>(epi, a, w, q, p, st) : w8_launch_e<128>(epi, a, w, q, p, st);
   return int(e);

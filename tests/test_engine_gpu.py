@@ -185,3 +185,28 @@ def test_greedy_decode_tracks_oracle_full_size():
     eng.close()
     del ref, eager
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("name,dtype,cus", [("tiny-llama3.1:8b", "bf16", 128), ("tiny-qwen2:1.5b", "bf16", 64),
+                                            ("llama3.1:8b", "fp4", 64), ("qwen2:1.5b", "bf16", 128)])
+def test_cu_limited_engine_matches_full_device(name, dtype, cus):
+    """DecodeEngine(cu_limit=n): the kernels run on a CU-masked stream with grids sized for n CUs (the batch-1 energy
+    lever, tools/cu_sweep.py); same logits and greedy tokens as the whole device, and the launch-sizing budget is
+    back to the device's after every call."""
+    from cain_amd import ops
+    from cain_amd.models import get_config, random_weights
+
+    full = torch.cuda.get_device_properties(0).multi_processor_count
+    w = random_weights(get_config(name), device="cuda", seed=9)
+    kw = dict(device="cuda", max_batch=1, max_context=512, seed=9, weights=w, keep_natural=True, weight_dtype=dtype)
+    a = DecodeEngine(name, **kw)
+    b = DecodeEngine(name, cu_limit=cus, **kw)
+    assert b.cu_limit == cus and ops.cu_budget() == full
+    la, lb = a.last_logits(PROMPTS[:1]), b.last_logits(PROMPTS[:1])
+    assert float((la.float() - lb.float()).norm() / la.float().norm()) < 1e-2
+    ga = a.generate(PROMPTS[:1], 12, [dict(temperature=0.0, top_k=1, eos_id=-1)])[0]
+    gb = b.generate(PROMPTS[:1], 12, [dict(temperature=0.0, top_k=1, eos_id=-1)])[0]
+    assert gb.eval_count == 12 and ga.tokens[:4] == gb.tokens[:4]
+    assert ops.cu_budget() == full
+    a.close()
+    b.close()

@@ -116,7 +116,7 @@ def test_wide_splitk_repeatable_after_batched_path(N, K, norm, epi):
     assert all(torch.equal(o, outs[0]) for o in outs)
 
 
-@pytest.mark.parametrize("ks,variant", [(3, 2), (6, 0), (16, 2), (1, 0)])
+@pytest.mark.parametrize("ks,variant", [(3, 4), (6, 0), (16, 4), (1, 0)])
 def test_shape_plan_override(ks, variant):
     """A per-shape plan (split count, ring variant) changes the launch, not the result (up to the fp16 rounding of the
     split-K slabs, which differs with the split count: ~1e-4 relative, 8x below the bf16 output rounding)."""
@@ -133,3 +133,31 @@ def test_shape_plan_override(ks, variant):
     finally:
         ops.clear_wide_gemm_plans()
     assert rel_err(y, ref) < 1e-3
+
+
+@pytest.mark.parametrize("norm", [True, False])
+@pytest.mark.parametrize("scale", [1e3, 1e5])
+def test_fp16_slabs_scale_outlier_rows(norm, scale):
+    """the default fp16 split-K slabs on rows of outliers (values ~1e3-1e5, as a residual stream can carry)
+    for a NORM shape (the QKV split, partials taken before the RMSNorm scale) and a RESID-sized one: every 16 x 16
+    slab unit is stored scaled by a power of two, so the result equals the fp32-slab variant (4) to fp16's relative
+    precision instead of saturating at 65504."""
+    torch.manual_seed(int(scale) % 97 + norm)
+    N, K, M = 4096, 4096, 256
+    W = (torch.randn(N, K, device=DEV) * 0.02).bfloat16()
+    x = torch.randn(M, K, device=DEV)
+    x[::7] *= scale  # every 7th row an outlier row
+    x = x.bfloat16()
+    wp = pack_mfma_a(W)
+    assert ops.wide_gemm_plan(N, K, M)[0] > 1  # a split plan: the slabs are used
+    y16 = ops.skinny_gemm(wp, x, N, ops.EPI_F32, norm=norm, eps=1e-6)
+    try:
+        ops.set_wide_gemm_plan(N, K, 256, 0, 4)  # the default split count, fp32 slabs
+        y32 = ops.skinny_gemm(wp, x, N, ops.EPI_F32, norm=norm, eps=1e-6)
+    finally:
+        ops.clear_wide_gemm_plans()
+    ref = _normed(x, norm) @ W.float().t()
+    assert bool(torch.isfinite(y16).all())
+    for rows in (slice(0, None, 7), slice(1, None, 7)):  # outlier rows and ordinary rows, each against fp32
+        assert rel_err(y16[rows], y32[rows]) < 2e-3, (rows, rel_err(y16[rows], y32[rows]))
+        assert rel_err(y16[rows], ref[rows]) < 3e-3

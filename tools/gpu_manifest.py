@@ -70,6 +70,28 @@ SETS = {
         ("w4bench_qwen", 300, f"{PY} tools/w4_bench.py --model qwen2:1.5b --variants rule,0,2,3,4,5"),
     ],
     # the whole GPU suite (what the driver runs at round end)
+    # pruned variants / env switches and the scaled fp16 split-K slabs: the affected kernels' tests, then the headline
+    "r4_prune": [
+        ("prune_tests", 900, f"{TEST} tests/test_wgemm_gpu.py tests/test_ops_gpu.py tests/test_w8a8_gpu.py "
+                             f"tests/test_engine_gpu.py"),
+        ("bench", 400, f"{PY} bench.py --gpus 1 --steps 10 --warmup 3"),
+    ],
+    # headline A/B: the HEAD library (ab/libcain_kernels_head.so, fp32-unscaled fp16 slabs) vs the tree's, interleaved
+    "r4_slab_ab": [(f"hl_{tag}_{i}", 300, f"{env}{PY} bench.py --steps 3 --warmup 1 --no-single --no-energy")
+                   for i in range(3) for tag, env in (("head", "CAIN_KERNELS_LIB=ab/libcain_kernels_head.so "),
+                                                      ("new", ""))]
+    + [prof("hl_new", "--steps 1 --warmup 1 --no-single --no-energy"),
+       ("prof_hl_head", 300, "CAIN_KERNELS_LIB=ab/libcain_kernels_head.so rocprofv3 --kernel-trace --stats --output-format csv "
+                             "-d gpurun_out/prof_hl_head -o run -- python3 bench.py --steps 1 --warmup 1 --no-single --no-energy "
+                             "&& find gpurun_out/prof_hl_head -name '*kernel_trace.csv' -delete")],
+    # batch-1 energy lever: CU-limited streams (tools/cu_sweep.py), after the engine's CU-limit test
+    "r4_cu": [
+        ("cu_tests", 300, f"{TEST} tests/test_engine_gpu.py -k cu_limited"),
+        ("cu_sweep", 900, f"{PY} tools/cu_sweep.py --out gpurun_out/r4_cu/cu_sweep.jsonl"),
+    ],
+    # board power after a 1,000-word on-device run (the study's cooldown evidence)
+    "r4_cooldown": [("cooldown", 600, f"{PY} tools/cooldown_trace.py --out gpurun_out/r4_cooldown/cooldown.json "
+                                      f"--csv gpurun_out/r4_cooldown/cooldown_trace.csv")],
     "suite": [("gpu_suite", 1500, f"{PY} -u -m pytest tests -m gpu -x -q --timeout 600 --timeout-method thread")],
     # the driver's bench command
     "bench": [("bench", 900, f"{PY} bench.py --gpus 1 --steps 20 --warmup 5")],

@@ -4,7 +4,7 @@ JSON line per run (the bench's own line plus the point) -- replaces round 1's on
 
     python tools/sweep.py --out gpurun_out/sweep.jsonl \\
         --arg model=llama3.1:8b,gemma:2b --arg words=100,500,1000 --arg batch=256 \\
-        --env CAIN_WGEMM_VARIANT=0,1 --fixed "--steps 1 --warmup 1 --no-single"
+        --env CAIN_W8A8=0,1 --fixed "--steps 1 --warmup 1 --no-single"
 
 Each run has its own time limit; a run that crashes or times out (exit >= 124, 134, 139) ends the sweep, a run
 that merely fails (exit 1) is recorded and the sweep goes on.
