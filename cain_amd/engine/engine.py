@@ -172,8 +172,9 @@ class DecodeEngine:
         activations quantised per row to e4m3, fp8 MFMA) up to 256 rows; CAIN_W8A8=0 keeps W8A16 only (<= 64
         rows).
         ``weight_dtype="fp4"``: OCP MXFP4 GEMM weights (e2m1, one e8m0 scale per 32 k; 0.53 bytes per parameter),
-        the reference's 4-bit precision class: W4A16 few-row kernels (gemm_w4.hip), up to 64 rows per forward;
-        every GEMM K (d_model, q_dim, ffn) must be a multiple of 128.
+        the reference's 4-bit precision class: W4A16 few-row kernels (gemm_w4.hip) up to 64 rows per forward, W4A8
+        above (wgemm8.hip FP4: the same bytes on the block-scaled fp4 x fp8 MFMA, activations per row to e4m3) up to
+        256; every GEMM K (d_model, q_dim, ffn) must be a multiple of 128 (>= 512 for W4A8).
         ``kv_dtype="fp8"``: the KV cache holds e4m3 elements (half the attention bytes per decode step and half
         the cache memory; csrc/attention.hip KV8).
         ``cu_limit``: run every kernel on a stream whose hardware queue may use only that many CUs (a multiple of
@@ -194,7 +195,11 @@ class DecodeEngine:
         # W8A8 needs whole 128-deep stages, >= 4 of them, on every GEMM's K (all real configs; not the tiny ones)
         self.w8a8 = (weight_dtype == "fp8" and os.environ.get("CAIN_W8A8", "1") != "0"
                      and all(k % 128 == 0 and k >= 512 for k in (self.cfg.d_model, self.cfg.q_dim, self.cfg.ffn)))
-        row_cap = W8_MAX_ROWS if weight_dtype == "fp4" or (weight_dtype == "fp8" and not self.w8a8) else MAX_ROWS
+        # MXFP4 above 64 rows: W4A8 on the same packed bytes (csrc/wgemm8.hip FP4), same shape rule as W8A8
+        self.w4a8 = (weight_dtype == "fp4"
+                     and all(k % 128 == 0 and k >= 512 for k in (self.cfg.d_model, self.cfg.q_dim, self.cfg.ffn)))
+        row_cap = W8_MAX_ROWS if (weight_dtype == "fp4" and not self.w4a8) or (weight_dtype == "fp8" and not self.w8a8) \
+            else MAX_ROWS
         self.device = torch.device(device)
         if backend is None:
             backend = "hip" if self.device.type == "cuda" else "torch"
@@ -237,6 +242,7 @@ class DecodeEngine:
         if self.device.type != "cuda":
             raise ValueError("hip backend needs a GPU device")
         w8a8 = self.w8a8 and max(self.max_batch, self.prefill_chunk) > W8A8_MIN_ROWS
+        w4a8 = self.w4a8 and max(self.max_batch, self.prefill_chunk) > W8A8_MIN_ROWS
         packed = pack_for_engine(self.weights, free_natural=not self.keep_natural, weight_dtype=self.weight_dtype,
                                  w8a8=w8a8)
         torch.cuda.synchronize(dev)
@@ -295,7 +301,7 @@ class DecodeEngine:
         shapes = [(cfg.qkv_dim, cfg.d_model), (cfg.d_model, cfg.q_dim), (2 * cfg.ffn, cfg.d_model),
                   (cfg.d_model, cfg.ffn), (cfg.vocab, cfg.d_model)]
         ws = max([ops.gemm_ws_bytes(n, k, m) for n, k in shapes for m in range(1, R + 1)] + [0])
-        if w8a8:
+        if w8a8 or w4a8:
             ws = max([ws] + [int(self.lib.cain_w8a8_ws_bytes(n, k, m)) for n, k in shapes for m in range(17, R + 1)])
             kmax = max(cfg.d_model, cfg.q_dim, cfg.ffn)
             self.x8 = torch.zeros(R, kmax, device=dev, dtype=torch.uint8)

@@ -66,9 +66,12 @@ def load() -> ctypes.CDLL:
             if not LIB_PATH.exists():
                 raise NativeOpsUnavailable(f"{LIB_PATH} missing: run `python -m cain_amd.build`")
         try:
-            lib = ctypes.CDLL(str(LIB_PATH))
+            real = ctypes.CDLL(str(LIB_PATH))
         except OSError as exc:
             raise NativeOpsUnavailable(f"cannot load {LIB_PATH}: {exc}") from exc
+        # an older build loaded for an A/B run (CAIN_KERNELS_LIB) may lack newer entry points: their signatures
+        # are skipped (a call to one then fails by name)
+        lib = _Lenient(real) if os.environ.get("CAIN_KERNELS_LIB") else real
         lib.cain_skinny_gemm_ex.argtypes = ([vp, vp, ci, ci, ci, ci, vp, ci, vp, ci, cf, vp, vp, vp, vp, vp, vp]
                                             + [ci] * 6 + [vp])
         lib.cain_gemm.argtypes = ([vp, vp, ci, ci, ci, ci, vp, ci, vp, ci, cf, vp, vp, vp, vp, vp, vp]
@@ -83,6 +86,8 @@ def load() -> ctypes.CDLL:
         lib.cain_gemm_w8a8.argtypes = ([vp, vp, vp, ci, vp, ci, ci, ci, vp, ci, vp, vp, vp, vp, vp, vp, vp]
                                        + [ci] * 4 + [vp, ctypes.c_longlong, ci, vp])
         lib.cain_quant_rows.argtypes = [vp, ci, ci, ci, vp, ci, vp, ci, cf, vp]
+        lib.cain_gemm_w4a8.argtypes = lib.cain_gemm_w8a8.argtypes
+        lib.cain_w4a8_set_min_rows.argtypes = [ci]
         lib.cain_w8a8_eligible.argtypes = [ci, ci, ci]
         lib.cain_w8a8_ws_bytes.restype = ctypes.c_longlong
         lib.cain_w8a8_ws_bytes.argtypes = [ci, ci, ci]
@@ -116,14 +121,30 @@ def load() -> ctypes.CDLL:
         lib.cain_plan_capture.argtypes = [vp, ci, vp, ci, vp, ctypes.POINTER(ci)]
         lib.cain_graph_launch.argtypes = [vp, vp]
         lib.cain_graph_destroy.argtypes = [vp]
-        if hasattr(lib, "cain_set_cu_budget"):  # (absent from older builds loaded by CAIN_KERNELS_LIB for A/B runs)
-            lib.cain_set_cu_budget.argtypes = [ci]
-            lib.cain_cu_mask.argtypes = [ci, ci, ctypes.POINTER(ctypes.c_uint32), ci]
-            lib.cain_stream_create_cu_limited.restype = vp
-            lib.cain_stream_create_cu_limited.argtypes = [ci]
-            lib.cain_stream_destroy.argtypes = [vp]
-        _lib = lib
-        return lib
+        lib.cain_set_cu_budget.argtypes = [ci]
+        lib.cain_cu_mask.argtypes = [ci, ci, ctypes.POINTER(ctypes.c_uint32), ci]
+        lib.cain_stream_create_cu_limited.restype = vp
+        lib.cain_stream_create_cu_limited.argtypes = [ci]
+        lib.cain_stream_destroy.argtypes = [vp]
+        _lib = real
+        return real
+
+
+class _Lenient:
+    """Signature setter over a CDLL that ignores symbols the library does not export."""
+
+    class _Sink:
+        def __setattr__(self, k, v):
+            pass
+
+    def __init__(self, lib):
+        object.__setattr__(self, "_lib", lib)
+
+    def __getattr__(self, name):
+        try:
+            return getattr(self._lib, name)
+        except AttributeError:
+            return _Lenient._Sink()
 
 
 def available() -> bool:
@@ -379,6 +400,46 @@ def gemm_w8a8(wq8: torch.Tensor, scale: torch.Tensor, x: torch.Tensor, n: int, e
                             _p(ws), nbytes, epi, _stream())
     _check(rc, "gemm_w8a8")
     return out
+
+
+def gemm_w4a8(wq: torch.Tensor, wsc: torch.Tensor, x: torch.Tensor, n: int, epi: int = EPI_BF16, bias=None,
+              out: Optional[torch.Tensor] = None, norm: bool = False, eps: float = 1e-6, rope=None) -> torch.Tensor:
+    """W4A8 wide GEMM (csrc/wgemm8.hip FP4, 16 < M <= 256): MXFP4 weights in the few-row kernel's packing
+    (``models.weights.pack_mxfp4``: wq uint8 [N/16, K/128, 64, 16], wsc e8m0 bytes [N/16, K/128, 64]) on the
+    block-scaled f8f6f4 MFMA against the per-row e4m3 quantisation of ``x`` (``quant_rows``); y = epi(xs * x8 . W^T).
+    Epilogues and ``rope`` as ``gemm_w8a8``."""
+    lib = load()
+    _gpu(wq, wsc, x)
+    M, K = x.shape
+    assert wq.dtype == torch.uint8 and tuple(wq.shape) == (n // 16, K // 128, 64, 16), (tuple(wq.shape), K, n)
+    assert wsc.dtype == torch.uint8 and wsc.numel() * 32 == n * K, (tuple(wsc.shape), K, n)
+    assert w8a8_eligible(n, K, M), (n, K, M)
+    n_out = n // 2 if epi in (EPI_SILU, EPI_GELU) else n
+    if epi == EPI_RESID:
+        assert out is not None and out.shape == (M, n_out), "EPI_RESID updates `out` (the residual) in place"
+    if out is None:
+        out = torch.empty(M, n_out, device=x.device, dtype=torch.float32 if epi == EPI_F32 else torch.bfloat16)
+    x8, xs = quant_rows(x, norm, eps)
+    r = rope or {}
+    if epi == EPI_QKV_ROPE:
+        assert rope is not None, "EPI_QKV_ROPE needs the rope/cache arguments"
+        if is_fp8_cache(r["kc"]):
+            epi |= EPI_KV_FP8
+    T_max = r["kc"].shape[-2] if rope else 0
+    nbytes = int(lib.cain_w8a8_ws_bytes(n, K, M))
+    ws = _workspace(x.device, nbytes)
+    rc = lib.cain_gemm_w4a8(_p(wq), _p(wsc), _p(x8), K, _p(xs), K, n, M, _p(out), out.stride(0), _p(bias),
+                            _p(r.get("slot")), _p(r.get("pos")), _p(r.get("cos_t")), _p(r.get("sin_t")),
+                            _p(r.get("kc")), _p(r.get("vtc")), r.get("H", 0), r.get("Hkv", 0), r.get("hd", 0), T_max,
+                            _p(ws), nbytes, epi, _stream())
+    _check(rc, "gemm_w4a8")
+    return out
+
+
+def set_w4a8_min_rows(m: int) -> None:
+    """Rows above which an MXFP4 engine's forwards run the W4A8 wide kernel instead of the W4A16 few-row one
+    (runtime.hip; default 64, the W4A16 kernels' limit).  Read at every forward / graph capture."""
+    load().cain_w4a8_set_min_rows(int(m))
 
 
 def rmsnorm(x: torch.Tensor, g: torch.Tensor, eps: float, out: Optional[torch.Tensor] = None) -> torch.Tensor:

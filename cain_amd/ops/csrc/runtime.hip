@@ -40,6 +40,10 @@ CAIN_API int cain_gemm_w8a8(const void* Wp8, const float* wscale, const void* X8
                             int N, int M, void* Y, int ldy, const float* bias, const int* slot, const int* pos,
                             const float* cos_t, const float* sin_t, void* kc, void* vtc, int H, int Hkv, int hd,
                             int T_max, void* ws, long long ws_bytes, int epi_flags, hipStream_t st);
+CAIN_API int cain_gemm_w4a8(const void* Wq, const void* wsc, const void* X8, int ld8, const float* xs, int K, int N,
+                            int M, void* Y, int ldy, const float* bias, const int* slot, const int* pos,
+                            const float* cos_t, const float* sin_t, void* kc, void* vtc, int H, int Hkv, int hd,
+                            int T_max, void* ws, long long ws_bytes, int epi_flags, hipStream_t st);
 CAIN_API int cain_quant_rows(const void* x, int ldx, int K, int M, void* x8, int ld8, float* xs, int norm, float eps,
                              hipStream_t st);
 CAIN_API int cain_w8a8_eligible(int N, int K, int M);
@@ -114,14 +118,15 @@ struct CainPlanDesc {
   void* gemm_ws;  // batched-GEMM workspace (counters zeroed once + split-K partials), see gemm.hip
   long long gemm_ws_bytes;
   // WFMT_FP8: e4m3 weights with per-row scales, W8A16 kernels (gemm_w8.hip) up to 64 rows (W8A8 above 16 rows
-  // when the <name>8 packings are present); WFMT_FP4: MXFP4 weights, W4A16 kernels (gemm_w4.hip), up to 64 rows
+  // when the <name>8 packings are present); WFMT_FP4: MXFP4 weights, W4A16 kernels (gemm_w4.hip) up to 64 rows,
+  // W4A8 (wgemm8.hip FP4, the same packed bytes) above cain_w4a8_min_rows when x8 / xs are present
   int wfmt;
   const void* lm_head_scale;  // fp8 / fp4: scales of the packed LM head
   // 1: the KV caches hold fp8 e4m3 elements (same fragment-major offsets, one byte each, unscaled and
   // saturated at +-448): the QKV epilogue writes them (gemm_epi.h EPI_KV_FP8), attention widens them
   int kv8;
-  // W8A8 (fp8 with the <name>8 packings): forwards of more than 16 rows quantise each GEMM input per row into
-  // x8 [Mpad][x8_ld] e4m3 + xs [Mpad] (wgemm8.hip quant_rows_kernel) and run the fp8-MFMA wide kernel
+  // W8A8 (fp8 with the <name>8 packings) / W4A8 (fp4): wide forwards quantise each GEMM input per row into
+  // x8 [Mpad][x8_ld] e4m3 + xs [Mpad] (wgemm8.hip quant_rows_kernel) and run the scaled-MFMA wide kernel
   const void* lm_head8;
   void* x8;
   float* xs;
@@ -172,9 +177,12 @@ thread_local char g_fail[160] = {0};
     }                                                                            \
   } while (0)
 
+// Rows above which an fp4 plan with x8 runs W4A8 (the W4A16 kernels take up to 64).
+static int g_w4a8_min_rows = 64;
+
 // rows a forward of this plan may have: 64 for the few-row-only weight formats
 int max_rows(const CainPlanDesc& d) {
-  if (d.wfmt == WFMT_FP4 || (d.wfmt == WFMT_FP8 && !d.x8)) return d.Mpad < 64 ? d.Mpad : 64;
+  if ((d.wfmt == WFMT_FP4 || d.wfmt == WFMT_FP8) && !d.x8) return d.Mpad < 64 ? d.Mpad : 64;
   return d.Mpad < CAIN_MAX_ROWS ? d.Mpad : CAIN_MAX_ROWS;
 }
 
@@ -191,6 +199,11 @@ int forward(const Plan& p, int M, const CainRows& r, int want_logits, int want_s
                   int ldy, const float* bias, int norm, const void* kc, const void* vc, int epi) -> int {
     void* kcm = const_cast<void*>(kc);
     void* vcm = const_cast<void*>(vc);
+    if (d.wfmt == WFMT_FP4 && d.x8 && (M > g_w4a8_min_rows || M > 64) && cain_w8a8_eligible(N, K, M)) {  // W4A8
+      CK(cain_quant_rows(X, ldx, K, M, d.x8, d.x8_ld, d.xs, norm, d.eps, st));
+      return cain_gemm_w4a8(W, ws, d.x8, d.x8_ld, d.xs, K, N, M, Y, ldy, bias, r.slot, r.pos, d.cos_t, d.sin_t, kcm,
+                            vcm, d.H, d.Hkv, d.hd, d.T_max, d.gemm_ws, d.gemm_ws_bytes, epi, st);
+    }
     if (d.wfmt == WFMT_FP4)
       return cain_gemm_w4(W, ws, X, ldx, K, N, M, Y, ldy, bias, norm, d.eps, r.slot, r.pos, d.cos_t, d.sin_t, kcm, vcm,
                           d.H, d.Hkv, d.hd, d.T_max, epi, st);
@@ -270,6 +283,8 @@ CAIN_API void* cain_plan_create(const CainPlanDesc* desc) {
 }
 
 CAIN_API void cain_plan_destroy(void* plan) { delete static_cast<Plan*>(plan); }
+
+CAIN_API void cain_w4a8_set_min_rows(int m) { g_w4a8_min_rows = m > 16 ? m : 16; }
 
 CAIN_API const char* cain_plan_last_failure() { return g_fail; }
 

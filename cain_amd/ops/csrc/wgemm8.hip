@@ -15,6 +15,13 @@
 // of bf16 and half the bytes through HBM, the per-CU load path and LDS.  A and B only need the same k order in
 // their 32 bytes: lane (r, g) holds k = 64h + 16g + j (h = read 0/1, j < 16) of the stage in both -- W by its
 // packing (pack_mfma_a_fp8_k128: [N/16][K/64][64 lanes][16 B]), X by the XOR-swizzled piece reads.
+//
+// FP4 = true is the W4A8 form for MXFP4 weights (the reference's 4-bit precision class at trial-batch widths):
+// the SAME packed bytes as the few-row W4A16 kernel (models/weights.py pack_mxfp4: [N/16][K/128][64 lanes][16 B],
+// lane (r, g) = row 16t + r, k = 128p + 32g + j at nibble j), which are exactly the fp4 A operand of the 16x16x128
+// scaled MFMA (cbsz 4: 16 B per lane), and the block scales ([N/16][K/128][64] e8m0 bytes, one per lane = one
+// 32-k block) go in as the MFMA's per-lane A scale.  A ring stage is 8 tiles x 1 KiB of W plus their 512 B of
+// scales; X (fp8 rows) is read as pieces 2g, 2g + 1 of its 128-B line, the lane's 32 k.  Y = xs[m] * sum.
 #include <algorithm>
 
 #include "common.h"
@@ -41,23 +48,33 @@ struct W8Scales {
   const float* ws;  // [N] per-output-row weight scale
 };
 
-// Scales of one lane's four outputs: rows n = 16 gt + 4 (lane >> 4) + i of W, activation row m.
+// Scales of one lane's four outputs: rows n = 16 gt + 4 (lane >> 4) + i of W, activation row m (FP4: the weight
+// scales were applied inside the MFMA).
+template <bool FP4 = false>
 __device__ __forceinline__ f32x4 w8_scaled(f32x4 v, const W8Scales& q, int gt, int m, int lane, int M) {
   const float x = q.xs[min(m, M - 1)];
+  if constexpr (FP4) return v * x;
   const f32x4 w = *reinterpret_cast<const f32x4*>(q.ws + gt * 16 + (lane >> 4) * 4);
   return v * w * x;
 }
 
-template <int BM, int DX, int DW, int EPI, int NDMA>
+// W bytes of one ring stage: fp8 8 tiles x 2 KiB; fp4 8 tiles x 1 KiB + 8 x 64 B of scales
+template <int BM, bool FP4>
+constexpr int w8_wbytes() { return FP4 ? WG_NT * 1024 + WG_NT * 64 : WgGeo<BM>::W_BYTES; }
+
+template <int BM, int DX, int DW, int EPI, int NDMA, bool FP4 = false>
 __global__ __launch_bounds__(64 * (8 + NDMA), (8 + NDMA) / 4) void wgemm8_kernel(const GemmArgs a, const WgArgs w,
                                                                                   const W8Scales q) {
   using G = WgGeo<BM>;
   constexpr int NX = DX + 1, NW = DW + 1;
   constexpr int NLOAD = NDMA ? NDMA : 8;
-  constexpr int WPW = 16 / NLOAD;
+  constexpr int WPW = (FP4 ? WG_NT : 16) / NLOAD;  // W LDS-DMA pieces (1 KiB) per loader per stage
+  // fp4: the stage's 512 scale bytes as two 256-B dword pieces, issued by loaders 0 and 1 (spw of them per wave)
   constexpr int XPW = (BM / 8) / NLOAD;
+  constexpr int WB = w8_wbytes<BM, FP4>();
   static_assert(DW >= DX && DX >= 1, "W is issued no later than X of the same stage");
-  static_assert(WPW * NLOAD == 16 && XPW * NLOAD == BM / 8, "loader split");
+  static_assert(WPW * NLOAD == (FP4 ? WG_NT : 16) && XPW * NLOAD == BM / 8, "loader split");
+  static_assert(!FP4 || NLOAD >= 2, "fp4 scale pieces: loaders 0 and 1");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -79,9 +96,24 @@ __global__ __launch_bounds__(64 * (8 + NDMA), (8 + NDMA) / 4) void wgemm8_kernel
   const char* wsrc[WPW];
 #pragma unroll
   for (int j = 0; j < WPW; ++j) {
-    const int qq = lw * WPW + j, tn = qq >> 1, h = qq & 1;
-    wsrc[j] = reinterpret_cast<const char*>(a.Wp) +
-              ((size_t)min(tile0 + tn, ntiles - 1) * KH + (size_t)st0 * 2 + h) * 1024 + lane * 16;
+    if constexpr (FP4) {  // tile tn's 1-KiB block of 128 k per stage
+      const int tn = lw * WPW + j;
+      wsrc[j] = reinterpret_cast<const char*>(a.Wp) +
+                ((size_t)min(tile0 + tn, ntiles - 1) * (KH >> 1) + (size_t)st0) * 1024 + lane * 16;
+    } else {
+      const int qq = lw * WPW + j, tn = qq >> 1, h = qq & 1;
+      wsrc[j] = reinterpret_cast<const char*>(a.Wp) +
+                ((size_t)min(tile0 + tn, ntiles - 1) * KH + (size_t)st0 * 2 + h) * 1024 + lane * 16;
+    }
+  }
+  // fp4 scales: loader lw < 2 copies the 64 scale bytes of tiles 4 lw .. 4 lw + 3 (lane: tile 4 lw + lane / 16,
+  // dword lane % 16)
+  const char* ssrc = nullptr;
+  const int spw = FP4 && loader && lw < 2 ? 1 : 0;
+  if constexpr (FP4) {
+    const int tn = 4 * max(min(lw, 1), 0) + (lane >> 4);
+    ssrc = reinterpret_cast<const char*>(q.ws) + ((size_t)min(tile0 + tn, ntiles - 1) * (KH >> 1) + (size_t)st0) * 64 +
+           (lane & 15) * 4;
   }
   const char* xsrc[XPW];
 #pragma unroll
@@ -91,11 +123,16 @@ __global__ __launch_bounds__(64 * (8 + NDMA), (8 + NDMA) / 4) void wgemm8_kernel
     const int p = (lane & 7) ^ ((r >> 1) & 7);
     xsrc[j] = reinterpret_cast<const char*>(a.X) + (size_t)min(r, a.M - 1) * a.ldx + (size_t)st0 * W8_BK + p * 16;
   }
-  char* const xring = smem + NW * G::W_BYTES;
+  char* const xring = smem + NW * WB;
   auto issue_w = [&](int t) {
-    char* base = smem + (t % NW) * G::W_BYTES;
+    char* base = smem + (t % NW) * WB;
 #pragma unroll
-    for (int j = 0; j < WPW; ++j) glds16(wsrc[j] + (size_t)t * 2048, base + (lw * WPW + j) * 1024, 1);
+    for (int j = 0; j < WPW; ++j) glds16(wsrc[j] + (size_t)t * (FP4 ? 1024 : 2048), base + (lw * WPW + j) * 1024, 1);
+    if constexpr (FP4) {
+      if (spw)
+        __builtin_amdgcn_global_load_lds((gbl_void_t*)(ssrc + (size_t)t * 64),
+                                         (lds_void_t*)(base + WG_NT * 1024 + lw * 256), 4, 0, 0);
+    }
   };
   auto issue_x = [&](int t) {
     char* base = xring + (t % NX) * G::X_BYTES;
@@ -105,7 +142,7 @@ __global__ __launch_bounds__(64 * (8 + NDMA), (8 + NDMA) / 4) void wgemm8_kernel
   auto younger_than = [&](int t) {
     int n = 0;
 #pragma unroll
-    for (int u = t - DX + 1; u < t; ++u) n += WPW * (u + DW < nst) + XPW * (u + DX < nst);
+    for (int u = t - DX + 1; u < t; ++u) n += (WPW + spw) * (u + DW < nst) + XPW * (u + DX < nst);
     return n;
   };
   auto issue_step = [&](int t) {
@@ -118,7 +155,10 @@ __global__ __launch_bounds__(64 * (8 + NDMA), (8 + NDMA) / 4) void wgemm8_kernel
   const int c = lane & 15, g = lane >> 4;
   int woff[G::TN];
 #pragma unroll
-  for (int tn = 0; tn < G::TN; ++tn) woff[tn] = (wn * G::TN + tn) * 2048 + lane * 16;
+  for (int tn = 0; tn < G::TN; ++tn) woff[tn] = (wn * G::TN + tn) * (FP4 ? 1024 : 2048) + lane * 16;
+  // X pieces 4h + g: k = 64h + 16g + j, the fp8 B operand's own k order (measured, tools/w4a8_probe.py: byte 16h + j
+  // of lane group g meets k 64h + 16g + j of A) -- the fp8 W packing uses the same order; the fp4 A operand holds
+  // k = 32g + j at nibble j, which is pack_mxfp4's order
   int xoff[2];
 #pragma unroll
   for (int h = 0; h < 2; ++h) xoff[h] = c * 128 + (((4 * h + g) ^ (c >> 1)) << 4);
@@ -151,9 +191,10 @@ __global__ __launch_bounds__(64 * (8 + NDMA), (8 + NDMA) / 4) void wgemm8_kernel
       if constexpr (!NDMA) wait_vmcnt_rt(younger_than(t));
       ring_barrier();
       if constexpr (!NDMA) issue_step(t);
-      const char* wbase = smem + (t % NW) * G::W_BYTES;
+      const char* wbase = smem + (t % NW) * WB;
       const char* xbase = xring + (t % NX) * G::X_BYTES + xrow0;
       i32x4 b0[G::MB], b1[G::MB], a0[G::TN], a1[G::TN];
+      int sa[G::TN];
 #pragma unroll
       for (int mb = 0; mb < G::MB; ++mb) {
         b0[mb] = *reinterpret_cast<const i32x4*>(xbase + mb * 2048 + xoff[0]);
@@ -162,15 +203,26 @@ __global__ __launch_bounds__(64 * (8 + NDMA), (8 + NDMA) / 4) void wgemm8_kernel
 #pragma unroll
       for (int tn = 0; tn < G::TN; ++tn) {
         a0[tn] = *reinterpret_cast<const i32x4*>(wbase + woff[tn]);
-        a1[tn] = *reinterpret_cast<const i32x4*>(wbase + 1024 + woff[tn]);
+        if constexpr (FP4)
+          sa[tn] = *reinterpret_cast<const uint8_t*>(wbase + WG_NT * 1024 + (wn * G::TN + tn) * 64 + lane);
+        else
+          a1[tn] = *reinterpret_cast<const i32x4*>(wbase + 1024 + woff[tn]);
       }
 #pragma unroll
       for (int tn = 0; tn < G::TN; ++tn) {
-        const i32x8 av = cat16(a0[tn], a1[tn]);
+        if constexpr (FP4) {
+          const i32x8 av = i32x8{a0[tn][0], a0[tn][1], a0[tn][2], a0[tn][3], 0, 0, 0, 0};  // 16 B of e2m1
 #pragma unroll
-        for (int mb = 0; mb < G::MB; ++mb)
-          acc[tn][mb] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(av, cat16(b0[mb], b1[mb]), acc[tn][mb],
-                                                                         0, 0, 0, 127, 0, 127);
+          for (int mb = 0; mb < G::MB; ++mb)
+            acc[tn][mb] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(av, cat16(b0[mb], b1[mb]), acc[tn][mb],
+                                                                           4, 0, 0, sa[tn], 0, 127);
+        } else {
+          const i32x8 av = cat16(a0[tn], a1[tn]);
+#pragma unroll
+          for (int mb = 0; mb < G::MB; ++mb)
+            acc[tn][mb] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(av, cat16(b0[mb], b1[mb]), acc[tn][mb],
+                                                                           0, 0, 0, 127, 0, 127);
+        }
       }
     }
   }
@@ -188,7 +240,7 @@ __global__ __launch_bounds__(64 * (8 + NDMA), (8 + NDMA) / 4) void wgemm8_kernel
         const int gt = tile0 + wn * G::TN + tn;
         const int unit = gt * G::RB + wm * G::MB + mb;
         const int m = (wm * G::MB + mb) * 16 + c;
-        const f32x4 v = gt < ntiles ? w8_scaled(acc[tn][mb], q, gt, m, lane, a.M) : acc[tn][mb];
+        const f32x4 v = gt < ntiles ? w8_scaled<FP4>(acc[tn][mb], q, gt, m, lane, a.M) : acc[tn][mb];
         f16x4 h;
 #pragma unroll
         for (int i = 0; i < 4; ++i) h[i] = (_Float16)fminf(fmaxf(v[i], -65504.f), 65504.f);
@@ -202,7 +254,7 @@ __global__ __launch_bounds__(64 * (8 + NDMA), (8 + NDMA) / 4) void wgemm8_kernel
 #pragma unroll
     for (int mb = 0; mb < G::MB; ++mb) {
       const int m = (wm * G::MB + mb) * 16 + c;
-      f32x4 v = gt < ntiles ? w8_scaled(acc[tn][mb], q, gt, m, lane, a.M) : acc[tn][mb];
+      f32x4 v = gt < ntiles ? w8_scaled<FP4>(acc[tn][mb], q, gt, m, lane, a.M) : acc[tn][mb];
       f32x4 pv;
 #pragma unroll
       for (int i = 0; i < 4; ++i) pv[i] = __shfl_xor(v[i], 32, 64);
@@ -323,18 +375,18 @@ W8Plan w8_plan(int N, int K, int M) {
   return p;
 }
 
-template <int BM, int DX, int DW, int EPI, int NDMA>
+template <int BM, int DX, int DW, int EPI, int NDMA, bool FP4 = false>
 hipError_t w8_launch(const GemmArgs& a, const WgArgs& w, const W8Scales& q, const W8Plan& p, hipStream_t st) {
   using G = WgGeo<BM>;
-  constexpr int lds = (DW + 1) * G::W_BYTES + (DX + 1) * G::X_BYTES;
+  constexpr int lds = (DW + 1) * w8_wbytes<BM, FP4>() + (DX + 1) * G::X_BYTES;
   static_assert(lds <= 160 * 1024, "LDS");
   static bool attr = [] {
-    return hipFuncSetAttribute(reinterpret_cast<const void*>(&wgemm8_kernel<BM, DX, DW, EPI, NDMA>),
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(&wgemm8_kernel<BM, DX, DW, EPI, NDMA, FP4>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, lds) == hipSuccess;
   }();
   if (!attr) return hipErrorInvalidConfiguration;
-  hipLaunchKernelGGL((wgemm8_kernel<BM, DX, DW, EPI, NDMA>), dim3(p.nblk * p.ks), dim3(64 * (8 + NDMA)), lds, st, a,
-                     w, q);
+  hipLaunchKernelGGL((wgemm8_kernel<BM, DX, DW, EPI, NDMA, FP4>), dim3(p.nblk * p.ks), dim3(64 * (8 + NDMA)), lds, st,
+                     a, w, q);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || p.ks == 1) return e;
   const int n_units = p.nblk * WG_NT * G::RB;
@@ -349,17 +401,18 @@ hipError_t w8_launch(const GemmArgs& a, const WgArgs& w, const W8Scales& q, cons
   return hipGetLastError();
 }
 
-template <int BM>
+template <int BM, bool FP4 = false>
 hipError_t w8_launch_e(int epi, const GemmArgs& a, const WgArgs& w, const W8Scales& q, const W8Plan& p,
                        hipStream_t st) {
-  constexpr int DX = BM == 256 ? 2 : 3, DW = BM == 256 ? 3 : 5;  // 160 KiB rings, as the bf16 defaults
+  // 160 KiB rings, as the bf16 defaults; fp4's 8.5-KiB W stages: the same X ring, 6 W stages (147 / 115 KiB)
+  constexpr int DX = BM == 256 ? 2 : 3, DW = FP4 ? 5 : (BM == 256 ? 3 : 5);
   switch (epi) {
-    case EPI_BF16: return w8_launch<BM, DX, DW, EPI_BF16, 4>(a, w, q, p, st);
-    case EPI_RESID: return w8_launch<BM, DX, DW, EPI_RESID, 4>(a, w, q, p, st);
-    case EPI_F32: return w8_launch<BM, DX, DW, EPI_F32, 4>(a, w, q, p, st);
-    case EPI_SILU: return w8_launch<BM, DX, DW, EPI_SILU, 4>(a, w, q, p, st);
-    case EPI_GELU: return w8_launch<BM, DX, DW, EPI_GELU, 4>(a, w, q, p, st);
-    case EPI_QKV_ROPE: return w8_launch<BM, DX, DW, EPI_QKV_ROPE, 4>(a, w, q, p, st);
+    case EPI_BF16: return w8_launch<BM, DX, DW, EPI_BF16, 4, FP4>(a, w, q, p, st);
+    case EPI_RESID: return w8_launch<BM, DX, DW, EPI_RESID, 4, FP4>(a, w, q, p, st);
+    case EPI_F32: return w8_launch<BM, DX, DW, EPI_F32, 4, FP4>(a, w, q, p, st);
+    case EPI_SILU: return w8_launch<BM, DX, DW, EPI_SILU, 4, FP4>(a, w, q, p, st);
+    case EPI_GELU: return w8_launch<BM, DX, DW, EPI_GELU, 4, FP4>(a, w, q, p, st);
+    case EPI_QKV_ROPE: return w8_launch<BM, DX, DW, EPI_QKV_ROPE, 4, FP4>(a, w, q, p, st);
     default: return hipErrorInvalidValue;
   }
 }
@@ -388,12 +441,12 @@ CAIN_API int cain_quant_rows(const void* x, int ldx, int K, int M, void* x8, int
   return int(hipGetLastError());
 }
 
-// Y = epi(xs[m] * ws[n] * X8 . W8^T).  Wp8: pack_mfma_a_fp8_k128; X8 [M][ld8] e4m3 rows (cain_quant_rows);
-// ws: >= cain_w8a8_ws_bytes of scratch; the rest as cain_gemm (gemm.hip), including the EPI_KV_FP8 flag.
-CAIN_API int cain_gemm_w8a8(const void* Wp8, const float* wscale, const void* X8, int ld8, const float* xs, int K,
-                            int N, int M, void* Y, int ldy, const float* bias, const int* slot, const int* pos,
-                            const float* cos_t, const float* sin_t, void* kc, void* vtc, int H, int Hkv, int hd,
-                            int T_max, void* ws, long long ws_bytes, int epi_flags, hipStream_t st) {
+namespace {
+
+int w8a8_run(bool fp4, const void* Wp8, const void* wscale, const void* X8, int ld8, const float* xs, int K, int N,
+             int M, void* Y, int ldy, const float* bias, const int* slot, const int* pos, const float* cos_t,
+             const float* sin_t, void* kc, void* vtc, int H, int Hkv, int hd, int T_max, void* ws, long long ws_bytes,
+             int epi_flags, hipStream_t st) {
   const int epi = epi_flags & EPI_MASK;
   if (!cain_w8a8_eligible(N, K, M) || ld8 % 16) return -1;
   if (epi == EPI_QKV_ROPE && (hd % 16 || (hd / 2) % 8)) return -1;
@@ -409,7 +462,32 @@ CAIN_API int cain_gemm_w8a8(const void* Wp8, const float* wscale, const void* X8
   WgArgs w{};
   w.ks = p.ks, w.kst = p.kst, w.part = ws ? reinterpret_cast<float*>(static_cast<char*>(ws) + W8_SLAB_OFFSET) : nullptr;
   w.xcd_blk = p.ks > 1 && p.nblk % 8 == 0;  // XCD-local split-K (wgemm_ring.h wg_block_of)
-  const W8Scales q{xs, wscale};
-  const hipError_t e = p.bm == 256 ? w8_launch_e<256>(epi, a, w, q, p, st) : w8_launch_e<128>(epi, a, w, q, p, st);
+  const W8Scales q{xs, static_cast<const float*>(wscale)};
+  hipError_t e;
+  if (fp4) e = p.bm == 256 ? w8_launch_e<256, true>(epi, a, w, q, p, st) : w8_launch_e<128, true>(epi, a, w, q, p, st);
+  else e = p.bm == 256 ? w8_launch_e<256>(epi, a, w, q, p, st) : w8_launch_e<128>(epi, a, w, q, p, st);
   return int(e);
+}
+
+}  // namespace
+
+// Y = epi(xs[m] * ws[n] * X8 . W8^T).  Wp8: pack_mfma_a_fp8_k128; X8 [M][ld8] e4m3 rows (cain_quant_rows);
+// ws: >= cain_w8a8_ws_bytes of scratch; the rest as cain_gemm (gemm.hip), including the EPI_KV_FP8 flag.
+CAIN_API int cain_gemm_w8a8(const void* Wp8, const float* wscale, const void* X8, int ld8, const float* xs, int K,
+                            int N, int M, void* Y, int ldy, const float* bias, const int* slot, const int* pos,
+                            const float* cos_t, const float* sin_t, void* kc, void* vtc, int H, int Hkv, int hd,
+                            int T_max, void* ws, long long ws_bytes, int epi_flags, hipStream_t st) {
+  return w8a8_run(false, Wp8, wscale, X8, ld8, xs, K, N, M, Y, ldy, bias, slot, pos, cos_t, sin_t, kc, vtc, H, Hkv, hd,
+                  T_max, ws, ws_bytes, epi_flags, st);
+}
+
+// W4A8: Y = epi(xs[m] * X8 . W^T) with MXFP4 weights in the few-row kernel's packing (pack_mxfp4: Wq
+// [N/16][K/128][64][16] e2m1 bytes, wsc [N/16][K/128][64] e8m0 bytes); same shapes, workspace and epilogues as
+// cain_gemm_w8a8 (cain_w8a8_eligible, cain_w8a8_ws_bytes).
+CAIN_API int cain_gemm_w4a8(const void* Wq, const void* wsc, const void* X8, int ld8, const float* xs, int K, int N,
+                            int M, void* Y, int ldy, const float* bias, const int* slot, const int* pos,
+                            const float* cos_t, const float* sin_t, void* kc, void* vtc, int H, int Hkv, int hd,
+                            int T_max, void* ws, long long ws_bytes, int epi_flags, hipStream_t st) {
+  return w8a8_run(true, Wq, wsc, X8, ld8, xs, K, N, M, Y, ldy, bias, slot, pos, cos_t, sin_t, kc, vtc, H, Hkv, hd,
+                  T_max, ws, ws_bytes, epi_flags, st);
 }

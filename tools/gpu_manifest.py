@@ -92,6 +92,12 @@ SETS = {
     # board power after a 1,000-word on-device run (the study's cooldown evidence)
     "r4_cooldown": [("cooldown", 600, f"{PY} tools/cooldown_trace.py --out gpurun_out/r4_cooldown/cooldown.json "
                                       f"--csv gpurun_out/r4_cooldown/cooldown_trace.csv")],
+    # W4A8: MXFP4 weights at trial-batch widths (wgemm8.hip FP4)
+    "r4_w4a8": [
+        ("w4a8_tests", 600, f"{TEST} tests/test_w4a8_gpu.py"),
+        ("b256_fp4", 400, f"{PY} bench.py --weights fp4 --steps 3 --warmup 1 --no-single --no-energy"),
+        prof("b256_fp4", "--weights fp4 --steps 1 --warmup 1 --no-single --no-energy"),
+    ],
     "suite": [("gpu_suite", 1500, f"{PY} -u -m pytest tests -m gpu -x -q --timeout 600 --timeout-method thread")],
     # the driver's bench command
     "bench": [("bench", 900, f"{PY} bench.py --gpus 1 --steps 20 --warmup 5")],
