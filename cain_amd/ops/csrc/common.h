@@ -32,17 +32,6 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
-// Maximum over each 16-lane row of the wave for NON-NEGATIVE floats (their bit patterns order as integers): four
-// DPP row rotations, VALU only -- no LDS round trip (wave_max's ds_bpermute chain costs ~6 waits per value).
-__device__ __forceinline__ float row16_max_nonneg(float v) {
-  int x = __float_as_int(v);
-  x = max(x, __builtin_amdgcn_update_dpp(x, x, 0x128, 0xf, 0xf, false));  // row_ror:8
-  x = max(x, __builtin_amdgcn_update_dpp(x, x, 0x124, 0xf, 0xf, false));  // row_ror:4
-  x = max(x, __builtin_amdgcn_update_dpp(x, x, 0x122, 0xf, 0xf, false));  // row_ror:2
-  x = max(x, __builtin_amdgcn_update_dpp(x, x, 0x121, 0xf, 0xf, false));  // row_ror:1
-  return __int_as_float(x);
-}
-
 // Epilogue math on the hardware reciprocal / reciprocal square root (v_rcp_f32 / v_rsq_f32, ~1 ulp): hipcc's IEEE
 // division and denormal-safe rsqrtf expand to ~10 dependent VALU instructions each, which made the 256-row gate/up
 // epilogue (4 SiLU divisions + 1 RMSNorm division per 16 x 16 tile) ~5 us of a ~70 us kernel

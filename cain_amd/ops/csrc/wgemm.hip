@@ -71,8 +71,9 @@ constexpr int WG_CTR_BYTES = 16 * 1024;  // the workspace region before the slab
 //
 // H16: split-K slabs in fp16 instead of fp32 (wgemm_reduce_kernel H16 = true reads them): half the slab bytes
 // stored, written back at the kernel boundary (MI355X_MICROARCH.md 'boundary': + dirty bytes / 6 TB/s) and read by
-// the reduce.  Partials saturate at +-65504 (the reduce sums in fp32); tests/test_wgemm_gpu.py compares them with
-// fp32 slabs on rows of outliers.  (Round 3's loader alternatives -- loader-wave sums of squares, W-only / X-only
+// the reduce.  Each lane's partials (one activation row) are stored scaled -- NORM: by rsqrt of the row's split sum
+// of squares, else by a power of two -- so rows of outliers keep fp16's relative precision (the reduce sums in
+// fp32); tests/test_wgemm_gpu.py compares them with fp32 slabs on such rows.  (Round 3's loader alternatives -- loader-wave sums of squares, W-only / X-only
 // loader roles, rotated k start, non-temporal X, stage-ordered prologue -- and the in-launch split-K combine all
 // measured within box-to-box noise or slower, profiles/r3/README.md, and were removed.)
 template <int BM, int DX, int DW, int EPI, bool NORM, int NDMA, int ABL = 0, bool H16 = false>
@@ -301,6 +302,12 @@ __global__ __launch_bounds__(64 * (8 + NDMA), (8 + NDMA) / 4) void wgemm_kernel(
     const int n_units = nblk * WG_NT * G::RB;
     // wgemm_reduce_kernel, the next launch on the stream, combines them
     if (compute) {
+      float rs[G::MB];  // NORM: 1 / sqrt(the lane's row sum of squares over this split)
+#pragma unroll
+      for (int mb = 0; mb < G::MB; ++mb) {
+        const int m = (wm * G::MB + mb) * 16 + c;
+        rs[mb] = MSQ ? __builtin_amdgcn_rsqf(s_ss[m] + s_ss[BM + m] + 1e-30f) : 1.f;
+      }
 #pragma unroll
       for (int tn = 0; tn < G::TN; ++tn)
 #pragma unroll
@@ -308,20 +315,26 @@ __global__ __launch_bounds__(64 * (8 + NDMA), (8 + NDMA) / 4) void wgemm_kernel(
           const int unit = (tile0 + wn * G::TN + tn) * G::RB + wm * G::MB + mb;
           const size_t e = ((size_t)kc * n_units + unit) * 64 + lane;
           if constexpr (H16) {
-            // scaled per (unit, 16-lane row group) by a power of two that keeps the group's largest partial < 2^14
-            // (the reducer multiplies it back): rows of outliers in the residual stream keep fp16's relative
-            // precision instead of saturating at 65504 (tests/test_wgemm_gpu.py test_fp16_slabs_scale_outlier_rows).
-            // The group maximum is four DPP rotations (a whole-unit wave_max -- 6 LDS permutes and waits per unit --
-            // cost ~3 us per split GEMM at 256 rows, profiles/r4/README.md).
+            // fp16 partials scaled per activation row (each lane holds one row m of the unit): NORM shapes by
+            // rsqrt of the row's split sum of squares (|partial| <= sqrt(ss) * |W row|, so a row of residual-stream
+            // outliers stores weight-sized values), the others by a power of two keeping the lane's largest
+            // partial < 2^14 (exponent byte per lane in part_ex); the reducer multiplies back -- no cross-lane work
+            // (tests/test_wgemm_gpu.py test_fp16_slabs_scale_outlier_rows; costs, profiles/r4/README.md)
             const f32x4 v = acc[tn][mb];
-            const float mx = row16_max_nonneg(fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
-            const int ex = max(__builtin_amdgcn_frexp_expf(mx) - 14, 0);  // mx < 2^(ex + 14)
-            const float inv = __builtin_amdgcn_ldexpf(1.f, -ex);
+            f32x4 sv;
+            if constexpr (MSQ) {
+              sv = v * rs[mb];
+            } else {
+              const float mx = fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3])));
+              const int ex = max(__builtin_amdgcn_frexp_expf(mx) - 14, 0);  // mx < 2^(ex + 14)
+#pragma unroll
+              for (int i = 0; i < 4; ++i) sv[i] = __builtin_amdgcn_ldexpf(v[i], -ex);
+              w.part_ex[e] = (uint8_t)ex;
+            }
             f16x4 h;  // (the clamp only bites on non-finite partials)
 #pragma unroll
-            for (int i = 0; i < 4; ++i) h[i] = (_Float16)fminf(fmaxf(v[i] * inv, -65504.f), 65504.f);
+            for (int i = 0; i < 4; ++i) h[i] = (_Float16)fminf(fmaxf(sv[i], -65504.f), 65504.f);
             reinterpret_cast<f16x4*>(w.part)[e] = h;
-            if ((lane & 15) == 0) w.part_sc[((size_t)kc * n_units + unit) * 4 + (lane >> 4)] = __builtin_amdgcn_ldexpf(1.f, ex);
           } else {
             reinterpret_cast<f32x4*>(w.part)[e] = acc[tn][mb];
           }
@@ -409,18 +422,24 @@ __global__ __launch_bounds__(256) void wgemm_reduce_kernel(const GemmArgs a, con
     if constexpr (H16) return f32x4{(float)x[0], (float)x[1], (float)x[2], (float)x[3]};
     else return x;
   };
-  const float* scsrc = w.part_sc + (size_t)unit * 4 + (lane >> 4);  // H16: the lane's row-group scale per split
+  auto unscale = [](f32x4 x, int ex) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) x[i] = __builtin_amdgcn_ldexpf(x[i], ex);
+    return x;
+  };
+  const uint8_t* exsrc = w.part_ex + (size_t)unit * 64 + lane;  // H16 without NORM: the lane's exponent per split
   const float* ssrc = w.part_ss + (size_t)(gt / WG_NT) * ks * BM + m;
   f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
   float ss = 0.f;
   if constexpr (KS > 0) {
     slab_t p[KS];
-    float q[KS], sc[KS];
+    float q[KS];
+    int ex[KS];
 #pragma unroll
     for (int k = 0; k < KS; ++k) p[k] = src[(size_t)k * n_units * 64];
-    if constexpr (H16) {
+    if constexpr (H16 && !NORM) {
 #pragma unroll
-      for (int k = 0; k < KS; ++k) sc[k] = scsrc[(size_t)k * n_units * 4];
+      for (int k = 0; k < KS; ++k) ex[k] = exsrc[(size_t)k * n_units * 64];
     }
     if constexpr (NORM) {
 #pragma unroll
@@ -428,14 +447,17 @@ __global__ __launch_bounds__(256) void wgemm_reduce_kernel(const GemmArgs a, con
     }
 #pragma unroll
     for (int k = 0; k < KS; ++k) {
-      if constexpr (H16) v += widen(p[k]) * sc[k];
+      if constexpr (H16 && NORM) v += widen(p[k]) * __builtin_sqrtf(q[k] + 1e-30f);
+      else if constexpr (H16) v += unscale(widen(p[k]), ex[k]);
       else v += widen(p[k]);
       if constexpr (NORM) ss += q[k];
     }
   } else {
     for (int k = 0; k < ks; ++k) {
-      if constexpr (H16) v += widen(src[(size_t)k * n_units * 64]) * scsrc[(size_t)k * n_units * 4];
-      else v += widen(src[(size_t)k * n_units * 64]);
+      const f32x4 pk = widen(src[(size_t)k * n_units * 64]);
+      if constexpr (H16 && NORM) v += pk * __builtin_sqrtf(ssrc[k * BM] + 1e-30f);
+      else if constexpr (H16) v += unscale(pk, exsrc[(size_t)k * n_units * 64]);
+      else v += pk;
     }
     if constexpr (NORM) {
       for (int k = 0; k < ks; ++k) ss += ssrc[k * BM];
@@ -511,7 +533,7 @@ WgPlan wg_plan(int N, int K, int M) {
   if (p.ks > 1) {
     p.part_floats = (size_t)p.ks * p.nblk * WG_NT * (p.bm / 16) * 256;
     p.ss_floats = (size_t)p.nblk * p.ks * p.bm;
-    p.sc_floats = (size_t)p.ks * p.nblk * WG_NT * (p.bm / 16) * 4;
+    p.sc_floats = (size_t)p.ks * p.nblk * WG_NT * (p.bm / 16) * 16;  // one exponent byte per lane per unit
   }
   return p;
 }
@@ -642,7 +664,7 @@ int wgemm_dispatch(const GemmArgs& a, int epi, bool norm, void* ws, long long ws
   w.stamps = g_wg_stamps;
   w.part = reinterpret_cast<float*>(static_cast<char*>(ws) + WG_CTR_BYTES);
   w.part_ss = w.part + p.part_floats;
-  w.part_sc = w.part_ss + p.ss_floats;
+  w.part_ex = reinterpret_cast<uint8_t*>(w.part_ss + p.ss_floats);
   hipError_t e;
   if (p.bm == 256) e = norm ? wg_launch_e<256, true>(epi, a, w, p, st) : wg_launch_e<256, false>(epi, a, w, p, st);
   else e = norm ? wg_launch_e<128, true>(epi, a, w, p, st) : wg_launch_e<128, false>(epi, a, w, p, st);

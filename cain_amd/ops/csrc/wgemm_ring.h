@@ -77,7 +77,7 @@ struct WgArgs {
   int kst;          // ring stages (64-deep k-steps) per split
   float* part;      // [ks][n_units][64 lanes] f32x4 (ks > 1)
   float* part_ss;   // [nblk][ks][BM] per-row partial sums of squares (ks > 1 && NORM)
-  float* part_sc;   // [ks][n_units][4] power-of-two scale of each fp16 slab unit's 16-lane row groups (value = half * scale)
+  uint8_t* part_ex; // [ks][n_units][64 lanes] power-of-two exponent of each non-NORM fp16 slab lane (value = half * 2^ex)
   int xcd_blk;      // 1: a column block's split partners and its reducers share one XCD (wgemm.hip)
   unsigned* counters;  // workspace head (WG_CTR_BYTES, zero at rest; unused by the kernels)
   unsigned long long* stamps;  // diagnostic build only (wgemm.hip ABL 3): [grid][2 waves][8] timestamps

@@ -76,14 +76,12 @@ SETS = {
                              f"tests/test_engine_gpu.py"),
         ("bench", 400, f"{PY} bench.py --gpus 1 --steps 10 --warmup 3"),
     ],
-    # headline A/B: the HEAD library (ab/libcain_kernels_head.so, fp32-unscaled fp16 slabs) vs the tree's, interleaved
+    # headline A/B, interleaved: the round-3 library (ab/libcain_kernels_head.so: unscaled fp16 slabs, before the
+    # pruning), the tree without the slab scaling (ab/libcain_kernels_noscale.so) and the tree
     "r4_slab_ab": [(f"hl_{tag}_{i}", 300, f"{env}{PY} bench.py --steps 3 --warmup 1 --no-single --no-energy")
-                   for i in range(3) for tag, env in (("head", "CAIN_KERNELS_LIB=ab/libcain_kernels_head.so "),
-                                                      ("new", ""))]
-    + [prof("hl_new", "--steps 1 --warmup 1 --no-single --no-energy"),
-       ("prof_hl_head", 300, "CAIN_KERNELS_LIB=ab/libcain_kernels_head.so rocprofv3 --kernel-trace --stats --output-format csv "
-                             "-d gpurun_out/prof_hl_head -o run -- python3 bench.py --steps 1 --warmup 1 --no-single --no-energy "
-                             "&& find gpurun_out/prof_hl_head -name '*kernel_trace.csv' -delete")],
+                   for i in range(2) for tag, env in (("head", "CAIN_KERNELS_LIB=ab/libcain_kernels_head.so "),
+                                                      ("noscale", "CAIN_KERNELS_LIB=ab/libcain_kernels_noscale.so "),
+                                                      ("new", ""))],
     # batch-1 energy lever: CU-limited streams (tools/cu_sweep.py), after the engine's CU-limit test
     "r4_cu": [
         ("cu_tests", 300, f"{TEST} tests/test_engine_gpu.py -k cu_limited"),
