@@ -203,7 +203,10 @@ def test_cu_limited_engine_matches_full_device(name, dtype, cus):
     b = DecodeEngine(name, cu_limit=cus, **kw)
     assert b.cu_limit == cus and ops.cu_budget() == full
     la, lb = a.last_logits(PROMPTS[:1]), b.last_logits(PROMPTS[:1])
-    assert float((la.float() - lb.float()).norm() / la.float().norm()) < 1e-2
+    # grids sized for fewer CUs split the k sums differently: rounding-level differences, which 32 random-init
+    # layers amplify to a few percent (tests/numerics.py), hence the looser bound at full size
+    tol = 1e-2 if name.startswith("tiny") else 5e-2
+    assert float((la.float() - lb.float()).norm() / la.float().norm()) < tol
     ga = a.generate(PROMPTS[:1], 12, [dict(temperature=0.0, top_k=1, eos_id=-1)])[0]
     gb = b.generate(PROMPTS[:1], 12, [dict(temperature=0.0, top_k=1, eos_id=-1)])[0]
     assert gb.eval_count == 12 and ga.tokens[:4] == gb.tokens[:4]

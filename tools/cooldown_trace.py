@@ -7,8 +7,10 @@ For each model: settle, measure the idle floor (board power from the amd-smi ene
 one batch-1 generation of the full request length (the study's on-device arm), then keep sampling for ``--tail``
 seconds.  Power is the energy counter's slope over ``--bin`` second bins.  Reported per model:
 
-* ``recover_s[p]``: seconds after the generation ends until the ``--window`` s rolling mean stays within p % of idle
-  for the rest of the tail (p = 2, 5, 10);
+* ``settle_s[p]``: seconds after the generation ends until the ``--window`` s rolling mean first falls within p % of
+  idle (p = 2, 5, 10);
+* ``recover_s[p]``: the same, but staying within p % for the rest of the tail (nan if a later excursion -- the
+  board's own ~1-2 s steps back to ~290 W, seen in idle windows too -- breaks it);
 * the trace itself (``--csv``: t after the end of generation, W).
 
     python3 tools/cooldown_trace.py --models llama3.1:8b,qwen2:1.5b,gemma:2b --out gpurun_out/cooldown.json
@@ -77,6 +79,20 @@ def recover_time(series, t_end_ns: int, idle_w: float, pct: float, window_s: flo
     return (nxt[0] - t_end_ns) * 1e-9 if nxt else float("nan")
 
 
+def settle_time(series, t_end_ns: int, idle_w: float, pct: float, window_s: float) -> float:
+    """Seconds after t_end until the rolling window_s mean first falls to <= idle * (1 + pct/100) (nan: never)."""
+    after = [(t, w) for t, w in series if t >= t_end_ns]
+    lim = idle_w * (1 + pct / 100.0)
+    win = int(window_s * 1e9)
+    for k, (t, _) in enumerate(after):
+        if after[-1][0] < t + win // 2:
+            break
+        vals = [w for tt, w in after[k:] if tt < t + win]
+        if sum(vals) / len(vals) <= lim:
+            return (t - t_end_ns) * 1e-9
+    return float("nan")
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--models", default="llama3.1:8b,qwen2:1.5b,gemma:2b")
@@ -119,9 +135,11 @@ def main() -> int:
         series = power_bins(pts, t_gen0 - int(2e9), t_tail, ns.bin)
         gen_w = [w for t, w in series if t_gen0 <= t <= t_end]
         rec = {p: recover_time(series, t_end, idle_w, p, ns.window) for p in (2, 5, 10)}
+        settle = {p: settle_time(series, t_end, idle_w, p, ns.window) for p in (2, 5, 10)}
         res = dict(model=model, weights=ns.weights, tokens=r.eval_count, gen_s=round((t_end - t_gen0) * 1e-9, 3),
                    idle_W=round(idle_w, 1), gen_mean_W=round(sum(gen_w) / max(1, len(gen_w)), 1),
                    first_bin_after_W=round(next((w for t, w in series if t >= t_end), float("nan")), 1),
+                   settle_s={str(k): (None if v != v else round(v, 2)) for k, v in settle.items()},
                    recover_s={str(k): (None if v != v else round(v, 2)) for k, v in rec.items()},
                    tail_s=ns.tail, bin_s=ns.bin, window_s=ns.window)
         print(json.dumps(res), flush=True)
