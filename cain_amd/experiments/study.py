@@ -79,17 +79,20 @@ GPU_MEM_BYTES = 288 * 10**9
 
 def server_footprint_bytes(models: List[str], max_batch: int, max_context: int, weights: str = "bf16",
                            kv: str = "bf16") -> int:
-    """Device memory of one ``cain_amd serve --preload`` process: every model's weights (bf16 = 2 B / param,
-    fp8 = 1 B / param for the projections plus bf16 embeddings) and KV cache for max_batch x max_context,
-    plus ~2 GB of workspaces and allocator slack per model."""
+    """Device memory of one ``cain_amd serve --preload`` process: every model's weights (bf16 = 2 B / param; fp8 =
+    1 B and MXFP4 = 0.53 B (e2m1 + one e8m0 scale per 32) per projection parameter, plus bf16 embeddings) and KV
+    cache for max_batch x max_context, plus ~2 GB of workspaces and allocator slack per model."""
     from ..models.config import get_config
 
+    per_param = {"bf16": 2.0, "fp8": 1.0, "fp4": 0.5 + 1.0 / 32}[weights]
     total = 0
     for m in models:
         cfg = get_config(m)
-        wb = cfg.weight_bytes(1 if weights == "fp8" else 2)
-        if weights == "fp8":
-            wb += cfg.vocab * cfg.d_model  # bf16 embedding beside the fp8 projections
+        wb = cfg.weight_bytes(2)
+        if weights != "bf16":
+            embed = cfg.vocab * cfg.d_model
+            # the projections at per_param bytes beside the bf16 embedding
+            wb = int((cfg.weight_bytes(1) - embed) * per_param) + 2 * embed
         if cfg.tie_embeddings:
             wb += cfg.vocab * cfg.d_model * 2  # the engine packs its own LM-head copy of a tied embedding
         total += wb + cfg.kv_bytes_per_token(1 if kv == "fp8" else 2) * max_batch * max_context + (2 << 30)
@@ -155,7 +158,8 @@ class StudySettings:
     # tracing: the on-device server records each generation with torch.profiler and the
     # Chrome trace is filed as run_dir/kernel_trace.json (adds profiler overhead to the measured window)
     trace: bool = False
-    # on-device weight storage: bf16, or fp8 (e4m3 per-row scaled weights; W8A8 above 16 rows, W8A16 below)
+    # on-device weight storage: bf16, fp8 (e4m3 per-row scaled weights; W8A8 above 16 rows, W8A16 below) or fp4
+    # (OCP MXFP4, the reference's 4-bit class: W4A16 up to 64 rows, W4A8 above)
     weights: str = "bf16"
     # on-device KV-cache storage: bf16, or fp8 (e4m3)
     kv: str = "bf16"
