@@ -80,26 +80,35 @@ def test_fullsize_fp8_weights_match_dequantised_oracle(name, monkeypatch):
 
 
 @pytest.mark.parametrize("name", sorted(MODELS))
-def test_fullsize_fp4_weights_match_dequantised_oracle(name):
+def test_fullsize_fp4_weights_match_dequantised_oracle(name, monkeypatch):
     """The MXFP4 path (the reference's 4-bit precision class) for all seven models at 1 and 64 rows (W4A16) and 256
     rows (W4A8): the fp32 oracle and the bf16-eager baseline both run on the dequantised MXFP4 weights, at 256 rows
     both with the kernels' per-row e4m3 rounding of every GEMM input (a relative criterion only: at full depth
     that rounding alone moves random-init logits to cos ~0.9, test_w8a8_gpu.py)."""
-    eng = DecodeEngine(name, device="cuda", max_batch=256, max_context=128, keep_natural=True, seed=29,
+    # 1 / 64 rows on a 64-row engine with 64-row prefill chunks, so every forward stays on W4A16 (wider prefill
+    # chunks run W4A8 with e4m3 activations, which the bf16-activation oracle does not model)
+    monkeypatch.setenv("CAIN_PREFILL_ROWS", "64")
+    eng = DecodeEngine(name, device="cuda", max_batch=64, max_context=128, keep_natural=True, seed=29,
                        weight_dtype="fp4")
+    monkeypatch.delenv("CAIN_PREFILL_ROWS")
     wq = mxfp4_roundtrip_weights(eng.weights)
     ref = ReferenceModel(wq, memo_weights=True)
     eager = eager_bf16(wq)
     for m, rows in ((1, [0]), (64, [0, 40, 63])):
         _check(eng, ref, eager, _prompts(m), rows, f"{name} fp4 M={m}")
-    del ref, eager
+    w = eng.weights
+    eng.close()
+    del ref, eager, eng
+    torch.cuda.empty_cache()
+    eng = DecodeEngine(name, device="cuda", max_batch=256, max_context=128, weights=w, keep_natural=True, seed=29,
+                       weight_dtype="fp4")
     if eng.w4a8:
         ref = ReferenceModel(wq, memo_weights=True, act_dtype="fp8")
         eager = eager_bf16(wq, act_dtype="fp8")
         _check(eng, ref, eager, _prompts(256), [0, 130, 255], f"{name} fp4 M=256", cos_floor=0.8)
         del ref, eager
     eng.close()
-    del wq
+    del wq, w
     torch.cuda.empty_cache()
 
 

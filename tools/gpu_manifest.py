@@ -96,6 +96,12 @@ SETS = {
         ("b256_fp4", 400, f"{PY} bench.py --weights fp4 --steps 3 --warmup 1 --no-single --no-energy"),
         prof("b256_fp4", "--weights fp4 --steps 1 --warmup 1 --no-single --no-energy"),
     ],
+    # the GPU suite in two calls (a gpurun call is limited to 20 min)
+    "suite_a": [("kernels", 1100, f"{PY} -u -m pytest -q --timeout 300 --timeout-method thread tests/test_ops_gpu.py "
+                                  f"tests/test_wgemm_gpu.py tests/test_w4_gpu.py tests/test_w4a8_gpu.py "
+                                  f"tests/test_w8_gpu.py tests/test_w8a8_gpu.py tests/test_kv8_gpu.py")],
+    "suite_b": [("engine", 1100, f"{PY} -u -m pytest -q --timeout 600 --timeout-method thread tests/test_engine_gpu.py "
+                                 f"tests/test_continuous_gpu.py tests/test_energy_gpu.py tests/test_fullsize_gpu.py")],
     "suite": [("gpu_suite", 1500, f"{PY} -u -m pytest tests -m gpu -x -q --timeout 600 --timeout-method thread")],
     # the driver's bench command
     "bench": [("bench", 900, f"{PY} bench.py --gpus 1 --steps 20 --warmup 5")],
