@@ -102,6 +102,12 @@ SETS = {
                                   f"tests/test_w8_gpu.py tests/test_w8a8_gpu.py tests/test_kv8_gpu.py")],
     "suite_b": [("engine", 1100, f"{PY} -u -m pytest -q --timeout 600 --timeout-method thread tests/test_engine_gpu.py "
                                  f"tests/test_continuous_gpu.py tests/test_energy_gpu.py tests/test_fullsize_gpu.py")],
+    # round-end evidence: the driver's bench command, then kernel stats of the headline and of batch-1 fp4
+    "r4_final": [
+        ("bench", 900, f"{PY} bench.py --gpus 1 --steps 20 --warmup 5"),
+        prof("headline_final", "--steps 1 --warmup 1 --no-single --no-energy"),
+        prof("b1_llama_fp4_final", "--batch 1 --steps 1 --warmup 1 --no-energy --no-single --weights fp4"),
+    ],
     "suite": [("gpu_suite", 1500, f"{PY} -u -m pytest tests -m gpu -x -q --timeout 600 --timeout-method thread")],
     # the driver's bench command
     "bench": [("bench", 900, f"{PY} bench.py --gpus 1 --steps 20 --warmup 5")],
