@@ -1,0 +1,51 @@
+"""CPU checks of round-4 helpers: the study's device-memory estimate per weight format and the cooldown-trace
+arithmetic of tools/cooldown_trace.py (power from a cumulative energy counter, settle / recover times)."""
+import sys
+from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parent.parent / "tools"))
+
+from cain_amd.experiments.study import server_footprint_bytes  # noqa: E402
+from cain_amd.models import get_config  # noqa: E402
+from cooldown_trace import power_bins, recover_time, settle_time  # noqa: E402
+
+
+def test_footprint_orders_and_fp4_size():
+    args = (["llama3.1:8b"], 4, 2048)
+    b16, f8, f4 = (server_footprint_bytes(*args, weights=w) for w in ("bf16", "fp8", "fp4"))
+    assert b16 > f8 > f4
+    cfg = get_config("llama3.1:8b")
+    embed = cfg.vocab * cfg.d_model
+    proj = cfg.weight_bytes(1) - embed
+    # the fp4 estimate differs from the bf16 one only by the projections' bytes per parameter
+    assert abs((b16 - f4) - (proj * (2 - 0.53125))) < 16
+
+
+def _trace(steps):
+    """Cumulative (t_ns, J) points every 10 ms from [(seconds, watts), ...] segments."""
+    pts, t, j = [], 0, 0.0
+    for dur, w in steps:
+        for _ in range(int(dur / 0.01)):
+            pts.append((t, j))
+            t += 10_000_000
+            j += w * 0.01
+    pts.append((t, j))
+    return pts
+
+
+def test_power_bins_recover_power():
+    pts = _trace([(1.0, 1000.0), (2.0, 300.0)])
+    ser = power_bins(pts, 0, pts[-1][0], 0.25)
+    assert abs(ser[0][1] - 1000.0) < 1e-6 and abs(ser[-1][1] - 300.0) < 1e-6
+
+
+def test_settle_and_recover_times():
+    # run ends at 2 s; 290 W for 5 s, then the 257 W floor, with one 2-s excursion to 290 W at +15 s
+    pts = _trace([(2.0, 1000.0), (5.0, 290.0), (8.0, 257.0), (2.0, 290.0), (10.0, 257.0)])
+    ser = power_bins(pts, 0, pts[-1][0], 0.25)
+    t_end = 2_000_000_000
+    st = settle_time(ser, t_end, 257.0, 2, 1.0)
+    assert 4.5 <= st <= 5.5, st
+    rec = recover_time(ser, t_end, 257.0, 2, 1.0)
+    assert rec > 14.0, rec  # the later excursion breaks "stays within" until it is over
+    assert settle_time(ser, t_end, 257.0, 20, 1.0) < 0.3  # 290 W is within 20 %: the first bin after the end
