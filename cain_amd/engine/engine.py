@@ -140,12 +140,8 @@ def _set_cu_budget(lib, n: int) -> None:
 def attention_splits(M: int, Hkv: int, T_max: int) -> int:
     """Position splits per (row, kv head): ~256 workgroups in flight, >= 4 blocks of 32 per split at
     full context, <= 64 splits (measured: 1024-WG targets lose more to the split combine than they
-    gain in parallelism, profiles/kernels.md).  ``CAIN_ATTN_SPLIT_BLOCKS`` = b > 0 additionally caps a
-    split at b blocks of 32 positions (bounds one workgroup's serial work at wide batches); ``CAIN_ATTN_NSPLIT``
-    forces the count (tuning)."""
-    forced = int(os.environ.get("CAIN_ATTN_NSPLIT", "0") or 0)
-    if forced > 0:
-        return min(64, forced)
+    gain in parallelism, profiles/kernels.md).  (Round 1-3's per-split block cap and forced split count were tuning
+    switches; their measurements are in profiles/r2/attn_occupancy.md.)"""
     if M * Hkv <= 64:
         # few (row, kv head) pairs run 8-wave workgroups (attention.hip): position splits up to ~64 workgroups
         # (<= 8 splits, >= 4 blocks of 32 positions per split at full context), and at most 64 blocks per split.
@@ -156,9 +152,6 @@ def attention_splits(M: int, Hkv: int, T_max: int) -> int:
         few = min(8, T_max // 128, 64 // (M * Hkv))
         return int(max(1, min(64, max(few, math.ceil((T_max // 32) / 64)))))
     ns = max(1, min(T_max // 128, math.ceil(256 / (M * Hkv))))
-    per = int(os.environ.get("CAIN_ATTN_SPLIT_BLOCKS", "0") or 0)
-    if per > 0:
-        ns = max(ns, math.ceil((T_max // 32) / per))
     return int(max(1, min(64, ns)))
 
 

@@ -108,6 +108,12 @@ SETS = {
         prof("headline_final", "--steps 1 --warmup 1 --no-single --no-energy"),
         prof("b1_llama_fp4_final", "--batch 1 --steps 1 --warmup 1 --no-energy --no-single --weights fp4"),
     ],
+    # separate precision configurations of the headline workload (bf16 stays the headline), then the smoke test
+    "r4_configs": [
+        ("cfg_fp4", 300, f"{PY} bench.py --weights fp4 --steps 3 --warmup 1 --no-single"),
+        ("cfg_fp4_kv8", 300, f"{PY} bench.py --weights fp4 --kv fp8 --steps 3 --warmup 1 --no-single"),
+        ("smoke", 300, f"{PY} -c 'import __graft_entry__ as g; g.smoke(); print(\"smoke ok\")'"),
+    ],
     "suite": [("gpu_suite", 1500, f"{PY} -u -m pytest tests -m gpu -x -q --timeout 600 --timeout-method thread")],
     # the driver's bench command
     "bench": [("bench", 900, f"{PY} bench.py --gpus 1 --steps 20 --warmup 5")],
