@@ -386,7 +386,9 @@ static int w4_variant(int N, int K, int M, int epi, int n_cu) {
     const int v = g_w4_var;
     if (!w4_is_stream(v) || w4_stream_fits(W4_WAVES[v], K, M)) return v;  // a stream shape needs its LDS copy
   }
-  const bool w4 = epi == EPI_QKV_ROPE && w4_stream_fits(4, K, M);
+  // 4 waves as well when K is short: below 3 quads per wave of the 8-wave shape its waves idle on the padding
+  // items (qwen2:1.5b, K = 1536: gate/up 7.4 vs 8.6 us, O 3.9 vs 4.1; profiles/r4/ab/w4_short_k.jsonl)
+  const bool w4 = (epi == EPI_QKV_ROPE || kq < 24) && w4_stream_fits(4, K, M);
   if (w4) return W4S_4_4;
   if (w4_stream_fits(8, K, M)) return W4S_8_4;
   if (M > 16) return kq >= 32 ? W4T_8_2_2 : W4T_4_2_2;
