@@ -109,6 +109,8 @@ def main() -> int:
     ap.add_argument("--single-settle", type=float, default=1.0, help="seconds of rest before each batch-1 trial")
     ap.add_argument("--single-models", default="qwen2:1.5b,gemma:2b",
                     help="other models measured at batch 1 (bf16 and MXFP4 weights), comma-separated")
+    ap.add_argument("--w4a8-min-rows", type=int, default=0,
+                    help="MXFP4: rows above which forwards run W4A8 instead of W4A16 (0: the runtime's default, 16)")
     ns = ap.parse_args()
 
     world_env = os.environ.get("WORLD_SIZE")
@@ -138,6 +140,10 @@ def main() -> int:
         torch.cuda.set_device(dev)
 
     from cain_amd.engine import DecodeEngine
+
+    if ns.w4a8_min_rows and not cpu:
+        from cain_amd import ops
+        ops.set_w4a8_min_rows(ns.w4a8_min_rows)
     from cain_amd.models.tokenizer import tokens_for_words
 
     n_tok = tokens_for_words(ns.words)

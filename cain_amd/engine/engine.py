@@ -165,7 +165,7 @@ class DecodeEngine:
         activations quantised per row to e4m3, fp8 MFMA) up to 256 rows; CAIN_W8A8=0 keeps W8A16 only (<= 64
         rows).
         ``weight_dtype="fp4"``: OCP MXFP4 GEMM weights (e2m1, one e8m0 scale per 32 k; 0.53 bytes per parameter),
-        the reference's 4-bit precision class: W4A16 few-row kernels (gemm_w4.hip) up to 64 rows per forward, W4A8
+        the reference's 4-bit precision class: W4A16 few-row kernels (gemm_w4.hip) up to 16 rows per forward, W4A8
         above (wgemm8.hip FP4: the same bytes on the block-scaled fp4 x fp8 MFMA, activations per row to e4m3) up to
         256; every GEMM K (d_model, q_dim, ffn) must be a multiple of 128 (>= 512 for W4A8).
         ``kv_dtype="fp8"``: the KV cache holds e4m3 elements (half the attention bytes per decode step and half
@@ -188,7 +188,7 @@ class DecodeEngine:
         # W8A8 needs whole 128-deep stages, >= 4 of them, on every GEMM's K (all real configs; not the tiny ones)
         self.w8a8 = (weight_dtype == "fp8" and os.environ.get("CAIN_W8A8", "1") != "0"
                      and all(k % 128 == 0 and k >= 512 for k in (self.cfg.d_model, self.cfg.q_dim, self.cfg.ffn)))
-        # MXFP4 above 64 rows: W4A8 on the same packed bytes (csrc/wgemm8.hip FP4), same shape rule as W8A8
+        # MXFP4 above 16 rows: W4A8 on the same packed bytes (csrc/wgemm8.hip FP4), same shape rule as W8A8
         self.w4a8 = (weight_dtype == "fp4"
                      and all(k % 128 == 0 and k >= 512 for k in (self.cfg.d_model, self.cfg.q_dim, self.cfg.ffn)))
         row_cap = W8_MAX_ROWS if (weight_dtype == "fp4" and not self.w4a8) or (weight_dtype == "fp8" and not self.w8a8) \

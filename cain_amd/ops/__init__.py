@@ -438,7 +438,8 @@ def gemm_w4a8(wq: torch.Tensor, wsc: torch.Tensor, x: torch.Tensor, n: int, epi:
 
 def set_w4a8_min_rows(m: int) -> None:
     """Rows above which an MXFP4 engine's forwards run the W4A8 wide kernel instead of the W4A16 few-row one
-    (runtime.hip; default 64, the W4A16 kernels' limit).  Read at every forward / graph capture."""
+    (runtime.hip; default 16, the W4A8 minimum: W4A8 is 1.5-2.7x faster at 24-64 rows,
+    profiles/r4/ab/w4a8_crossover.txt).  Read at every forward / graph capture."""
     load().cain_w4a8_set_min_rows(int(m))
 
 

@@ -119,7 +119,7 @@ struct CainPlanDesc {
   long long gemm_ws_bytes;
   // WFMT_FP8: e4m3 weights with per-row scales, W8A16 kernels (gemm_w8.hip) up to 64 rows (W8A8 above 16 rows
   // when the <name>8 packings are present); WFMT_FP4: MXFP4 weights, W4A16 kernels (gemm_w4.hip) up to 64 rows,
-  // W4A8 (wgemm8.hip FP4, the same packed bytes) above cain_w4a8_min_rows when x8 / xs are present
+  // W4A8 (wgemm8.hip FP4, the same packed bytes) above 16 rows (cain_w4a8_set_min_rows) when x8 / xs are present
   int wfmt;
   const void* lm_head_scale;  // fp8 / fp4: scales of the packed LM head
   // 1: the KV caches hold fp8 e4m3 elements (same fragment-major offsets, one byte each, unscaled and
@@ -177,8 +177,10 @@ thread_local char g_fail[160] = {0};
     }                                                                            \
   } while (0)
 
-// Rows above which an fp4 plan with x8 runs W4A8 (the W4A16 kernels take up to 64).
-static int g_w4a8_min_rows = 64;
+// Rows above which an fp4 plan with x8 runs W4A8 (the W4A16 kernels take up to 64): 16, the W4A8 minimum -- at 24 /
+// 48 / 64 rows W4A8 decodes 7.7k / 13.6k / 16.6k tok/s against W4A16's 5.1k / 5.0k / 6.4k
+// (profiles/r4/ab/w4a8_crossover.txt)
+static int g_w4a8_min_rows = 16;
 
 // rows a forward of this plan may have: 64 for the few-row-only weight formats
 int max_rows(const CainPlanDesc& d) {

@@ -114,6 +114,10 @@ SETS = {
         ("cfg_fp4_kv8", 300, f"{PY} bench.py --weights fp4 --kv fp8 --steps 3 --warmup 1 --no-single"),
         ("smoke", 300, f"{PY} -c 'import __graft_entry__ as g; g.smoke(); print(\"smoke ok\")'"),
     ],
+    # W4A16 vs W4A8 at mid widths (MXFP4 engines; runtime default: W4A8 above 64 rows)
+    "r4_w4a8_cross": [(f"b{b}_t{t}", 240, f"{PY} bench.py --weights fp4 --batch {b} --steps 2 --warmup 1 --no-single "
+                                          f"--no-energy --w4a8-min-rows {t}")
+                      for b in (24, 48, 64) for t in (16, 64)],
     "suite": [("gpu_suite", 1500, f"{PY} -u -m pytest tests -m gpu -x -q --timeout 600 --timeout-method thread")],
     # the driver's bench command
     "bench": [("bench", 900, f"{PY} bench.py --gpus 1 --steps 20 --warmup 5")],
