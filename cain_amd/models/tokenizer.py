@@ -40,6 +40,9 @@ class SyntheticTokenizer:
         self.vocab = vocab
         self.bos_id = bos_id
         self.eos_id = eos_id
+        # id -> piece table, built on the first decode: detokenising a 256-row x 1,334-token step otherwise rebuilt
+        # ~341k strings in Python (0.75 s, ~6 % of the step), where a real (Rust) tokenizer's decode is a table lookup
+        self._table = None
 
     def _piece_id(self, piece: str) -> int:
         h = int.from_bytes(hashlib.blake2b(piece.encode("utf-8"), digest_size=8).digest(), "little")
@@ -53,6 +56,9 @@ class SyntheticTokenizer:
         return ids
 
     def piece(self, tid: int) -> str:
+        return self._make_piece(tid)
+
+    def _make_piece(self, tid: int) -> str:
         if tid < self.n_special:
             return ""
         x = tid * 2654435761 & 0xFFFFFFFF
@@ -62,7 +68,14 @@ class SyntheticTokenizer:
         return (" " + s) if tid % 4 else s
 
     def decode(self, ids: List[int]) -> str:
-        return "".join(self.piece(int(t)) for t in ids).lstrip()
+        import numpy as np
+
+        if self._table is None:
+            self._table = np.array([self._make_piece(t) for t in range(self.vocab)], dtype=object)
+        a = np.asarray(ids, dtype=np.int64).reshape(-1)
+        if a.size and (a.min() < 0 or a.max() >= self.vocab):  # out-of-vocabulary ids (tests): piece by piece
+            return "".join(self._make_piece(int(t)) for t in a).lstrip()
+        return "".join(self._table[a].tolist()).lstrip()
 
     @staticmethod
     def count_words(text: str) -> int:
