@@ -49,3 +49,17 @@ def test_settle_and_recover_times():
     rec = recover_time(ser, t_end, 257.0, 2, 1.0)
     assert rec > 14.0, rec  # the later excursion breaks "stays within" until it is over
     assert settle_time(ser, t_end, 257.0, 20, 1.0) < 0.3  # 290 W is within 20 %: the first bin after the end
+
+
+def test_lenient_signature_setter_skips_missing_symbols():
+    """A/B runs load older kernel builds (CAIN_KERNELS_LIB): signatures of entry points they lack are skipped."""
+    import ctypes
+
+    from cain_amd.ops import _Lenient
+
+    libc = ctypes.CDLL(None)
+    lib = _Lenient(libc)
+    lib.strlen.argtypes = [ctypes.c_char_p]            # present: set on the real function
+    lib.no_such_entry_point_xyz.argtypes = [ctypes.c_int]  # absent: ignored
+    assert libc.strlen.argtypes == [ctypes.c_char_p]
+    assert not hasattr(libc, "no_such_entry_point_xyz")
