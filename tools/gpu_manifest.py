@@ -118,6 +118,9 @@ SETS = {
     "r4_w4a8_cross": [(f"b{b}_t{t}", 240, f"{PY} bench.py --weights fp4 --batch {b} --steps 2 --warmup 1 --no-single "
                                           f"--no-energy --w4a8-min-rows {t}")
                       for b in (24, 48, 64) for t in (16, 64)],
+    # decode steps per captured graph (host launches per generation), headline, interleaved
+    "r4_spg": [(f"spg{k}_{i}", 240, f"{PY} bench.py --steps 3 --warmup 1 --no-single --no-energy --steps-per-graph {k}")
+               for i in range(2) for k in (16, 32, 64)],
     "suite": [("gpu_suite", 1500, f"{PY} -u -m pytest tests -m gpu -x -q --timeout 600 --timeout-method thread")],
     # the driver's bench command
     "bench": [("bench", 900, f"{PY} bench.py --gpus 1 --steps 20 --warmup 5")],
