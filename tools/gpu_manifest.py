@@ -121,6 +121,10 @@ SETS = {
     # decode steps per captured graph (host launches per generation), headline, interleaved
     "r4_spg": [(f"spg{k}_{i}", 240, f"{PY} bench.py --steps 3 --warmup 1 --no-single --no-energy --steps-per-graph {k}")
                for i in range(2) for k in (16, 32, 64)],
+    # wave-per-row activation quantiser (wgemm8.hip quant_rows_wave_kernel) vs the 256-thread one, fp4 256 rows
+    "r4_quant_ab": [("quant_tests", 300, f"{TEST} tests/test_w8a8_gpu.py tests/test_w4a8_gpu.py")]
+    + [(f"q_{tag}_{i}", 240, f"{env}{PY} bench.py --weights fp4 --steps 3 --warmup 1 --no-single --no-energy")
+       for i in range(2) for tag, env in (("head", "CAIN_KERNELS_LIB=ab/libcain_kernels_head.so "), ("new", ""))],
     "suite": [("gpu_suite", 1500, f"{PY} -u -m pytest tests -m gpu -x -q --timeout 600 --timeout-method thread")],
     # the driver's bench command
     "bench": [("bench", 900, f"{PY} bench.py --gpus 1 --steps 20 --warmup 5")],
