@@ -25,8 +25,9 @@ After the timed steps and a ``--settle`` every rank also runs the reference's on
 (batch 1; reference experiment/RunnerConfig.py:120-131): the median of ``--single-trials`` full-length
 generations, each in its own energy window, for the bench model on bf16 (``single_stream_tok_per_s`` /
 ``single_stream_J_per_token``), fp8 e4m3 (``single_stream_fp8_*``) and MXFP4 weights (``single_stream_fp4_*``,
-the reference's 4-bit precision class: Ollama serves 4-bit builds), and for ``--single-models`` (default
-qwen2:1.5b, gemma:2b) on bf16 and MXFP4: ``single_stream_by_model`` with each cell's BASELINE.md numbers.
+the reference's 4-bit precision class: Ollama serves 4-bit builds), for ``--single-models`` (default
+qwen2:1.5b, gemma:2b) on bf16 and MXFP4 and for ``--single-fp4-models`` (default phi3:3.8b, qwen2:7b, gemma:7b,
+mistral:7b) on MXFP4: ``single_stream_by_model``, all 7 study models, with each cell's BASELINE.md numbers.
 """
 from __future__ import annotations
 
@@ -98,7 +99,8 @@ def main() -> int:
     ap.add_argument("--no-energy", action="store_true")
     ap.add_argument("--weights", choices=("bf16", "fp8", "fp4"), default="bf16",
                     help="GEMM weight storage: bf16 (headline), fp8 e4m3 per-row scaled (W8A8 above 16 rows, W8A16 "
-                         "below) or MXFP4 (W4A16, <= 64 rows)")
+                         "below) or MXFP4 (W4A16 with bf16 activations at <= 16 rows, W4A8 with per-row e4m3 "
+                         "activations above: --w4a8-min-rows)")
     ap.add_argument("--kv", choices=("bf16", "fp8"), default="bf16",
                     help="KV-cache storage: bf16 (headline) or fp8 e4m3 (half the attention bytes; separate config)")
     ap.add_argument("--device", choices=("cuda", "cpu"), default="cuda",
@@ -109,6 +111,9 @@ def main() -> int:
     ap.add_argument("--single-settle", type=float, default=1.0, help="seconds of rest before each batch-1 trial")
     ap.add_argument("--single-models", default="qwen2:1.5b,gemma:2b",
                     help="other models measured at batch 1 (bf16 and MXFP4 weights), comma-separated")
+    ap.add_argument("--single-fp4-models", default="phi3:3.8b,qwen2:7b,gemma:7b,mistral:7b",
+                    help="models measured at batch 1 on MXFP4 weights only (the reference's 4-bit class), "
+                         "comma-separated: with --single-models and the bench model, the 7 study models")
     ap.add_argument("--w4a8-min-rows", type=int, default=0,
                     help="MXFP4: rows above which forwards run W4A8 instead of W4A16 (0: the runtime's default, 16)")
     ns = ap.parse_args()
@@ -246,6 +251,8 @@ def main() -> int:
             cases += [(ns.model, "fp8"), (ns.model, "fp4")]
             cases += [(m, dt) for m in filter(None, ns.single_models.split(",")) if m != ns.model
                       for dt in ("bf16", "fp4")]
+            cases += [(m, "fp4") for m in filter(None, ns.single_fp4_models.split(","))
+                      if m != ns.model and (m, "fp4") not in cases]
         sync()
         time.sleep(max(0.0, ns.settle))  # the board returns toward idle after the batched steps
     for model, dtype in cases:
@@ -295,7 +302,10 @@ def main() -> int:
             "scaling": "weak",
             "vs_baseline": round(value / base_tps, 2) if base_tps else None,
             "dtype": ("bf16" if ns.weights == "bf16" else
-                      "bf16 activations, MXFP4 (e2m1 + e8m0 block-32) weights" if ns.weights == "fp4" else
+                      (f"MXFP4 (e2m1 + e8m0 block-32) weights; GEMM activations per-row e4m3 above "
+                       f"{max(16, ns.w4a8_min_rows)} rows (W4A8: this {ns.batch}-row run), bf16 at or below (W4A16)"
+                       if getattr(eng, "w4a8", False) and ns.batch > max(16, ns.w4a8_min_rows) else
+                       "bf16 activations, MXFP4 (e2m1 + e8m0 block-32) weights (W4A16)") if ns.weights == "fp4" else
                       "fp8-e4m3 weights and per-row e4m3 GEMM activations (W8A8), bf16 elsewhere"
                       if getattr(eng, "w8a8", False) else "bf16 activations, fp8-e4m3 weights")
                      + (", fp8-e4m3 KV cache" if ns.kv == "fp8" else ""),

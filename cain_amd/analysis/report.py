@@ -14,6 +14,11 @@ Pipeline (``data-analysis/analysis-visualization.ipynb``):
 7. optional PDFs: density / violin / QQ / scatter (ipynb:560-1003, 1404-1530), per-LLM energy violins
 8. new: per (model, method, length) cells incl. measured J/token and tokens/s when the run table carries
    ``tokens_generated`` (this framework captures the Ollama ``eval_count`` that the reference discarded)
+9. new: energy views (``energy_views.md``): the on-device / remote ratio of mean energy and H1 on both the gross
+   client-device energy (``energy_usage_J``, the reference's quantity) and the idle-subtracted energy
+   (``idle_subtracted_J``), per length.  ``--rederive-remote-board`` re-charges remote rows of run tables written
+   before the one-definition accounting (round 4: a remote server sharing the client's GPU left the client's board
+   at 0 J) with the board's recorded idle power x window, the definition ``experiments/study.py`` now records.
 
 Outputs go to ``--out`` (default: next to the CSV, ``analysis/``): ``summary.{tex,md}``, ``h1.{tex,md}``,
 ``h2.{tex,md}``, ``shapiro.md``, ``per_model.md``, ``results.json``.
@@ -50,10 +55,34 @@ def _title(label: str) -> str:
     return label[:1].upper() + label[1:]
 
 
-def load_run_table(path):
+def rederive_remote_board(df):
+    """Remote rows whose client board was charged 0 J because the remote server shared the client's GPU (run tables
+    from before the one-definition accounting): charge the board at the row's recorded idle power x energy window,
+    as ``StudyConfig.energy_sources_for`` now does ("gpu_idle"), and add it to ``energy_usage_J``.  Idle-subtracted
+    energy is unchanged (the board's part is idle - idle = 0).  Returns the number of rows re-charged."""
+    import pandas as pd
+
+    need = {"method", "gpu_energy_J", "idle_power_W", "energy_window_s", ENERGY}
+    if not need <= set(df.columns):
+        return 0
+    src = df["gpu_energy_source"].astype(str) if "gpu_energy_source" in df.columns else pd.Series("", index=df.index)
+    gpu = pd.to_numeric(df["gpu_energy_J"], errors="coerce")
+    idle = pd.to_numeric(df["idle_power_W"], errors="coerce")
+    win = pd.to_numeric(df["energy_window_s"], errors="coerce")
+    sel = (df["method"] == REMOTE) & (gpu == 0) & idle.notna() & win.notna() & ~src.isin(["measured", "idle_model"])
+    add = (idle * win).where(sel, 0.0)
+    df.loc[sel, "gpu_energy_J"] = add[sel].round(3)
+    df.loc[sel, ENERGY] = (pd.to_numeric(df.loc[sel, ENERGY], errors="coerce") + add[sel]).round(3)
+    df.loc[sel, "gpu_energy_source"] = "idle_model(rederived)"
+    return int(sel.sum())
+
+
+def load_run_table(path, rederive: bool = False):
     import pandas as pd
 
     df = pd.read_csv(path)
+    if rederive:
+        rederive_remote_board(df)
     if ENERGY not in df.columns and "codecarbon__energy_consumed" in df.columns:
         df[ENERGY] = (pd.to_numeric(df["codecarbon__energy_consumed"], errors="coerce") * 3_600_000).round(3)
     if "__done" in df.columns:
@@ -102,6 +131,35 @@ def h1_rows(subsets) -> List[dict]:
         c = S.cliff_delta(a[ENERGY], b[ENERGY])
         rows.append({"length": label, "words": L, "W": w.statistic, "p": w.p_value, "cliffs_delta": c.estimate,
                      "lower_ci": c.lower, "upper_ci": c.upper, "magnitude": c.magnitude})
+    return rows
+
+
+IDLE_SUB = "idle_subtracted_J"
+
+
+def energy_view_rows(subsets) -> List[dict]:
+    """Per length: mean energy per arm, the on-device / remote ratio and H1 (Wilcoxon + Cliff's delta) on the gross
+    client-device energy and, where recorded, on the idle-subtracted energy (same IQR-filtered subsets)."""
+    import pandas as pd
+
+    rows = []
+    for label, L in LENGTH_MAP.items():
+        a, b = subsets.get(f"{ON_DEVICE}_{label}"), subsets.get(f"{REMOTE}_{label}")
+        if a is None or b is None:
+            continue
+        for view, col in (("gross", ENERGY), ("idle_subtracted", IDLE_SUB)):
+            if col not in a.columns or col not in b.columns:
+                continue
+            x = pd.to_numeric(a[col], errors="coerce").dropna()
+            y = pd.to_numeric(b[col], errors="coerce").dropna()
+            if not len(x) or not len(y):
+                continue
+            w, c = S.wilcox_test(x, y), S.cliff_delta(x, y)
+            mx, my = float(x.mean()), float(y.mean())
+            rows.append({"length": label, "words": L, "view": view, "n_on_device": int(len(x)),
+                         "n_remote": int(len(y)), "mean_on_device": mx, "mean_remote": my,
+                         "ratio": mx / my if my > 0 else float("nan"), "W": w.statistic, "p": w.p_value,
+                         "cliffs_delta": c.estimate, "magnitude": c.magnitude})
     return rows
 
 
@@ -245,6 +303,17 @@ def h2_markdown(rows) -> str:
     return "\n".join(out) + "\n"
 
 
+def energy_views_markdown(rows) -> str:
+    lines = ["| Length | View | On-device J (mean) | Remote J (mean) | On-device / remote | W | p | Cliff's delta |",
+             "|---|---|---|---|---|---|---|---|"]
+    for r in rows:
+        ratio = f"{r['ratio']:.2f}x" if r["ratio"] == r["ratio"] else "n/a"
+        lines.append(f"| {_title(r['length'])} ({r['words']}) | {r['view']} | {r['mean_on_device']:.2f} | "
+                     f"{r['mean_remote']:.2f} | {ratio} | {r['W']:.0f} | {_p_fmt(r['p'])} | "
+                     f"{r['cliffs_delta']:.3f} ({r['magnitude']}) |")
+    return "\n".join(lines) + "\n"
+
+
 def per_model_markdown(rows) -> str:
     tok = rows and "J_per_token" in rows[0]
     out = ["| model | method | length | n | energy J | time s |" + (" tokens | J/token | tok/s |" if tok else ""),
@@ -372,15 +441,17 @@ def make_plots(df, subsets, out: Path) -> List[Path]:
 
 
 # ---------------------------------------------------------------------------------------------- entry points
-def analyze(path, out: Optional[Path] = None, plots: bool = False, fmt: str = "both", quiet: bool = False) -> dict:
+def analyze(path, out: Optional[Path] = None, plots: bool = False, fmt: str = "both", quiet: bool = False,
+            rederive: bool = False) -> dict:
     path = Path(path)
     out = Path(out) if out else path.parent / "analysis"
     out.mkdir(parents=True, exist_ok=True)
-    df = load_run_table(path)
+    df = load_run_table(path, rederive=rederive)
     subsets = make_subsets(df)
     res = {"source": str(path), "n_rows": int(len(df)), "subset_sizes": {k: int(len(v)) for k, v in subsets.items()},
            "summary": summary_rows(subsets), "shapiro": shapiro_rows(subsets), "h1": h1_rows(subsets),
-           "h2": h2_rows(subsets), "per_model": per_model_rows(df) if "model" in df.columns else []}
+           "h2": h2_rows(subsets), "per_model": per_model_rows(df) if "model" in df.columns else [],
+           "energy_views": energy_view_rows(subsets), "rederived_remote_board": bool(rederive)}
     texts = {}
     if fmt in ("latex", "both"):
         texts.update({"summary.tex": summary_latex(res["summary"]), "h1.tex": h1_latex(res["h1"]),
@@ -390,14 +461,15 @@ def analyze(path, out: Optional[Path] = None, plots: bool = False, fmt: str = "b
                                                         for r in res["shapiro"] if "W" in r]
         texts.update({"summary.md": summary_markdown(res["summary"]), "h1.md": h1_markdown(res["h1"]),
                       "h2.md": h2_markdown(res["h2"]), "shapiro.md": "\n".join(sh) + "\n",
-                      "per_model.md": per_model_markdown(res["per_model"])})
+                      "per_model.md": per_model_markdown(res["per_model"]),
+                      "energy_views.md": energy_views_markdown(res["energy_views"])})
     for name, t in texts.items():
         (out / name).write_text(t)
     if plots:
         res["plots"] = [str(p) for p in make_plots(df, subsets, out)]
     (out / "results.json").write_text(json.dumps(res, indent=1, default=float))
     if not quiet:
-        for name in ("summary.md", "h1.md", "h2.md"):
+        for name in ("summary.md", "h1.md", "h2.md", "energy_views.md"):
             if name in texts:
                 print(texts[name])
         print(f"wrote {len(texts)} tables{' and plots' if plots else ''} to {out}")
@@ -410,8 +482,11 @@ def main(argv: Optional[List[str]] = None) -> None:
     ap.add_argument("--out", default=None)
     ap.add_argument("--plots", action="store_true", help="also write density/violin/QQ/scatter PDFs")
     ap.add_argument("--format", choices=["latex", "markdown", "both"], default="both")
+    ap.add_argument("--rederive-remote-board", action="store_true",
+                    help="charge remote rows of older run tables (client board 0 J on a shared GPU) at the board's "
+                         "recorded idle power x window")
     a = ap.parse_args(argv)
-    analyze(a.run_table, a.out, a.plots, a.format)
+    analyze(a.run_table, a.out, a.plots, a.format, rederive=a.rederive_remote_board)
 
 
 if __name__ == "__main__":

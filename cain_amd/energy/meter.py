@@ -10,6 +10,9 @@ Energy sources, per window:
 * ``gpu``  — amd-smi energy accumulator of the tracked GPUs, integrated on the
   native sampler's piecewise-linear trace (exact counter deltas, interpolated
   at the window edges);
+* ``gpu_idle`` — the tracked GPUs charged at their measured idle board power x the window
+  (``measure_idle``): the client device's board while another process -- a remote server
+  co-located on the client's GPU -- runs on it, i.e. what the client's idle board costs;
 * ``cpu``  — the host CPU energy counter the native sampler can read (amd-smi
   CPU sockets through HSMP, RAPL package zones, hwmon ``amd_energy``; wrap-aware),
   otherwise codecarbon's CPU-load model ``TDP × mean CPU utilisation × duration``
@@ -349,6 +352,11 @@ class EnergyMeter:
             self._pending = [s for s in self._pending if s["t_ns"] > t1]
         per_gpu = [self.sampler.energy_between(i, t0, t1) for i in range(self.n_gpus)] if "gpu" in self.sources else []
         gpu_j = float(sum(x for x in per_gpu if not math.isnan(x))) if per_gpu else 0.0
+        if "gpu_idle" in self.sources and self.n_gpus and not math.isnan(self.idle_power_w):
+            # the client's board while another process (a co-located remote server) runs on it: charged at the
+            # board's measured idle power, what the client device would have drawn waiting on a remote server
+            gpu_j = self.idle_power_w * dur
+            per_gpu = [gpu_j / self.n_gpus] * self.n_gpus
 
         def mean(key, gpu_only=False):
             vals = [s[key] for s in samples if not math.isnan(s[key]) and (not gpu_only or s["gpu"] >= 0)]
@@ -373,7 +381,7 @@ class EnergyMeter:
         # is the client's working set, charged as is
         idle_sub = float("nan")
         parts = []
-        if "gpu" in self.sources and self.n_gpus:
+        if ("gpu" in self.sources or "gpu_idle" in self.sources) and self.n_gpus:
             parts.append(gpu_j - self.idle_power_w * dur)
         if "cpu" in self.sources:
             parts.append(cpu_j - self.idle_cpu_power_w * dur)

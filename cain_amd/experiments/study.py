@@ -23,11 +23,15 @@ MI355X-native differences:
   every client rank reuses it.  A single-rank study may share its one GPU with the server (runs are strictly
   sequential); the remote arm's ``gpu_usage`` then stays the client's own residency (0) and the board's
   activity goes to ``server_gpu_usage``;
-* energy is the amd-smi hardware accumulator of the measured GPU plus the client's CPU energy -- by default
-  attributed to the client process tree (the rank's run process, its curl child and, for the on-device arm,
-  its own local server: the reference's client laptop ran Ollama itself), CPU seconds x the per-CPU share of
-  the socket TDP, so neither the remote server nor another rank's work is charged (``cpu_attribution``) -- and
-  the client's RAM, on a native sampler thread (``cain_amd.energy``); the remote arm measures the client only;
+* energy is the CLIENT DEVICE's, with one definition in both arms and at every world size (the reference's
+  codecarbon charged its one laptop whole, idle included, in both arms): the device's GPU board (amd-smi
+  hardware accumulator; for the remote arm on a GPU shared with the server, the board's measured idle power x
+  the window, ``gpu_energy_source = idle_model``) plus the client's CPU energy -- by default attributed to the
+  client process tree (the rank's run process, its curl child and, for the on-device arm, its own local
+  server: the reference's client laptop ran Ollama itself), CPU seconds x the per-CPU share of the socket TDP,
+  so neither the remote server nor another rank's work is charged (``cpu_attribution``) -- and the client's
+  RAM, on a native sampler thread (``cain_amd.energy``).  ``idle_subtracted_J`` subtracts the same idle
+  baselines in both arms (a remote row's board part is then ~0);
 * the response JSON is captured (the reference's curl printed it and dropped it), so the run table gains
   ``tokens_generated``, ``J_per_token``, ``tok_per_s``, ``ttft_s`` ... after the reference's columns;
 * topics are drawn with a per-run seeded RNG (reproducible), prompts/lengths are the reference's.
@@ -69,7 +73,7 @@ DEFAULT_TOPICS = REPO_ROOT / "experiments" / "topics.csv"
 REFERENCE_COLUMNS = ["topic", "execution_time", "cpu_usage", "gpu_usage", "memory_usage"]
 EXTRA_COLUMNS = ["tokens_generated", "prompt_tokens", "J_per_token", "tok_per_s", "ttft_s", "gen_time_s",
                  "server_total_s", "server_eval_s", "client_wall_s", "device", "server", "server_gpu_usage",
-                 "idle_power_W", "dp_rank"]
+                 "idle_power_W", "dp_rank", "gpu_energy_source"]
 
 #: c10d store key under which rank 0 publishes the node's one remote server URL ("error:<msg>" on failure)
 REMOTE_URL_KEY = "cain/remote_url/{name}"
@@ -569,11 +573,23 @@ class _StudyBase:
             self._lock_fh = None
 
     def energy_sources_for(self, context: RunnerContext):
-        """The client's energy, as codecarbon counted it: CPU + RAM, plus the client GPU -- except for the remote
-        arm when its server shares that GPU (then the board's energy is the server's, not the client's)."""
-        if context.run_variation.get("method") == "remote" and self.remote_shares_gpu:
-            return ("cpu", "ram")
+        """The client device's energy, ONE definition in both arms and at every world size, as codecarbon counted
+        the reference's one laptop whole, idle included (CodecarbonWrapper.py:53-67): the device's GPU board +
+        the client's CPU + RAM.  The board is measured, except for the remote arm when the remote server shares
+        the client's GPU (a single-GPU study): the board then runs the server's decode, so the client's board is
+        charged at its measured idle power over the window ("gpu_idle") -- the same quantity a data-parallel
+        job measures on a client GPU that idles while its request runs on the dedicated server GPU."""
+        if self._shared_remote(context):
+            return ("gpu_idle", "cpu", "ram")
         return ("gpu", "cpu", "ram")
+
+    def _shared_remote(self, context: RunnerContext) -> bool:
+        return context.run_variation.get("method") == "remote" and self.remote_shares_gpu
+
+    def gpu_energy_source(self, context: RunnerContext) -> str:
+        """Provenance of the row's gpu_energy_J: "measured" (amd-smi accumulator) or "idle_model" (idle board
+        power x window, the remote arm on a GPU shared with the server)."""
+        return "idle_model" if self._shared_remote(context) else "measured"
 
     def start_measurement(self, context: RunnerContext) -> None:
         # the energy window (opened by the plugin just before this body) covers the request; with
@@ -684,5 +700,6 @@ class StudyConfig(_MeasuredStudy):
             "server_gpu_usage": getattr(self, "_server_gpu_usage", ""),
             "idle_power_W": round(float(self.idle_power_w), 2) if self.idle_power_w is not None else "",
             "dp_rank": self.rank,
+            "gpu_energy_source": self.gpu_energy_source(context),
         })
         return data

@@ -275,28 +275,39 @@ def fold_gain(w: torch.Tensor, g: torch.Tensor) -> torch.Tensor:
     return (w.float() * g.float()[None, :]).to(w.dtype)
 
 
-def fp8_roundtrip_weights(mw: ModelWeights) -> ModelWeights:
-    """Copy of ``mw`` whose GEMM weights are dequant(quant_fp8(W)) in bf16 (LM head untied from the
-    embedding table, which the engine keeps in bf16): the torch oracle of a ``weight_dtype="fp8"`` engine."""
-    def rt(w):
-        return dequantize_fp8_rows(*quantize_fp8_rows(w)).to(w.dtype)
+def _unit_gain(cfg: ModelConfig, g: torch.Tensor) -> torch.Tensor:
+    """The stored RMSNorm gain whose effective gain is 1 (0 under Gemma's (1 + w) convention)."""
+    return torch.zeros_like(g) if cfg.norm_add_one else torch.ones_like(g)
 
-    layers = [LayerWeights(attn_norm=lw.attn_norm, wqkv=rt(lw.wqkv), bqkv=lw.bqkv, wo=rt(lw.wo), mlp_norm=lw.mlp_norm,
-                           w_gate=rt(lw.w_gate), w_up=rt(lw.w_up), w_down=rt(lw.w_down)) for lw in mw.layers]
-    return ModelWeights(mw.cfg, mw.embed, mw.final_norm, rt(mw.lm_head), layers)
+
+def _roundtrip(mw: ModelWeights, rt) -> ModelWeights:
+    """Copy of ``mw`` whose GEMM weights are ``rt`` of exactly the matrices the engine quantises: each norm gain
+    folded into the weight it feeds first (``fold_gain``, as ``pack_for_engine``), the gains then set to 1 -- so a
+    block / row scale sees W diag(g), not W, for any gains.  The LM head is untied from the embedding table, which
+    the engine keeps in bf16."""
+    cfg = mw.cfg
+    layers = []
+    for lw in mw.layers:
+        ga, gm = effective_gain(cfg, lw.attn_norm), effective_gain(cfg, lw.mlp_norm)
+        layers.append(LayerWeights(attn_norm=_unit_gain(cfg, lw.attn_norm), wqkv=rt(fold_gain(lw.wqkv, ga)),
+                                   bqkv=lw.bqkv, wo=rt(lw.wo), mlp_norm=_unit_gain(cfg, lw.mlp_norm),
+                                   w_gate=rt(fold_gain(lw.w_gate, gm)), w_up=rt(fold_gain(lw.w_up, gm)),
+                                   w_down=rt(lw.w_down)))
+    lm = rt(fold_gain(mw.lm_head, effective_gain(cfg, mw.final_norm)))
+    return ModelWeights(cfg, mw.embed, _unit_gain(cfg, mw.final_norm), lm, layers)
+
+
+def fp8_roundtrip_weights(mw: ModelWeights) -> ModelWeights:
+    """The torch oracle of a ``weight_dtype="fp8"`` engine: dequant(quant_fp8_rows(W diag(g))) in bf16, unit
+    gains (``_roundtrip``)."""
+    return _roundtrip(mw, lambda w: dequantize_fp8_rows(*quantize_fp8_rows(w)).to(w.dtype))
 
 
 def mxfp4_roundtrip_weights(mw: ModelWeights) -> ModelWeights:
-    """Copy of ``mw`` whose GEMM weights are dequant(quant_mxfp4(W)) in bf16 (LM head untied from the embedding
-    table, which the engine keeps in bf16): the torch oracle of a ``weight_dtype="fp4"`` engine.  The RMSNorm
-    gains stay separate here while the engine quantises W diag(g); with the unit gains of random init the two
-    are the same matrix."""
-    def rt(w):
-        return dequantize_mxfp4(*quantize_mxfp4(w)).to(w.dtype)
-
-    layers = [LayerWeights(attn_norm=lw.attn_norm, wqkv=rt(lw.wqkv), bqkv=lw.bqkv, wo=rt(lw.wo), mlp_norm=lw.mlp_norm,
-                           w_gate=rt(lw.w_gate), w_up=rt(lw.w_up), w_down=rt(lw.w_down)) for lw in mw.layers]
-    return ModelWeights(mw.cfg, mw.embed, mw.final_norm, rt(mw.lm_head), layers)
+    """The torch oracle of a ``weight_dtype="fp4"`` engine: dequant(quant_mxfp4(W diag(g))) in bf16, unit gains
+    (``_roundtrip``): the block scales of the oracle and of the engine are taken over the same gain-folded
+    matrix, so non-unit norm gains are pinned too (tests/test_fp4_pack.py, tests/test_w4_gpu.py)."""
+    return _roundtrip(mw, lambda w: dequantize_mxfp4(*quantize_mxfp4(w)).to(w.dtype))
 
 
 def roundtrip_weights(mw: ModelWeights, weight_dtype: str) -> ModelWeights:

@@ -28,8 +28,8 @@
 // 16x16 partials into a double-buffered LDS slab, one raw barrier, and wave 0 runs the fused epilogue while the
 // others go on.  The activation rows (XL: M x K <= 32 KiB) are staged into LDS once per workgroup by plain loads
 // issued ahead of the weight prologue (the compiler counts both load streams, so nothing drains early); the
-// RMSNorm sums of squares are taken once per workgroup from those staged chunks (8 VALU ops per MFMA when taken
-// from every activation fragment: +2-4 us per GEMM, profiles/r4/).
+// RMSNorm sums of squares are taken once per workgroup from that LDS copy, one wave per row in a fixed order (8
+// VALU ops per MFMA when taken from every activation fragment: +2-4 us per GEMM, profiles/r4/).
 // Wider problems (w4_tile_kernel: up to 64 rows, or activation rows beyond the LDS copy) run one workgroup per
 // (tile, 16*NB-row block) with the activation fragments loaded beside each weight quad.
 #include <algorithm>
@@ -87,7 +87,6 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(4, 4
   const int wave = threadIdx.x >> 6;
   const int KQ = a.K >> 7;                    // 128-wide k quads per tile
   const int qmax = (KQ + WAVES - 1) / WAVES;  // items per tile (every wave walks the same sequence length)
-  if (NORM && threadIdx.x < 16) row_ss[threadIdx.x] = 0.f;
   const int G = gridDim.x;
   const int my_tiles = (npairs - (int)blockIdx.x + G - 1) / G;
   const int n_items = my_tiles * qmax;
@@ -138,17 +137,22 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(4, 4
   }
   w4_barrier();
   if constexpr (NORM) {
-    // RMSNorm sums of squares once per workgroup, from the staged chunks still in registers (every element of X
-    // once: 8 squares per chunk) -- not per weight fragment, where they cost 8 VALU ops per MFMA (+2-4 us per GEMM)
+    // RMSNorm sums of squares once per workgroup from the staged copy (not per weight fragment, where they cost 8
+    // VALU ops per MFMA, +2-4 us per GEMM), in a fixed order so identical seeded runs agree bit for bit (ADVICE r4:
+    // LDS float atomics summed in arrival order): wave w owns rows w, w + WAVES, ...; each lane sums its chunks in
+    // k order, then the wave reduces by xor shuffles.  The first tile_end barrier orders these stores before the
+    // epilogue reads them.
+    for (int r = wave; r < a.M; r += WAVES) {
+      const char* xr = w4_xs + (size_t)r * cpr * 16;
+      float v = 0.f;
+      for (int c = lane; c < cpr; c += 64) {
+        const bf16x8 x8 = *reinterpret_cast<const bf16x8*>(xr + (size_t)c * 16);
 #pragma unroll
-    for (int i = 0; i < XCH; ++i) {
-      const int c = (int)threadIdx.x + i * WAVES * 64;
-      if (c < nch) {
-        float v = 0.f;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) v += bf2f(xst[i][j]) * bf2f(xst[i][j]);
-        atomicAdd(&row_ss[c / cpr], v);
+        for (int j = 0; j < 8; ++j) v += bf2f(x8[j]) * bf2f(x8[j]);
       }
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+      if (lane == 0) row_ss[r] = v;
     }
   }
   // this lane's activation row in LDS and its k group: fragment s of quad p starts at 128p + 32g + 8s.  Lanes of

@@ -260,12 +260,21 @@ def _work_queue(store, prefix: str, todo_ids: List[str], by_id: Dict[str, Dict[s
         if config.operation_type is OperationType.SEMI:
             EventSubscriptionController.raise_event(RunnerEvents.CONTINUE)
     if writer:
-        if budget > 0:
+        stopped = [False]
+
+        def stop_claims() -> None:
             # indices nobody claimed stay TODO: wait for the claimed ones only.  Set the stop key (also when the
             # queue simply ran out) before counting, so an index claimed after the count is handed back
             store.set(f"{prefix}stop", "1")
             claimed = min(n, int(store.add(f"{prefix}next", 0)))
             pending.difference_update(range(claimed, n))
+            stopped[0] = True
+
+        # a claiming writer has stopped claiming by now (queue empty or its budget spent).  A server-only writer
+        # (claims_runs False, e.g. remote=local:0) keeps committing while the other ranks claim, and stops the
+        # claims only when its own budget runs out
+        if budget > 0 and claims:
+            stop_claims()
         last_progress = time.monotonic()
         beats: Dict[int, tuple] = {}  # rank -> (last counter value, when it changed, writer clock)
 
@@ -290,7 +299,14 @@ def _work_queue(store, prefix: str, todo_ids: List[str], by_id: Dict[str, Dict[s
                 last_progress = now
             if not pending:
                 break
-            dead = [i for i in sorted(pending) if not alive(claimant(i), now)]
+            if budget > 0 and not stopped[0] and now - _SESSION_T0[0] > budget:
+                output.console_log_WARNING(f"run budget of {budget:.0f} s used: the remaining runs stay TODO (resume)")
+                stop_claims()
+                if not pending:
+                    break
+            # an index nobody has claimed yet (claimant -1) is waiting for a client rank, not lost: only a claimed
+            # index whose claimant's heartbeat stopped is recorded as failed (the deadline covers the rest)
+            dead = [i for i in sorted(pending) if claimant(i) >= 0 and not alive(claimant(i), now)]
             for i in dead:
                 output.console_log_FAIL(f"run {todo_ids[i]} (queue index {i}) was claimed by rank {claimant(i)}, "
                                         f"whose heartbeat stopped: left TODO")

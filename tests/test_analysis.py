@@ -136,3 +136,41 @@ def test_cliff_delta_complete_separation_has_a_point_interval():
     not the [-1, 1] a 0/0 made of it."""
     r = S.cliff_delta([10.0, 11.0, 12.0, 13.0], [1.0, 2.0, 3.0])
     assert r.estimate == 1.0 and r.lower == 1.0 and r.upper == 1.0 and r.magnitude == "Large"
+
+
+def test_energy_views_and_remote_board_rederivation(tmp_path):
+    """H1 and the arm ratio on gross AND idle-subtracted energy; an older run table whose
+    remote rows left the client board at 0 J (server on the client's GPU) is re-charged at the recorded idle power x
+    window, so gross means the same in both arms."""
+    import csv as _csv
+
+    from cain_amd.analysis.report import analyze
+
+    rows = []
+    for i in range(12):
+        for length, t in ((100, 0.4), (500, 1.6), (1000, 3.2)):
+            w = t * (1 + 0.01 * i)
+            rows.append(dict(__run_id=f"o{i}_{length}", __done="DONE", model="m", method="on_device", length=length,
+                             execution_time=w, cpu_usage=5, gpu_usage=90, memory_usage=3,
+                             energy_usage_J=round(1000 * w, 3), gpu_energy_J=round(999 * w, 3),
+                             idle_subtracted_J=round(740 * w, 3), idle_power_W=260.0, energy_window_s=w))
+            rows.append(dict(__run_id=f"r{i}_{length}", __done="DONE", model="m", method="remote", length=length,
+                             execution_time=w, cpu_usage=6, gpu_usage=0, memory_usage=3,
+                             energy_usage_J=round(1 * w, 3), gpu_energy_J=0.0, idle_subtracted_J=round(1 * w, 3),
+                             idle_power_W=260.0, energy_window_s=w))
+    p = tmp_path / "run_table.csv"
+    with open(p, "w", newline="") as fh:
+        wr = _csv.DictWriter(fh, fieldnames=list(rows[0].keys()))
+        wr.writeheader()
+        wr.writerows(rows)
+    raw = analyze(p, tmp_path / "raw", quiet=True)
+    fixed = analyze(p, tmp_path / "fixed", quiet=True, rederive=True)
+    v_raw = {(r["length"], r["view"]): r for r in raw["energy_views"]}
+    v_fix = {(r["length"], r["view"]): r for r in fixed["energy_views"]}
+    assert set(v_fix) == {(L, v) for L in ("short", "medium", "long") for v in ("gross", "idle_subtracted")}
+    # as written: remote gross is the client's CPU only -> a 1000x ratio; rederived: board idle included -> 1000/261
+    assert v_raw[("long", "gross")]["ratio"] == pytest.approx(1000.0, rel=1e-3)
+    assert v_fix[("long", "gross")]["ratio"] == pytest.approx(1000.0 / 261.0, rel=1e-3)
+    # the idle-subtracted view does not change: the board's part is idle - idle = 0
+    assert v_fix[("long", "idle_subtracted")]["ratio"] == pytest.approx(v_raw[("long", "idle_subtracted")]["ratio"])
+    assert (tmp_path / "fixed" / "energy_views.md").read_text().count("idle_subtracted") == 3

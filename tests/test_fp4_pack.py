@@ -82,3 +82,57 @@ def test_torch_backend_fp4_uses_dequantised_oracle():
     for n in odd:
         with pytest.raises(ValueError):
             DecodeEngine(n, device="cpu", weight_dtype="fp4")
+
+
+def _nonunit_gains(mw, seed=4):
+    g = torch.Generator().manual_seed(seed)
+    cfg = mw.cfg
+
+    def gain(t):
+        v = 1.0 + 0.6 * torch.randn(t.shape, generator=g)  # effective gains spread over ~[-0.8, 2.8]
+        return (v - 1.0 if cfg.norm_add_one else v).to(t.dtype)
+
+    for lw in mw.layers:
+        lw.attn_norm, lw.mlp_norm = gain(lw.attn_norm), gain(lw.mlp_norm)
+    mw.final_norm = gain(mw.final_norm)
+    return mw
+
+
+@pytest.mark.parametrize("name", ["tiny-llama3.1:8b", "tiny-gemma:2b"])
+def test_fp4_oracle_quantises_the_gain_folded_weights(name):
+    """the oracle's MXFP4 block scales are taken over W diag(g), exactly the matrix the engine packs, so
+    the oracle matches the packed bytes for NON-unit norm gains too (it used to quantise W and keep g separate)."""
+    from cain_amd.models.weights import effective_gain, fold_gain, qkv_row_permutation
+
+    cfg = get_config(name)
+    mw = _nonunit_gains(random_weights(cfg, seed=1))
+    rt = mxfp4_roundtrip_weights(mw)
+    assert torch.equal(effective_gain(cfg, rt.layers[0].attn_norm).float(), torch.ones(cfg.d_model))
+    pk = pack_for_engine(mw, weight_dtype="fp4")
+    lp = pk["layers"][0]
+    perm = qkv_row_permutation(cfg)
+    wqkv = dequantize_mxfp4(*unpack_mxfp4(lp["wqkv"], lp["sqkv"])).bfloat16()
+    assert torch.equal(wqkv, rt.layers[0].wqkv[perm])
+    wgu = dequantize_mxfp4(*unpack_mxfp4(lp["wgu"], lp["sgu"])).bfloat16()
+    f = cfg.ffn
+    assert torch.equal(wgu.reshape(f // 8, 2, 8, -1)[:, 0].reshape(f, -1), rt.layers[0].w_gate)
+    assert torch.equal(wgu.reshape(f // 8, 2, 8, -1)[:, 1].reshape(f, -1), rt.layers[0].w_up)
+    lm = dequantize_mxfp4(*unpack_mxfp4(pk["lm_head"], pk["lm_head_scale"])).bfloat16()
+    assert torch.equal(lm, rt.lm_head)
+    # and the old oracle (quantise W, keep g) is a different matrix once the gains are not 1
+    ga = effective_gain(cfg, mw.layers[0].attn_norm)
+    old = fold_gain(dequantize_mxfp4(*quantize_mxfp4(mw.layers[0].wqkv)).bfloat16(), ga)
+    assert not torch.equal(old, rt.layers[0].wqkv)
+
+
+def test_fp8_oracle_quantises_the_gain_folded_weights():
+    from cain_amd.models.weights import dequantize_fp8_rows, fp8_roundtrip_weights, unpack_mfma_a_fp8
+
+    cfg = get_config("tiny-llama3.1:8b")
+    mw = _nonunit_gains(random_weights(cfg, seed=2))
+    rt = fp8_roundtrip_weights(mw)
+    pk = pack_for_engine(mw, weight_dtype="fp8")
+    lp = pk["layers"][0]
+    f = cfg.ffn
+    wgu = dequantize_fp8_rows(unpack_mfma_a_fp8(lp["wgu"]), lp["sgu"]).bfloat16()
+    assert torch.equal(wgu.reshape(f // 8, 2, 8, -1)[:, 0].reshape(f, -1), rt.layers[0].w_gate)

@@ -184,7 +184,7 @@ class _DictStore:
         return all(k in self.d for k in keys)
 
 
-def _writer_pass(monkeypatch, store, todo, **kw):
+def _writer_pass(monkeypatch, store, todo, claims_runs=True, **kw):
     from cain_amd.parallel import fanout
     from cain_amd.runner import store as store_mod
     from cain_amd.runner.models import OperationType
@@ -211,6 +211,8 @@ def _writer_pass(monkeypatch, store, todo, **kw):
 
     class _Cfg:
         operation_type = OperationType.AUTO
+
+    _Cfg.claims_runs = claims_runs
 
     by_id = {t: {"__run_id": t} for t in todo}
     return fanout._work_queue(store, "cain/0/", todo, by_id, _Ctrl(), _Cfg(), True, 2, poll_s=0.01, **kw), committed
@@ -287,3 +289,66 @@ def test_budget_stop_hands_back_a_late_claim(monkeypatch):
     monkeypatch.setattr(fanout, "_SESSION_T0", [time.monotonic() - 10])  # the writer's budget is spent
     failed, committed = _writer_pass(monkeypatch, store, ["a", "b"], rank=0, hb_timeout_s=30, deadline_s=5)
     assert failed == [] and committed == [] and store.check(["cain/0/stop"])
+
+
+def _client(store, todo, rank=1, delay_s=0.02, stop=None):
+    """A client rank's claim loop on the in-process store (claim, run for ``delay_s``, publish), with its heartbeat."""
+    import pickle
+    import threading
+    import time
+
+    from cain_amd.parallel import fanout
+
+    def body():
+        while stop is None or not stop.is_set():
+            store.add(f"cain/hb/{rank}", 1)
+            i = int(store.add("cain/0/next", 1)) - 1
+            if i >= len(todo):
+                return
+            store.set(f"cain/0/claim/{i}", str(rank))
+            if store.check(["cain/0/stop"]):
+                store.set(f"cain/0/res/{i}", pickle.dumps(fanout._SKIPPED))
+                return
+            time.sleep(delay_s)
+            store.set(f"cain/0/res/{i}", pickle.dumps({"__run_id": todo[i]}))
+
+    t = threading.Thread(target=body, daemon=True)
+    t.start()
+    return t
+
+
+def test_server_only_writer_commits_every_client_run(monkeypatch):
+    """the writer (rank 0) hosting only the remote server (claims_runs False, remote=local:0) must not
+    treat not-yet-claimed indices as runs of a dead rank: it commits every row the client ranks publish."""
+    import time
+
+    from cain_amd.parallel import fanout
+
+    monkeypatch.delenv("CAIN_RUN_BUDGET_S", raising=False)
+    monkeypatch.setattr(fanout, "_SESSION_T0", [time.monotonic()])
+    store = _DictStore()
+    todo = [f"run_{i}" for i in range(12)]
+    t = _client(store, todo, delay_s=0.05)
+    failed, committed = _writer_pass(monkeypatch, store, todo, claims_runs=False, rank=0, hb_timeout_s=0.1,
+                                     deadline_s=30)
+    t.join(5)
+    assert failed == [] and sorted(committed) == sorted(todo)
+
+
+def test_server_only_writer_budget_stops_claims_when_spent(monkeypatch):
+    """With CAIN_RUN_BUDGET_S, a server-only writer keeps committing until its own budget runs out, then stops the
+    claims: the client's runs before the stop are committed, the rest stay TODO (no failures)."""
+    import time
+
+    from cain_amd.parallel import fanout
+
+    monkeypatch.setenv("CAIN_RUN_BUDGET_S", "0.5")
+    monkeypatch.setattr(fanout, "_SESSION_T0", [time.monotonic()])
+    store = _DictStore()
+    todo = [f"run_{i}" for i in range(200)]
+    t = _client(store, todo, delay_s=0.05)
+    failed, committed = _writer_pass(monkeypatch, store, todo, claims_runs=False, rank=0, hb_timeout_s=30,
+                                     deadline_s=30)
+    t.join(5)
+    assert failed == [] and 3 <= len(committed) < len(todo)
+    assert committed == todo[:len(committed)] and store.check(["cain/0/stop"])

@@ -177,3 +177,69 @@ def test_study_both_arms_against_real_engine_servers(tmp_path):
     assert all(float(x["gpu_usage"]) == 0.0 and float(x["server_gpu_usage"]) > 0 for x in remote)
     assert all(x["server_gpu_usage"] == "" for x in local)
     assert all(x["server"] != local[0]["server"] for x in remote)
+
+
+class _IdleBoardSampler:
+    """Stand-in for the native sampler of one GPU whose board idles at ``watts`` (a client GPU of a data-parallel
+    job while its remote request runs on the dedicated server GPU)."""
+
+    n, thread_id, host_energy_source = 1, 0, ""
+
+    def __init__(self, watts):
+        self.watts = watts
+
+    def energy_between(self, i, t0, t1):
+        return self.watts * (t1 - t0) * 1e-9
+
+    def drain(self):
+        return []
+
+    def trim(self, t):
+        pass
+
+    def trace_points(self, i):
+        return 0
+
+    def close(self):
+        pass
+
+
+def test_remote_row_energy_has_one_definition_at_every_world_size(monkeypatch):
+    """a remote-arm row means the same thing at world 1 (the remote server shares the client's
+    GPU) and at world 8 (a dedicated server GPU): client board + client CPU + RAM, the board at idle.  At world 1 the
+    board is charged at its measured idle power (``gpu_idle``; it runs the server's decode), at world 8 it is
+    measured while it idles -- the same columns, the same composition, the same idle subtraction."""
+    import time
+
+    from cain_amd.energy.meter import EnergyMeter
+    from cain_amd.experiments.study import StudyConfig
+    from cain_amd.runner.models import RunnerContext
+
+    monkeypatch.setenv("CAIN_STUDY_REMOTE", "local:0")
+    cfg = StudyConfig()
+    ctx = RunnerContext({"__run_id": "r", "method": "remote", "model": "m", "length": "100"}, 0, Path("/tmp"))
+    ondev = RunnerContext({"__run_id": "o", "method": "on_device", "model": "m", "length": "100"}, 0, Path("/tmp"))
+    idle_w, cpu_idle = 260.0, 0.05
+    readings = {}
+    for world, shared in ((1, True), (8, False)):
+        cfg.remote_shares_gpu = shared
+        cfg.dp_world = world
+        srcs = cfg.energy_sources_for(ctx)
+        assert cfg.energy_sources_for(ondev) == ("gpu", "cpu", "ram")
+        assert cfg.gpu_energy_source(ctx) == ("idle_model" if shared else "measured")
+        m = EnergyMeter(smi_indices=[], period_ms=10, cpu_tdp_w=100.0, sources=srcs, cpu_attribution="process")
+        m.sampler.close()
+        m.sampler = _IdleBoardSampler(idle_w)
+        m.idle_power_w, m.idle_cpu_power_w = idle_w, cpu_idle
+        m.start()
+        time.sleep(0.2)
+        readings[world] = m.stop(settle_ms=0)
+    for r in readings.values():
+        # the client's board is charged at idle in both topologies, never 0 and never the server's decode power
+        assert r.gpu_energy_j == pytest.approx(idle_w * r.duration_s, rel=1e-6)
+        assert r.total_energy_j == pytest.approx(r.gpu_energy_j + r.cpu_energy_j + r.ram_energy_j)
+        # idle-subtracted: the board's part is ~0 in both, so what is left is the client's own work
+        assert r.idle_subtracted_j == pytest.approx(r.cpu_energy_j - cpu_idle * r.duration_s + r.ram_energy_j,
+                                                    abs=1e-6)
+    w1, w8 = readings[1], readings[8]
+    assert w1.gpu_power_w == pytest.approx(w8.gpu_power_w, rel=1e-6)
