@@ -167,6 +167,9 @@ class StudySettings:
     weights: str = "bf16"
     # on-device KV-cache storage: bf16, or fp8 (e4m3)
     kv: str = "bf16"
+    # weight storage of a "local:<device>" remote server ("" = the on-device arm's ``weights``: the reference's
+    # Ollama served the same 4-bit builds in both arms)
+    remote_weights: str = ""
     # client CPU energy: "process" (the client process tree's CPU seconds x TDP per CPU) or "system" (this
     # rank's share of the whole host's CPU energy, the round-3 model)
     cpu_attribution: str = "process"
@@ -465,8 +468,9 @@ class _StudyBase:
             return val
         try:
             backend = s.remote_backend or ""
+            rweights = s.remote_weights or s.weights
             if backend != "fake" and dev.isdigit():
-                need = server_footprint_bytes(list(s.models), s.max_batch, s.max_context)
+                need = server_footprint_bytes(list(s.models), s.max_batch, s.max_context, rweights)
                 # a data-parallel job never co-locates (the GPU's rank serves only); a single-rank study may
                 co_located = "on_device" in s.methods and self.remote_shares_gpu
                 if co_located:
@@ -486,6 +490,8 @@ class _StudyBase:
                 args += ["--fake-tok-s", str(s.remote_fake_tok_s), "--fake-prefill-s", str(s.remote_fake_prefill_s)]
             else:
                 args.append("--preload")
+                if rweights != "bf16":
+                    args += ["--weights", rweights]
             srv = _ServerProc(args, log_dir / "remote_node.log", env, role="remote")
             self._servers.append(srv)
             atexit.register(srv.stop)

@@ -200,6 +200,12 @@ def set_wide_gemm_plan(n: int, k: int, bm: int, ks: int, variant: int = -1) -> N
         raise RuntimeError("wide-GEMM plan table full")
 
 
+def set_wide_gemm_variant(v: int) -> None:
+    """Global wide-GEMM ring variant (csrc/wgemm.hip; per-shape plans override it): 0 default, 4 fp32 slabs, 5 the
+    256-column kernel (csrc/wgemm256.hip; 256-row tiles with N % 256 == 0, else the default)."""
+    load().cain_wgemm_set_variant(int(v))
+
+
 def clear_wide_gemm_plans() -> None:
     load().cain_wgemm_clear_shapes()
 

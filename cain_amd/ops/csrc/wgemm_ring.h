@@ -79,6 +79,7 @@ struct WgArgs {
   float* part_ss;   // [nblk][ks][BM] per-row partial sums of squares (ks > 1 && NORM)
   uint8_t* part_ex; // [ks][n_units][64 lanes] power-of-two exponent of each non-NORM fp16 slab lane (value = half * 2^ex)
   int xcd_blk;      // 1: a column block's split partners and its reducers share one XCD (wgemm.hip)
+  int bnt;          // 16-column tiles per column block of the main kernel (wgemm.hip: WG_NT = 8, wgemm256.hip: 16)
   unsigned* counters;  // workspace head (WG_CTR_BYTES, zero at rest; unused by the kernels)
   unsigned long long* stamps;  // diagnostic build only (wgemm.hip ABL 3): [grid][2 waves][8] timestamps
 };

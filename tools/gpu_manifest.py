@@ -28,6 +28,9 @@ def prof(tag: str, args: str, limit: int = 300):
             f"{PY} bench.py {args} && find gpurun_out/prof_{tag} -name '*kernel_trace.csv' -delete")
 
 
+#: every llama3.1:8b wide-GEMM shape on the 256-column kernel (csrc/wgemm256.hip), default split counts
+PL_V5 = "6144:4096:256:0:5,4096:4096:256:0:5,28672:4096:256:0:5,4096:14336:256:0:5,128256:4096:256:0:5"
+
 SETS = {
     # round 4: MXFP4 weights (gemm_w4.hip) -- kernels vs fp32, engine vs oracle, then the single-stream rates
     "r4_fp4": [
@@ -125,6 +128,52 @@ SETS = {
     "r4_quant_ab": [("quant_tests", 300, f"{TEST} tests/test_w8a8_gpu.py tests/test_w4a8_gpu.py")]
     + [(f"q_{tag}_{i}", 240, f"{env}{PY} bench.py --weights fp4 --steps 3 --warmup 1 --no-single --no-energy")
        for i in range(2) for tag, env in (("head", "CAIN_KERNELS_LIB=ab/libcain_kernels_head.so "), ("new", ""))],
+    # round 5: deterministic W4 row sums + the gain-folded fp4 oracle at full size, then batch-1 fp4 rates
+    "r5_check": [
+        ("w4_tests", 600, f"{TEST} tests/test_w4_gpu.py"),
+        ("fp4_gains", 600, f"{TEST} tests/test_fullsize_gpu.py -k nonunit"),
+        ("b1_llama_fp4", 300, f"{B1} --weights fp4"),
+        ("b1_qwen_fp4", 300, f"{B1} --weights fp4 --model qwen2:1.5b"),
+    ],
+    # round 5: the reference's design on MXFP4 weights (both arms fp4), n = 10, 10 s cooldown, one session per call
+    "r5_fp4_study": [("study", 1150, "CAIN_STUDY_WEIGHTS=fp4 STUDY_NAME=fp4_r5 COOLDOWN_MS=10000 REPS=10 "
+                                     "IDLE_SETTLE_S=12 bash tools/study_chunk.sh 960")],
+    # round 5: the 256-column wide GEMM (wgemm256.hip): numerics first (a new kernel), then isolated shape timings
+    # against the 128-column ring, then the headline with every llama shape on it (interleaved with the default)
+    "r5_w256": [
+        ("w256_tests", 300, f"{TEST} tests/test_wgemm256_gpu.py"),
+        ("wgemm_bench", 300, f"{PY} tools/wgemm_bench.py --rows 256 --variants 0,5 --no-lt --no-old "
+                             f"--splits 256:16,256:8,192:16"),
+    ] + [(f"hl_{tag}_{i}", 240, f"{env}{PY} bench.py --steps 3 --warmup 1 --no-single --no-energy")
+         for i in range(2) for tag, env in (("v0", ""), ("v5", f"CAIN_WGEMM_PLANS={PL_V5} "))],
+    # 256-column kernel after the fixed-operand X X^T: numerics, isolated timings, PMC of both kernels
+    "r5_w256b": [
+        ("w256_tests", 300, f"{TEST} tests/test_wgemm256_gpu.py"),
+        ("wgemm_bench", 300, f"{PY} tools/wgemm_bench.py --rows 256 --variants 0,5 --no-lt --no-old"),
+        ("pmc", 300, "bash tools/pmc_wgemm.sh r5_w256b/pmc --rows 256 --variants 0,5 --only gateup,down,o"),
+    ],
+    # ablations of both wide kernels: full / DMA only / MFMA only (old: 0, 8, 9; 256-column: 5, 6, 7), kernel stats
+    "r5_w256_abl": [
+        ("abl", 300, "rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r5_w256_abl/prof -o run -- "
+                     f"{PY} tools/wgemm_bench.py --rows 256 --variants 0,8,9,5,6,7 --no-lt --no-old "
+                     "--splits 256:16 --only gateup,down,o"),
+    ],
+    # the 256-column kernel with 64-deep X stages (whole 128-B lines): numerics, ablations, headline A/B
+    "r5_w256c": [
+        ("w256_tests", 300, f"{TEST} tests/test_wgemm256_gpu.py"),
+        ("abl", 300, "rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r5_w256c/prof -o run -- "
+                     f"{PY} tools/wgemm_bench.py --rows 256 --variants 0,8,9,5,6,7 --no-lt --no-old "
+                     "--splits 256:16"),
+    ] + [(f"hl_{tag}_{i}", 240, f"{env}{PY} bench.py --steps 3 --warmup 1 --no-single --no-energy")
+         for i in range(1) for tag, env in (("v0", ""), ("v5", f"CAIN_WGEMM_PLANS={PL_V5} "))],
+    "r5_w256d": [
+        ("w256_tests", 300, f"{TEST} tests/test_wgemm256_gpu.py"),
+        ("hl_v11", 240, f"CAIN_WGEMM_PLANS={PL_V5.replace(':5', ':11')} {PY} bench.py --steps 3 --warmup 1 --no-single "
+                        "--no-energy"),
+        ("abl", 300, "rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r5_w256d/prof -o run -- "
+                     f"{PY} tools/wgemm_bench.py --rows 256 --variants 0,5,11 --no-lt --no-old "
+                     "--splits 256:16 --only gateup,down,o,qkv"),
+    ],
     "suite": [("gpu_suite", 1500, f"{PY} -u -m pytest tests -m gpu -x -q --timeout 600 --timeout-method thread")],
     # the driver's bench command
     "bench": [("bench", 900, f"{PY} bench.py --gpus 1 --steps 20 --warmup 5")],
