@@ -174,6 +174,20 @@ SETS = {
                      f"{PY} tools/wgemm_bench.py --rows 256 --variants 0,5,11 --no-lt --no-old "
                      "--splits 256:16 --only gateup,down,o,qkv"),
     ],
+    # batch-1 QKV: where its 9 us go (the RoPE / KV-append epilogue, the fused norm, the kernel shape)
+    "r5_qkv": [
+        ("w4_qkv", 300, f"{PY} tools/w4_bench.py --roles qkv,qkv_plain,qkv_plain_nonorm,o --variants rule,0,1,2 "
+                        "--dtypes fp4"),
+    ],
+    # batch 1: the attention merge with its partial outputs loaded beside (m, l); QKV diagnostics; rates; kernel stats
+    "r5_b1": [
+        ("attn_tests", 300, f"{TEST} tests/test_ops_gpu.py -k 'attention or sample'"),
+        ("w4_qkv", 300, f"{PY} tools/w4_bench.py --roles qkv,qkv_plain,qkv_plain_nonorm,o --variants rule,0,1,2 "
+                        "--dtypes fp4"),
+        ("b1_llama_fp4", 300, f"{B1} --weights fp4"),
+        ("b1_qwen_fp4", 300, f"{B1} --weights fp4 --model qwen2:1.5b"),
+        prof("b1_llama_fp4_r5", "--batch 1 --steps 1 --warmup 1 --no-energy --no-single --weights fp4"),
+    ],
     "suite": [("gpu_suite", 1500, f"{PY} -u -m pytest tests -m gpu -x -q --timeout 600 --timeout-method thread")],
     # the driver's bench command
     "bench": [("bench", 900, f"{PY} bench.py --gpus 1 --steps 20 --warmup 5")],

@@ -61,7 +61,9 @@ def main() -> int:
     d, F = cfg.d_model, cfg.ffn
     roles = {"qkv": (cfg.qkv_dim, d, ops.EPI_QKV_ROPE, True), "o": (d, cfg.q_dim, ops.EPI_RESID, False),
              "gateup": (2 * F, d, ops.EPI_SILU, True), "down": (d, F, ops.EPI_RESID, False),
-             "lm_head": (cfg.vocab, d, ops.EPI_F32, True)}
+             "lm_head": (cfg.vocab, d, ops.EPI_F32, True),
+             # the QKV shape without its RoPE / KV-append epilogue (bf16 output), with and without the fused norm
+             "qkv_plain": (cfg.qkv_dim, d, ops.EPI_BF16, True), "qkv_plain_nonorm": (cfg.qkv_dim, d, ops.EPI_BF16, False)}
     M = ns.rows
     x = torch.randn(M, max(d, F, cfg.q_dim), device=dev).bfloat16()
     # the fused QKV epilogue's operands: RoPE tables, fragment-major caches, one slot / position per row
