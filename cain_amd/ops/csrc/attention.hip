@@ -260,20 +260,6 @@ __global__ __launch_bounds__(AW * 64, OCC) void attn_decode_kernel(
     s_ticket = __hip_atomic_fetch_add(counters + mk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
   if (s_ticket != unsigned(nsplit - 1)) return;
-  // the partial outputs this thread merges are requested first, beside the (m, l) pairs: one memory round trip for
-  // both instead of two (the merge weights need (m, l) only after the loads return).  Up to 16 splits in
-  // registers; more (long contexts at few rows) load in the merge loop below.
-  constexpr int NJR = 16;
-  const int e0 = threadIdx.x;  // this thread's first (gg, d) of the merge loop below
-  float pre_o[NJR];
-  const bool pre = nsplit <= NJR && e0 < nout;
-  if (pre) {
-    const int gg = e0 / HD, d = e0 - (e0 / HD) * HD;
-    const float* po = part_o + (pbase + (size_t)gg * nsplit) * HD + d;
-#pragma unroll
-    for (int j = 0; j < NJR; ++j)
-      pre_o[j] = j < nsplit ? __hip_atomic_load(po + (size_t)j * HD, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.f;
-  }
   // split weights into LDS once (sc1 loads: never served from this CU's stale L1)
   __shared__ float s_w[16 * 64];   // [gg][j] merge weight 2^(m_j - M) / den
   const int nw = G * nsplit;      // <= 16 * 64
@@ -300,16 +286,11 @@ __global__ __launch_bounds__(AW * 64, OCC) void attn_decode_kernel(
   __syncthreads();
   for (int e = threadIdx.x; e < nout; e += AW * 64) {
     const int gg = e / HD, d = e - (e / HD) * HD;
+    const float* po = part_o + (pbase + (size_t)gg * nsplit) * HD + d;
     float num = 0.f;
-    if (pre && e == e0) {
-#pragma unroll
-      for (int j = 0; j < NJR; ++j) num += j < nsplit ? s_w[gg * 64 + j] * pre_o[j] : 0.f;
-    } else {
-      const float* po = part_o + (pbase + (size_t)gg * nsplit) * HD + d;
 #pragma unroll 8
-      for (int j = 0; j < nsplit; ++j)
-        num += s_w[gg * 64 + j] * __hip_atomic_load(po + (size_t)j * HD, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    for (int j = 0; j < nsplit; ++j)
+      num += s_w[gg * 64 + j] * __hip_atomic_load(po + (size_t)j * HD, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     out[(size_t)m * ldo + (kh * G + gg) * HD + d] = f2bf(num * s_l[0][gg]);
   }
 }

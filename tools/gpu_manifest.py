@@ -188,6 +188,16 @@ SETS = {
         ("b1_qwen_fp4", 300, f"{B1} --weights fp4 --model qwen2:1.5b"),
         prof("b1_llama_fp4_r5", "--batch 1 --steps 1 --warmup 1 --no-energy --no-single --weights fp4"),
     ],
+    # attention merge: partial outputs loaded beside (m, l) (tree) vs round 4's two round trips (ab/ library),
+    # interleaved on one box; then the driver's bench command (7-model single-stream table)
+    "r5_attn_ab": [prof(f"b1_attn_{tag}_{i}", "--batch 1 --steps 1 --warmup 1 --no-energy --no-single --weights fp4")
+                   if tag == "new" else
+                   (f"prof_b1_attn_{tag}_{i}", 300,
+                    f"CAIN_KERNELS_LIB=ab/libcain_kernels_attnold.so rocprofv3 --kernel-trace --stats --output-format csv "
+                    f"-d gpurun_out/prof_b1_attn_{tag}_{i} -o run -- {PY} bench.py --batch 1 --steps 1 --warmup 1 "
+                    f"--no-energy --no-single --weights fp4 && find gpurun_out/prof_b1_attn_{tag}_{i} "
+                    f"-name '*kernel_trace.csv' -delete")
+                   for i in range(2) for tag in ("old", "new")],
     "suite": [("gpu_suite", 1500, f"{PY} -u -m pytest tests -m gpu -x -q --timeout 600 --timeout-method thread")],
     # the driver's bench command
     "bench": [("bench", 900, f"{PY} bench.py --gpus 1 --steps 20 --warmup 5")],
