@@ -201,6 +201,13 @@ SETS = {
     "suite": [("gpu_suite", 1500, f"{PY} -u -m pytest tests -m gpu -x -q --timeout 600 --timeout-method thread")],
     # the driver's bench command
     "bench": [("bench", 900, f"{PY} bench.py --gpus 1 --steps 20 --warmup 5")],
+    # round-5 evidence: the driver's bench command (7-model single stream, must fit the driver's 540 s), kernel stats
+    # of the headline and of batch-1 fp4, the smoke test
+    "r5_final": [
+        ("bench", 900, f"{PY} bench.py --gpus 1 --steps 20 --warmup 5"),
+        prof("headline_r5", "--steps 1 --warmup 1 --no-single --no-energy"),
+        ("smoke", 300, f"{PY} -c 'import __graft_entry__ as g; g.smoke(); print(\"smoke ok\")'"),
+    ],
 }
 
 
