@@ -138,6 +138,9 @@ SETS = {
     # round 5: the reference's design on MXFP4 weights (both arms fp4), n = 10, 10 s cooldown, one session per call
     "r5_fp4_study": [("study", 1150, "CAIN_STUDY_WEIGHTS=fp4 STUDY_NAME=fp4_r5 COOLDOWN_MS=10000 REPS=10 "
                                      "IDLE_SETTLE_S=12 bash tools/study_chunk.sh 960")],
+    # its second replicate (another seed): n = 20 per cell with the first
+    "r5_fp4_study_b": [("study", 1150, "CAIN_STUDY_WEIGHTS=fp4 STUDY_NAME=fp4_r5b SEED=2026 COOLDOWN_MS=10000 REPS=10 "
+                                       "IDLE_SETTLE_S=12 bash tools/study_chunk.sh 960")],
     # round 5: the 256-column wide GEMM (wgemm256.hip): numerics first (a new kernel), then isolated shape timings
     # against the 128-column ring, then the headline with every llama shape on it (interleaved with the default)
     "r5_w256": [

@@ -10,6 +10,7 @@
 #   METHODS        arms (default remote,on_device)
 #   REPS           repetitions per (model, arm, length) cell (default 30)
 #   IDLE_SETTLE_S  rest before each session's idle baseline (default 5; round 4: 12)
+#   SEED           shuffle seed (default 2025; a second replicate of a design uses another seed and name)
 #
 # usage (inside gpurun): bash tools/study_chunk.sh [budget_s]
 set -o pipefail
@@ -21,7 +22,7 @@ if [ -d "study_resume/$NAME" ] && [ ! -d "$OUT/$NAME" ]; then
   cp -r "study_resume/$NAME" "$OUT/"
 fi
 export CAIN_STUDY_RESULTS_DIR="$PWD/$OUT" CAIN_STUDY_NAME="$NAME" CAIN_STUDY_REMOTE=local:0 \
-       CAIN_STUDY_COOLDOWN_MS="${COOLDOWN_MS:-1000}" CAIN_STUDY_SEED=2025 CAIN_ASSUME_YES=1 \
+       CAIN_STUDY_COOLDOWN_MS="${COOLDOWN_MS:-1000}" CAIN_STUDY_SEED="${SEED:-2025}" CAIN_ASSUME_YES=1 \
        CAIN_STUDY_METHODS="${METHODS:-remote,on_device}" CAIN_STUDY_REPETITIONS="${REPS:-30}" \
        CAIN_STUDY_IDLE_SETTLE_S="${IDLE_SETTLE_S:-5}" CAIN_RUN_BUDGET_S="${1:-960}"
 timeout -k 30 1140 python -u -m cain_amd experiments/study.py --gpus 1 --yes > "$OUT/session_$(date +%s).log" 2>&1
