@@ -78,8 +78,21 @@ def rederive_remote_board(df):
 
 
 def load_run_table(path, rederive: bool = False):
+    """One run table, or several replicates of one design (a list of paths): those are concatenated, each run id
+    prefixed by its replicate index and a `replicate` column added, so the cells pool n = sum of repetitions."""
     import pandas as pd
 
+    if isinstance(path, (list, tuple)):
+        if len(path) == 1:
+            return load_run_table(path[0], rederive)
+        parts = []
+        for i, p in enumerate(path):
+            d = load_run_table(p, rederive)
+            d = d.assign(replicate=i)
+            if "__run_id" in d.columns:
+                d["__run_id"] = f"r{i}_" + d["__run_id"].astype(str)
+            parts.append(d)
+        return pd.concat(parts, ignore_index=True)
     df = pd.read_csv(path)
     if rederive:
         rederive_remote_board(df)
@@ -443,12 +456,12 @@ def make_plots(df, subsets, out: Path) -> List[Path]:
 # ---------------------------------------------------------------------------------------------- entry points
 def analyze(path, out: Optional[Path] = None, plots: bool = False, fmt: str = "both", quiet: bool = False,
             rederive: bool = False) -> dict:
-    path = Path(path)
-    out = Path(out) if out else path.parent / "analysis"
+    paths = [Path(p) for p in path] if isinstance(path, (list, tuple)) else [Path(path)]
+    out = Path(out) if out else paths[0].parent / "analysis"
     out.mkdir(parents=True, exist_ok=True)
-    df = load_run_table(path, rederive=rederive)
+    df = load_run_table(paths, rederive=rederive)
     subsets = make_subsets(df)
-    res = {"source": str(path), "n_rows": int(len(df)), "subset_sizes": {k: int(len(v)) for k, v in subsets.items()},
+    res = {"source": ", ".join(str(p) for p in paths), "n_rows": int(len(df)), "subset_sizes": {k: int(len(v)) for k, v in subsets.items()},
            "summary": summary_rows(subsets), "shapiro": shapiro_rows(subsets), "h1": h1_rows(subsets),
            "h2": h2_rows(subsets), "per_model": per_model_rows(df) if "model" in df.columns else [],
            "energy_views": energy_view_rows(subsets), "rederived_remote_board": bool(rederive)}
@@ -478,7 +491,7 @@ def analyze(path, out: Optional[Path] = None, plots: bool = False, fmt: str = "b
 
 def main(argv: Optional[List[str]] = None) -> None:
     ap = argparse.ArgumentParser(prog="python -m cain_amd analyze", description=__doc__.split("\n")[0])
-    ap.add_argument("run_table")
+    ap.add_argument("run_table", nargs="+", help="run_table.csv; several = replicates of one design, pooled")
     ap.add_argument("--out", default=None)
     ap.add_argument("--plots", action="store_true", help="also write density/violin/QQ/scatter PDFs")
     ap.add_argument("--format", choices=["latex", "markdown", "both"], default="both")

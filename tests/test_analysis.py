@@ -174,3 +174,35 @@ def test_energy_views_and_remote_board_rederivation(tmp_path):
     # the idle-subtracted view does not change: the board's part is idle - idle = 0
     assert v_fix[("long", "idle_subtracted")]["ratio"] == pytest.approx(v_raw[("long", "idle_subtracted")]["ratio"])
     assert (tmp_path / "fixed" / "energy_views.md").read_text().count("idle_subtracted") == 3
+
+
+def test_replicate_run_tables_pool(tmp_path):
+    """Two replicates of one design (same run ids, different seeds) pool into one analysis: run ids are prefixed by
+    the replicate, every cell's n is the sum, and a single path still behaves as before."""
+    import csv as _csv
+
+    from cain_amd.analysis.report import analyze, load_run_table
+
+    paths = []
+    for rep in range(2):
+        rows = []
+        for i in range(6):
+            for method, e in (("on_device", 900.0), ("remote", 300.0)):
+                w = 1.0 + 0.01 * i + 0.001 * rep
+                rows.append(dict(__run_id=f"run_{i}_{method}", __done="DONE", model="m", method=method, length=500,
+                                 execution_time=w, cpu_usage=5, gpu_usage=50, memory_usage=3,
+                                 energy_usage_J=round(e * w, 3), idle_subtracted_J=round((e - 280) * w, 3)))
+        p = tmp_path / f"rep{rep}" / "run_table.csv"
+        p.parent.mkdir()
+        with open(p, "w", newline="") as fh:
+            wr = _csv.DictWriter(fh, fieldnames=list(rows[0].keys()))
+            wr.writeheader()
+            wr.writerows(rows)
+        paths.append(p)
+    one = load_run_table(paths[0])
+    both = load_run_table(paths)
+    assert len(both) == 2 * len(one) and both["__run_id"].is_unique
+    assert sorted(both["replicate"].unique()) == [0, 1]
+    res = analyze(paths, tmp_path / "pooled", quiet=True)
+    assert res["subset_sizes"]["on_device_medium"] == 12 and res["subset_sizes"]["remote_medium"] == 12
+    assert "rep0" in res["source"] and "rep1" in res["source"]
