@@ -128,6 +128,10 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(4, 4
   for (int u = 0; u < U; ++u) load_next(ring[u]);
 
   int cp_t = blockIdx.x;
+  // FOLD: the fused QKV epilogue at 8 waves sums each unit once into LDS before the epilogue (below); summing the
+  // own and the partner unit per lane straight from the 8 partial slabs spilled that kernel (28 B per lane at the
+  // 128-register budget of 4 waves per SIMD; 84-102 registers folded)
+  constexpr bool FOLD = EPI == EPI_QKV_ROPE && WAVES == 8;
   EpiIn pre{};
   if (wave == 0 && my_tiles > 0) pre = epi_load_at<EPI>(a, cp_t, lane & 15, lane);
 #pragma unroll
@@ -188,7 +192,15 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(4, 4
         if constexpr (NORM) v *= rms_inv(row_ss[min(l & 15, a.M - 1)], a.K, a.eps);
         return v;
       };
-      epi_store<EPI>(a, cp_t, lane & 15, lane, pre, [&](int off) { return unit_sum(lane + off); });
+      if constexpr (FOLD) {
+        // pair epilogue at 8 waves: each lane sums its own unit once and writes it back, the epilogue reads its
+        // units (own and partner row) from there -- summing both units per lane held 2 x 8 partials in flight
+        // and spilled.  One wave: its LDS operations complete in order, so the reads see the writes.
+        red[buf][0][lane] = unit_sum(lane);
+        epi_store<EPI>(a, cp_t, lane & 15, lane, pre, [&](int off) { return red[buf][0][lane + off]; });
+      } else {
+        epi_store<EPI>(a, cp_t, lane & 15, lane, pre, [&](int off) { return unit_sum(lane + off); });
+      }
     }
     buf ^= 1;
   };

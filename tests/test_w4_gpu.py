@@ -36,6 +36,7 @@ def _rule_variant():
     ops.set_w4_variant(-1)
     yield
     ops.set_w4_variant(-1)
+    ops.set_w4_occupancy(0)
 
 
 def test_e2m1_convert_semantics():
@@ -154,8 +155,15 @@ def _rot(x, c, s_):
 @pytest.mark.parametrize("H,Hkv,hd", [(32, 8, 128), (8, 1, 256), (32, 32, 96)])
 @pytest.mark.parametrize("M", [1, 40])
 @pytest.mark.parametrize("kv8", [False, True])
-def test_w4_qkv_rope_kv_append(H, Hkv, hd, M, kv8):
+@pytest.mark.parametrize("var,occ", [(-1, 0), (0, 0), (0, 1)])
+def test_w4_qkv_rope_kv_append(H, Hkv, hd, M, kv8, var, occ):
+    """The rule's kernel, and the 8-wave stream kernel (its epilogue sums each unit once into LDS, FOLD) with one
+    tile per workgroup and, at one workgroup per CU, several (the double-buffered partial slabs reused)."""
     torch.manual_seed(8)
+    if var >= 0 and M > 16:
+        pytest.skip("the stream kernels take <= 16 rows")
+    ops.set_w4_variant(var)
+    ops.set_w4_occupancy(occ)
     K, T_max, S = 512, 256, 64
     qkv_dim = (H + 2 * Hkv) * hd
     W = (torch.randn(qkv_dim, K, device=DEV) * 0.05).bfloat16()
@@ -190,6 +198,7 @@ def test_w4_qkv_rope_kv_append(H, Hkv, hd, M, kv8):
         assert rel_err(kn[sl, :, p], _rot(ref[m, H * hd:(H + Hkv) * hd].view(Hkv, hd), cc, ss)) < tol
         assert rel_err(vn[sl, :, p], ref[m, (H + Hkv) * hd:].view(Hkv, hd)) < tol
     assert int((kn != 0).any(-1).sum()) == M * Hkv and int((vn != 0).any(-1).sum()) == M * Hkv
+    ops.set_w4_occupancy(0)
 
 
 FP4_TINY = sorted(n for n, c in TINY.items() if not (c.d_model % 128 or c.q_dim % 128 or c.ffn % 128))
