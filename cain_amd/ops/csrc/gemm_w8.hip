@@ -243,7 +243,7 @@ static hipError_t w8_launch(const GemmArgs& a, const float* wscale, bool xl, hip
 
 // kernel variants: (waves, pairs in flight, 16-row tiles of N, 16-row blocks of M) per workgroup
 enum W8Var { W8_4_2_1_1, W8_8_2_1_1, W8_4_4_1_1, W8_8_4_1_1, W8_4_2_2_1, W8_8_2_2_1, W8_4_2_4_1, W8_4_2_1_2, W8_8_2_1_2,
-              W8_4_8_1_1, W8_8_8_1_1, W8_4_4_2_1, W8_8_4_2_1 };
+              W8_4_4_2_1, W8_8_4_2_1 };
 
 template <bool NORM>
 static hipError_t w8_launch_e(int epi, int var, const GemmArgs& a, const float* wscale, bool xl, hipStream_t st) {
@@ -257,8 +257,6 @@ static hipError_t w8_launch_e(int epi, int var, const GemmArgs& a, const float* 
     case W8_8_2_2_1: return w8_launch<8, 2, 2, 1, E, NORM>(a, wscale, xl, st);   \
     case W8_4_2_4_1: return w8_launch<4, 2, 4, 1, E, NORM>(a, wscale, xl, st);   \
     case W8_4_2_1_2: return w8_launch<4, 2, 1, 2, E, NORM>(a, wscale, xl, st);   \
-    case W8_4_8_1_1: return w8_launch<4, 8, 1, 1, E, NORM>(a, wscale, xl, st);   \
-    case W8_8_8_1_1: return w8_launch<8, 8, 1, 1, E, NORM>(a, wscale, xl, st);   \
     case W8_4_4_2_1: return w8_launch<4, 4, 2, 1, E, NORM>(a, wscale, xl, st);   \
     case W8_8_4_2_1: return w8_launch<8, 4, 2, 1, E, NORM>(a, wscale, xl, st);   \
     default: return w8_launch<8, 2, 1, 2, E, NORM>(a, wscale, xl, st);           \
@@ -310,9 +308,10 @@ CAIN_API int cain_gemm_w8(const void* Wp, const float* wscale, const void* X, in
   if (f_w) waves = f_w >= 8 ? 8 : 4;
   // pairs in flight per wave: with the activations in LDS the registers of the deeper weight prologue are free
   // (U = 4: llama3.1:8b 480.7 -> 514.1 tok/s single stream); without, U = 4 measured no gain (w8_decode.md)
-  int u = (nb == 1 && f_u >= 4) ? (f_u >= 8 ? 8 : 4) : 2;
+  // (U = 8 spilled 92-168 B per lane at 8 waves and was never selected: removed)
+  int u = (nb == 1 && f_u >= 4) ? 4 : 2;
   if (!f_u && xl) u = 4;
-  if (nt == 4 || (nt == 2 && u == 8)) u = std::min(u, nt == 4 ? 2 : 4);
+  if (nt == 4) u = 2;
   int var;
   if (nb == 2)
     var = waves == 8 ? W8_8_2_1_2 : W8_4_2_1_2;
@@ -320,8 +319,6 @@ CAIN_API int cain_gemm_w8(const void* Wp, const float* wscale, const void* X, in
     var = W8_4_2_4_1;
   else if (nt == 2)
     var = u == 4 ? (waves == 8 ? W8_8_4_2_1 : W8_4_4_2_1) : (waves == 8 ? W8_8_2_2_1 : W8_4_2_2_1);
-  else if (u == 8)
-    var = waves == 8 ? W8_8_8_1_1 : W8_4_8_1_1;
   else
     var = u == 4 ? (waves == 8 ? W8_8_4_1_1 : W8_4_4_1_1) : (waves == 8 ? W8_8_2_1_1 : W8_4_2_1_1);
   const hipError_t e = norm ? w8_launch_e<true>(epi, var, a, wscale, xl, st)
