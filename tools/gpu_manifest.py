@@ -201,10 +201,11 @@ SETS = {
                     f"--no-energy --no-single --weights fp4 && find gpurun_out/prof_b1_attn_{tag}_{i} "
                     f"-name '*kernel_trace.csv' -delete")
                    for i in range(2) for tag in ("old", "new")],
-    # batch-1 fp4 QKV: the 8-wave stream kernel (one 128-k quad round per wave, FOLD epilogue, no spill) against the
-    # rule's 4-wave kernel, every model's QKV shape, interleaved twice
-    "r5_qkv8": [("w4_qkv_tests", 300, f"{TEST} tests/test_w4_gpu.py -k qkv")] + [
-        (f"w4b_{m.replace(':', '_')}_{i}", 240, f"{PY} tools/w4_bench.py --model {m} --roles qkv --variants rule,0 --dtypes fp4")
+    # batch-1 fp4: the 8-wave stream kernel on QKV (one 128-k quad round per wave, FOLD epilogue, no spill) and the
+    # 16-wave one (W4S_16_4) on QKV / O / down against the rule's kernels, every model's shapes, interleaved twice
+    "r5_qkv8": [("w4_tests", 400, f"{TEST} tests/test_w4_gpu.py")] + [
+        (f"w4b_{m.replace(':', '_')}_{i}", 240,
+         f"{PY} tools/w4_bench.py --model {m} --roles qkv,o,down --variants rule,0,6 --dtypes fp4")
         for i in range(2) for m in ("llama3.1:8b", "qwen2:7b", "mistral:7b", "phi3:3.8b", "gemma:7b", "qwen2:1.5b",
                                      "gemma:2b")],
     "suite": [("gpu_suite", 1500, f"{PY} -u -m pytest tests -m gpu -x -q --timeout 600 --timeout-method thread")],
