@@ -72,7 +72,7 @@ __device__ __forceinline__ void w4_pair_tile(int j, int msp, int ntg, int& t, in
 // LDS copy of the activation rows: 48 KiB for 8-wave workgroups (2 per CU), 28 KiB for 4-wave ones (4 per CU) --
 // every real model's down projection (K <= 24576) fits at one row
 template <int WAVES>
-constexpr int w4_xl_bytes() { return WAVES == 16 ? 65536 : WAVES == 8 ? 49152 : 28672; }
+constexpr int w4_xl_bytes() { return WAVES == 8 ? 49152 : 28672; }
 
 // 4 waves per SIMD (<= 128 VGPRs): the grid below assumes 16 resident waves per CU
 template <int WAVES, int U, int EPI, bool NORM>
@@ -131,8 +131,7 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(4, 4
   // FOLD: the fused QKV epilogue at 8 waves sums each unit once into LDS before the epilogue (below); summing the
   // own and the partner unit per lane straight from the 8 partial slabs spilled that kernel (28 B per lane at the
   // 128-register budget of 4 waves per SIMD; 84-102 registers folded)
-  // (and every epilogue at 16 waves: 16 partials per unit)
-  constexpr bool FOLD = (EPI == EPI_QKV_ROPE && WAVES == 8) || WAVES == 16;
+  constexpr bool FOLD = EPI == EPI_QKV_ROPE && WAVES == 8;
   EpiIn pre{};
   if (wave == 0 && my_tiles > 0) pre = epi_load_at<EPI>(a, cp_t, lane & 15, lane);
 #pragma unroll
@@ -344,18 +343,15 @@ __global__ __launch_bounds__(WAVES * 64) void w4_tile_kernel(const GemmArgs a, c
 
 // ================================================================ launch
 // kernel shapes (W4Var): stream kernels (waves, items in flight) and tile kernels (waves, quads in flight, row blocks)
-// W4S_16_4: one 16-wave workgroup per CU, for grids of at most one 8-wave workgroup per CU (O / down at 4096
-// columns: 256 tiles), which left half the CU's wave slots -- and half its loads in flight -- unused
-enum W4Var { W4S_8_4, W4S_4_4, W4T_8_2_1, W4T_4_4_1, W4T_8_2_2, W4T_4_2_2, W4S_16_4, W4_N_VARS };
-static const int W4_WAVES[W4_N_VARS] = {8, 4, 8, 4, 8, 4, 16};
-static const int W4_NB[W4_N_VARS] = {1, 1, 1, 1, 2, 2, 1};
-static bool w4_is_stream(int v) { return v <= W4S_4_4 || v == W4S_16_4; }
+enum W4Var { W4S_8_4, W4S_4_4, W4T_8_2_1, W4T_4_4_1, W4T_8_2_2, W4T_4_2_2, W4_N_VARS };
+static const int W4_WAVES[W4_N_VARS] = {8, 4, 8, 4, 8, 4};
+static const int W4_NB[W4_N_VARS] = {1, 1, 1, 1, 2, 2};
+static bool w4_is_stream(int v) { return v <= W4S_4_4; }
 
 template <bool NORM, int EPI>
 static hipError_t w4_launch_var(int var, const GemmArgs& a, const uint8_t* wsc, int grid, int npairs, hipStream_t st) {
-  const dim3 g(grid), b16(1024), b8(512), b4(256);
+  const dim3 g(grid), b8(512), b4(256);
   switch (var) {
-    case W4S_16_4: hipLaunchKernelGGL((w4_stream_kernel<16, 4, EPI, NORM>), g, b16, 0, st, a, wsc, npairs); break;
     case W4S_8_4: hipLaunchKernelGGL((w4_stream_kernel<8, 4, EPI, NORM>), g, b8, 0, st, a, wsc, npairs); break;
     case W4S_4_4: hipLaunchKernelGGL((w4_stream_kernel<4, 4, EPI, NORM>), g, b4, 0, st, a, wsc, npairs); break;
     case W4T_8_2_1: hipLaunchKernelGGL((w4_tile_kernel<8, 2, 1, EPI, NORM>), g, b8, 0, st, a, wsc); break;
@@ -391,8 +387,7 @@ static int w4_n_cu() {
 }
 
 static bool w4_stream_fits(int waves, int K, int M) {
-  return M <= 16 && (long long)M * K * 2 <= (waves == 16 ? w4_xl_bytes<16>() : waves == 8 ? w4_xl_bytes<8>()
-                                                                                          : w4_xl_bytes<4>());
+  return M <= 16 && (long long)M * K * 2 <= (waves == 8 ? w4_xl_bytes<8>() : w4_xl_bytes<4>());
 }
 
 // Shape rule (tools/w4_bench.py, in-graph, llama3.1:8b shapes at one row: profiles/r4/README.md).  Up to 16 rows
@@ -440,9 +435,9 @@ CAIN_API int cain_gemm_w4(const void* Wp, const void* wsc, const void* X, int ld
   a.msplit = (M + 16 * nb - 1) / (16 * nb);
   const int npairs = N / 16 * a.msplit;
   int grid = npairs;
-  if (w4_is_stream(var)) {  // persistent: at most the resident workgroups (1 of 16 / 2 of 8 / 4 of 4 waves per CU)
+  if (w4_is_stream(var)) {  // persistent: at most the resident workgroups (2 of 8 waves / 4 of 4 waves per CU)
     a.msplit = 1;
-    grid = std::min(npairs, n_cu * (g_w4_wgs_per_cu ? g_w4_wgs_per_cu : (waves == 16 ? 1 : waves == 8 ? 2 : 4)));
+    grid = std::min(npairs, n_cu * (g_w4_wgs_per_cu ? g_w4_wgs_per_cu : (waves == 8 ? 2 : 4)));
   }
   const uint8_t* sc = reinterpret_cast<const uint8_t*>(wsc);
   const hipError_t e = norm ? w4_launch<true>(epi, var, a, sc, grid, npairs, st)

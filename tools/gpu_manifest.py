@@ -201,8 +201,9 @@ SETS = {
                     f"--no-energy --no-single --weights fp4 && find gpurun_out/prof_b1_attn_{tag}_{i} "
                     f"-name '*kernel_trace.csv' -delete")
                    for i in range(2) for tag in ("old", "new")],
-    # batch-1 fp4: the 8-wave stream kernel on QKV (one 128-k quad round per wave, FOLD epilogue, no spill) and the
-    # 16-wave one (W4S_16_4) on QKV / O / down against the rule's kernels, every model's shapes, interleaved twice
+    # batch-1 fp4: the 8-wave stream kernel on QKV (one 128-k quad round per wave, FOLD epilogue, no spill) and a
+    # 16-wave one (variant 6 then; removed after this A/B: profiles/r5/README.md) on QKV / O / down against the
+    # rule's kernels, every model's shapes, interleaved twice
     "r5_qkv8": [("w4_tests", 400, f"{TEST} tests/test_w4_gpu.py")] + [
         (f"w4b_{m.replace(':', '_')}_{i}", 240,
          f"{PY} tools/w4_bench.py --model {m} --roles qkv,o,down --variants rule,0,6 --dtypes fp4")
