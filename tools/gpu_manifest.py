@@ -209,6 +209,10 @@ SETS = {
          f"{PY} tools/w4_bench.py --model {m} --roles qkv,o,down --variants rule,0,6 --dtypes fp4")
         for i in range(2) for m in ("llama3.1:8b", "qwen2:7b", "mistral:7b", "phi3:3.8b", "gemma:7b", "qwen2:1.5b",
                                      "gemma:2b")],
+    # batch-1 fp4 GEMMs with the weights cold (decode), Infinity-Cache-hot (8 copies) and cache-hot (1 copy): what a
+    # prefetch of the next kernel's weights could buy
+    "r5_mall": [(f"w4_mall_{m.replace(':', '_')}", 240, f"{PY} tools/w4_bench.py --model {m} --roles qkv,o,gateup,down "
+                 f"--variants rule --dtypes fp4 --copies 0,8,1,0") for m in ("llama3.1:8b", "qwen2:1.5b")],
     "suite": [("gpu_suite", 1500, f"{PY} -u -m pytest tests -m gpu -x -q --timeout 600 --timeout-method thread")],
     # the driver's bench command
     "bench": [("bench", 900, f"{PY} bench.py --gpus 1 --steps 20 --warmup 5")],

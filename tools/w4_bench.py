@@ -55,6 +55,9 @@ def main() -> int:
     ap.add_argument("--norm", choices=("model", "on", "off"), default="model",
                     help="fused RMSNorm: as in the model (QKV / gate-up / LM head), or forced on / off for every role")
     ap.add_argument("--roles", default="qkv,o,gateup,down,lm_head")
+    ap.add_argument("--copies", default="0",
+                    help="weight copies rotated per call, comma list: 0 = enough to exceed the 256 MiB Infinity Cache "
+                         "(cold, as in decode); 1 = one copy (cache-hot); e.g. 8 = Infinity-Cache-hot, beyond L2")
     ns = ap.parse_args()
     cfg = get_config(ns.model)
     dev = torch.device("cuda")
@@ -83,10 +86,10 @@ def main() -> int:
             n_out = cfg.q_dim
         out = torch.zeros(M, n_out, device=dev, dtype=torch.float32 if epi == ops.EPI_F32 else torch.bfloat16)
         rp = rope if epi == ops.EPI_QKV_ROPE else None
-        for dt in ns.dtypes.split(","):
+        for dt, cp in [(dt, cp) for dt in ns.dtypes.split(",") for cp in ns.copies.split(",")]:
             bpp = {"fp4": 0.5 + 1 / 32, "fp8": 1.0, "bf16": 2.0}[dt]
             wbytes = int(N * K * bpp)
-            ncopy = max(2, min(16, (768 << 20) // max(1, wbytes) + 1))
+            ncopy = int(cp) if int(cp) > 0 else max(2, min(16, (768 << 20) // max(1, wbytes) + 1))
             if dt == "fp4":
                 ws = [(torch.randint(0, 256, (N // 16, K // 128, 64, 16), device=dev, dtype=torch.uint8),
                        torch.randint(118, 122, (N // 16, K // 128, 64), device=dev, dtype=torch.uint8))
@@ -102,7 +105,7 @@ def main() -> int:
                             ops.gemm_w4(wq, sc, xk, N, epi, out=out, norm=norm, rope=rp)
                         us = graph_time(fn)
                         print(json.dumps(dict(role=role, dtype=dt, N=N, K=K, M=M, variant=v, used=used, occ=int(occ), norm=norm,
-                                              us=round(us, 2), TBps=round(wbytes / us / 1e6, 2))), flush=True)
+                                              copies=ncopy, us=round(us, 2), TBps=round(wbytes / us / 1e6, 2))), flush=True)
                 ops.set_w4_variant(-1)
                 ops.set_w4_occupancy(0)
             elif dt == "fp8":
