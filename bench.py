@@ -114,9 +114,6 @@ def main() -> int:
     ap.add_argument("--single-fp4-models", default="phi3:3.8b,qwen2:7b,gemma:7b,mistral:7b",
                     help="models measured at batch 1 on MXFP4 weights only (the reference's 4-bit class), "
                          "comma-separated: with --single-models and the bench model, the 7 study models")
-    ap.add_argument("--prefetch-mb", type=int, default=0,
-                    help="MXFP4 few-row forwards: MiB of the next GEMMs' weights prefetched beside each attention "
-                         "(ops.set_prefetch_mb; 0 = off)")
     ap.add_argument("--w4a8-min-rows", type=int, default=0,
                     help="MXFP4: rows above which forwards run W4A8 instead of W4A16 (0: the runtime's default, 16)")
     ns = ap.parse_args()
@@ -149,12 +146,9 @@ def main() -> int:
 
     from cain_amd.engine import DecodeEngine
 
-    if (ns.prefetch_mb or ns.w4a8_min_rows) and not cpu:
+    if ns.w4a8_min_rows and not cpu:
         from cain_amd import ops
-        if ns.prefetch_mb:
-            ops.set_prefetch_mb(ns.prefetch_mb)
-        if ns.w4a8_min_rows:
-            ops.set_w4a8_min_rows(ns.w4a8_min_rows)
+        ops.set_w4a8_min_rows(ns.w4a8_min_rows)
     from cain_amd.models.tokenizer import tokens_for_words
 
     n_tok = tokens_for_words(ns.words)

@@ -88,7 +88,6 @@ def load() -> ctypes.CDLL:
         lib.cain_quant_rows.argtypes = [vp, ci, ci, ci, vp, ci, vp, ci, cf, vp]
         lib.cain_gemm_w4a8.argtypes = lib.cain_gemm_w8a8.argtypes
         lib.cain_w4a8_set_min_rows.argtypes = [ci]
-        lib.cain_set_prefetch_mb.argtypes = [ci]
         lib.cain_w8a8_eligible.argtypes = [ci, ci, ci]
         lib.cain_w8a8_ws_bytes.restype = ctypes.c_longlong
         lib.cain_w8a8_ws_bytes.argtypes = [ci, ci, ci]
@@ -448,13 +447,6 @@ def set_w4a8_min_rows(m: int) -> None:
     (runtime.hip; default 16, the W4A8 minimum: W4A8 is 1.5-2.7x faster at 24-64 rows,
     profiles/r4/ab/w4a8_crossover.txt).  Read at every forward / graph capture."""
     load().cain_w4a8_set_min_rows(int(m))
-
-
-def set_prefetch_mb(mb: int) -> None:
-    """MiB of the next GEMMs' weights (O, then the head of gate/up) a side stream touches beside each layer's
-    attention in few-row MXFP4 forwards, so their streams start from the Infinity Cache (runtime.hip; 0 = off, the
-    default).  Read at every forward / graph capture."""
-    load().cain_set_prefetch_mb(int(mb))
 
 
 def rmsnorm(x: torch.Tensor, g: torch.Tensor, eps: float, out: Optional[torch.Tensor] = None) -> torch.Tensor:

@@ -16,7 +16,6 @@
 // the device, a whole generation is a handful of graph launches with no host
 // round trip per token (graph-replay floor instead of ~290 host launches per
 // token: MI355X_MICROARCH.md rows 'boundary', 'graph-replay-floor').
-#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
@@ -152,38 +151,9 @@ struct CainRows {
 
 namespace {
 
-// Weight prefetch beside attention (few-row MXFP4 decode; off unless cain_set_prefetch_mb > 0).  Attention at one
-// row is latency-bound and leaves HBM mostly idle; a side stream touches the next GEMMs' weights meanwhile -- O's,
-// then the head of gate/up's, up to the budget -- one dword per 64-byte line, so those kernels' streams start from
-// the Infinity Cache instead of HBM.  The loads are plain (cache-allocating); their values are folded into one word
-// that is stored only if it equals a constant the data never produces in practice (it keeps the loads live).
-struct PrefetchRanges {
-  const uint32_t* p[4];
-  long long lines[4];  // 64-byte lines of each range
-};
-
-__global__ __launch_bounds__(256) void prefetch_kernel(const PrefetchRanges r, uint32_t* __restrict__ sink) {
-  uint32_t acc = 0;
-  const long long stride = (long long)gridDim.x * 256;
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const uint32_t* base = r.p[k];
-    const long long n = r.lines[k];
-#pragma unroll 4
-    for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) acc ^= base[i * 16];
-  }
-  if (acc == 0x9e3779b9u) sink[threadIdx.x] = acc;
-}
-
-static int g_prefetch_mb = 0;
-
 struct Plan {
   CainPlanDesc d;
   std::vector<CainLayer> layers;
-  // weight prefetch (fp4 plans): side stream, fork / join events, the kernel's sink word
-  hipStream_t side = nullptr;
-  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
-  uint32_t* sink = nullptr;
   // two-stage sampler workspace (sample.hip cain_sample_ex) for decode forwards of <= 64 rows, zeroed once
   void* sample_ws = nullptr;
   long long sample_ws_bytes = 0;
@@ -192,10 +162,6 @@ struct Plan {
   ~Plan() {
     if (sample_ws) (void)hipFree(sample_ws);
     if (cmax) (void)hipFree(cmax);
-    if (sink) (void)hipFree(sink);
-    if (ev_fork) (void)hipEventDestroy(ev_fork);
-    if (ev_join) (void)hipEventDestroy(ev_join);
-    if (side) (void)hipStreamDestroy(side);
   }
 };
 
@@ -256,9 +222,6 @@ int forward(const Plan& p, int M, const CainRows& r, int want_logits, int want_s
                      d.Hkv, d.hd, d.T_max, d.gemm_ws, d.gemm_ws_bytes, epi, d.waves, st);
   };
   CK(cain_embed(r.tok, d.embed, d.x, d.d, M, d.d, d.embed_scale, st));
-  // weight prefetch beside attention: MXFP4 few-row forwards on the W4A16 stream kernels only
-  const bool pf = g_prefetch_mb > 0 && d.wfmt == WFMT_FP4 && M <= 16 && p.side && p.sink;
-  const long long pf_budget = (long long)g_prefetch_mb << 20;
   for (int l = 0; l < d.n_layers; ++l) {
     const CainLayer& L = p.layers[l];
     const size_t kv_off = (size_t)l * d.kv_layer_elems * (d.kv8 ? 1 : 2);  // bytes
@@ -266,29 +229,12 @@ int forward(const Plan& p, int M, const CainRows& r, int want_logits, int want_s
     char* vc = static_cast<char*>(d.vtcache) + kv_off;
     CK(gemm(L.wqkv, L.wqkv8, L.sqkv, d.x, d.d, d.d, qkv_dim, d.q, q_dim, L.bqkv, 1, kc, vc,
             /*EPI_QKV_ROPE*/ 5 | (d.kv8 ? /*EPI_KV_FP8*/ 0x100 : 0)));
-    if (pf) {
-      // O: d x q_dim e2m1 (half a byte each) + one scale byte per 32; gate/up: 2 ffn x d, its head up to the budget
-      const long long o_w = (long long)d.d * q_dim / 2, o_s = (long long)d.d * q_dim / 32;
-      const long long gu_w = (long long)2 * d.ffn * d.d / 2;
-      long long left = pf_budget - o_w - o_s;
-      PrefetchRanges pr{};
-      pr.p[0] = static_cast<const uint32_t*>(L.wo), pr.lines[0] = std::min(o_w, pf_budget) / 64;
-      pr.p[1] = static_cast<const uint32_t*>(L.so), pr.lines[1] = pf_budget > o_w ? o_s / 64 : 0;
-      pr.p[2] = static_cast<const uint32_t*>(L.wgu), pr.lines[2] = left > 0 ? std::min(left, gu_w) / 64 : 0;
-      pr.p[3] = pr.p[2], pr.lines[3] = 0;
-      CK(int(hipEventRecord(p.ev_fork, st)));
-      CK(int(hipStreamWaitEvent(p.side, p.ev_fork, 0)));
-      hipLaunchKernelGGL(prefetch_kernel, dim3(128), dim3(256), 0, p.side, pr, p.sink);
-      CK(int(hipGetLastError()));
-      CK(int(hipEventRecord(p.ev_join, p.side)));
-    }
     CK(cain_attention_ex(d.q, kc, vc, r.slot, r.pos, d.part_o, d.part_ml, d.counters, d.attn, q_dim, M, d.H, d.Hkv,
                          d.hd, d.T_max, d.nsplit, d.attn_scale, d.kv8, 1.f, 1.f, st));
     CK(gemm(L.wo, L.wo8, L.so, d.attn, q_dim, q_dim, d.d, d.x, d.d, nullptr, 0, nullptr, nullptr, /*EPI_RESID*/ 1));
     CK(gemm(L.wgu, L.wgu8, L.sgu, d.x, d.d, d.d, 2 * d.ffn, d.act, d.ffn, nullptr, 1, nullptr, nullptr, epi_act));
     CK(gemm(L.wdown, L.wdown8, L.sdown, d.act, d.ffn, d.ffn, d.d, d.x, d.d, nullptr, 0, nullptr, nullptr,
             /*EPI_RESID*/ 1));
-    if (pf) CK(int(hipStreamWaitEvent(st, p.ev_join, 0)));  // join the side stream (graph capture needs it)
   }
   if (want_logits) {
     // the LM head also writes the chunk maxima the chunk-max sampler starts from (skinny or wide bf16 kernel)
@@ -331,14 +277,6 @@ CAIN_API void* cain_plan_create(const CainPlanDesc* desc) {
       p->sample_ws = nullptr;  // the one-workgroup sampler needs no workspace
     }
   }
-  // weight prefetch resources (fp4 plans; used only when cain_set_prefetch_mb > 0)
-  if (desc->wfmt == WFMT_FP4) {
-    if (hipStreamCreateWithFlags(&p->side, hipStreamNonBlocking) != hipSuccess) p->side = nullptr;
-    if (hipEventCreateWithFlags(&p->ev_fork, hipEventDisableTiming) != hipSuccess) p->ev_fork = nullptr;
-    if (hipEventCreateWithFlags(&p->ev_join, hipEventDisableTiming) != hipSuccess) p->ev_join = nullptr;
-    if (hipMalloc(&p->sink, 256 * sizeof(uint32_t)) != hipSuccess) p->sink = nullptr;
-    if (!p->ev_fork || !p->ev_join) p->side = nullptr;  // (the destructor frees what was created)
-  }
   // LM-head chunk maxima ([Mpad][V / 16]): bf16 weights only (the kernels that write them)
   if (desc->wfmt == WFMT_BF16 && desc->V % 64 == 0 && desc->Mpad > 0) {
     if (hipMalloc(&p->cmax, (size_t)desc->Mpad * (desc->V / 16) * sizeof(float)) != hipSuccess) p->cmax = nullptr;
@@ -349,9 +287,6 @@ CAIN_API void* cain_plan_create(const CainPlanDesc* desc) {
 CAIN_API void cain_plan_destroy(void* plan) { delete static_cast<Plan*>(plan); }
 
 CAIN_API void cain_w4a8_set_min_rows(int m) { g_w4a8_min_rows = m > 16 ? m : 16; }
-
-// MiB of weights prefetched beside each layer's attention in few-row MXFP4 forwards (0: off)
-CAIN_API void cain_set_prefetch_mb(int mb) { g_prefetch_mb = mb > 0 ? mb : 0; }
 
 CAIN_API const char* cain_plan_last_failure() { return g_fail; }
 

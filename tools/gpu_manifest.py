@@ -212,10 +212,7 @@ SETS = {
     # batch-1 fp4 GEMMs with the weights cold (decode), Infinity-Cache-hot (8 copies) and cache-hot (1 copy): what a
     # prefetch of the next kernel's weights could buy
     "r5_mall": [(f"w4_mall_{m.replace(':', '_')}", 240, f"{PY} tools/w4_bench.py --model {m} --roles qkv,o,gateup,down "
-                 f"--variants rule --dtypes fp4 --copies 0,8,1,0") for m in ("llama3.1:8b", "qwen2:1.5b")] + [
-        ("pf_test", 300, f"{TEST} tests/test_w4_gpu.py -k prefetch")] + [
-        (f"pf_{mb}_{i}", 240, f"{PY} bench.py --batch 1 --steps 3 --warmup 1 --no-single --no-energy --weights fp4 "
-                              f"--prefetch-mb {mb}") for i in range(2) for mb in (0, 16, 48)],
+                 f"--variants rule --dtypes fp4 --copies 0,8,1,0") for m in ("llama3.1:8b", "qwen2:1.5b")],
     "suite": [("gpu_suite", 1500, f"{PY} -u -m pytest tests -m gpu -x -q --timeout 600 --timeout-method thread")],
     # the driver's bench command
     "bench": [("bench", 900, f"{PY} bench.py --gpus 1 --steps 20 --warmup 5")],
