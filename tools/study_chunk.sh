@@ -25,7 +25,10 @@ export CAIN_STUDY_RESULTS_DIR="$PWD/$OUT" CAIN_STUDY_NAME="$NAME" CAIN_STUDY_REM
        CAIN_STUDY_COOLDOWN_MS="${COOLDOWN_MS:-1000}" CAIN_STUDY_SEED="${SEED:-2025}" CAIN_ASSUME_YES=1 \
        CAIN_STUDY_METHODS="${METHODS:-remote,on_device}" CAIN_STUDY_REPETITIONS="${REPS:-30}" \
        CAIN_STUDY_IDLE_SETTLE_S="${IDLE_SETTLE_S:-5}" CAIN_RUN_BUDGET_S="${1:-960}"
-timeout -k 30 1140 python -u -m cain_amd experiments/study.py --gpus 1 --yes > "$OUT/session_$(date +%s).log" 2>&1
+log="$OUT/session_$(date +%s).log"
+# provenance: which kernel library this session ran (CAIN_KERNELS_LIB or the in-tree build)
+echo "kernels $(md5sum "${CAIN_KERNELS_LIB:-cain_amd/ops/libcain_kernels.so}")" > "$log"
+timeout -k 30 1140 python -u -m cain_amd experiments/study.py --gpus 1 --yes >> "$log" 2>&1
 rc=$?
 grep -c ",DONE," "$OUT/$NAME/run_table.csv" || true
 # one archive instead of ~5k per-run files: gpurun merges back at most 2,000 files, and a partial merge once lost
