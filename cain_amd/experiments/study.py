@@ -45,6 +45,7 @@ import atexit
 import csv
 import dataclasses
 import json
+import math
 import os
 import random
 import shutil
@@ -594,8 +595,14 @@ class _StudyBase:
 
     def gpu_energy_source(self, context: RunnerContext) -> str:
         """Provenance of the row's gpu_energy_J: "measured" (amd-smi accumulator) or "idle_model" (idle board
-        power x window, the remote arm on a GPU shared with the server)."""
-        return "idle_model" if self._shared_remote(context) else "measured"
+        power x window, the remote arm on a GPU shared with the server; "none(no idle baseline)" when that idle power
+        was not measured, and the row then carries no board energy)."""
+        if not self._shared_remote(context):
+            return "measured"
+        idle = self.idle_power_w
+        if idle is None or math.isnan(float(idle)):
+            return "none(no idle baseline)"
+        return "idle_model"
 
     def start_measurement(self, context: RunnerContext) -> None:
         # the energy window (opened by the plugin just before this body) covers the request; with

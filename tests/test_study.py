@@ -148,8 +148,9 @@ def test_study_on_device_arm_on_gpu_measures_energy(tmp_path):
 def test_study_both_arms_against_real_engine_servers(tmp_path):
     """Both arms through curl against this framework's own engine: the on-device server and a remote server
     (``CAIN_STUDY_REMOTE=local:0``: a separate engine process on the box's GPU).  The remote rows decode at the
-    engine's rate (not the 70 tok/s modelled server) and are charged client-side energy only: the GPU board
-    belongs to the server, so gpu_energy_J is 0 and the CPU + RAM energy is what remains."""
+    engine's rate (not the 70 tok/s modelled server).  One client-device definition (round 5): the board the remote
+    server shares is charged to the client at the session's measured idle power x the window (idle_model), the
+    on-device rows' board is measured."""
     import torch
 
     if not torch.cuda.is_available():
@@ -170,8 +171,12 @@ def test_study_both_arms_against_real_engine_servers(tmp_path):
     remote = [x for x in rows if x["method"] == "remote"]
     local = [x for x in rows if x["method"] == "on_device"]
     assert all(float(x["tok_per_s"]) > 150 for x in remote), [x["tok_per_s"] for x in remote]
-    assert all(float(x["gpu_energy_J"]) == 0.0 for x in remote)
-    assert all(float(x["gpu_energy_J"]) > 0 for x in local)
+    for x in remote:
+        assert x["gpu_energy_source"] == "idle_model"
+        assert float(x["gpu_energy_J"]) == pytest.approx(float(x["idle_power_W"]) * float(x["energy_window_s"]),
+                                                         rel=2e-2, abs=0.05)
+        assert float(x["gpu_energy_J"]) > 0
+    assert all(float(x["gpu_energy_J"]) > 0 and x["gpu_energy_source"] == "measured" for x in local)
     # gpu_usage keeps the reference meaning (the client's own GPU residency: none, the client never opens the
     # GPU); the shared board's activity is the server's and goes to server_gpu_usage
     assert all(float(x["gpu_usage"]) == 0.0 and float(x["server_gpu_usage"]) > 0 for x in remote)
@@ -226,6 +231,9 @@ def test_remote_row_energy_has_one_definition_at_every_world_size(monkeypatch):
         cfg.dp_world = world
         srcs = cfg.energy_sources_for(ctx)
         assert cfg.energy_sources_for(ondev) == ("gpu", "cpu", "ram")
+        cfg.idle_power_w = None
+        assert cfg.gpu_energy_source(ctx) == ("none(no idle baseline)" if shared else "measured")
+        cfg.idle_power_w = idle_w
         assert cfg.gpu_energy_source(ctx) == ("idle_model" if shared else "measured")
         m = EnergyMeter(smi_indices=[], period_ms=10, cpu_tdp_w=100.0, sources=srcs, cpu_attribution="process")
         m.sampler.close()
