@@ -141,6 +141,9 @@ SETS = {
     # its second replicate (another seed): n = 20 per cell with the first
     "r5_fp4_study_b": [("study", 1150, "CAIN_STUDY_WEIGHTS=fp4 STUDY_NAME=fp4_r5b SEED=2026 COOLDOWN_MS=10000 REPS=10 "
                                        "IDLE_SETTLE_S=12 bash tools/study_chunk.sh 960")],
+    # its third replicate (n = 30 per cell with the first two)
+    "r5_fp4_study_c": [("study", 1150, "CAIN_STUDY_WEIGHTS=fp4 STUDY_NAME=fp4_r5c SEED=2027 COOLDOWN_MS=10000 REPS=10 "
+                                       "IDLE_SETTLE_S=12 bash tools/study_chunk.sh 960")],
     # round 5: the 256-column wide GEMM (wgemm256.hip): numerics first (a new kernel), then isolated shape timings
     # against the 128-column ring, then the headline with every llama shape on it (interleaved with the default)
     "r5_w256": [
