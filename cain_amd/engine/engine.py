@@ -36,6 +36,7 @@ import numpy as np
 import torch
 
 from ..models.config import ModelConfig, get_config, rope_inv_freq
+from ..models.hf import checkpoint_for, load_hf_weights, load_pretrained, load_tokenizer
 from ..models.tokenizer import SyntheticTokenizer, get_tokenizer
 from ..models.weights import WEIGHT_DTYPES, ModelWeights, pack_for_engine, random_weights, roundtrip_weights
 
@@ -156,6 +157,15 @@ def attention_splits(M: int, Hkv: int, T_max: int) -> int:
 
 
 class DecodeEngine:
+    @classmethod
+    def from_pretrained(cls, path: str, device: Union[str, torch.device] = "cuda", name: Optional[str] = None,
+                        **kw) -> "DecodeEngine":
+        """An engine on a Hugging Face checkpoint directory (``config.json`` + safetensors + ``tokenizer.json``;
+        ``models/hf.py``): the same kernels and options as a tag's engine (``weight_dtype="fp4"`` quantises the
+        checkpoint's bf16 weights to MXFP4 at load, as the packing of random weights does)."""
+        cfg, weights, tok = load_pretrained(path, name=name, device=torch.device(device))
+        return cls(cfg, device=device, weights=weights, tokenizer=tok, **kw)
+
     def __init__(self, model: Union[str, ModelConfig], device: Union[str, torch.device] = "cuda",
                  max_batch: int = 16, max_context: int = 2048, seed: int = 0, backend: Optional[str] = None,
                  steps_per_graph: int = 8, weights: Optional[ModelWeights] = None, tokenizer=None,
@@ -205,11 +215,16 @@ class DecodeEngine:
         self.T_max = int(math.ceil(min(max_context, self.cfg.max_context) / 32) * 32)
         self.seed = seed
         self.steps_per_graph = max(1, int(steps_per_graph))
+        # a checkpoint registered under the tag (CAIN_CHECKPOINTS, models/hf.py): its weights and tokenizer
+        ckpt = checkpoint_for(model) if isinstance(model, str) and weights is None else None
+        if tokenizer is None and ckpt:
+            tokenizer = load_tokenizer(ckpt, self.cfg)
         self.tokenizer = tokenizer or get_tokenizer(self.cfg)
         self.keep_natural = keep_natural
         t0 = time.perf_counter_ns()
         if weights is None:
-            weights = random_weights(self.cfg, device=self.device, seed=seed)
+            weights = (load_hf_weights(ckpt, self.cfg, device=self.device) if ckpt
+                       else random_weights(self.cfg, device=self.device, seed=seed))
         self.weights = weights
         if backend == "hip":
             self._init_hip()

@@ -11,6 +11,8 @@ from __future__ import annotations
 
 import math
 from dataclasses import asdict, dataclass, replace
+from functools import lru_cache
+from pathlib import Path
 from typing import Dict, Optional
 
 
@@ -127,6 +129,16 @@ TINY: Dict[str, ModelConfig] = {
 
 
 def get_config(name: str) -> ModelConfig:
+    """The tag's architecture: a checkpoint registered under it in ``CAIN_CHECKPOINTS`` (``hf.py``) first, else
+    the built-in config."""
+    import os
+
+    if os.environ.get("CAIN_CHECKPOINTS"):
+        from .hf import checkpoint_for
+
+        path = checkpoint_for(name)
+        if path:
+            return _checkpoint_config(name, path)
     if name in MODELS:
         return MODELS[name]
     if name in TINY:
@@ -136,6 +148,14 @@ def get_config(name: str) -> ModelConfig:
     if base in MODELS:
         return MODELS[base]
     raise KeyError(f"unknown model {name!r}; known: {sorted(MODELS) + sorted(TINY)}")
+
+
+@lru_cache(maxsize=64)
+def _checkpoint_config(name: str, path: str) -> ModelConfig:
+    from .hf import _Tensors, config_from_hf
+
+    p = Path(path)
+    return config_from_hf(p, name=name, tensor_names=_Tensors(p).names())
 
 
 def rope_inv_freq(cfg: ModelConfig):

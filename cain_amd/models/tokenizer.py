@@ -82,18 +82,29 @@ class SyntheticTokenizer:
         return len(text.split())
 
 
-class HFTokenizer:  # pragma: no cover - needs a local tokenizer.json
-    def __init__(self, path: str):
+class HFTokenizer:
+    """A checkpoint's ``tokenizer.json`` (``tokenizers``, Rust).  ``add_bos`` maps onto the file's own special-token
+    template, as transformers does: Llama 3 and Gemma prepend their BOS there, Qwen2 adds none."""
+
+    def __init__(self, path: str, bos_id: Optional[int] = None):
         from tokenizers import Tokenizer
 
         self.tok = Tokenizer.from_file(path)
         self.vocab = self.tok.get_vocab_size()
+        self.bos_id = bos_id
 
     def encode(self, text: str, add_bos: bool = True) -> List[int]:
-        return self.tok.encode(text).ids
+        return self.tok.encode(text, add_special_tokens=add_bos).ids
+
+    def piece(self, tid: int) -> str:
+        return self.tok.decode([int(tid)], skip_special_tokens=True)
 
     def decode(self, ids: List[int]) -> str:
-        return self.tok.decode(list(ids))
+        return self.tok.decode([int(t) for t in ids], skip_special_tokens=True)
+
+    @staticmethod
+    def count_words(text: str) -> int:
+        return len(text.split())
 
 
 def get_tokenizer(cfg, path: Optional[str] = None):

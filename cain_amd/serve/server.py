@@ -39,6 +39,7 @@ from __future__ import annotations
 import argparse
 import datetime
 import json
+import os
 import queue
 import re
 import sys
@@ -94,6 +95,26 @@ class Backend:
         return {}
 
 
+# Ollama's quantization_level names for the engine's weight storage
+QUANT_LEVEL = {"bf16": "BF16", "fp8": "F8_E4M3", "fp4": "MXFP4"}
+
+
+def register_checkpoints(specs: Optional[List[str]]) -> List[str]:
+    """``--checkpoint TAG=PATH`` options: added to ``CAIN_CHECKPOINTS`` (so engines, and processes started from
+    here, load the checkpoint for TAG; models/hf.py); returns the tags."""
+    from ..models.hf import registered_checkpoints
+
+    if not specs:
+        return []
+    os.environ["CAIN_CHECKPOINTS"] = ",".join(filter(None, [os.environ.get("CAIN_CHECKPOINTS", "")] + list(specs)))
+    reg = registered_checkpoints()  # validates the syntax
+    tags = [s.partition("=")[0].strip() for s in specs]
+    for t in tags:
+        if not os.path.isdir(reg[t]):
+            raise SystemExit(f"--checkpoint {t}: {reg[t]} is not a directory")
+    return tags
+
+
 class EngineBackend(Backend):
     """Backed by one DecodeEngine per model on ``device`` (created on first use, then resident)."""
 
@@ -144,10 +165,14 @@ class EngineBackend(Backend):
     def model_info(self, model: str) -> Dict[str, Any]:
         from ..models import get_config
 
+        from ..models.hf import checkpoint_for
+
         cfg = get_config(model)
+        ckpt = checkpoint_for(model)
+        info = cfg.as_dict() | ({"checkpoint": ckpt} if ckpt else {"weights": "random-init"})
         return {"details": {"family": cfg.name.split(":")[0], "parameter_size": f"{cfg.n_params() / 1e9:.1f}B",
-                            "quantization_level": "BF16", "format": "cain-packed"},
-                "model_info": cfg.as_dict()}
+                            "quantization_level": QUANT_LEVEL[self.weight_dtype], "format": "cain-packed"},
+                "model_info": info}
 
     def run(self, model: str, jobs: List[Job]) -> None:
         eng = self.engine(model)
@@ -581,11 +606,15 @@ def main(argv: Optional[List[str]] = None) -> None:
     ap.add_argument("--static-batching", action="store_true",
                     help="batch requests that arrive within --batch-window-ms and run each batch to completion "
                          "(default on the HIP engine: continuous batching)")
+    ap.add_argument("--checkpoint", action="append", metavar="TAG=PATH",
+                    help="serve a Hugging Face checkpoint directory under TAG (repeatable; models/hf.py)")
     ap.add_argument("-v", "--verbose", action="store_true")
     ns = ap.parse_args(argv)
+    ck_tags = register_checkpoints(ns.checkpoint)
     models = [m for m in ns.models.split(",") if m]
+    models += [t for t in ck_tags if t not in models]
     for m in models:
-        if m not in MODELS and m not in TINY:
+        if m not in MODELS and m not in TINY and m not in ck_tags:
             raise SystemExit(f"unknown model {m}")
     if ns.backend == "fake":
         be: Backend = FakeBackend(models, tokens_per_s=ns.fake_tok_s, prefill_s=ns.fake_prefill_s)
@@ -612,7 +641,10 @@ def generate_main(argv: Optional[List[str]] = None) -> None:
     ap.add_argument("--seed", type=int, default=None)
     ap.add_argument("--weights", choices=["bf16", "fp8", "fp4"], default="bf16")
     ap.add_argument("--kv", choices=["bf16", "fp8"], default="bf16")
+    ap.add_argument("--checkpoint", metavar="PATH", help="a Hugging Face checkpoint directory, served as --model")
     ns = ap.parse_args(argv)
+    if ns.checkpoint:
+        register_checkpoints([f"{ns.model}={ns.checkpoint}"])
     be = EngineBackend([ns.model], device=ns.device, max_batch=1, weight_dtype=ns.weights, kv_dtype=ns.kv)
     opts = {k: v for k, v in (("temperature", ns.temperature), ("seed", ns.seed)) if v is not None}
     job = Job(ns.model, ns.prompt, ns.num_predict or default_num_predict(ns.prompt), opts)
