@@ -13,7 +13,7 @@ import math
 from dataclasses import asdict, dataclass, replace
 from functools import lru_cache
 from pathlib import Path
-from typing import Dict, Optional
+from typing import Dict, Optional, Tuple
 
 
 @dataclass(frozen=True)
@@ -47,6 +47,9 @@ class ModelConfig:
     max_context: int = 8192
     bos_id: int = 1
     eos_id: int = 2
+    # per-frequency divisors of the inverse frequencies (GGUF's rope_freqs tensor: llama.cpp bakes Llama 3.1's
+    # scaling into it); applied instead of rope_scaling when set
+    rope_freq_factors: Optional[Tuple[float, ...]] = None
 
     @property
     def group(self) -> int:
@@ -152,18 +155,22 @@ def get_config(name: str) -> ModelConfig:
 
 @lru_cache(maxsize=64)
 def _checkpoint_config(name: str, path: str) -> ModelConfig:
-    from .hf import _Tensors, config_from_hf
+    from .hf import checkpoint_config
 
-    p = Path(path)
-    return config_from_hf(p, name=name, tensor_names=_Tensors(p).names())
+    return checkpoint_config(Path(path), name=name)
 
 
 def rope_inv_freq(cfg: ModelConfig):
-    """Inverse frequencies (numpy float64), with Llama-3 scaling when configured."""
+    """Inverse frequencies (numpy float64), with Llama-3 scaling or explicit per-frequency factors when configured."""
     import numpy as np
 
     hd = cfg.head_dim
     inv = 1.0 / (cfg.rope_theta ** (np.arange(0, hd, 2, dtype=np.float64) / hd))
+    if cfg.rope_freq_factors is not None:
+        fac = np.asarray(cfg.rope_freq_factors, dtype=np.float64)
+        if fac.shape != inv.shape:
+            raise ValueError(f"rope_freq_factors has {fac.size} entries, head_dim {hd} needs {inv.size}")
+        return inv / fac
     rs = cfg.rope_scaling
     if rs is None:
         return inv

@@ -10,7 +10,8 @@ no network for checkpoints), and this module is how a user points it at real one
   q / k / v (or Phi-3's fused ``qkv_proj``) concatenated into ``wqkv``, Phi-3's fused ``gate_up_proj`` split, the LM
   head tied to the embedding table when the checkpoint has none;
 * ``load_pretrained`` returns config, weights and the checkpoint's ``tokenizer.json`` tokenizer;
-* ``CAIN_CHECKPOINTS="tag=/path,tag2=/path2"`` registers checkpoints under model tags: every place that builds an
+* ``CAIN_CHECKPOINTS="tag=/path,tag2=/path2"`` registers checkpoints (directories, or GGUF files: ``gguf.py``)
+  under model tags: every place that builds an
   engine from a tag (``DecodeEngine(tag)``, the Ollama-compatible server, the study, ``bench.py``) and
   ``get_config(tag)`` then use the checkpoint.
 
@@ -180,8 +181,13 @@ class _Tensors:
 
 def load_hf_weights(path: PathLike, cfg: Optional[ModelConfig] = None, device="cpu",
                     dtype: torch.dtype = torch.bfloat16) -> ModelWeights:
-    """``ModelWeights`` (natural layout, ``dtype``) of a checkpoint directory."""
+    """``ModelWeights`` (natural layout, ``dtype``) of a checkpoint directory (or a GGUF file: models/gguf.py)."""
     p = Path(path)
+    if is_gguf(p):
+        from .gguf import GGUFFile, config_from_gguf, load_gguf_weights
+
+        g = GGUFFile(p)
+        return load_gguf_weights(g, cfg or config_from_gguf(g, name=p.stem), device=device, dtype=dtype)
     t = _Tensors(p)
     if cfg is None:
         cfg = config_from_hf(_read_config(p), name=p.name, tensor_names=t.names())
@@ -236,17 +242,41 @@ def load_tokenizer(path: PathLike, cfg: Optional[ModelConfig] = None):
     """The checkpoint's ``tokenizer.json`` (``HFTokenizer``), or None when it has none."""
     from .tokenizer import HFTokenizer
 
+    if is_gguf(path):
+        from .gguf import GGUFFile, load_gguf_tokenizer
+
+        return load_gguf_tokenizer(GGUFFile(path), cfg)
     f = Path(path) / "tokenizer.json"
     return HFTokenizer(str(f), bos_id=cfg.bos_id if cfg else None) if f.exists() else None
 
 
 def load_pretrained(path: PathLike, name: Optional[str] = None, device="cpu",
                     dtype: torch.dtype = torch.bfloat16):
-    """(config, weights, tokenizer or None) of a checkpoint directory."""
+    """(config, weights, tokenizer or None) of a checkpoint directory or a GGUF file."""
     p = Path(path)
+    if is_gguf(p):
+        from .gguf import load_gguf
+
+        return load_gguf(p, name=name or p.stem, device=device, dtype=dtype)
     t = _Tensors(p)
     cfg = config_from_hf(_read_config(p), name=name or p.name, tensor_names=t.names())
     return cfg, load_hf_weights(p, cfg, device=device, dtype=dtype), load_tokenizer(p, cfg)
+
+
+def is_gguf(path: PathLike) -> bool:
+    from .gguf import is_gguf as _is_gguf
+
+    return _is_gguf(path)
+
+
+def checkpoint_config(path: PathLike, name: Optional[str] = None) -> ModelConfig:
+    """The ``ModelConfig`` of a checkpoint directory or GGUF file."""
+    p = Path(path)
+    if is_gguf(p):
+        from .gguf import GGUFFile, config_from_gguf
+
+        return config_from_gguf(GGUFFile(p), name=name or p.stem)
+    return config_from_hf(p, name=name, tensor_names=_Tensors(p).names())
 
 
 def registered_checkpoints() -> Dict[str, str]:

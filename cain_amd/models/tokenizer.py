@@ -93,6 +93,13 @@ class HFTokenizer:
         self.vocab = self.tok.get_vocab_size()
         self.bos_id = bos_id
 
+    @classmethod
+    def from_tokenizer(cls, tok, bos_id: Optional[int] = None) -> "HFTokenizer":
+        """Around an in-memory ``tokenizers.Tokenizer`` (a GGUF vocabulary, models/gguf.py)."""
+        obj = cls.__new__(cls)
+        obj.tok, obj.vocab, obj.bos_id = tok, tok.get_vocab_size(), bos_id
+        return obj
+
     def encode(self, text: str, add_bos: bool = True) -> List[int]:
         return self.tok.encode(text, add_special_tokens=add_bos).ids
 

@@ -1,0 +1,238 @@
+"""GGUF files (models/gguf.py) on CPU.
+
+* Block decoders: every quantised type against a per-element scalar decoder written from ggml's reference loops
+  (``dequantize_row_*``), on random blocks; Q8_0 / Q4_0 also through this module's quantisers.  No independent GGUF
+  implementation is importable here, so these pin the vectorisation, not the format against llama.cpp (parity
+  unpinned, documented in gguf.py).
+* Conventions: the q / k un-permutation against transformers' own GGUF processor; Gemma's stored 1 + w.
+* End to end, per family: a transformers checkpoint written as GGUF with llama.cpp's conventions (``export_gguf``)
+  and read back gives the oracle logits transformers computes on the original checkpoint.
+"""
+import dataclasses
+
+import numpy as np
+import pytest
+import torch
+
+from hf_fixtures import FAMILIES, hf_logits, make_checkpoint
+
+from cain_amd.engine import DecodeEngine
+from cain_amd.models.gguf import (GGML_TYPES, TYPE_ID, GGUFFile, dequantize, export_gguf, load_gguf, permute_qk,
+                                  quantize_q4_0, quantize_q8_0, unpermute_qk, write_gguf)
+from cain_amd.models.hf import load_pretrained
+from cain_amd.models.reference import ReferenceModel
+
+pytest.importorskip("transformers")
+GGUF_ARCH = {"llama": "llama", "mistral": "llama", "qwen2": "qwen2", "gemma": "gemma", "phi3": "phi3"}
+
+
+# ------------------------------------------------------------------ scalar reference decoders (ggml loop order)
+def _h(b, i):
+    return float(np.frombuffer(bytes(b[i:i + 2]), np.float16)[0])
+
+
+def _scale_min_k4(j, q):
+    if j < 4:
+        return q[j] & 63, q[j + 4] & 63
+    return (q[j + 4] & 0xF) | ((q[j - 4] >> 6) << 4), (q[j + 4] >> 4) | ((q[j] >> 6) << 4)
+
+
+def ref_block(name, b):
+    b = [int(x) for x in b]
+    y = [0.0] * GGML_TYPES[TYPE_ID[name]][1]
+    if name in ("Q4_0", "Q4_1"):
+        d = _h(b, 0)
+        m = _h(b, 2) if name == "Q4_1" else 0.0
+        qs = b[4:] if name == "Q4_1" else b[2:]
+        off = 0 if name == "Q4_1" else 8
+        for j in range(16):
+            y[j] = ((qs[j] & 0xF) - off) * d + m
+            y[j + 16] = ((qs[j] >> 4) - off) * d + m
+    elif name in ("Q5_0", "Q5_1"):
+        d = _h(b, 0)
+        m = _h(b, 2) if name == "Q5_1" else 0.0
+        p = 4 if name == "Q5_1" else 2
+        qh = int.from_bytes(bytes(b[p:p + 4]), "little")
+        qs = b[p + 4:]
+        off = 0 if name == "Q5_1" else 16
+        for j in range(16):
+            xh0 = ((qh >> j) << 4) & 0x10
+            xh1 = (qh >> (j + 12)) & 0x10
+            y[j] = (((qs[j] & 0xF) | xh0) - off) * d + m
+            y[j + 16] = (((qs[j] >> 4) | xh1) - off) * d + m
+    elif name == "Q8_0":
+        d = _h(b, 0)
+        for j in range(32):
+            y[j] = d * (b[2 + j] - 256 if b[2 + j] > 127 else b[2 + j])
+    elif name in ("Q4_K", "Q5_K"):
+        d, dmin, sc = _h(b, 0), _h(b, 2), b[4:16]
+        qh = b[16:48] if name == "Q5_K" else None
+        ql = b[48:176] if name == "Q5_K" else b[16:144]
+        u1, u2, is_, yi, qi = 1, 2, 0, 0, 0
+        for _ in range(4):
+            s1, m1 = _scale_min_k4(is_, sc)
+            s2, m2 = _scale_min_k4(is_ + 1, sc)
+            for l in range(32):
+                h = (16 if qh[l] & u1 else 0) if qh else 0
+                y[yi + l] = d * s1 * ((ql[qi + l] & 0xF) + h) - dmin * m1
+            for l in range(32):
+                h = (16 if qh[l] & u2 else 0) if qh else 0
+                y[yi + 32 + l] = d * s2 * ((ql[qi + l] >> 4) + h) - dmin * m2
+            qi += 32
+            yi += 64
+            is_ += 2
+            u1 <<= 2
+            u2 <<= 2
+    elif name == "Q6_K":
+        ql, qh = b[0:128], b[128:192]
+        sc = [x - 256 if x > 127 else x for x in b[192:208]]
+        d = _h(b, 208)
+        for n in range(2):
+            for l in range(32):
+                is_ = l // 16
+                q1 = ((ql[64 * n + l] & 0xF) | (((qh[32 * n + l] >> 0) & 3) << 4)) - 32
+                q2 = ((ql[64 * n + l + 32] & 0xF) | (((qh[32 * n + l] >> 2) & 3) << 4)) - 32
+                q3 = ((ql[64 * n + l] >> 4) | (((qh[32 * n + l] >> 4) & 3) << 4)) - 32
+                q4 = ((ql[64 * n + l + 32] >> 4) | (((qh[32 * n + l] >> 6) & 3) << 4)) - 32
+                y[128 * n + l] = d * sc[8 * n + is_] * q1
+                y[128 * n + l + 32] = d * sc[8 * n + is_ + 2] * q2
+                y[128 * n + l + 64] = d * sc[8 * n + is_ + 4] * q3
+                y[128 * n + l + 96] = d * sc[8 * n + is_ + 6] * q4
+    return np.array(y, np.float32)
+
+
+def _random_blocks(name, n, seed=0):
+    rng = np.random.default_rng(seed)
+    _, bs, bb = GGML_TYPES[TYPE_ID[name]]
+    raw = rng.integers(0, 256, (n, bb), dtype=np.uint8)
+    fp16_at = {"Q6_K": [208]}.get(name, [0, 2] if name in ("Q4_1", "Q5_1", "Q4_K", "Q5_K") else [0])
+    for p in fp16_at:  # finite, moderate half-precision scales
+        raw[:, p:p + 2] = np.frombuffer(rng.uniform(-2, 2, n).astype(np.float16).tobytes(), np.uint8).reshape(n, 2)
+    return raw
+
+
+@pytest.mark.parametrize("name", ["Q4_0", "Q4_1", "Q5_0", "Q5_1", "Q8_0", "Q4_K", "Q5_K", "Q6_K"])
+def test_block_decoders_match_the_scalar_reference(name):
+    raw = _random_blocks(name, 6)
+    bs = GGML_TYPES[TYPE_ID[name]][1]
+    got = dequantize(raw.reshape(-1), TYPE_ID[name], 6 * bs).reshape(6, bs)
+    for i in range(6):
+        np.testing.assert_allclose(got[i], ref_block(name, raw[i]), rtol=1e-6, atol=1e-6, err_msg=name)
+
+
+def test_q8_0_and_q4_0_round_trip():
+    x = np.random.default_rng(1).normal(0, 1, 32 * 64).astype(np.float32)
+    y8 = dequantize(quantize_q8_0(x), TYPE_ID["Q8_0"], x.size)
+    y4 = dequantize(quantize_q4_0(x), TYPE_ID["Q4_0"], x.size)
+    amax = np.abs(x.reshape(-1, 32)).max(1, keepdims=True)
+    assert np.all(np.abs(y8 - x).reshape(-1, 32) <= amax / 127 * 0.5 + 1e-3 * amax)
+    # Q4_0's 16 levels run -8 d .. 7 d around the signed maximum: half a step inside, one step at the far end
+    assert np.all(np.abs(y4 - x).reshape(-1, 32) <= amax / 8 + 1e-3 * amax)
+    # the block's largest-magnitude element is exact up to the fp16 scale (Q4_0 maps it to -8 * d)
+    i = np.abs(x.reshape(-1, 32)).argmax(1)
+    np.testing.assert_allclose(y4.reshape(-1, 32)[np.arange(64), i], x.reshape(-1, 32)[np.arange(64), i], rtol=1e-3)
+
+
+def test_container_round_trip(tmp_path):
+    rng = np.random.default_rng(2)
+    a = rng.normal(0, 1, (64, 96)).astype(np.float32)
+    meta = {"general.architecture": "llama", "general.name": "t", "x.int": 7, "x.big": 2 ** 40, "x.neg": -3,
+            "x.float": 0.5, "x.bool": True, "x.strs": ["a", "bb", ""], "x.ints": [1, -2, 3], "x.floats": [0.25, 1.5]}
+    T = {"f32": (a, "F32"), "f16": (a, "F16"), "bf16": (a, "BF16"), "q8": (a, "Q8_0"), "q4": (a, "Q4_0"),
+         "vec": (a[0], "F32")}
+    write_gguf(tmp_path / "t.gguf", meta, T)
+    g = GGUFFile(tmp_path / "t.gguf")
+    for k, v in meta.items():
+        assert g.metadata[k] == v, k
+    assert g.version == 3 and g.tensors["q8"].shape == (64, 96) and g.tensors["vec"].shape == (96,)
+    at = torch.from_numpy(a)
+    assert torch.equal(g.tensor("f32"), at)
+    assert torch.equal(g.tensor("f16"), at.half().float())
+    assert torch.equal(g.tensor("bf16"), at.bfloat16().float())
+    assert torch.equal(g.tensor("q8"), torch.from_numpy(dequantize(quantize_q8_0(a), TYPE_ID["Q8_0"], a.size)
+                                                        .reshape(a.shape)))
+    assert float((g.tensor("q4") - at).abs().max()) < 0.6
+    for bad in ("Q2_K", "Q3_K"):
+        with pytest.raises(NotImplementedError):
+            dequantize(np.zeros(GGML_TYPES[TYPE_ID[bad]][2], np.uint8), TYPE_ID[bad], 256)
+
+
+def test_qk_permutation_matches_transformers():
+    from transformers.modeling_gguf_pytorch_utils import LlamaTensorProcessor
+
+    w = torch.randn(8 * 64, 32)
+    for heads in (8, 2):
+        p = permute_qk(w[: heads * 64], heads)
+        theirs = LlamaTensorProcessor()._reverse_permute_weights(p.numpy(), heads, heads)
+        assert np.array_equal(unpermute_qk(p, heads).numpy(), theirs)
+        assert torch.equal(unpermute_qk(p, heads), w[: heads * 64])
+        assert not torch.equal(p, w[: heads * 64])
+
+
+@pytest.mark.parametrize("family", sorted(FAMILIES))
+def test_gguf_export_and_load_match_transformers(family, tmp_path):
+    """HF checkpoint -> GGUF (llama.cpp conventions, F32) -> load_gguf: the oracle's logits equal transformers' on
+    the original checkpoint (Llama 3.1's scaling travels as a rope_freqs tensor)."""
+    model = make_checkpoint(family, tmp_path / "hf", scale=4.0)
+    _, mw, _ = load_pretrained(tmp_path / "hf", dtype=torch.float32)
+    export_gguf(mw, tmp_path / "m.gguf", GGUF_ARCH[family], tensor_type="F32")
+    cfg, mg, tok = load_gguf(tmp_path / "m.gguf", dtype=torch.float32)
+    assert tok is None and cfg.name == "m"
+    assert (cfg.n_layers, cfg.d_model, cfg.n_heads, cfg.n_kv_heads, cfg.head_dim, cfg.ffn, cfg.vocab) == \
+        (mw.cfg.n_layers, mw.cfg.d_model, mw.cfg.n_heads, mw.cfg.n_kv_heads, mw.cfg.head_dim, mw.cfg.ffn, mw.cfg.vocab)
+    assert (cfg.tie_embeddings, cfg.qkv_bias, cfg.norm_add_one) == (mw.cfg.tie_embeddings, mw.cfg.qkv_bias,
+                                                                    mw.cfg.norm_add_one)
+    assert (cfg.rope_freq_factors is not None) == (family == "llama")
+    assert torch.equal(mg.layers[1].wqkv, mw.layers[1].wqkv)  # un-permuted back to the checkpoint's row order
+    if family == "gemma":
+        raw = GGUFFile(tmp_path / "m.gguf").tensor("blk.0.attn_norm.weight")
+        assert torch.allclose(raw - 1.0, mw.layers[0].attn_norm, atol=1e-6)  # stored 1 + w (transformers subtracts 1)
+    tokens = torch.randint(3, 1024, (2, 10), generator=torch.Generator().manual_seed(5))
+    positions = (torch.arange(10) + (3000 if family == "llama" else 0)).expand(2, 10)
+    theirs = hf_logits(model, tokens, positions)
+    ours = ReferenceModel(mg).forward(tokens, positions=positions)
+    err = float((ours - theirs).abs().max() / theirs.abs().max())
+    assert err < (1e-4 if family == "llama" else 2e-5), f"{family}: {err:.2e}"
+
+
+def test_q8_0_gguf_is_close_and_engine_loads_it(tmp_path, monkeypatch):
+    """A Q8_0 file through CAIN_CHECKPOINTS: get_config / DecodeEngine(tag) use it; logits near the fp32 model's."""
+    model = make_checkpoint("mistral", tmp_path / "hf", scale=4.0)
+    _, mw, _ = load_pretrained(tmp_path / "hf", dtype=torch.float32)
+    export_gguf(mw, tmp_path / "q8.gguf", "llama", tensor_type="Q8_0")
+    monkeypatch.setenv("CAIN_CHECKPOINTS", f"mistral-q8:tiny={tmp_path / 'q8.gguf'}")
+    eng = DecodeEngine("mistral-q8:tiny", device="cpu", max_batch=1, max_context=64)
+    assert eng.cfg.name == "mistral-q8:tiny" and eng.cfg.n_kv_heads == 1
+    tokens = torch.randint(3, 1024, (1, 8), generator=torch.Generator().manual_seed(6))
+    theirs = hf_logits(model, tokens, torch.arange(8)[None])[0, -1]
+    ours = eng.last_logits([tokens[0].tolist()])[0]
+    rel = float((ours - theirs).norm() / theirs.norm())
+    assert rel < 0.03, rel
+
+
+def test_gguf_tokenizer_through_transformers_converter(tmp_path):
+    """A byte-level BPE vocabulary stored the GGUF way (tokens, merges) comes back as a working tokenizer."""
+    from tokenizers import Tokenizer, decoders, models, pre_tokenizers, trainers
+
+    tok = Tokenizer(models.BPE())
+    tok.pre_tokenizer = pre_tokenizers.ByteLevel(add_prefix_space=False)
+    tok.decoder = decoders.ByteLevel()
+    text = ["In 100 words, please give me information about India", "energy of remote and on device inference"] * 20
+    tok.train_from_iterator(text, trainers.BpeTrainer(vocab_size=300, special_tokens=["<|endoftext|>"],
+                                                      initial_alphabet=pre_tokenizers.ByteLevel.alphabet()))
+    import json
+    spec = json.loads(tok.to_str())
+    vocab = spec["model"]["vocab"]
+    tokens = [t for t, _ in sorted(vocab.items(), key=lambda kv: kv[1])]
+    merges = [m if isinstance(m, str) else " ".join(m) for m in spec["model"]["merges"]]
+    model = make_checkpoint("qwen2", tmp_path / "hf")
+    _, mw, _ = load_pretrained(tmp_path / "hf")
+    fields = {"tokenizer.ggml.model": "gpt2", "tokenizer.ggml.tokens": tokens, "tokenizer.ggml.merges": merges,
+              "tokenizer.ggml.token_type": [1] * len(tokens)}
+    export_gguf(mw, tmp_path / "t.gguf", "qwen2", tokenizer_fields=fields)
+    _, _, gt = load_gguf(tmp_path / "t.gguf")
+    s = "please give me information about remote energy"
+    ids = gt.encode(s, add_bos=False)
+    assert ids == tok.encode(s).ids
+    assert gt.decode(ids) == s
+    del model

@@ -42,3 +42,31 @@ def test_hip_engine_on_a_checkpoint(family, weights, tmp_path):
         err_eager.append(rel(ref_e, want))
     assert_within_eager(err, err_eager, f"{family} {weights}")
     eng.close()
+
+
+@pytest.mark.parametrize("weights", ["bf16", "fp4"])
+def test_hip_engine_on_a_gguf_file(weights, tmp_path):
+    """A Q4_0 GGUF file (llama.cpp conventions: permuted q / k rows, Llama 3.1 scaling as rope_freqs) on the HIP
+    engine, against the oracle on the same dequantised weights."""
+    from cain_amd.models.gguf import export_gguf
+    from cain_amd.models.hf import load_pretrained
+    from cain_amd.models.reference import ReferenceModel
+    from cain_amd.models.weights import roundtrip_weights
+
+    make_checkpoint("llama", tmp_path / "hf", scale=4.0)
+    _, mw, _ = load_pretrained(tmp_path / "hf", dtype=torch.float32)
+    export_gguf(mw, tmp_path / "m.gguf", "llama", tensor_type="Q4_0")
+    eng = DecodeEngine.from_pretrained(str(tmp_path / "m.gguf"), device="cuda", max_batch=4, max_context=128,
+                                       keep_natural=True, weight_dtype=weights)
+    assert eng.cfg.rope_freq_factors is not None
+    got = eng.last_logits(PROMPTS).float().cpu()
+    base = roundtrip_weights(eng.weights, weights)
+    ref, eager = ReferenceModel(base), eager_bf16(base)
+    err, err_eager = [], []
+    for i, p in enumerate(PROMPTS):
+        toks = torch.tensor([p], device="cuda")
+        want = ref.forward(toks)[0, -1].float().cpu()
+        err.append(rel(got[i], want))
+        err_eager.append(rel(eager.forward(toks)[0, -1].float().cpu(), want))
+    assert_within_eager(err, err_eager, f"gguf {weights}")
+    eng.close()
