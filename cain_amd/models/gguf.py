@@ -41,6 +41,7 @@ from .config import ModelConfig
 from .weights import LayerWeights, ModelWeights
 
 GGUF_MAGIC = b"GGUF"
+SLICE_ELEMS = 1 << 24  # elements dequantised per slice of a tensor (GGUFFile.tensor)
 
 # ggml tensor types: id -> (name, elements per block, bytes per block)
 GGML_TYPES: Dict[int, Tuple[str, int, int]] = {
@@ -128,7 +129,15 @@ class GGUFFile:
         if t is None:
             raise KeyError(f"GGUF file has no tensor {name!r}")
         n = int(np.prod(t.shape))
-        return torch.from_numpy(dequantize(self.raw(name), t.type, n).reshape(t.shape))
+        _, bs, bb = GGML_TYPES.get(t.type, ("?", 1, 0))
+        raw = self.raw(name)
+        out = np.empty(n, np.float32)
+        # in slices of whole blocks: a 128k x 4096 Q4_K embedding would otherwise hold ~4x its fp32 size in temporaries
+        step = max(1, SLICE_ELEMS // bs) * bs
+        for e0 in range(0, n, step):
+            e1 = min(n, e0 + step)
+            out[e0:e1] = dequantize(raw[e0 // bs * bb: e1 // bs * bb], t.type, e1 - e0)
+        return torch.from_numpy(out.reshape(t.shape))
 
     def has(self, name: str) -> bool:
         return name in self.tensors

@@ -157,6 +157,19 @@ def test_container_round_trip(tmp_path):
             dequantize(np.zeros(GGML_TYPES[TYPE_ID[bad]][2], np.uint8), TYPE_ID[bad], 256)
 
 
+def test_tensor_slices_cover_block_boundaries(tmp_path, monkeypatch):
+    """GGUFFile.tensor dequantises in slices of whole blocks: the slices join exactly."""
+    import cain_amd.models.gguf as G
+
+    a = np.random.default_rng(3).normal(0, 1, (40, 512)).astype(np.float32)
+    write_gguf(tmp_path / "s.gguf", {"general.architecture": "llama"}, {"k": (a, "Q4_0"), "f": (a, "F16")})
+    whole = GGUFFile(tmp_path / "s.gguf")
+    ref_k, ref_f = whole.tensor("k"), whole.tensor("f")
+    monkeypatch.setattr(G, "SLICE_ELEMS", 1000)  # not a multiple of the 32-element block or of a row
+    assert torch.equal(GGUFFile(tmp_path / "s.gguf").tensor("k"), ref_k)
+    assert torch.equal(GGUFFile(tmp_path / "s.gguf").tensor("f"), ref_f)
+
+
 def test_qk_permutation_matches_transformers():
     from transformers.modeling_gguf_pytorch_utils import LlamaTensorProcessor
 
