@@ -116,10 +116,15 @@ class OllamaClient:
             return False
 
     def generate(self, model: str, prompt: str, stream: bool = False, options: Optional[Dict] = None,
-                 on_chunk=None) -> GenerateResponse:
+                 on_chunk=None, system: Optional[str] = None, raw: bool = False) -> GenerateResponse:
+        """``POST /api/generate``; ``system`` / ``raw`` as Ollama's fields (raw: no prompt template)."""
         body: Dict[str, Any] = {"model": model, "prompt": prompt, "stream": stream}
         if options:
             body["options"] = options
+        if system is not None:
+            body["system"] = system
+        if raw:
+            body["raw"] = True
         return self._post_gen("/api/generate", body, stream, on_chunk)
 
     def chat(self, model: str, messages: List[Dict[str, str]], stream: bool = False,

@@ -446,7 +446,14 @@ def load_gguf_tokenizer(g: GGUFFile, cfg: Optional[ModelConfig] = None):
         return None
     from .tokenizer import HFTokenizer
 
-    return HFTokenizer.from_tokenizer(conv(fields).converted(), cfg.bos_id if cfg else None)
+    tok = HFTokenizer.from_tokenizer(conv(fields).converted(), cfg.bos_id if cfg else None)
+    tok.chat_template = md.get("tokenizer.chat_template") or None
+    toks = md["tokenizer.ggml.tokens"]
+    for key, field in (("bos_token", "bos_token_id"), ("eos_token", "eos_token_id")):
+        i = md.get(f"tokenizer.ggml.{field}")
+        if isinstance(i, int) and 0 <= i < len(toks):
+            tok.special_tokens[key] = toks[i]
+    return tok
 
 
 def load_gguf(path: Union[str, os.PathLike], name: Optional[str] = None, device="cpu", dtype=torch.bfloat16):

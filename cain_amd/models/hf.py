@@ -92,6 +92,14 @@ def _first(v, default: int) -> int:
     return int(v[0]) if isinstance(v, (list, tuple)) else int(v)
 
 
+def _last(v, default: int) -> int:
+    """The stop id of a list of end ids: the last (Llama 3.1 Instruct: [end_of_text, eom, eot] -> eot, the turn end
+    Ollama stops on; the engine keeps one stop id per request)."""
+    if v is None:
+        return default
+    return int(v[-1]) if isinstance(v, (list, tuple)) else int(v)
+
+
 def config_from_hf(hf: Union[Dict, PathLike], name: Optional[str] = None,
                    tensor_names: Optional[List[str]] = None) -> ModelConfig:
     """``ModelConfig`` of a transformers ``config.json`` (a dict, the file or its directory).  ``tensor_names`` (the
@@ -139,7 +147,7 @@ def config_from_hf(hf: Union[Dict, PathLike], name: Optional[str] = None,
         vocab=int(hf["vocab_size"]), act=act, tie_embeddings=tie, qkv_bias=qkv_bias, rope_theta=theta,
         rope_scaling=scaling, norm_eps=float(hf.get("rms_norm_eps", 1e-6)), norm_add_one=fam == "gemma",
         embed_scale=fam == "gemma", max_context=max_ctx, bos_id=_first(hf.get("bos_token_id"), 1),
-        eos_id=_first(hf.get("eos_token_id"), 2))
+        eos_id=_last(hf.get("eos_token_id"), 2))
 
 
 def _shards(path: Path) -> List[Path]:
@@ -247,7 +255,33 @@ def load_tokenizer(path: PathLike, cfg: Optional[ModelConfig] = None):
 
         return load_gguf_tokenizer(GGUFFile(path), cfg)
     f = Path(path) / "tokenizer.json"
-    return HFTokenizer(str(f), bos_id=cfg.bos_id if cfg else None) if f.exists() else None
+    if not f.exists():
+        return None
+    tok = HFTokenizer(str(f), bos_id=cfg.bos_id if cfg else None)
+    tok.chat_template, tok.special_tokens = _chat_template(Path(path))
+    return tok
+
+
+def _chat_template(path: Path) -> Tuple[Optional[str], Dict[str, str]]:
+    """(chat template, special-token strings) of a checkpoint directory: ``chat_template.jinja`` or
+    ``tokenizer_config.json``'s ``chat_template`` (a string, or named templates: "default" is used)."""
+    tc = path / "tokenizer_config.json"
+    conf = json.loads(tc.read_text()) if tc.exists() else {}
+    special = {}
+    for k in ("bos_token", "eos_token", "unk_token", "pad_token"):
+        v = conf.get(k)
+        if isinstance(v, dict):
+            v = v.get("content")
+        if isinstance(v, str):
+            special[k] = v
+    tmpl = conf.get("chat_template")
+    if isinstance(tmpl, list):
+        named = {t.get("name"): t.get("template") for t in tmpl if isinstance(t, dict)}
+        tmpl = named.get("default") or next(iter(named.values()), None)
+    jf = path / "chat_template.jinja"
+    if jf.exists():
+        tmpl = jf.read_text()
+    return (tmpl if isinstance(tmpl, str) and tmpl else None), special
 
 
 def load_pretrained(path: PathLike, name: Optional[str] = None, device="cpu",

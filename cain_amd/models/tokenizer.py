@@ -19,7 +19,7 @@ from __future__ import annotations
 import hashlib
 import math
 import re
-from typing import List, Optional
+from typing import Dict, List, Optional
 
 _SYL_C = "bdfghklmnprstvz"
 _SYL_V = "aeiou"
@@ -86,19 +86,50 @@ class HFTokenizer:
     """A checkpoint's ``tokenizer.json`` (``tokenizers``, Rust).  ``add_bos`` maps onto the file's own special-token
     template, as transformers does: Llama 3 and Gemma prepend their BOS there, Qwen2 adds none."""
 
+    # the model's chat template (jinja, from tokenizer_config.json / chat_template.jinja / GGUF metadata) and the
+    # special-token strings it refers to; None: prompts are used as given
+    chat_template: Optional[str] = None
+    special_tokens: Dict[str, str] = {}
+
     def __init__(self, path: str, bos_id: Optional[int] = None):
         from tokenizers import Tokenizer
 
         self.tok = Tokenizer.from_file(path)
         self.vocab = self.tok.get_vocab_size()
         self.bos_id = bos_id
+        self.special_tokens = {}
 
     @classmethod
     def from_tokenizer(cls, tok, bos_id: Optional[int] = None) -> "HFTokenizer":
         """Around an in-memory ``tokenizers.Tokenizer`` (a GGUF vocabulary, models/gguf.py)."""
         obj = cls.__new__(cls)
-        obj.tok, obj.vocab, obj.bos_id = tok, tok.get_vocab_size(), bos_id
+        obj.tok, obj.vocab, obj.bos_id, obj.special_tokens = tok, tok.get_vocab_size(), bos_id, {}
         return obj
+
+    def render_chat(self, messages: List[Dict[str, str]], add_generation_prompt: bool = True) -> str:
+        """``messages`` through the model's chat template, as Ollama does for ``/api/generate`` (one user message,
+        unless ``raw``) and ``/api/chat``: a sandboxed jinja environment with the helpers transformers provides
+        (``raise_exception``, ``strftime_now``, ``tojson``), so templates written for transformers render the same
+        (tests/test_hf_checkpoint.py compares with ``apply_chat_template``)."""
+        import datetime
+        import json
+
+        from jinja2.sandbox import ImmutableSandboxedEnvironment
+
+        if not self.chat_template:
+            raise ValueError("this tokenizer has no chat template")
+
+        def raise_exception(msg):
+            raise ValueError(msg)
+
+        env = ImmutableSandboxedEnvironment(trim_blocks=True, lstrip_blocks=True)
+        env.filters["tojson"] = lambda x, indent=None, ensure_ascii=False: json.dumps(x, indent=indent,
+                                                                                      ensure_ascii=ensure_ascii)
+        env.globals["raise_exception"] = raise_exception
+        env.globals["strftime_now"] = lambda fmt: datetime.datetime.now().strftime(fmt)
+        return env.from_string(self.chat_template).render(messages=messages,
+                                                          add_generation_prompt=add_generation_prompt,
+                                                          **self.special_tokens)
 
     def encode(self, text: str, add_bos: bool = True) -> List[int]:
         return self.tok.encode(text, add_special_tokens=add_bos).ids

@@ -88,6 +88,15 @@ class Backend:
     def run(self, model: str, jobs: List[Job]) -> None:
         raise NotImplementedError
 
+    def prompt_for(self, model: str, body: Dict[str, Any], chat: bool) -> Any:
+        """The decoder input of a request: Ollama's prompt handling.  A model without a chat template (every
+        random-init tag) gets the text as given (a chat's turns as "role: content" lines); ``EngineBackend`` renders
+        a checkpoint's template."""
+        if chat:
+            return "\n".join(f"{m.get('role', 'user')}: {m.get('content', '')}" for m in body.get("messages") or [])
+        prompt = body.get("prompt", "")
+        return f"{body['system']}\n{prompt}" if body.get("system") else prompt
+
     def max_batch(self, model: str) -> int:
         return 1
 
@@ -162,9 +171,22 @@ class EngineBackend(Backend):
                 self.engines[model] = eng
             return eng
 
+    def prompt_for(self, model: str, body: Dict[str, Any], chat: bool) -> Any:
+        """As Ollama: a model with a chat template (a checkpoint's) gets ``/api/generate``'s prompt as one user turn
+        (after ``system``) and ``/api/chat``'s messages through the template, with the generation prompt; ``raw``
+        skips it.  The rendered text is tokenized without a second BOS (the template writes its own)."""
+        tok = getattr(self.engine(model), "tokenizer", None) if model in self._models else None
+        if tok is None or not getattr(tok, "chat_template", None) or body.get("raw"):
+            return super().prompt_for(model, body, chat)
+        if chat:
+            msgs = [{"role": m.get("role", "user"), "content": m.get("content", "")} for m in body.get("messages") or []]
+        else:
+            msgs = ([{"role": "system", "content": body["system"]}] if body.get("system") else []) + \
+                   [{"role": "user", "content": body.get("prompt", "")}]
+        return tok.encode(tok.render_chat(msgs), add_bos=False)
+
     def model_info(self, model: str) -> Dict[str, Any]:
         from ..models import get_config
-
         from ..models.hf import checkpoint_for
 
         cfg = get_config(model)
@@ -493,14 +515,17 @@ class OllamaHandler(BaseHTTPRequestHandler):
             return self._send_json(400, {"error": "model is required"})
         if chat:
             msgs = body.get("messages") or []
-            prompt = "\n".join(f"{m.get('role', 'user')}: {m.get('content', '')}" for m in msgs)
+            text = msgs[-1].get("content", "") if msgs else ""
         else:
-            prompt = body.get("prompt", "")
-            if body.get("system"):
-                prompt = f"{body['system']}\n{prompt}"
+            text = body.get("prompt", "")
+        try:
+            prompt = self.scheduler.backend.prompt_for(model, body, chat)
+        except KeyError as exc:
+            return self._send_json(404, {"error": str(exc).strip("'\"")})
         opts = dict(body.get("options") or {})
         n = opts.get("num_predict")
-        num_predict = int(n) if n is not None and int(n) > 0 else default_num_predict(prompt)
+        # the length policy reads the user's words ("In N words ..."), not the template around them
+        num_predict = int(n) if n is not None and int(n) > 0 else default_num_predict(text)
         stream = body.get("stream", True)
         created = _now()
         chunks: "queue.Queue[str]" = queue.Queue()

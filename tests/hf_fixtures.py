@@ -65,16 +65,30 @@ def make_checkpoint(family: str, path: Path, n_layers: int = 2, vocab: int = 102
     return model
 
 
-def write_tokenizer(path: Path, vocab: int = 1024, bos_token: str = "<s>") -> None:
-    """A word-level ``tokenizer.json`` whose template prepends ``bos_token`` (as Llama 3's and Gemma's do)."""
+CHAT_TOKENS = ["<|system|>", "<|user|>", "<|assistant|>"]
+# a llama-3-like template: BOS, one marker per turn, the assistant marker as the generation prompt
+CHAT_TEMPLATE = ("{{ bos_token }}{% for m in messages %}{{ '<|' + m['role'] + '|>' }} {{ m['content'] }} {% endfor %}"
+                 "{% if add_generation_prompt %}<|assistant|>{% endif %}")
+
+
+def write_tokenizer(path: Path, vocab: int = 1024, bos_token: str = "<s>", chat: bool = False) -> None:
+    """A word-level ``tokenizer.json`` whose template prepends ``bos_token`` (as Llama 3's and Gemma's do); with
+    ``chat`` also turn-marker tokens and a ``tokenizer_config.json`` carrying ``CHAT_TEMPLATE``."""
+    import json
+
     from tokenizers import Tokenizer, models, pre_tokenizers, processors
 
-    words = ["<unk>", bos_token, "</s>"] + [f"w{i}" for i in range(vocab - 3)]
+    special = [bos_token, "</s>"] + (CHAT_TOKENS if chat else [])
+    words = ["<unk>", bos_token, "</s>"] + special[2:]
+    words += [f"w{i}" for i in range(vocab - len(words))]
     tok = Tokenizer(models.WordLevel({w: i for i, w in enumerate(words)}, unk_token="<unk>"))
     tok.pre_tokenizer = pre_tokenizers.WhitespaceSplit()
     tok.post_processor = processors.TemplateProcessing(single=f"{bos_token} $A", special_tokens=[(bos_token, 1)])
-    tok.add_special_tokens([bos_token, "</s>"])
+    tok.add_special_tokens(special)
     tok.save(str(path / "tokenizer.json"))
+    if chat:
+        (path / "tokenizer_config.json").write_text(json.dumps({"bos_token": bos_token, "eos_token": "</s>",
+                                                                "chat_template": CHAT_TEMPLATE}))
 
 
 def hf_logits(model, tokens: torch.Tensor, positions: torch.Tensor) -> torch.Tensor:

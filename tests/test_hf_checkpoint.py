@@ -230,3 +230,41 @@ def test_server_serves_a_checkpoint(tmp_path, monkeypatch):
                               pad_token_id=0)[0, len(ids):].tolist()
     assert r.eval_count == 5
     assert r.text == be.engine("gemma-real:2b").tokenizer.decode(want)
+
+
+def test_chat_template_renders_like_transformers_and_the_server_applies_it(tmp_path, monkeypatch):
+    """Ollama wraps /api/generate prompts in the model's template (unless raw) and /api/chat messages always: the
+    checkpoint's tokenizer_config.json template renders as transformers' apply_chat_template does, and the server
+    decodes the templated ids (greedy tokens = transformers' generate on them)."""
+    from hf_fixtures import CHAT_TEMPLATE
+    from transformers import PreTrainedTokenizerFast
+
+    from cain_amd.client import OllamaClient
+    from cain_amd.serve import EngineBackend, ServerThread
+
+    model = make_checkpoint("llama", tmp_path / "ck", scale=4.0)
+    write_tokenizer(tmp_path / "ck", chat=True)
+    _, _, tok = load_pretrained(tmp_path / "ck")
+    assert tok.chat_template == CHAT_TEMPLATE
+    msgs = [{"role": "system", "content": "w7 w8"}, {"role": "user", "content": "w3 w4 w5"}]
+    ref = PreTrainedTokenizerFast(tokenizer_file=str(tmp_path / "ck" / "tokenizer.json"), bos_token="<s>",
+                                  eos_token="</s>", chat_template=CHAT_TEMPLATE)
+    assert tok.render_chat(msgs) == ref.apply_chat_template(msgs, tokenize=False, add_generation_prompt=True)
+    ids = tok.encode(tok.render_chat(msgs), add_bos=False)
+    assert ids == ref.apply_chat_template(msgs, tokenize=True, add_generation_prompt=True, return_dict=False)
+    assert ids[0] == 1 and ids.count(1) == 1  # one BOS: the template's
+
+    monkeypatch.setenv("CAIN_CHECKPOINTS", f"llama-chat:tiny={tmp_path / 'ck'}")
+    be = EngineBackend(["llama-chat:tiny"], device="cpu", max_batch=2, max_context=64)
+    with ServerThread(be) as s:
+        c = OllamaClient(s.url)
+        r = c.generate("llama-chat:tiny", "w3 w4 w5", options={"temperature": 0, "num_predict": 4}, system="w7 w8")
+        raw = c.generate("llama-chat:tiny", "w3 w4 w5", options={"temperature": 0, "num_predict": 4}, raw=True)
+        chat = c.chat("llama-chat:tiny", msgs, options={"temperature": 0, "num_predict": 4})
+    assert r.prompt_eval_count == len(ids) and chat.prompt_eval_count == len(ids)
+    assert chat.text == r.text
+    with torch.no_grad():
+        want = model.generate(torch.tensor([ids]), max_new_tokens=4, do_sample=False, eos_token_id=None,
+                              pad_token_id=0)[0, len(ids):].tolist()
+    assert r.text == tok.decode(want)
+    assert raw.prompt_eval_count == len(tok.encode("w3 w4 w5"))  # raw: the prompt as given, BOS from the file
