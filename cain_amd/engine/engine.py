@@ -99,7 +99,16 @@ def _row_options(opts: Optional[Dict], cfg: ModelConfig, index: int, base_seed: 
                 repeat_penalty=float(o["repeat_penalty"]), top_k=int(o["top_k"]),
                 repeat_last_n=int(o["repeat_last_n"]),
                 eos_id=int(opts.get("eos_id", cfg.eos_id)) if opts and "eos_id" in opts else int(cfg.eos_id),
+                # further stop ids: the caller's, else the model's unless the caller set eos_id (forced lengths:
+                # eos_id -1 disables every stop)
+                stop=tuple(int(x) for x in (opts["stop_ids"] if opts and "stop_ids" in opts else
+                                            () if opts and "eos_id" in opts else cfg.stop_ids))[:3],
                 seed=int(seed) & 0xFFFFFFFFFFFFFFFF)
+
+
+def _stopped(toks: List[int], o: Dict) -> bool:
+    """A generation that ended on one of its row's stop ids (done_reason "stop")."""
+    return bool(toks) and ((o["eos_id"] >= 0 and toks[-1] == o["eos_id"]) or toks[-1] in o.get("stop", ()))
 
 
 # ============================================================== ctypes structs
@@ -468,8 +477,7 @@ class DecodeEngine:
         out = []
         for i in range(B):
             toks = gen[i]
-            eos = row_opts[i]["eos_id"]
-            reason = "stop" if (eos >= 0 and toks and toks[-1] == eos) else "length"
+            reason = "stop" if _stopped(toks, row_opts[i]) else "length"
             out.append(GenResult(self.cfg.name, ids[i], toks, self.tokenizer.decode(toks), reason,
                                  load_duration_ns=load, prompt_eval_duration_ns=t_pref,
                                  eval_duration_ns=int(t_dec * len(toks) / max(1, steps)),
@@ -493,7 +501,7 @@ class DecodeEngine:
             r["n_gen"][:B].zero_()
             r["done"][:B].zero_()
             r["max_new"][:B].copy_(torch.tensor(nps, dtype=torch.int32))
-            self.sample_params[: 32 * B].copy_(ops.sample_params_tensor(row_opts, "cpu").to(dev))
+            self.sample_params[: ops.SAMPLE_BYTES * B].copy_(ops.sample_params_tensor(row_opts, "cpu").to(dev))
             self.stream.synchronize()
             t1 = time.perf_counter_ns()
             steps = max(nps)
@@ -522,7 +530,7 @@ class DecodeEngine:
             t_first = time.perf_counter_ns()
             done_steps = 1
             emitted = [0] * B
-            watch = on_tokens is not None or any(o["eos_id"] >= 0 for o in row_opts)
+            watch = on_tokens is not None or any(o["eos_id"] >= 0 or o["stop"] for o in row_opts)
             chunk = self.steps_per_graph * max(1, int(check_every))
 
             def poll() -> bool:
@@ -609,7 +617,7 @@ class DecodeEngine:
                 nxt = sample_host(logits, out, o, rng)
                 out.append(nxt)
                 step = torch.tensor([[nxt]], device=self.device)
-                if o["eos_id"] >= 0 and nxt == o["eos_id"]:
+                if _stopped(out, o):
                     break
             gens.append(out)
         t1 = time.perf_counter_ns()
@@ -693,7 +701,7 @@ class ContinuousBatch:
             r["n_gen"][sl].zero_()
             r["done"][sl].zero_()
             r["max_new"][sl].copy_(torch.tensor(nps, dtype=torch.int32))
-            eng.sample_params[32 * self.n: 32 * (self.n + k)].copy_(ops.sample_params_tensor(row_opts, "cpu").to(eng.device))
+            eng.sample_params[ops.SAMPLE_BYTES * self.n: ops.SAMPLE_BYTES * (self.n + k)].copy_(ops.sample_params_tensor(row_opts, "cpu").to(eng.device))
         self.n += k
         self.row_slot += slots
         self.emitted += [0] * k
@@ -767,7 +775,9 @@ class ContinuousBatch:
                 h64 = r["hist"].view(-1, 64)
                 h64[dst] = h64[src]
                 eng.gen[dst] = eng.gen[src]
-                sp = eng.sample_params.view(-1, 32)
+                from .. import ops
+
+                sp = eng.sample_params.view(-1, ops.SAMPLE_BYTES)
                 sp[dst] = sp[src]
             for j, h in moves.items():
                 self.row_slot[h] = self.row_slot[j]

@@ -50,6 +50,9 @@ class ModelConfig:
     # per-frequency divisors of the inverse frequencies (GGUF's rope_freqs tensor: llama.cpp bakes Llama 3.1's
     # scaling into it); applied instead of rope_scaling when set
     rope_freq_factors: Optional[Tuple[float, ...]] = None
+    # further stop ids beside eos_id (at most 3 reach the sampler): a checkpoint's other end ids and its chat
+    # template's turn-end tokens (hf.py / gguf.py), as Ollama stops on its templates' stop strings
+    stop_ids: Tuple[int, ...] = ()
 
     @property
     def group(self) -> int:

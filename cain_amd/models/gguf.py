@@ -375,7 +375,7 @@ def config_from_gguf(g: GGUFFile, name: Optional[str] = None) -> ModelConfig:
     if window and int(window) < ctx:
         ctx = int(window)
     gemma = arch == "gemma"
-    return ModelConfig(
+    cfg = ModelConfig(
         name=name or md.get("general.name", arch), display_name=md.get("general.name", name or arch),
         n_layers=int(k("block_count")), d_model=d, n_heads=n_heads, n_kv_heads=n_kv, head_dim=head_dim,
         ffn=int(k("feed_forward_length")), vocab=vocab, act="gelu_tanh" if gemma else "silu",
@@ -384,6 +384,9 @@ def config_from_gguf(g: GGUFFile, name: Optional[str] = None) -> ModelConfig:
         norm_add_one=gemma, embed_scale=gemma, max_context=ctx,
         bos_id=int(md.get("tokenizer.ggml.bos_token_id", 1)), eos_id=int(md.get("tokenizer.ggml.eos_token_id", 2)),
         rope_freq_factors=factors)
+    from .hf import with_stop_ids
+
+    return with_stop_ids(cfg, gguf_stop_ids(g))
 
 
 def load_gguf_weights(g: GGUFFile, cfg: ModelConfig, device="cpu", dtype=torch.bfloat16) -> ModelWeights:
@@ -461,6 +464,18 @@ def load_gguf(path: Union[str, os.PathLike], name: Optional[str] = None, device=
     g = GGUFFile(path)
     cfg = config_from_gguf(g, name=name or Path(path).stem)
     return cfg, load_gguf_weights(g, cfg, device=device, dtype=dtype), load_gguf_tokenizer(g, cfg)
+
+
+def gguf_stop_ids(g: GGUFFile) -> List[int]:
+    """End ids beside EOS: llama.cpp's ``tokenizer.ggml.eot_token_id`` / ``eom_token_id`` and the vocabulary's
+    turn-end tokens (hf.TURN_END_TOKENS)."""
+    from .hf import TURN_END_TOKENS
+
+    md = g.metadata
+    ids = [int(md[k]) for k in ("tokenizer.ggml.eot_token_id", "tokenizer.ggml.eom_token_id") if k in md]
+    toks = md.get("tokenizer.ggml.tokens") or []
+    index = {t: i for i, t in enumerate(toks) if t in TURN_END_TOKENS}
+    return ids + [index[t] for t in TURN_END_TOKENS if t in index]
 
 
 def export_gguf(mw: ModelWeights, path: Union[str, os.PathLike], arch: str, tensor_type: str = "F16",

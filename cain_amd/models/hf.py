@@ -147,7 +147,37 @@ def config_from_hf(hf: Union[Dict, PathLike], name: Optional[str] = None,
         vocab=int(hf["vocab_size"]), act=act, tie_embeddings=tie, qkv_bias=qkv_bias, rope_theta=theta,
         rope_scaling=scaling, norm_eps=float(hf.get("rms_norm_eps", 1e-6)), norm_add_one=fam == "gemma",
         embed_scale=fam == "gemma", max_context=max_ctx, bos_id=_first(hf.get("bos_token_id"), 1),
-        eos_id=_last(hf.get("eos_token_id"), 2))
+        eos_id=_last(hf.get("eos_token_id"), 2), stop_ids=_other_ends(hf.get("eos_token_id")))
+
+
+def _other_ends(v) -> Tuple[int, ...]:
+    """The end ids of a list besides the one ``_last`` picks."""
+    return tuple(int(x) for x in v[:-1]) if isinstance(v, (list, tuple)) else ()
+
+
+# turn-end tokens of the families' chat templates, on which Ollama's templates stop
+TURN_END_TOKENS = ("<|eot_id|>", "<|eom_id|>", "<|end|>", "<end_of_turn>", "<|im_end|>", "<|endoftext|>", "</s>")
+
+
+def with_stop_ids(cfg: ModelConfig, extra_ids) -> ModelConfig:
+    """``cfg`` with ``extra_ids`` added to its stop ids (kept distinct from eos_id, order kept, first 3)."""
+    import dataclasses
+
+    ids = []
+    for i in list(cfg.stop_ids) + [int(x) for x in extra_ids]:
+        if i != cfg.eos_id and i >= 0 and i not in ids:
+            ids.append(i)
+    return dataclasses.replace(cfg, stop_ids=tuple(ids[:3]))
+
+
+def template_stop_ids(tok) -> List[int]:
+    """Ids of the turn-end tokens a tokenizer knows (``TURN_END_TOKENS``)."""
+    out = []
+    for t in TURN_END_TOKENS:
+        i = tok.tok.token_to_id(t) if tok is not None and hasattr(tok, "tok") else None
+        if i is not None:
+            out.append(int(i))
+    return out
 
 
 def _shards(path: Path) -> List[Path]:
@@ -292,9 +322,9 @@ def load_pretrained(path: PathLike, name: Optional[str] = None, device="cpu",
         from .gguf import load_gguf
 
         return load_gguf(p, name=name or p.stem, device=device, dtype=dtype)
-    t = _Tensors(p)
-    cfg = config_from_hf(_read_config(p), name=name or p.name, tensor_names=t.names())
-    return cfg, load_hf_weights(p, cfg, device=device, dtype=dtype), load_tokenizer(p, cfg)
+    cfg = checkpoint_config(p, name=name or p.name)
+    w = load_hf_weights(p, cfg, device=device, dtype=dtype)
+    return cfg, w, load_tokenizer(p, cfg)
 
 
 def is_gguf(path: PathLike) -> bool:
@@ -310,7 +340,12 @@ def checkpoint_config(path: PathLike, name: Optional[str] = None) -> ModelConfig
         from .gguf import GGUFFile, config_from_gguf
 
         return config_from_gguf(GGUFFile(p), name=name or p.stem)
-    return config_from_hf(p, name=name, tensor_names=_Tensors(p).names())
+    cfg = config_from_hf(p, name=name, tensor_names=_Tensors(p).names())
+    gc = p / "generation_config.json"  # the generation end ids (Llama 3.1 Instruct: end_of_text, eom, eot)
+    if gc.exists():
+        ends = json.loads(gc.read_text()).get("eos_token_id")
+        cfg = with_stop_ids(cfg, ends if isinstance(ends, list) else [ends] if ends is not None else [])
+    return with_stop_ids(cfg, template_stop_ids(load_tokenizer(p)))
 
 
 def registered_checkpoints() -> Dict[str, str]:

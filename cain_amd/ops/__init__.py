@@ -72,6 +72,9 @@ def load() -> ctypes.CDLL:
         # an older build loaded for an A/B run (CAIN_KERNELS_LIB) may lack newer entry points: their signatures
         # are skipped (a call to one then fails by name)
         lib = _Lenient(real) if os.environ.get("CAIN_KERNELS_LIB") else real
+        if not os.environ.get("CAIN_KERNELS_LIB") and int(real.cain_sample_params_size()) != SAMPLE_BYTES:
+            raise NativeOpsUnavailable(f"{LIB_PATH} packs {int(real.cain_sample_params_size())}-byte sampling "
+                                       f"options, this package {SAMPLE_BYTES}: rebuild (python -m cain_amd.build)")
         lib.cain_skinny_gemm_ex.argtypes = ([vp, vp, ci, ci, ci, ci, vp, ci, vp, ci, cf, vp, vp, vp, vp, vp, vp]
                                             + [ci] * 6 + [vp])
         lib.cain_gemm.argtypes = ([vp, vp, ci, ci, ci, ci, vp, ci, vp, ci, cf, vp, vp, vp, vp, vp, vp]
@@ -592,18 +595,25 @@ def set_attention_ring(variant: int) -> None:
 
 
 SAMPLE_DTYPE = [("temperature", "f4"), ("top_p", "f4"), ("repeat_penalty", "f4"), ("top_k", "i4"),
-                ("repeat_last_n", "i4"), ("eos_id", "i4"), ("seed", "u8")]
+                ("repeat_last_n", "i4"), ("eos_id", "i4"), ("stop", "i4", (3,)), ("seed", "u8")]
+SAMPLE_BYTES = 48  # sizeof(SampleParams), csrc/sample.hip (cain_sample_params_size)
 
 
 def sample_params_tensor(rows, device) -> torch.Tensor:
-    """Pack per-row sampling options (list of dicts) into the kernel's 32-byte struct array."""
+    """Pack per-row sampling options (list of dicts; ``stop``: up to 3 further stop ids, default none) into the
+    kernel's 48-byte struct array."""
     import numpy as np
 
     arr = np.zeros(len(rows), dtype=np.dtype(SAMPLE_DTYPE, align=True))
     for i, r in enumerate(rows):
-        for k, _ in SAMPLE_DTYPE:
-            arr[i][k] = r[k]
-    assert arr.dtype.itemsize == 32
+        for f in SAMPLE_DTYPE:
+            k = f[0]
+            if k == "stop":
+                st = [int(x) for x in r.get("stop", ())][:3]
+                arr[i][k] = st + [-1] * (3 - len(st))
+            else:
+                arr[i][k] = r[k]
+    assert arr.dtype.itemsize == SAMPLE_BYTES
     return torch.from_numpy(arr.view(np.uint8).copy()).to(device)
 
 

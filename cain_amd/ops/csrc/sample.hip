@@ -26,6 +26,7 @@ struct SampleParams {
   int top_k;
   int repeat_last_n;
   int eos_id;
+  int stop[3];  // further stop ids (a chat model's turn ends: <|eot_id|>, <|end|>, <end_of_turn>, ...); -1 unused
   uint64_t seed;
 };
 
@@ -110,7 +111,9 @@ __device__ void advance_row(int m, int choice, int ng, const SampleParams& P, in
   n_gen[m] = n1;
   tok[m] = choice;
   const int p1 = pos[m] + 1;
-  if ((P.eos_id >= 0 && choice == P.eos_id) || n1 >= max_new[m] || p1 >= T_max) {
+  const bool stop = (P.eos_id >= 0 && choice == P.eos_id) || (P.stop[0] >= 0 && choice == P.stop[0]) ||
+                    (P.stop[1] >= 0 && choice == P.stop[1]) || (P.stop[2] >= 0 && choice == P.stop[2]);
+  if (stop || n1 >= max_new[m] || p1 >= T_max) {
     done[m] = 1;
   } else {
     pos[m] = p1;

@@ -296,8 +296,7 @@ class EngineBackend(Backend):
         for r in done_rows:
             st, j = live[r], live[r]["job"]
             toks = cb.tokens(r)
-            eos = cb.options[r]["eos_id"]
-            reason = "stop" if (eos >= 0 and toks and toks[-1] == eos) else "length"
+            reason = "stop" if _stopped(toks, cb.options[r]) else "length"
             j.result = GenResult(model, list(cb.prompt_tokens[r]), toks, tok.decode(toks), reason,
                                  load_duration_ns=0, prompt_eval_duration_ns=int(st["t_pre"] - st["t0"]),
                                  eval_duration_ns=int(now - st["t_pre"]),

@@ -268,3 +268,31 @@ def test_chat_template_renders_like_transformers_and_the_server_applies_it(tmp_p
                               pad_token_id=0)[0, len(ids):].tolist()
     assert r.text == tok.decode(want)
     assert raw.prompt_eval_count == len(tok.encode("w3 w4 w5"))  # raw: the prompt as given, BOS from the file
+
+
+def test_stop_ids_from_generation_config_and_template_tokens(tmp_path, monkeypatch):
+    """A checkpoint's other end ids (generation_config.json) and its tokenizer's turn-end tokens become stop ids;
+    a generation ends on them ("stop"), unless the caller forces the length (eos_id -1, as the study and bench do)."""
+    import json
+
+    from cain_amd.models.hf import checkpoint_config
+
+    make_checkpoint("mistral", tmp_path, scale=4.0)
+    write_tokenizer(tmp_path, chat=True)
+    tj = json.loads((tmp_path / "tokenizer.json").read_text())
+    tj["added_tokens"].append({"id": 40, "content": "<|eot_id|>", "single_word": False, "lstrip": False,
+                               "rstrip": False, "normalized": False, "special": True})
+    tj["model"]["vocab"] = {("<|eot_id|>" if i == 40 else w): i for w, i in tj["model"]["vocab"].items()}
+    (tmp_path / "tokenizer.json").write_text(json.dumps(tj))
+    (tmp_path / "generation_config.json").write_text(json.dumps({"eos_token_id": [2, 33]}))
+    cfg = checkpoint_config(tmp_path, name="m")
+    assert cfg.eos_id == 2 and cfg.stop_ids == (33, 40)
+    eng = DecodeEngine.from_pretrained(str(tmp_path), device="cpu", max_batch=1, max_context=64)
+    assert eng.cfg.stop_ids == (33, 40)
+    free = eng.generate(["w5 w6"], 8, [dict(temperature=0.0, eos_id=-1)])[0]
+    assert len(free.tokens) == 8 and free.done_reason == "length"
+    k = 3
+    stop_at = free.tokens[k]
+    first = free.tokens.index(stop_at)
+    got = eng.generate(["w5 w6"], 8, [dict(temperature=0.0, eos_id=-1, stop_ids=[stop_at])])[0]
+    assert got.tokens == free.tokens[:first + 1] and got.done_reason == "stop"

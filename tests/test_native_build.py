@@ -20,7 +20,7 @@ def test_struct_layouts_match_native():
     assert lib.cain_plan_desc_size() == ctypes.sizeof(_CainPlanDesc)
     assert lib.cain_rows_size() == ctypes.sizeof(_CainRows)
     assert lib.cain_layer_size() == ctypes.sizeof(_CainLayer)
-    assert lib.cain_sample_params_size() == 32
+    assert lib.cain_sample_params_size() == ops.SAMPLE_BYTES == 48
 
 
 def test_energy_library_loads_without_gpu():

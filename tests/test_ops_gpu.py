@@ -512,3 +512,27 @@ def test_split_sampler_draws_the_same_tokens(V, M):
             assert torch.equal(out[0][k], out[1][k]), (rep, k)
     # greedy rows are the argmax (lowest index on ties)
     assert int(out[1]["tok"][0]) == int(torch.argmax(logits[0]).item()) or rows[0]["repeat_penalty"] != 1.0
+
+
+@pytest.mark.parametrize("mode", ["one", "split", "cm"])
+def test_sample_stop_ids_end_rows(mode):
+    """A sampled token equal to any of a row's stop ids (beside eos_id) ends the row (done = 1, position kept), in
+    every sampler kernel; a row whose stop ids miss the token goes on."""
+    V, M = 32064, 4
+    logits = torch.randn(M, V, device=DEV)
+    win = [101, 202, 303, 404]
+    for i, w in enumerate(win):
+        logits[i, w] = 50.0  # greedy picks it
+    rows = [dict(temperature=0.0, top_p=1.0, repeat_penalty=1.0, top_k=40, repeat_last_n=0, eos_id=-1, seed=1,
+                 stop=st) for st in ([101], [7, 202], [1, 2, 303], [1, 2, 3])]
+    z = lambda: torch.zeros(M, device=DEV, dtype=torch.int32)  # noqa: E731
+    tok, n_gen, done = z(), z(), z()
+    pos = torch.full((M,), 10, device=DEV, dtype=torch.int32)
+    cmax = logits.view(M, V // 16, 16).amax(-1).contiguous() if mode == "cm" else None
+    ops.sample(logits.clone(), tok, pos, torch.zeros(M, 8, device=DEV, dtype=torch.int32), n_gen,
+               torch.full((M,), 8, device=DEV, dtype=torch.int32), done, torch.zeros(M * 64, device=DEV,
+               dtype=torch.int32), torch.arange(M, device=DEV, dtype=torch.int32), ops.sample_params_tensor(rows, DEV),
+               2048, split=(mode == "split"), cmax=cmax)
+    assert tok.cpu().tolist() == win
+    assert done.cpu().tolist() == [1, 1, 1, 0]
+    assert pos.cpu().tolist() == [10, 10, 10, 11]
