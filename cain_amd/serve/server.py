@@ -261,7 +261,7 @@ class EngineBackend(Backend):
         finish the rows that are done.  Timing matches the static path (engine._generate_hip): the newly admitted
         rows' first token is decoded by a one-step graph and synchronised, so ``t_first`` is exact;
         ``eval_duration`` runs from the end of admission (first token included), ``ttft`` from its start."""
-        from ..engine.engine import GenResult
+        from ..engine.engine import GenResult, _stopped
 
         ok: List[Job] = []
         ids: List[List[int]] = []
