@@ -72,7 +72,7 @@ def load() -> ctypes.CDLL:
         # an older build loaded for an A/B run (CAIN_KERNELS_LIB) may lack newer entry points: their signatures
         # are skipped (a call to one then fails by name)
         lib = _Lenient(real) if os.environ.get("CAIN_KERNELS_LIB") else real
-        if not os.environ.get("CAIN_KERNELS_LIB") and int(real.cain_sample_params_size()) != SAMPLE_BYTES:
+        if int(real.cain_sample_params_size()) != SAMPLE_BYTES:  # also an A/B build from an older source
             raise NativeOpsUnavailable(f"{LIB_PATH} packs {int(real.cain_sample_params_size())}-byte sampling "
                                        f"options, this package {SAMPLE_BYTES}: rebuild (python -m cain_amd.build)")
         lib.cain_skinny_gemm_ex.argtypes = ([vp, vp, ci, ci, ci, ci, vp, ci, vp, ci, cf, vp, vp, vp, vp, vp, vp]
