@@ -318,6 +318,8 @@ class DecodeEngine:
         shapes = [(cfg.qkv_dim, cfg.d_model), (cfg.d_model, cfg.q_dim), (2 * cfg.ffn, cfg.d_model),
                   (cfg.d_model, cfg.ffn), (cfg.vocab, cfg.d_model)]
         ws = max([ops.gemm_ws_bytes(n, k, m) for n, k in shapes for m in range(1, R + 1)] + [0])
+        if self.weight_dtype == "fp4":  # split-K tickets + partials of the few-row MXFP4 stream kernel
+            ws = max([ws] + [int(self.lib.cain_gemm_w4_ws_bytes(n, k, 1)) for n, k in shapes])
         if w8a8 or w4a8:
             ws = max([ws] + [int(self.lib.cain_w8a8_ws_bytes(n, k, m)) for n, k in shapes for m in range(17, R + 1)])
             kmax = max(cfg.d_model, cfg.q_dim, cfg.ffn)

@@ -83,6 +83,12 @@ def load() -> ctypes.CDLL:
                                      + [ci] * 5 + [vp])
         lib.cain_gemm_w4.argtypes = ([vp, vp, vp, ci, ci, ci, ci, vp, ci, vp, ci, cf, vp, vp, vp, vp, vp, vp]
                                      + [ci] * 5 + [vp])
+        lib.cain_gemm_w4_ex.argtypes = ([vp, vp, vp, ci, ci, ci, ci, vp, ci, vp, ci, cf, vp, vp, vp, vp, vp, vp]
+                                        + [ci] * 4 + [vp, ctypes.c_longlong, ci, vp])
+        lib.cain_gemm_w4_ws_bytes.restype = ctypes.c_longlong
+        lib.cain_gemm_w4_ws_bytes.argtypes = [ci, ci, ci]
+        lib.cain_gemm_w4_split.argtypes = [ci, ci, ci, ci, ctypes.c_longlong]
+        lib.cain_gemm_w4_set_split.argtypes = [ci]
         lib.cain_gemm_w4_set_variant.argtypes = [ci]
         lib.cain_gemm_w4_variant.argtypes = [ci, ci, ci, ci]
         lib.cain_gemm_w4_set_occupancy.argtypes = [ci]
@@ -337,12 +343,36 @@ def gemm_w4(wq: torch.Tensor, wsc: torch.Tensor, x: torch.Tensor, n: int, epi: i
     T_max = r["kc"].shape[-2] if rope else 0
     if rope and is_fp8_cache(r["kc"]):
         epi |= EPI_KV_FP8
-    rc = lib.cain_gemm_w4(_p(wq), _p(wsc), _p(x), x.stride(0), K, n, M, _p(out), out.stride(0), _p(bias),
-                          int(bool(norm)), eps, _p(r.get("slot")), _p(r.get("pos")), _p(r.get("cos_t")),
-                          _p(r.get("sin_t")), _p(r.get("kc")), _p(r.get("vtc")), r.get("H", 0), r.get("Hkv", 0),
-                          r.get("hd", 0), T_max, epi, _stream())
+    nb = int(lib.cain_gemm_w4_ws_bytes(n, K, M))
+    ws = _w4_ws(x.device, nb)
+    rc = lib.cain_gemm_w4_ex(_p(wq), _p(wsc), _p(x), x.stride(0), K, n, M, _p(out), out.stride(0), _p(bias),
+                             int(bool(norm)), eps, _p(r.get("slot")), _p(r.get("pos")), _p(r.get("cos_t")),
+                             _p(r.get("sin_t")), _p(r.get("kc")), _p(r.get("vtc")), r.get("H", 0), r.get("Hkv", 0),
+                             r.get("hd", 0), T_max, _p(ws), nb, epi, _stream())
     _check(rc, "gemm_w4")
     return out
+
+
+_W4_WS: dict = {}
+
+
+def _w4_ws(device, nbytes: int) -> torch.Tensor:
+    """Zeroed split-K workspace of the W4 GEMMs (its tickets are left zero by every launch), grown as needed."""
+    t = _W4_WS.get(device)
+    if t is None or t.numel() < nbytes:
+        t = _W4_WS[device] = torch.zeros(max(nbytes, 1 << 16), device=device, dtype=torch.uint8)
+    return t
+
+
+def set_w4_split(ks: int) -> None:
+    """Split-K of the few-row MXFP4 stream kernel (csrc/gemm_w4.hip w4_split): 0 = the rule (narrow outputs over
+    fewer tiles than CUs get up to 4 k ranges), 1 = off, k > 1 = k ranges wherever the shape allows."""
+    load().cain_gemm_w4_set_split(int(ks))
+
+
+def w4_split(n: int, k: int, m: int, epi: int, ws_bytes: int = 1 << 30) -> int:
+    """k ranges the W4 GEMM of this shape runs with (given a workspace of ``ws_bytes``)."""
+    return int(load().cain_gemm_w4_split(n, k, m, epi, ws_bytes))
 
 
 def set_w4_variant(v: int) -> None:

@@ -74,10 +74,23 @@ __device__ __forceinline__ void w4_pair_tile(int j, int msp, int ntg, int& t, in
 template <int WAVES>
 constexpr int w4_xl_bytes() { return WAVES == 8 ? 49152 : 28672; }
 
+// Split-K of the stream kernel for narrow outputs (fewer 16-row tiles than CUs: the small models' O and down
+// projections, 96-128 tiles, left half the chip idle): pair j = (tile j / ks, k range j % ks).  Wave 0 of each pair
+// publishes its 16x16 partial write-through (sc1) and, after its stores drain, takes the tile's ticket with one
+// agent-scope atomic add; the LAST arriving pair sums the ks partials with sc1 loads, applies the RMSNorm factor and
+// runs the tile's epilogue, and resets the ticket (cdna_hip_programming.md 'In-launch split-K reduction'; the
+// attention kernel's merge).  No workgroup ever waits for another.
+struct W4Split {
+  int ks;          // k ranges per tile (1: no split)
+  float* part;     // [tiles * ks][64 lanes][4] fp32 partial blocks
+  unsigned* ctr;   // [tiles] tickets, zero at rest
+};
+constexpr long long W4_CTR_BYTES = 16 * 1024;  // the workspace's ticket region (4,096 tiles), partials after it
+
 // 4 waves per SIMD (<= 128 VGPRs): the grid below assumes 16 resident waves per CU
 template <int WAVES, int U, int EPI, bool NORM>
 __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(4, 4))) void w4_stream_kernel(
-    const GemmArgs a, const uint8_t* __restrict__ wsc, int npairs) {
+    const GemmArgs a, const uint8_t* __restrict__ wsc, int npairs, const W4Split sp) {
   constexpr int XLB = w4_xl_bytes<WAVES>();
   constexpr int XCH = XLB / (WAVES * 64 * 16);  // 16-byte activation chunks staged per thread
   __shared__ __attribute__((aligned(16))) char w4_xs[XLB];
@@ -85,8 +98,10 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(4, 4
   __shared__ float row_ss[16];  // NORM: the sum of squares of each activation row
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
-  const int KQ = a.K >> 7;                    // 128-wide k quads per tile
-  const int qmax = (KQ + WAVES - 1) / WAVES;  // items per tile (every wave walks the same sequence length)
+  const int KS = sp.ks;
+  const int KQT = a.K >> 7;                   // 128-wide k quads per tile
+  const int KQ = KQT / KS;                    // k quads per pair (the host keeps KQT % KS == 0)
+  const int qmax = (KQ + WAVES - 1) / WAVES;  // items per pair (every wave walks the same sequence length)
   const int G = gridDim.x;
   const int my_tiles = (npairs - (int)blockIdx.x + G - 1) / G;
   const int n_items = my_tiles * qmax;
@@ -117,7 +132,8 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(4, 4
     // hipcc then loses its counted waits and drains the ring (vmcnt(0)) at every item
     const bool in = ld_i < n_items;
     const int p = min(wave + (in ? ld_e : qmax - 1) * WAVES, KQ - 1);
-    const size_t off = ((size_t)(in ? ld_t : last_t) * KQ + p) * 64;
+    const int j = in ? ld_t : last_t, jt = j / KS;  // pair -> (tile, k range)
+    const size_t off = ((size_t)jt * KQT + (j - jt * KS) * KQ + p) * 64;
     q.w = __builtin_nontemporal_load(wbase + off);
     q.s = __builtin_nontemporal_load(sbase + off);
     ++ld_i;
@@ -133,7 +149,7 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(4, 4
   // 128-register budget of 4 waves per SIMD; 84-102 registers folded)
   constexpr bool FOLD = EPI == EPI_QKV_ROPE && WAVES == 8;
   EpiIn pre{};
-  if (wave == 0 && my_tiles > 0) pre = epi_load_at<EPI>(a, cp_t, lane & 15, lane);
+  if (wave == 0 && my_tiles > 0) pre = epi_load_at<EPI>(a, cp_t / KS, lane & 15, lane);
 #pragma unroll
   for (int i = 0; i < XCH; ++i) {
     const int c = (int)threadIdx.x + i * WAVES * 64;
@@ -184,7 +200,38 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(4, 4
     acc = f32x4{0.f, 0.f, 0.f, 0.f};
     w4_barrier();
     if (wave == 0) {
-      if (cp_n > 0) pre = epi_load_at<EPI>(a, cp_t, lane & 15, lane);  // later tiles (none for fp32 / act epis)
+      const int tile = cp_t / KS;
+      if (cp_n > 0) pre = epi_load_at<EPI>(a, tile, lane & 15, lane);  // later tiles (none for fp32 / act epis)
+      if (KS > 1) {
+        // split-K: publish this pair's partial, take the tile's ticket; the last arriver finishes the tile
+        f32x4 v = red[buf][0][lane];
+#pragma unroll
+        for (int w = 1; w < WAVES; ++w) v += red[buf][w][lane];
+        uint64_t* pp = reinterpret_cast<uint64_t*>(sp.part + ((size_t)cp_t * 64 + lane) * 4);
+        __hip_atomic_store(pp, __builtin_bit_cast(uint64_t, f32x2{v[0], v[1]}), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(pp + 1, __builtin_bit_cast(uint64_t, f32x2{v[2], v[3]}), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        unsigned t = 0;
+        if (lane == 0) t = __hip_atomic_fetch_add(sp.ctr + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        t = __shfl(t, 0, 64);
+        if (t == unsigned(KS - 1)) {
+          f32x4 sum = f32x4{0.f, 0.f, 0.f, 0.f};
+          for (int k = 0; k < KS; ++k) {  // every pair's partial, this one's included, in k order
+            const uint64_t* q = reinterpret_cast<const uint64_t*>(sp.part + (((size_t)tile * KS + k) * 64 + lane) * 4);
+            const f32x2 lo = __builtin_bit_cast(f32x2, __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+            const f32x2 hi = __builtin_bit_cast(f32x2, __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+            sum += f32x4{lo[0], lo[1], hi[0], hi[1]};
+          }
+          if constexpr (NORM) sum *= rms_inv(row_ss[min(lane & 15, a.M - 1)], a.K, a.eps);
+          if (lane == 0) sp.ctr[tile] = 0u;  // ready for the next launch (launch-ordered)
+          red[buf][0][lane] = sum;  // one wave: its LDS operations complete in order
+          epi_store<EPI>(a, tile, lane & 15, lane, pre, [&](int off) { return red[buf][0][lane + off]; });
+        }
+        buf ^= 1;
+        return;
+      }
       auto unit_sum = [&](int l) -> f32x4 {
         f32x4 v = red[buf][0][l];
 #pragma unroll
@@ -197,9 +244,9 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(4, 4
         // units (own and partner row) from there -- summing both units per lane held 2 x 8 partials in flight
         // and spilled.  One wave: its LDS operations complete in order, so the reads see the writes.
         red[buf][0][lane] = unit_sum(lane);
-        epi_store<EPI>(a, cp_t, lane & 15, lane, pre, [&](int off) { return red[buf][0][lane + off]; });
+        epi_store<EPI>(a, tile, lane & 15, lane, pre, [&](int off) { return red[buf][0][lane + off]; });
       } else {
-        epi_store<EPI>(a, cp_t, lane & 15, lane, pre, [&](int off) { return unit_sum(lane + off); });
+        epi_store<EPI>(a, tile, lane & 15, lane, pre, [&](int off) { return unit_sum(lane + off); });
       }
     }
     buf ^= 1;
@@ -208,13 +255,13 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(4, 4
   for (int i0 = 0; i0 < n_pad; i0 += R) {
 #pragma unroll
     for (int u = 0; u < R; ++u) {
-      const int p = wave + cp_e * WAVES;
+      const int p = wave + cp_e * WAVES;  // k quad within the pair's range
       const bool live = i0 + u < n_items;
       // item i0 + u + U goes into the spare slot (the one consumed by the previous item) BEFORE this item's math: a
       // ring of U + 1 slots walked in whole rounds keeps every slot index a constant (a register copy of an
       // in-flight load would force the compiler to drain the ring: vmcnt(0) at every round)
       load_next(ring[(u + U) % (U + 1)]);
-      if (live && p < KQ) step(ring[u], p);
+      if (live && p < KQ) step(ring[u], (cp_t - (cp_t / KS) * KS) * KQ + p);
       if (live && cp_e == qmax - 1) tile_end();
       if (++cp_e == qmax) cp_e = 0, ++cp_n, cp_t += G;
     }
@@ -349,11 +396,12 @@ static const int W4_NB[W4_N_VARS] = {1, 1, 1, 1, 2, 2};
 static bool w4_is_stream(int v) { return v <= W4S_4_4; }
 
 template <bool NORM, int EPI>
-static hipError_t w4_launch_var(int var, const GemmArgs& a, const uint8_t* wsc, int grid, int npairs, hipStream_t st) {
+static hipError_t w4_launch_var(int var, const GemmArgs& a, const uint8_t* wsc, int grid, int npairs,
+                                const W4Split& sp, hipStream_t st) {
   const dim3 g(grid), b8(512), b4(256);
   switch (var) {
-    case W4S_8_4: hipLaunchKernelGGL((w4_stream_kernel<8, 4, EPI, NORM>), g, b8, 0, st, a, wsc, npairs); break;
-    case W4S_4_4: hipLaunchKernelGGL((w4_stream_kernel<4, 4, EPI, NORM>), g, b4, 0, st, a, wsc, npairs); break;
+    case W4S_8_4: hipLaunchKernelGGL((w4_stream_kernel<8, 4, EPI, NORM>), g, b8, 0, st, a, wsc, npairs, sp); break;
+    case W4S_4_4: hipLaunchKernelGGL((w4_stream_kernel<4, 4, EPI, NORM>), g, b4, 0, st, a, wsc, npairs, sp); break;
     case W4T_8_2_1: hipLaunchKernelGGL((w4_tile_kernel<8, 2, 1, EPI, NORM>), g, b8, 0, st, a, wsc); break;
     case W4T_4_4_1: hipLaunchKernelGGL((w4_tile_kernel<4, 4, 1, EPI, NORM>), g, b4, 0, st, a, wsc); break;
     case W4T_8_2_2: hipLaunchKernelGGL((w4_tile_kernel<8, 2, 2, EPI, NORM>), g, b8, 0, st, a, wsc); break;
@@ -364,21 +412,23 @@ static hipError_t w4_launch_var(int var, const GemmArgs& a, const uint8_t* wsc, 
 
 template <bool NORM>
 static hipError_t w4_launch(int epi, int var, const GemmArgs& a, const uint8_t* wsc, int grid, int npairs,
-                            hipStream_t st) {
+                            const W4Split& sp, hipStream_t st) {
   switch (epi) {
-    case EPI_BF16: return w4_launch_var<NORM, EPI_BF16>(var, a, wsc, grid, npairs, st);
-    case EPI_RESID: return w4_launch_var<NORM, EPI_RESID>(var, a, wsc, grid, npairs, st);
-    case EPI_F32: return w4_launch_var<NORM, EPI_F32>(var, a, wsc, grid, npairs, st);
-    case EPI_SILU: return w4_launch_var<NORM, EPI_SILU>(var, a, wsc, grid, npairs, st);
-    case EPI_GELU: return w4_launch_var<NORM, EPI_GELU>(var, a, wsc, grid, npairs, st);
-    case EPI_QKV_ROPE: return w4_launch_var<NORM, EPI_QKV_ROPE>(var, a, wsc, grid, npairs, st);
+    case EPI_BF16: return w4_launch_var<NORM, EPI_BF16>(var, a, wsc, grid, npairs, sp, st);
+    case EPI_RESID: return w4_launch_var<NORM, EPI_RESID>(var, a, wsc, grid, npairs, sp, st);
+    case EPI_F32: return w4_launch_var<NORM, EPI_F32>(var, a, wsc, grid, npairs, sp, st);
+    case EPI_SILU: return w4_launch_var<NORM, EPI_SILU>(var, a, wsc, grid, npairs, sp, st);
+    case EPI_GELU: return w4_launch_var<NORM, EPI_GELU>(var, a, wsc, grid, npairs, sp, st);
+    case EPI_QKV_ROPE: return w4_launch_var<NORM, EPI_QKV_ROPE>(var, a, wsc, grid, npairs, sp, st);
     default: return hipErrorInvalidValue;
   }
 }
 
 // Tuning / test overrides (-1 / 0: the rules below): the kernel shape (W4Var) and the stream grid's workgroups per CU
-static int g_w4_var = -1, g_w4_wgs_per_cu = 0;
+static int g_w4_var = -1, g_w4_wgs_per_cu = 0, g_w4_split = 0;
 CAIN_API void cain_gemm_w4_set_variant(int v) { g_w4_var = v < W4_N_VARS ? v : -1; }
+// split-K of the stream kernel: 0 = the rule (w4_split), 1 = off, k > 1 = k ranges wherever the shape allows it
+CAIN_API void cain_gemm_w4_set_split(int ks) { g_w4_split = ks > 0 ? ks : 0; }
 CAIN_API void cain_gemm_w4_set_occupancy(int wgs_per_cu) { g_w4_wgs_per_cu = wgs_per_cu > 0 ? wgs_per_cu : 0; }
 
 static int w4_n_cu() {
@@ -413,11 +463,55 @@ static int w4_variant(int N, int K, int M, int epi, int n_cu) {
 
 CAIN_API int cain_gemm_w4_variant(int N, int K, int M, int epi) { return w4_variant(N, K, M, epi & EPI_MASK, w4_n_cu()); }
 
-// Same arguments as cain_gemm_w8 (gemm_w8.hip); Wp is the MXFP4 packing, wsc its e8m0 scale bytes.
+static long long w4_split_bytes(int N, int ks) { return W4_CTR_BYTES + (long long)(N / 16) * ks * 64 * 16; }
+
+// k ranges per tile of a stream-kernel GEMM: the most (up to 4) that keep tiles x ks <= CUs (one pair per CU: the
+// ticket's last arriver adds a memory round trip, so pairs beyond the CU count buy nothing), every wave >= one quad
+// per range, and the workspace large enough.  Wider outputs (>= one tile per CU) are not split.
+static int w4_split(int var, int N, int K, int n_cu, long long ws_bytes) {
+  if (!w4_is_stream(var) || g_w4_split == 1) return 1;
+  const int tiles = N / 16, kq = K / 128, waves = W4_WAVES[var];
+  auto ok = [&](int k) {
+    return k > 1 && kq % k == 0 && kq / k >= waves && tiles <= 4096 && w4_split_bytes(N, k) <= ws_bytes;
+  };
+  if (g_w4_split > 1) return ok(g_w4_split) ? g_w4_split : 1;
+  int best = 1;
+  for (int k = 2; k <= 4; ++k)
+    if (tiles * k <= n_cu && ok(k)) best = k;
+  return best;
+}
+
+CAIN_API int cain_gemm_w4_split(int N, int K, int M, int epi, long long ws_bytes) {
+  const int n_cu = w4_n_cu();
+  return w4_split(w4_variant(N, K, M, epi & EPI_MASK, n_cu), N, K, n_cu, ws_bytes);
+}
+
+// Workspace a W4 GEMM of this shape may use (split-K tickets + partials; 0: none)
+CAIN_API long long cain_gemm_w4_ws_bytes(int N, int K, int M) {
+  (void)K, (void)M;
+  return N % 16 ? 0 : w4_split_bytes(N, 4);
+}
+
+CAIN_API int cain_gemm_w4_ex(const void* Wp, const void* wsc, const void* X, int ldx, int K, int N, int M, void* Y,
+                             int ldy, const float* bias, int norm, float eps, const int* slot, const int* pos,
+                             const float* cos_t, const float* sin_t, void* kc, void* vtc, int H, int Hkv, int hd,
+                             int T_max, void* ws, long long ws_bytes, int epi_flags, hipStream_t st);
+
+// Same arguments as cain_gemm_w8 (gemm_w8.hip); Wp is the MXFP4 packing, wsc its e8m0 scale bytes.  No workspace:
+// never split (cain_gemm_w4_ex is the engine's entry).
 CAIN_API int cain_gemm_w4(const void* Wp, const void* wsc, const void* X, int ldx, int K, int N, int M, void* Y, int ldy,
                           const float* bias, int norm, float eps, const int* slot, const int* pos, const float* cos_t,
                           const float* sin_t, void* kc, void* vtc, int H, int Hkv, int hd, int T_max, int epi_flags,
                           hipStream_t st) {
+  return cain_gemm_w4_ex(Wp, wsc, X, ldx, K, N, M, Y, ldy, bias, norm, eps, slot, pos, cos_t, sin_t, kc, vtc, H, Hkv,
+                         hd, T_max, nullptr, 0, epi_flags, st);
+}
+
+// ws: zeroed at allocation; its first W4_CTR_BYTES are tickets that every split launch leaves zero
+CAIN_API int cain_gemm_w4_ex(const void* Wp, const void* wsc, const void* X, int ldx, int K, int N, int M, void* Y,
+                             int ldy, const float* bias, int norm, float eps, const int* slot, const int* pos,
+                             const float* cos_t, const float* sin_t, void* kc, void* vtc, int H, int Hkv, int hd,
+                             int T_max, void* ws, long long ws_bytes, int epi_flags, hipStream_t st) {
   const int epi = epi_flags & EPI_MASK;
   if (K % 128 || N % 16 || M < 1 || M > 64) return -1;
   if (epi == EPI_QKV_ROPE && (hd % 16 || (hd / 2) % 8)) return -1;
@@ -435,12 +529,20 @@ CAIN_API int cain_gemm_w4(const void* Wp, const void* wsc, const void* X, int ld
   a.msplit = (M + 16 * nb - 1) / (16 * nb);
   const int npairs = N / 16 * a.msplit;
   int grid = npairs;
+  W4Split sp{1, nullptr, nullptr};
+  int np = npairs;
   if (w4_is_stream(var)) {  // persistent: at most the resident workgroups (2 of 8 waves / 4 of 4 waves per CU)
     a.msplit = 1;
-    grid = std::min(npairs, n_cu * (g_w4_wgs_per_cu ? g_w4_wgs_per_cu : (waves == 8 ? 2 : 4)));
+    sp.ks = ws ? w4_split(var, N, K, n_cu, ws_bytes) : 1;
+    if (sp.ks > 1) {
+      sp.ctr = static_cast<unsigned*>(ws);
+      sp.part = reinterpret_cast<float*>(static_cast<char*>(ws) + W4_CTR_BYTES);
+      np = npairs * sp.ks;
+    }
+    grid = std::min(np, n_cu * (g_w4_wgs_per_cu ? g_w4_wgs_per_cu : (waves == 8 ? 2 : 4)));
   }
   const uint8_t* sc = reinterpret_cast<const uint8_t*>(wsc);
-  const hipError_t e = norm ? w4_launch<true>(epi, var, a, sc, grid, npairs, st)
-                            : w4_launch<false>(epi, var, a, sc, grid, npairs, st);
+  const hipError_t e = norm ? w4_launch<true>(epi, var, a, sc, grid, np, sp, st)
+                            : w4_launch<false>(epi, var, a, sc, grid, np, sp, st);
   return int(e);
 }

@@ -32,10 +32,10 @@ CAIN_API int cain_gemm_w8(const void* Wp, const float* wscale, const void* X, in
                           int ldy, const float* bias, int norm, float eps, const int* slot, const int* pos,
                           const float* cos_t, const float* sin_t, void* kc, void* vtc, int H, int Hkv, int hd,
                           int T_max, int epi, hipStream_t st);
-CAIN_API int cain_gemm_w4(const void* Wp, const void* wsc, const void* X, int ldx, int K, int N, int M, void* Y, int ldy,
-                          const float* bias, int norm, float eps, const int* slot, const int* pos, const float* cos_t,
-                          const float* sin_t, void* kc, void* vtc, int H, int Hkv, int hd, int T_max, int epi_flags,
-                          hipStream_t st);
+CAIN_API int cain_gemm_w4_ex(const void* Wp, const void* wsc, const void* X, int ldx, int K, int N, int M, void* Y,
+                             int ldy, const float* bias, int norm, float eps, const int* slot, const int* pos,
+                             const float* cos_t, const float* sin_t, void* kc, void* vtc, int H, int Hkv, int hd,
+                             int T_max, void* ws, long long ws_bytes, int epi_flags, hipStream_t st);
 CAIN_API int cain_gemm_w8a8(const void* Wp8, const float* wscale, const void* X8, int ld8, const float* xs, int K,
                             int N, int M, void* Y, int ldy, const float* bias, const int* slot, const int* pos,
                             const float* cos_t, const float* sin_t, void* kc, void* vtc, int H, int Hkv, int hd,
@@ -207,8 +207,8 @@ int forward(const Plan& p, int M, const CainRows& r, int want_logits, int want_s
                             vcm, d.H, d.Hkv, d.hd, d.T_max, d.gemm_ws, d.gemm_ws_bytes, epi, st);
     }
     if (d.wfmt == WFMT_FP4)
-      return cain_gemm_w4(W, ws, X, ldx, K, N, M, Y, ldy, bias, norm, d.eps, r.slot, r.pos, d.cos_t, d.sin_t, kcm, vcm,
-                          d.H, d.Hkv, d.hd, d.T_max, epi, st);
+      return cain_gemm_w4_ex(W, ws, X, ldx, K, N, M, Y, ldy, bias, norm, d.eps, r.slot, r.pos, d.cos_t, d.sin_t, kcm,
+                             vcm, d.H, d.Hkv, d.hd, d.T_max, d.gemm_ws, d.gemm_ws_bytes, epi, st);
     const float* wsf = static_cast<const float*>(ws);
     if (d.wfmt == WFMT_FP8 && W8 && d.x8 && cain_w8a8_eligible(N, K, M)) {  // W8A8: per-row fp8 activations
       CK(cain_quant_rows(X, ldx, K, M, d.x8, d.x8_ld, d.xs, norm, d.eps, st));

@@ -111,6 +111,58 @@ def test_w4_stream_grid_occupancy(occ):
     assert rel_err(y, x.float() @ Wd.t()) < 1e-3
 
 
+@pytest.mark.parametrize("ks", [1, 2, 3, 4])
+@pytest.mark.parametrize("N,K,epi", [(2048, 16384, "resid"), (1536, 8960, "resid"), (2048, 2048, "f32_norm"),
+                                     (4096, 3072, "silu"), (1024, 12288, "f32_norm")])
+def test_w4_split_k_stream(ks, N, K, epi):
+    """Split-K of the few-row stream kernel (narrow outputs: gemma:2b / qwen2:1.5b down and O, a gate/up, forced k
+    ranges 1-4): every split count gives the fp32 result, RMSNorm applied by the last arriver, residual added
+    once, and the tickets are left at zero for the next launch."""
+    torch.manual_seed(ks + N)
+    M = 1
+    W = (torch.randn(N, K, device=DEV) * 0.02).bfloat16()
+    x = (3 * torch.randn(M, K, device=DEV)).bfloat16()
+    n_out = N // 2 if epi == "silu" else N
+    r = torch.randn(M, n_out, device=DEV).bfloat16()
+    wq, ws, Wd = q4(W)
+    ops.set_w4_split(ks)
+    try:
+        kq = K // 128
+        want_ks = ks if ks > 1 and kq % ks == 0 and kq // ks >= (4 if kq < 24 else 8) else 1
+        assert ops.w4_split(N, K, M, ops.EPI_F32) == want_ks
+        if epi == "resid":
+            ref = x.float() @ Wd.t() + r.float()
+            ops.gemm_w4(wq, ws, x, N, ops.EPI_RESID, out=r)
+            assert rel_err(r, ref) < 1e-2
+        elif epi == "silu":
+            h = x.float() @ Wd.t()
+            hh = h.view(M, N // 16, 2, 8)  # interleaved 8-row blocks: gate rows, then up rows
+            ref = (torch.nn.functional.silu(hh[:, :, 0]) * hh[:, :, 1]).reshape(M, n_out)
+            y = ops.gemm_w4(wq, ws, x, N, ops.EPI_SILU)
+            assert rel_err(y, ref) < 1e-2
+        else:
+            y = ops.gemm_w4(wq, ws, x, N, ops.EPI_F32, norm=True, eps=1e-6)
+            xn = x.float() * torch.rsqrt(x.float().pow(2).mean(-1, keepdim=True) + 1e-6)
+            assert rel_err(y, xn @ Wd.t()) < 2e-3
+        torch.cuda.synchronize()
+        assert int(ops._W4_WS[x.device][:16384].count_nonzero()) == 0  # tickets reset
+    finally:
+        ops.set_w4_split(0)
+
+
+def test_w4_split_rule_on_the_study_shapes():
+    """The default rule splits only outputs of fewer 16-row tiles than CUs (the small models' O / down)."""
+    n_cu = torch.cuda.get_device_properties(DEV).multi_processor_count
+    if n_cu != 256:
+        pytest.skip("rule values below are for 256 CUs")
+    assert ops.w4_split(2048, 16384, 1, ops.EPI_RESID) == 2   # gemma:2b down: 128 tiles
+    assert ops.w4_split(1536, 8960, 1, ops.EPI_RESID) == 2    # qwen2:1.5b down: 96 tiles
+    assert ops.w4_split(1536, 1536, 1, ops.EPI_RESID) == 2    # qwen2:1.5b O
+    assert ops.w4_split(4096, 14336, 1, ops.EPI_RESID) == 1   # llama3.1:8b down: 256 tiles
+    assert ops.w4_split(6144, 4096, 1, ops.EPI_QKV_ROPE) == 1  # llama3.1:8b QKV: 384 tiles
+    assert ops.w4_split(128256, 4096, 1, ops.EPI_F32) == 1    # LM head
+
+
 @pytest.mark.parametrize("M", [1, 32])
 def test_w4_resid_and_norm(M):
     torch.manual_seed(1)
