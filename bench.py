@@ -114,10 +114,16 @@ def main() -> int:
     ap.add_argument("--single-fp4-models", default="phi3:3.8b,qwen2:7b,gemma:7b,mistral:7b",
                     help="models measured at batch 1 on MXFP4 weights only (the reference's 4-bit class), "
                          "comma-separated: with --single-models and the bench model, the 7 study models")
+    ap.add_argument("--checkpoint", default=None,
+                    help="a Hugging Face checkpoint directory or GGUF file for --model (default: random-init weights of "
+                         "the model's architecture; models/hf.py, models/gguf.py)")
     ap.add_argument("--w4a8-min-rows", type=int, default=0,
                     help="MXFP4: rows above which forwards run W4A8 instead of W4A16 (0: the runtime's default, 16)")
     ns = ap.parse_args()
 
+    if ns.checkpoint:  # before any engine (and inherited by spawned ranks): --model's engines load the checkpoint
+        os.environ["CAIN_CHECKPOINTS"] = ",".join(filter(None, [os.environ.get("CAIN_CHECKPOINTS", ""),
+                                                                f"{ns.model}={ns.checkpoint}"]))
     world_env = os.environ.get("WORLD_SIZE")
     if world_env is None and ns.gpus > 1:
         return spawn_ranks(ns.gpus, sys.argv[1:])
@@ -310,7 +316,8 @@ def main() -> int:
                       if getattr(eng, "w8a8", False) else "bf16 activations, fp8-e4m3 weights")
                      + (", fp8-e4m3 KV cache" if ns.kv == "fp8" else ""),
             "device": "cpu (torch oracle)" if cpu else "MI355X",
-            "data": "synthetic (reference topics.csv prompts, random-init weights)",
+            "data": ("synthetic (reference topics.csv prompts, random-init weights)" if not ns.checkpoint else
+                     f"synthetic prompts (reference topics.csv), checkpoint weights ({os.path.basename(ns.checkpoint)})"),
             "config": {"model": ns.model, "global_batch": ns.batch * world, "seq_len": n_tok,
                        "parallelism": f"dp{world}", "words": ns.words, "trials_per_gpu": ns.batch,
                        "sampling": "ollama defaults (T=0.8, top_k=40, top_p=0.9, repeat_penalty=1.1), eos disabled"},

@@ -39,3 +39,17 @@ def test_bench_spawns_n_ranks(n):
 def test_bench_rejects_mismatched_launcher():
     r = _run(["--gpus", "2"], env={"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
     assert r.returncode != 0 and "WORLD_SIZE=1" in (r.stderr + r.stdout)
+
+
+def test_bench_on_a_checkpoint(tmp_path):
+    """--checkpoint: the bench model's engine loads a Hugging Face checkpoint (here a tiny one written by
+    transformers) instead of random-init weights, and the JSON line says so."""
+    pytest.importorskip("transformers")
+    sys.path.insert(0, str(ROOT / "tests"))
+    from hf_fixtures import make_checkpoint
+
+    make_checkpoint("llama", tmp_path / "ck")
+    r = _run(["--checkpoint", str(tmp_path / "ck")])
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = _line(r.stdout)
+    assert "checkpoint weights (ck)" in d["data"] and d["tokens_generated"] == 2 * d["config"]["seq_len"]
