@@ -175,7 +175,11 @@ class EngineBackend(Backend):
         """As Ollama: a model with a chat template (a checkpoint's) gets ``/api/generate``'s prompt as one user turn
         (after ``system``) and ``/api/chat``'s messages through the template, with the generation prompt; ``raw``
         skips it.  The rendered text is tokenized without a second BOS (the template writes its own)."""
-        tok = getattr(self.engine(model), "tokenizer", None) if model in self._models else None
+        from ..models.hf import checkpoint_for
+
+        # only a checkpoint brings a template: random-init tags keep the lazy engine load in the scheduler thread
+        tok = (getattr(self.engine(model), "tokenizer", None)
+               if model in self._models and checkpoint_for(model) else None)
         if tok is None or not getattr(tok, "chat_template", None) or body.get("raw"):
             return super().prompt_for(model, body, chat)
         if chat:
