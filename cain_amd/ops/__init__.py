@@ -89,6 +89,7 @@ def load() -> ctypes.CDLL:
         lib.cain_gemm_w4_ws_bytes.argtypes = [ci, ci, ci]
         lib.cain_gemm_w4_split.argtypes = [ci, ci, ci, ci, ctypes.c_longlong]
         lib.cain_gemm_w4_set_split.argtypes = [ci]
+        lib.cain_gemm_w4_set_split_cap.argtypes = [ci]
         lib.cain_gemm_w4_set_variant.argtypes = [ci]
         lib.cain_gemm_w4_variant.argtypes = [ci, ci, ci, ci]
         lib.cain_gemm_w4_set_occupancy.argtypes = [ci]
@@ -368,6 +369,11 @@ def set_w4_split(ks: int) -> None:
     """Split-K of the few-row MXFP4 stream kernel (csrc/gemm_w4.hip w4_split): 0 = the rule (narrow outputs over
     fewer tiles than CUs get up to 4 k ranges), 1 = off, k > 1 = k ranges wherever the shape allows."""
     load().cain_gemm_w4_set_split(int(ks))
+
+
+def set_w4_split_cap(cap: int) -> None:
+    """A/B of the split rule's budget: tiles x k ranges <= ``cap`` x CUs (1: the rule)."""
+    load().cain_gemm_w4_set_split_cap(int(cap))
 
 
 def w4_split(n: int, k: int, m: int, epi: int, ws_bytes: int = 1 << 30) -> int:

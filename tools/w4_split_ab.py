@@ -25,12 +25,18 @@ def main() -> int:
     ap.add_argument("--tokens", type=int, default=512)
     ap.add_argument("--trials", type=int, default=3)
     ap.add_argument("--rounds", type=int, default=2)
+    ap.add_argument("--cap", type=int, default=0,
+                    help="compare the rule (cap 1) with a pair budget of cap x CUs instead of split off vs rule")
     a = ap.parse_args()
     opts = dict(eos_id=-1, seed=7)
     for model in filter(None, a.models.split(",")):
         for rnd in range(a.rounds):
-            for split in (1, 0):  # 1 = off, 0 = the rule
-                ops.set_w4_split(split)
+            for split in ((1, 0) if not a.cap else ("cap1", f"cap{a.cap}")):  # 1 = off, 0 = the rule
+                if isinstance(split, str):
+                    ops.set_w4_split(0)
+                    ops.set_w4_split_cap(int(split[3:]))
+                else:
+                    ops.set_w4_split(split)
                 eng = DecodeEngine(model, device="cuda", max_batch=1, max_context=1024, weight_dtype="fp4",
                                    steps_per_graph=16, seed=1)
                 eng.generate(["warm up"], 32, [opts])
@@ -42,15 +48,17 @@ def main() -> int:
                     torch.cuda.synchronize()
                     rates.append(r.eval_count / (time.perf_counter() - t0))
                 cfg = eng.cfg
-                print(json.dumps({"model": model, "round": rnd, "split": "rule" if split == 0 else "off",
+                label = split if isinstance(split, str) else ("rule" if split == 0 else "off")
+                print(json.dumps({"model": model, "round": rnd, "split": label,
                                   "tok_per_s": round(statistics.median(rates), 1),
-                                  "o_ks": ops.w4_split(cfg.d_model, cfg.q_dim, 1, ops.EPI_RESID) if split == 0 else 1,
-                                  "down_ks": ops.w4_split(cfg.d_model, cfg.ffn, 1, ops.EPI_RESID) if split == 0 else 1}),
+                                  "o_ks": ops.w4_split(cfg.d_model, cfg.q_dim, 1, ops.EPI_RESID) if split != 1 else 1,
+                                  "down_ks": ops.w4_split(cfg.d_model, cfg.ffn, 1, ops.EPI_RESID) if split != 1 else 1}),
                       flush=True)
                 eng.close()
                 del eng
                 torch.cuda.empty_cache()
     ops.set_w4_split(0)
+    ops.set_w4_split_cap(1)
     return 0
 
 
