@@ -360,4 +360,36 @@ def registered_checkpoints() -> Dict[str, str]:
 
 
 def checkpoint_for(tag: str) -> Optional[str]:
-    return registered_checkpoints().get(tag)
+    """The checkpoint registered for ``tag``: a path, or ``ollama`` / ``ollama:<models dir>`` for the GGUF blob a
+    local Ollama installation serves under that tag (``ollama_blob``)."""
+    path = registered_checkpoints().get(tag)
+    if path and (path == "ollama" or path.startswith("ollama:")):
+        return str(ollama_blob(tag, path[7:] or None))
+    return path
+
+
+def ollama_blob(tag: str, models_dir: Optional[PathLike] = None) -> Path:
+    """The GGUF model blob Ollama stores for ``tag`` (``name[:tag]``, default tag ``latest``; a ``namespace/name``
+    or ``host/namespace/name`` prefix as Ollama writes it): the manifest at
+    ``<models>/manifests/<host>/<namespace>/<name>/<tag>`` names its layers; the one of media type
+    ``application/vnd.ollama.image.model`` is ``<models>/blobs/sha256-<hex>``.  ``models_dir`` defaults to
+    ``$OLLAMA_MODELS`` or ``~/.ollama/models``.  JSON only: nothing from the store is executed."""
+    root = Path(models_dir or os.environ.get("OLLAMA_MODELS") or Path.home() / ".ollama" / "models").expanduser()
+    name, _, version = tag.partition(":")
+    parts = name.split("/")
+    host, ns = "registry.ollama.ai", "library"
+    if len(parts) == 2:
+        ns, name = parts
+    elif len(parts) >= 3:
+        host, ns, name = parts[0], parts[1], "/".join(parts[2:])
+    manifest = root / "manifests" / host / ns / name / (version or "latest")
+    if not manifest.is_file():
+        raise FileNotFoundError(f"no Ollama manifest for {tag!r} at {manifest}")
+    layers = json.loads(manifest.read_text()).get("layers") or []
+    model = [lay for lay in layers if str(lay.get("mediaType", "")).endswith(".image.model")]
+    if not model:
+        raise ValueError(f"Ollama manifest {manifest} has no model layer")
+    blob = root / "blobs" / str(model[0]["digest"]).replace(":", "-")
+    if not blob.is_file():
+        raise FileNotFoundError(f"Ollama blob {blob} (for {tag!r}) is missing")
+    return blob

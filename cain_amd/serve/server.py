@@ -116,11 +116,17 @@ def register_checkpoints(specs: Optional[List[str]]) -> List[str]:
     if not specs:
         return []
     os.environ["CAIN_CHECKPOINTS"] = ",".join(filter(None, [os.environ.get("CAIN_CHECKPOINTS", "")] + list(specs)))
-    reg = registered_checkpoints()  # validates the syntax
+    from ..models.hf import checkpoint_for
+
+    registered_checkpoints()  # validates the syntax
     tags = [s.partition("=")[0].strip() for s in specs]
     for t in tags:
-        if not os.path.isdir(reg[t]):
-            raise SystemExit(f"--checkpoint {t}: {reg[t]} is not a directory")
+        try:
+            path = checkpoint_for(t)  # resolves "ollama" entries to the local store's blob
+        except (OSError, ValueError) as exc:
+            raise SystemExit(f"--checkpoint {t}: {exc}")
+        if not (os.path.isdir(path) or os.path.isfile(path)):
+            raise SystemExit(f"--checkpoint {t}: {path} is neither a checkpoint directory nor a GGUF file")
     return tags
 
 
@@ -635,7 +641,8 @@ def main(argv: Optional[List[str]] = None) -> None:
                     help="batch requests that arrive within --batch-window-ms and run each batch to completion "
                          "(default on the HIP engine: continuous batching)")
     ap.add_argument("--checkpoint", action="append", metavar="TAG=PATH",
-                    help="serve a Hugging Face checkpoint directory under TAG (repeatable; models/hf.py)")
+                    help="serve a Hugging Face checkpoint directory or GGUF file under TAG (repeatable; models/hf.py); "
+                         "PATH 'ollama' takes the blob a local Ollama store keeps for TAG")
     ap.add_argument("-v", "--verbose", action="store_true")
     ns = ap.parse_args(argv)
     ck_tags = register_checkpoints(ns.checkpoint)

@@ -249,3 +249,45 @@ def test_gguf_tokenizer_through_transformers_converter(tmp_path):
     assert ids == tok.encode(s).ids
     assert gt.decode(ids) == s
     del model
+
+
+def test_ollama_store_blob_drives_the_tag(tmp_path, monkeypatch):
+    """CAIN_CHECKPOINTS="qwen2:1.5b=ollama:<models dir>": the tag resolves through a local Ollama store (manifest ->
+    model layer -> sha256 blob, a GGUF file) and the engine decodes it as transformers decodes the original."""
+    import hashlib
+    import json
+
+    from cain_amd.models import get_config
+    from cain_amd.models.hf import ollama_blob
+
+    model = make_checkpoint("qwen2", tmp_path / "hf", scale=4.0)
+    _, mw, _ = load_pretrained(tmp_path / "hf", dtype=torch.float32)
+    store = tmp_path / "ollama"
+    (store / "blobs").mkdir(parents=True)
+    export_gguf(mw, tmp_path / "m.gguf", "qwen2", tensor_type="F32")
+    data = (tmp_path / "m.gguf").read_bytes()
+    digest = hashlib.sha256(data).hexdigest()
+    (store / "blobs" / f"sha256-{digest}").write_bytes(data)
+    man = store / "manifests" / "registry.ollama.ai" / "library" / "qwen2" / "1.5b"
+    man.parent.mkdir(parents=True)
+    man.write_text(json.dumps({"schemaVersion": 2, "layers": [
+        {"mediaType": "application/vnd.ollama.image.template", "digest": "sha256:" + "0" * 64, "size": 1},
+        {"mediaType": "application/vnd.ollama.image.model", "digest": f"sha256:{digest}", "size": len(data)}]}))
+    assert ollama_blob("qwen2:1.5b", store) == store / "blobs" / f"sha256-{digest}"
+    with pytest.raises(FileNotFoundError):
+        ollama_blob("qwen2:7b", store)
+    ns = store / "manifests" / "registry.ollama.ai" / "someone" / "tiny" / "latest"
+    ns.parent.mkdir(parents=True)
+    ns.write_text(man.read_text())
+    assert ollama_blob("someone/tiny", store) == ollama_blob("qwen2:1.5b", store)
+
+    monkeypatch.setenv("CAIN_CHECKPOINTS", f"qwen2:1.5b=ollama:{store}")
+    cfg = get_config("qwen2:1.5b")
+    assert (cfg.d_model, cfg.n_layers, cfg.qkv_bias) == (384, 2, True)  # the blob's, not the built-in 1.5B
+    eng = DecodeEngine("qwen2:1.5b", device="cpu", max_batch=1, max_context=64)
+    ids = [5, 9, 33, 100]
+    got = eng.generate([ids], 5, [dict(temperature=0.0, eos_id=-1)])[0].tokens
+    with torch.no_grad():
+        want = model.generate(torch.tensor([ids]), max_new_tokens=5, do_sample=False, eos_token_id=None,
+                              pad_token_id=0)[0, len(ids):].tolist()
+    assert got == want
