@@ -473,7 +473,8 @@ static long long w4_split_bytes(int N, int ks) { return W4_CTR_BYTES + (long lon
 // CU) are not split.  Measured in the graph-replayed batch-1 decode (tools/w4_split_ab.py, profiles/r5/w4split/):
 // splitting every narrow output in two, gemma:2b (down K = 16,384, O K = 2,048) 1,087 -> 1,099-1,106 tok/s and
 // qwen2:1.5b (down K = 8,960, O K = 1,536) 981 -> 921 -- ranges of 35 and 6 quads save less stream time than the
-// ticket's round trip; with this rule (gemma:2b's down alone) 1,084 -> 1,127 tok/s, qwen2:1.5b unchanged.
+// ticket's round trip; with this rule (gemma:2b's down alone) 1,084 -> 1,127 tok/s, qwen2:1.5b unchanged.  A budget
+// of 2 x CUs (gemma:7b / qwen2:7b down, 192 / 224 tiles, in two) measured slower: 559 -> 548, 628 -> 615.
 static int w4_split(int var, int N, int K, int n_cu, long long ws_bytes) {
   if (!w4_is_stream(var) || g_w4_split == 1) return 1;
   const int tiles = N / 16, kq = K / 128, waves = W4_WAVES[var];
