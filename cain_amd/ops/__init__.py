@@ -90,6 +90,7 @@ def load() -> ctypes.CDLL:
         lib.cain_gemm_w4_split.argtypes = [ci, ci, ci, ci, ctypes.c_longlong]
         lib.cain_gemm_w4_set_split.argtypes = [ci]
         lib.cain_gemm_w4_set_split_cap.argtypes = [ci]
+        lib.cain_gemm_w4_set_split_min_quads.argtypes = [ci]
         lib.cain_gemm_w4_set_variant.argtypes = [ci]
         lib.cain_gemm_w4_variant.argtypes = [ci, ci, ci, ci]
         lib.cain_gemm_w4_set_occupancy.argtypes = [ci]
@@ -374,6 +375,11 @@ def set_w4_split(ks: int) -> None:
 def set_w4_split_cap(cap: int) -> None:
     """A/B of the split rule's budget: tiles x k ranges <= ``cap`` x CUs (1: the rule)."""
     load().cain_gemm_w4_set_split_cap(int(cap))
+
+
+def set_w4_split_min_quads(q: int) -> None:
+    """A/B of the split rule's shortest k range, in 128-wide quads (64: the rule)."""
+    load().cain_gemm_w4_set_split_min_quads(int(q))
 
 
 def w4_split(n: int, k: int, m: int, epi: int, ws_bytes: int = 1 << 30) -> int:

@@ -425,12 +425,14 @@ static hipError_t w4_launch(int epi, int var, const GemmArgs& a, const uint8_t* 
 }
 
 // Tuning / test overrides (-1 / 0: the rules below): the kernel shape (W4Var) and the stream grid's workgroups per CU
-static int g_w4_var = -1, g_w4_wgs_per_cu = 0, g_w4_split = 0, g_w4_split_cap = 1;
+static int g_w4_var = -1, g_w4_wgs_per_cu = 0, g_w4_split = 0, g_w4_split_cap = 1, g_w4_split_min_q = 64;
 CAIN_API void cain_gemm_w4_set_variant(int v) { g_w4_var = v < W4_N_VARS ? v : -1; }
 // split-K of the stream kernel: 0 = the rule (w4_split), 1 = off, k > 1 = k ranges wherever the shape allows it
 CAIN_API void cain_gemm_w4_set_split(int ks) { g_w4_split = ks > 0 ? ks : 0; }
 // A/B of the rule's pair budget: tiles x ks <= cap x CUs (1: the rule)
 CAIN_API void cain_gemm_w4_set_split_cap(int cap) { g_w4_split_cap = cap > 0 ? cap : 1; }
+// A/B of the rule's shortest k range in quads (64: the rule)
+CAIN_API void cain_gemm_w4_set_split_min_quads(int q) { g_w4_split_min_q = q > 0 ? q : 64; }
 CAIN_API void cain_gemm_w4_set_occupancy(int wgs_per_cu) { g_w4_wgs_per_cu = wgs_per_cu > 0 ? wgs_per_cu : 0; }
 
 static int w4_n_cu() {
@@ -484,7 +486,7 @@ static int w4_split(int var, int N, int K, int n_cu, long long ws_bytes) {
   if (g_w4_split > 1) return ok(g_w4_split) ? g_w4_split : 1;
   int best = 1;
   for (int k = 2; k <= 4; ++k)
-    if (tiles * k <= g_w4_split_cap * n_cu && kq / k >= 64 && ok(k)) best = k;
+    if (tiles * k <= g_w4_split_cap * n_cu && kq / k >= g_w4_split_min_q && ok(k)) best = k;
   return best;
 }
 

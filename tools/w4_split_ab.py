@@ -27,14 +27,21 @@ def main() -> int:
     ap.add_argument("--rounds", type=int, default=2)
     ap.add_argument("--cap", type=int, default=0,
                     help="compare the rule (cap 1) with a pair budget of cap x CUs instead of split off vs rule")
+    ap.add_argument("--min-quads", type=int, default=0,
+                    help="compare the rule (64) with this shortest k range (in quads) instead of split off vs rule")
     a = ap.parse_args()
     opts = dict(eos_id=-1, seed=7)
     for model in filter(None, a.models.split(",")):
         for rnd in range(a.rounds):
-            for split in ((1, 0) if not a.cap else ("cap1", f"cap{a.cap}")):  # 1 = off, 0 = the rule
-                if isinstance(split, str):
+            settings = (("cap1", f"cap{a.cap}") if a.cap else ("minq64", f"minq{a.min_quads}") if a.min_quads
+                        else (1, 0))  # 1 = off, 0 = the rule
+            for split in settings:
+                if isinstance(split, str) and split.startswith("cap"):
                     ops.set_w4_split(0)
                     ops.set_w4_split_cap(int(split[3:]))
+                elif isinstance(split, str):
+                    ops.set_w4_split(0)
+                    ops.set_w4_split_min_quads(int(split[4:]))
                 else:
                     ops.set_w4_split(split)
                 eng = DecodeEngine(model, device="cuda", max_batch=1, max_context=1024, weight_dtype="fp4",
@@ -59,6 +66,7 @@ def main() -> int:
                 torch.cuda.empty_cache()
     ops.set_w4_split(0)
     ops.set_w4_split_cap(1)
+    ops.set_w4_split_min_quads(64)
     return 0
 
 
