@@ -368,7 +368,7 @@ def _w4_ws(device, nbytes: int) -> torch.Tensor:
 
 def set_w4_split(ks: int) -> None:
     """Split-K of the few-row MXFP4 stream kernel (csrc/gemm_w4.hip w4_split): 0 = the rule (narrow outputs over
-    fewer tiles than CUs get up to 4 k ranges), 1 = off, k > 1 = k ranges wherever the shape allows."""
+    fewer tiles than CUs get up to 4 k ranges of >= 32 quads), 1 = off, k > 1 = k ranges wherever the shape allows."""
     load().cain_gemm_w4_set_split(int(ks))
 
 
@@ -378,7 +378,7 @@ def set_w4_split_cap(cap: int) -> None:
 
 
 def set_w4_split_min_quads(q: int) -> None:
-    """A/B of the split rule's shortest k range, in 128-wide quads (64: the rule)."""
+    """A/B of the split rule's shortest k range, in 128-wide quads (32: the rule)."""
     load().cain_gemm_w4_set_split_min_quads(int(q))
 
 

@@ -425,14 +425,14 @@ static hipError_t w4_launch(int epi, int var, const GemmArgs& a, const uint8_t* 
 }
 
 // Tuning / test overrides (-1 / 0: the rules below): the kernel shape (W4Var) and the stream grid's workgroups per CU
-static int g_w4_var = -1, g_w4_wgs_per_cu = 0, g_w4_split = 0, g_w4_split_cap = 1, g_w4_split_min_q = 64;
+static int g_w4_var = -1, g_w4_wgs_per_cu = 0, g_w4_split = 0, g_w4_split_cap = 1, g_w4_split_min_q = 32;
 CAIN_API void cain_gemm_w4_set_variant(int v) { g_w4_var = v < W4_N_VARS ? v : -1; }
 // split-K of the stream kernel: 0 = the rule (w4_split), 1 = off, k > 1 = k ranges wherever the shape allows it
 CAIN_API void cain_gemm_w4_set_split(int ks) { g_w4_split = ks > 0 ? ks : 0; }
 // A/B of the rule's pair budget: tiles x ks <= cap x CUs (1: the rule)
 CAIN_API void cain_gemm_w4_set_split_cap(int cap) { g_w4_split_cap = cap > 0 ? cap : 1; }
-// A/B of the rule's shortest k range in quads (64: the rule)
-CAIN_API void cain_gemm_w4_set_split_min_quads(int q) { g_w4_split_min_q = q > 0 ? q : 64; }
+// A/B of the rule's shortest k range in quads (32: the rule)
+CAIN_API void cain_gemm_w4_set_split_min_quads(int q) { g_w4_split_min_q = q > 0 ? q : 32; }
 CAIN_API void cain_gemm_w4_set_occupancy(int wgs_per_cu) { g_w4_wgs_per_cu = wgs_per_cu > 0 ? wgs_per_cu : 0; }
 
 static int w4_n_cu() {
@@ -470,13 +470,14 @@ CAIN_API int cain_gemm_w4_variant(int N, int K, int M, int epi) { return w4_vari
 static long long w4_split_bytes(int N, int ks) { return W4_CTR_BYTES + (long long)(N / 16) * ks * 64 * 16; }
 
 // k ranges per tile of a stream-kernel GEMM: the most (up to 4) that keep tiles x ks <= CUs (one pair per CU: the
-// ticket's last arriver adds a memory round trip, so pairs beyond the CU count buy nothing), every range >= 64 k
-// quads (8,192 k), every wave >= one quad per range, and the workspace large enough.  Wider outputs (>= one tile per
+// ticket's last arriver adds a memory round trip, so pairs beyond the CU count buy nothing), every range >= 32 k
+// quads (4,096 k), every wave >= one quad per range, and the workspace large enough.  Wider outputs (>= one tile per
 // CU) are not split.  Measured in the graph-replayed batch-1 decode (tools/w4_split_ab.py, profiles/r5/w4split/):
 // splitting every narrow output in two, gemma:2b (down K = 16,384, O K = 2,048) 1,087 -> 1,099-1,106 tok/s and
 // qwen2:1.5b (down K = 8,960, O K = 1,536) 981 -> 921 -- ranges of 35 and 6 quads save less stream time than the
 // ticket's round trip; with this rule (gemma:2b's down alone) 1,084 -> 1,127 tok/s, qwen2:1.5b unchanged.  A budget
-// of 2 x CUs (gemma:7b / qwen2:7b down, 192 / 224 tiles, in two) measured slower: 559 -> 548, 628 -> 615.
+// of 2 x CUs (gemma:7b / qwen2:7b down, 192 / 224 tiles, in two) measured slower: 559 -> 548, 628 -> 615.  Ranges
+// down to 32 quads (qwen2:1.5b's down alone, 35): 985 / 978 -> 991 / 993 tok/s; its O (6 quads) stays unsplit.
 static int w4_split(int var, int N, int K, int n_cu, long long ws_bytes) {
   if (!w4_is_stream(var) || g_w4_split == 1) return 1;
   const int tiles = N / 16, kq = K / 128, waves = W4_WAVES[var];

@@ -151,14 +151,15 @@ def test_w4_split_k_stream(ks, N, K, epi):
 
 
 def test_w4_split_rule_on_the_study_shapes():
-    """The default rule splits only outputs of fewer 16-row tiles than CUs with long k ranges (gemma:2b's down)."""
+    """The default rule splits only outputs of fewer 16-row tiles than CUs into ranges of >= 32 quads (the small
+    models' down projections)."""
     n_cu = torch.cuda.get_device_properties(DEV).multi_processor_count
     if n_cu != 256:
         pytest.skip("rule values below are for 256 CUs")
     assert ops.w4_split(2048, 16384, 1, ops.EPI_RESID) == 2   # gemma:2b down: 128 tiles, 128 quads
     assert ops.w4_split(2048, 2048, 1, ops.EPI_RESID) == 1    # gemma:2b O: 16 quads (measured: no gain)
-    assert ops.w4_split(1536, 8960, 1, ops.EPI_RESID) == 1    # qwen2:1.5b down: 70 quads (measured slower split)
-    assert ops.w4_split(1536, 1536, 1, ops.EPI_RESID) == 1    # qwen2:1.5b O
+    assert ops.w4_split(1536, 8960, 1, ops.EPI_RESID) == 2    # qwen2:1.5b down: 96 tiles, 70 quads -> 2 x 35
+    assert ops.w4_split(1536, 1536, 1, ops.EPI_RESID) == 1    # qwen2:1.5b O: 12 quads (measured slower split)
     assert ops.w4_split(4096, 14336, 1, ops.EPI_RESID) == 1   # llama3.1:8b down: 256 tiles
     assert ops.w4_split(6144, 4096, 1, ops.EPI_QKV_ROPE) == 1  # llama3.1:8b QKV: 384 tiles
     assert ops.w4_split(128256, 4096, 1, ops.EPI_F32) == 1    # LM head

@@ -28,12 +28,12 @@ def main() -> int:
     ap.add_argument("--cap", type=int, default=0,
                     help="compare the rule (cap 1) with a pair budget of cap x CUs instead of split off vs rule")
     ap.add_argument("--min-quads", type=int, default=0,
-                    help="compare the rule (64) with this shortest k range (in quads) instead of split off vs rule")
+                    help="compare the rule (32) with this shortest k range (in quads) instead of split off vs rule")
     a = ap.parse_args()
     opts = dict(eos_id=-1, seed=7)
     for model in filter(None, a.models.split(",")):
         for rnd in range(a.rounds):
-            settings = (("cap1", f"cap{a.cap}") if a.cap else ("minq64", f"minq{a.min_quads}") if a.min_quads
+            settings = (("cap1", f"cap{a.cap}") if a.cap else ("minq32", f"minq{a.min_quads}") if a.min_quads
                         else (1, 0))  # 1 = off, 0 = the rule
             for split in settings:
                 if isinstance(split, str) and split.startswith("cap"):
@@ -66,7 +66,7 @@ def main() -> int:
                 torch.cuda.empty_cache()
     ops.set_w4_split(0)
     ops.set_w4_split_cap(1)
-    ops.set_w4_split_min_quads(64)
+    ops.set_w4_split_min_quads(32)
     return 0
 
 
