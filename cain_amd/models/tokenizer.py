@@ -145,6 +145,27 @@ class HFTokenizer:
         return len(text.split())
 
 
+class StreamDecoder:
+    """Incremental detokenisation of a streamed response: the pieces ``push`` returns concatenate to
+    ``decode(all ids)``, as Ollama's stream concatenates to its response.  Each push decodes the whole sequence so
+    far and returns the new suffix; a character whose bytes are split over tokens (a trailing U+FFFD) is held back
+    until its last byte arrives.  Single-token decodes (``piece``) break such characters and drop SentencePiece's
+    word-boundary spaces."""
+
+    def __init__(self, tok):
+        self.tok = tok
+        self.ids: List[int] = []
+        self.sent = 0
+
+    def push(self, ids) -> str:
+        self.ids.extend(int(t) for t in ids)
+        text = self.tok.decode(self.ids)
+        if text.endswith("\ufffd"):
+            return ""
+        out, self.sent = text[self.sent:], len(text)
+        return out
+
+
 def get_tokenizer(cfg, path: Optional[str] = None):
     if path:
         return HFTokenizer(path)

@@ -49,7 +49,7 @@ from dataclasses import dataclass, field
 from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
 from typing import Any, Callable, Dict, List, Optional
 
-from ..models.tokenizer import tokens_for_words
+from ..models.tokenizer import StreamDecoder, tokens_for_words
 
 VERSION = "0.5.0-cain-amd"
 _WORDS = re.compile(r"\bin\s+(\d+)\s+words\b", re.IGNORECASE)
@@ -210,11 +210,14 @@ class EngineBackend(Backend):
         eng = self.engine(model)
         tok = eng.tokenizer
         streams = [j.stream for j in jobs]
+        decs = [StreamDecoder(tok) for _ in jobs]
 
         def on_tokens(new_per_row: List[List[int]]) -> None:
-            for j, ids in zip(jobs, new_per_row):
+            for j, d, ids in zip(jobs, decs, new_per_row):
                 if j.stream is not None and ids:
-                    j.stream("".join(tok.piece(t) for t in ids))
+                    piece = d.push(ids)
+                    if piece:
+                        j.stream(piece)
 
         def gen():
             return eng.generate([j.prompt for j in jobs], [j.num_predict for j in jobs], [j.options for j in jobs],
@@ -295,13 +298,15 @@ class EngineBackend(Backend):
             eng.stream.synchronize()
             t_first = time.perf_counter_ns()
             for r, j in zip(rows, ok):
-                live[r] = {"job": j, "t0": t0, "t_pre": t_pre, "t_first": t_first}
+                live[r] = {"job": j, "t0": t0, "t_pre": t_pre, "t_first": t_first, "dec": StreamDecoder(tok)}
         cb.step()
         new, fin = cb.poll()
         now = time.perf_counter_ns()
         for r, new_ids in enumerate(new):
             if new_ids and live[r]["job"].stream is not None:
-                live[r]["job"].stream("".join(tok.piece(t) for t in new_ids))
+                piece = live[r]["dec"].push(new_ids)
+                if piece:
+                    live[r]["job"].stream(piece)
         done_rows = [r for r, f in enumerate(fin) if f]
         for r in done_rows:
             st, j = live[r], live[r]["job"]

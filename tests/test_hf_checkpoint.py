@@ -296,3 +296,46 @@ def test_stop_ids_from_generation_config_and_template_tokens(tmp_path, monkeypat
     first = free.tokens.index(stop_at)
     got = eng.generate(["w5 w6"], 8, [dict(temperature=0.0, eos_id=-1, stop_ids=[stop_at])])[0]
     assert got.tokens == free.tokens[:first + 1] and got.done_reason == "stop"
+
+
+def test_stream_decoder_holds_split_characters():
+    """Streamed pieces concatenate to the full decode, also when a character's UTF-8 bytes span tokens (a byte-level
+    vocabulary of single bytes here), and for the synthetic tokenizer (its decode strips the first space)."""
+    from tokenizers import Tokenizer, decoders, models, pre_tokenizers
+
+    from cain_amd.models.tokenizer import HFTokenizer, StreamDecoder, SyntheticTokenizer
+
+    alphabet = pre_tokenizers.ByteLevel.alphabet()
+    tok = Tokenizer(models.BPE({c: i for i, c in enumerate(sorted(alphabet))}, []))
+    tok.pre_tokenizer = pre_tokenizers.ByteLevel(add_prefix_space=False)
+    tok.decoder = decoders.ByteLevel()
+    t = HFTokenizer.from_tokenizer(tok)
+    text = "energy é 世界 ok"
+    ids = t.encode(text, add_bos=False)
+    assert len(ids) == len(text.encode("utf-8"))  # one token per byte: 世 and 界 span three tokens each
+    d = StreamDecoder(t)
+    pieces = [d.push([i]) for i in ids]
+    assert "".join(pieces) == text and all("�" not in p for p in pieces)
+    assert pieces[0] == "e"
+    syn = SyntheticTokenizer(1024)
+    sd = StreamDecoder(syn)
+    gen = [17, 18, 19, 20, 21, 22]
+    assert "".join(sd.push(gen[i:i + 2]) for i in range(0, 6, 2)) == syn.decode(gen)
+
+
+def test_streamed_response_concatenates_to_the_final_text(tmp_path, monkeypatch):
+    """/api/generate with stream: the NDJSON pieces join to the same text the non-streamed response carries."""
+    from cain_amd.client import OllamaClient
+    from cain_amd.serve import EngineBackend, ServerThread
+
+    make_checkpoint("qwen2", tmp_path / "ck", scale=4.0)
+    write_tokenizer(tmp_path / "ck")
+    monkeypatch.setenv("CAIN_CHECKPOINTS", f"q:tiny={tmp_path / 'ck'}")
+    be = EngineBackend(["q:tiny"], device="cpu", max_batch=2, max_context=64)
+    with ServerThread(be) as s:
+        c = OllamaClient(s.url)
+        pieces = []
+        st = c.generate("q:tiny", "w3 w4", stream=True, options={"temperature": 0, "num_predict": 6},
+                        on_chunk=pieces.append)
+        full = c.generate("q:tiny", "w3 w4", options={"temperature": 0, "num_predict": 6})
+    assert st.eval_count == 6 and "".join(pieces) == full.text
