@@ -28,6 +28,7 @@ from __future__ import annotations
 
 import json
 import os
+import re
 from pathlib import Path
 from typing import Dict, List, Optional, Tuple, Union
 
@@ -389,7 +390,10 @@ def ollama_blob(tag: str, models_dir: Optional[PathLike] = None) -> Path:
     model = [lay for lay in layers if str(lay.get("mediaType", "")).endswith(".image.model")]
     if not model:
         raise ValueError(f"Ollama manifest {manifest} has no model layer")
-    blob = root / "blobs" / str(model[0]["digest"]).replace(":", "-")
+    digest = str(model[0].get("digest", ""))
+    if not re.fullmatch(r"sha256:[0-9a-f]{64}", digest):
+        raise ValueError(f"Ollama manifest {manifest}: malformed model digest {digest!r}")
+    blob = root / "blobs" / digest.replace(":", "-")
     if not blob.is_file():
         raise FileNotFoundError(f"Ollama blob {blob} (for {tag!r}) is missing")
     return blob

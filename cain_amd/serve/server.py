@@ -536,6 +536,8 @@ class OllamaHandler(BaseHTTPRequestHandler):
             prompt = self.scheduler.backend.prompt_for(model, body, chat)
         except KeyError as exc:
             return self._send_json(404, {"error": str(exc).strip("'\"")})
+        except Exception as exc:  # noqa: BLE001 - a template that fails to render, a model that fails to load
+            return self._send_json(400, {"error": f"{type(exc).__name__}: {exc}"})
         opts = dict(body.get("options") or {})
         n = opts.get("num_predict")
         # the length policy reads the user's words ("In N words ..."), not the template around them

@@ -276,6 +276,12 @@ def test_ollama_store_blob_drives_the_tag(tmp_path, monkeypatch):
     assert ollama_blob("qwen2:1.5b", store) == store / "blobs" / f"sha256-{digest}"
     with pytest.raises(FileNotFoundError):
         ollama_blob("qwen2:7b", store)
+    bad = store / "manifests" / "registry.ollama.ai" / "library" / "evil" / "latest"
+    bad.parent.mkdir(parents=True)
+    bad.write_text(json.dumps({"layers": [{"mediaType": "application/vnd.ollama.image.model",
+                                           "digest": "sha256:../../../etc/passwd"}]}))
+    with pytest.raises(ValueError, match="malformed"):
+        ollama_blob("evil", store)
     ns = store / "manifests" / "registry.ollama.ai" / "someone" / "tiny" / "latest"
     ns.parent.mkdir(parents=True)
     ns.write_text(man.read_text())

@@ -339,3 +339,26 @@ def test_streamed_response_concatenates_to_the_final_text(tmp_path, monkeypatch)
                         on_chunk=pieces.append)
         full = c.generate("q:tiny", "w3 w4", options={"temperature": 0, "num_predict": 6})
     assert st.eval_count == 6 and "".join(pieces) == full.text
+
+
+def test_template_errors_are_http_400(tmp_path, monkeypatch):
+    """A chat template that raises (raise_exception, as real templates do on unsupported roles) is the request's
+    error (HTTP 400 with Ollama's {"error": ...}), not a server failure."""
+    import json
+
+    from cain_amd.client import OllamaClient, OllamaError
+    from cain_amd.serve import EngineBackend, ServerThread
+
+    make_checkpoint("gemma", tmp_path / "ck")
+    write_tokenizer(tmp_path / "ck", chat=True)
+    conf = json.loads((tmp_path / "ck" / "tokenizer_config.json").read_text())
+    conf["chat_template"] = ("{% for m in messages %}{% if m['role'] == 'system' %}"
+                             "{{ raise_exception('System role not supported') }}{% endif %}{{ m['content'] }}{% endfor %}")
+    (tmp_path / "ck" / "tokenizer_config.json").write_text(json.dumps(conf))
+    monkeypatch.setenv("CAIN_CHECKPOINTS", f"g:tiny={tmp_path / 'ck'}")
+    be = EngineBackend(["g:tiny"], device="cpu", max_batch=1, max_context=64)
+    with ServerThread(be) as s:
+        c = OllamaClient(s.url)
+        with pytest.raises(OllamaError, match="System role not supported"):
+            c.generate("g:tiny", "w3", system="w4", options={"num_predict": 2})
+        assert c.generate("g:tiny", "w3", options={"temperature": 0, "num_predict": 2}).eval_count == 2
