@@ -307,6 +307,10 @@ class _StudyBase:
         self.cpu_attribution = s.cpu_attribution
         # False on a rank that only hosts the node's remote server (parallel/fanout.py: it claims no runs)
         self.claims_runs = True
+        # weights provenance, printed with the config at start: tag -> checkpoint (CAIN_CHECKPOINTS, models/hf.py);
+        # tags not listed run random-init weights of their architecture
+        from ..models.hf import registered_checkpoints
+        self.checkpoints = registered_checkpoints()
         EventSubscriptionController.subscribe_to_multiple_events([
             (RunnerEvents.BEFORE_EXPERIMENT, self.before_experiment),
             (RunnerEvents.BEFORE_RUN, self.before_run),
