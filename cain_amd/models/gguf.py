@@ -444,6 +444,8 @@ def load_gguf_tokenizer(g: GGUFFile, cfg: Optional[ModelConfig] = None):
                      ("add_space_prefix", "add_prefix_space")):
         if f"tokenizer.ggml.{src}" in md:
             fields[dst] = md[f"tokenizer.ggml.{src}"]
+    for k in ("bos_token_id", "eos_token_id", "unk_token_id", "pad_token_id"):  # the converters read all four
+        fields.setdefault(k, None)
     conv = GGUF_TO_FAST_CONVERTERS.get({"gemma": "gemma2"}.get(arch, arch))
     if conv is None:
         return None
