@@ -10,8 +10,8 @@ format (one e8m0 scale per 32 weights, where Q4_K has a 6-bit scale and min per 
 
 * Container: GGUF v2 / v3, little-endian, every metadata value type, ``general.alignment``.  Tensors are read
   through ``numpy.memmap`` (nothing executes from the file).
-* Tensor types: F32, F16, BF16, Q8_0, Q4_0, Q4_1, Q5_0, Q5_1, Q4_K, Q5_K, Q6_K (Q4_K_M / Q4_0 / Q8_0 files, Ollama's
-  defaults).  Others (Q2_K, Q3_K, IQ*) are refused.  Each dequantiser follows the ggml block layout; it is
+* Tensor types: F32, F16, BF16, Q8_0, Q4_0, Q4_1, Q5_0, Q5_1, Q2_K, Q3_K, Q4_K, Q5_K, Q6_K (Ollama's q4_0 /
+  q4_K_M defaults and its q2_K / q3_K_* / q5_* / q6_K / q8_0 tags).  Others (IQ*, Q8_K, ...) are refused.  Each dequantiser follows the ggml block layout; it is
   vectorised with numpy over all blocks of a tensor.
 * Architectures: ``llama`` (Llama 3.1 and Mistral: llama.cpp converts both as ``llama``, with q / k rows permuted
   to interleaved RoPE pairs, undone here -- the same inverse transformers applies, ``tests/test_gguf.py``),
@@ -250,8 +250,37 @@ def _q6_k(b):
     return (d[:, :, None, None] * s * q).reshape(-1, 256)
 
 
-_DEQUANT = {"Q8_0": _q8_0, "Q4_0": _q4_0, "Q4_1": _q4_1, "Q5_0": _q5_0, "Q5_1": _q5_1, "Q4_K": _q4_k,
-            "Q5_K": _q5_k, "Q6_K": _q6_k}
+def _q2_k(b):
+    sc = b[:, 0:16].astype(np.int16)                   # 16 sub-blocks of 16: low nibble scale, high nibble min
+    qs = b[:, 16:80].reshape(-1, 2, 32).astype(np.int16)  # two halves of 128 values
+    d, dmin = _f16(b[:, 80:82]), _f16(b[:, 82:84])
+    shift = (2 * np.arange(4, dtype=np.int16))[None, None, :, None]
+    q = ((qs[:, :, None, :] >> shift) & 3).astype(np.float32)  # [n, half, j, 32]: value 128 h + 32 j + l
+    s = sc.reshape(-1, 2, 4, 2)[:, :, :, np.arange(32) // 16]  # scale index 8 h + 2 j + l // 16
+    return (d[:, :, None, None] * (s & 0xF) * q - dmin[:, :, None, None] * (s >> 4)).reshape(-1, 256)
+
+
+def _q3_k(b):
+    hm = b[:, 0:32].astype(np.int16)                   # high bit of each value: bit 4 h + j of byte l (+16)
+    qs = b[:, 32:96].reshape(-1, 2, 32).astype(np.int16)
+    raw = np.ascontiguousarray(b[:, 96:108]).view("<u4").astype(np.uint32)  # [n, 3]: the packed 6-bit scales
+    d = _f16(b[:, 108:110])
+    k1, k2 = np.uint32(0x03030303), np.uint32(0x0F0F0F0F)
+    a0, a1, t = raw[:, 0], raw[:, 1], raw[:, 2]
+    aux = np.stack([(a0 & k2) | (((t >> 0) & k1) << 4), (a1 & k2) | (((t >> 2) & k1) << 4),
+                    ((a0 >> 4) & k2) | (((t >> 4) & k1) << 4), ((a1 >> 4) & k2) | (((t >> 6) & k1) << 4)], 1)
+    scales = aux.astype("<u4").view(np.int8).reshape(-1, 16).astype(np.float32) - 32.0  # 16 six-bit scales
+    shift = (2 * np.arange(4, dtype=np.int16))[None, None, :, None]
+    lo = (qs[:, :, None, :] >> shift) & 3                   # [n, half, j, 32]
+    bit = (4 * np.arange(2, dtype=np.int16))[None, :, None, None] + np.arange(4, dtype=np.int16)[None, None, :, None]
+    hi = (hm[:, None, None, :] >> bit) & 1
+    q = (lo - np.where(hi == 1, 0, 4)).astype(np.float32)
+    s = scales.reshape(-1, 2, 4, 2)[:, :, :, np.arange(32) // 16]
+    return (d[:, :, None, None] * s * q).reshape(-1, 256)
+
+
+_DEQUANT = {"Q8_0": _q8_0, "Q4_0": _q4_0, "Q4_1": _q4_1, "Q5_0": _q5_0, "Q5_1": _q5_1, "Q2_K": _q2_k, "Q3_K": _q3_k,
+            "Q4_K": _q4_k, "Q5_K": _q5_k, "Q6_K": _q6_k}
 
 
 # ---------------------------------------------------------------------------------------------------- quantisers

@@ -83,6 +83,42 @@ def ref_block(name, b):
             is_ += 2
             u1 <<= 2
             u2 <<= 2
+    elif name == "Q2_K":
+        sc, qs = b[0:16], b[16:80]
+        d, dmin = _h(b, 80), _h(b, 82)
+        is_, yi = 0, 0
+        for n in range(2):
+            q = qs[32 * n: 32 * n + 32]
+            for j in range(4):
+                shift = 2 * j
+                for half16 in range(2):
+                    s = sc[is_]
+                    is_ += 1
+                    for l in range(16):
+                        y[yi + 16 * half16 + l] = d * (s & 0xF) * ((q[16 * half16 + l] >> shift) & 3) - dmin * (s >> 4)
+                yi += 32
+    elif name == "Q3_K":
+        hm, qs, raw = b[0:32], b[32:96], b[96:108]
+        d = _h(b, 108)
+        aux = [int.from_bytes(bytes(raw[4 * i:4 * i + 4]), "little") for i in range(3)]
+        k1, k2, tmp = 0x03030303, 0x0F0F0F0F, aux[2]
+        aux = [(aux[0] & k2) | (((tmp >> 0) & k1) << 4), (aux[1] & k2) | (((tmp >> 2) & k1) << 4),
+               ((aux[0] >> 4) & k2) | (((tmp >> 4) & k1) << 4), ((aux[1] >> 4) & k2) | (((tmp >> 6) & k1) << 4)]
+        scales = [((a >> (8 * i)) & 0xFF) for a in aux for i in range(4)]
+        m, is_, yi = 1, 0, 0
+        for n in range(2):
+            q = qs[32 * n: 32 * n + 32]
+            shift = 0
+            for j in range(4):
+                for half16 in range(2):
+                    dl = d * (scales[is_] - 32)
+                    is_ += 1
+                    for l in range(16):
+                        ll = 16 * half16 + l
+                        y[yi + ll] = dl * (((q[ll] >> shift) & 3) - (0 if hm[ll] & m else 4))
+                yi += 32
+                shift += 2
+                m <<= 1
     elif name == "Q6_K":
         ql, qh = b[0:128], b[128:192]
         sc = [x - 256 if x > 127 else x for x in b[192:208]]
@@ -105,13 +141,14 @@ def _random_blocks(name, n, seed=0):
     rng = np.random.default_rng(seed)
     _, bs, bb = GGML_TYPES[TYPE_ID[name]]
     raw = rng.integers(0, 256, (n, bb), dtype=np.uint8)
-    fp16_at = {"Q6_K": [208]}.get(name, [0, 2] if name in ("Q4_1", "Q5_1", "Q4_K", "Q5_K") else [0])
+    fp16_at = {"Q6_K": [208], "Q2_K": [80, 82], "Q3_K": [108]}.get(
+        name, [0, 2] if name in ("Q4_1", "Q5_1", "Q4_K", "Q5_K") else [0])
     for p in fp16_at:  # finite, moderate half-precision scales
         raw[:, p:p + 2] = np.frombuffer(rng.uniform(-2, 2, n).astype(np.float16).tobytes(), np.uint8).reshape(n, 2)
     return raw
 
 
-@pytest.mark.parametrize("name", ["Q4_0", "Q4_1", "Q5_0", "Q5_1", "Q8_0", "Q4_K", "Q5_K", "Q6_K"])
+@pytest.mark.parametrize("name", ["Q4_0", "Q4_1", "Q5_0", "Q5_1", "Q8_0", "Q2_K", "Q3_K", "Q4_K", "Q5_K", "Q6_K"])
 def test_block_decoders_match_the_scalar_reference(name):
     raw = _random_blocks(name, 6)
     bs = GGML_TYPES[TYPE_ID[name]][1]
@@ -152,9 +189,8 @@ def test_container_round_trip(tmp_path):
     assert torch.equal(g.tensor("q8"), torch.from_numpy(dequantize(quantize_q8_0(a), TYPE_ID["Q8_0"], a.size)
                                                         .reshape(a.shape)))
     assert float((g.tensor("q4") - at).abs().max()) < 0.6
-    for bad in ("Q2_K", "Q3_K"):
-        with pytest.raises(NotImplementedError):
-            dequantize(np.zeros(GGML_TYPES[TYPE_ID[bad]][2], np.uint8), TYPE_ID[bad], 256)
+    with pytest.raises(NotImplementedError):  # an IQ type
+        dequantize(np.zeros(64, np.uint8), 16, 256)
 
 
 def test_tensor_slices_cover_block_boundaries(tmp_path, monkeypatch):
