@@ -123,57 +123,60 @@ class GGUFFile:
         t = self.tensors[name]
         return np.memmap(self.path, dtype=np.uint8, mode="r", offset=t.offset, shape=(t.nbytes,))
 
-    def tensor(self, name: str) -> torch.Tensor:
-        """fp32 tensor (torch order) of ``name``, dequantised."""
+    def tensor(self, name: str, device="cpu", dtype: torch.dtype = torch.float32) -> torch.Tensor:
+        """``name`` dequantised (torch order) as ``dtype`` on ``device``: the quantised bytes travel, the blocks are
+        decoded there."""
         t = self.tensors.get(name)
         if t is None:
             raise KeyError(f"GGUF file has no tensor {name!r}")
         n = int(np.prod(t.shape))
         _, bs, bb = GGML_TYPES.get(t.type, ("?", 1, 0))
         raw = self.raw(name)
-        out = np.empty(n, np.float32)
+        out = torch.empty(n, dtype=dtype, device=device)
         # in slices of whole blocks: a 128k x 4096 Q4_K embedding would otherwise hold ~4x its fp32 size in temporaries
         step = max(1, SLICE_ELEMS // bs) * bs
         for e0 in range(0, n, step):
             e1 = min(n, e0 + step)
-            out[e0:e1] = dequantize(raw[e0 // bs * bb: e1 // bs * bb], t.type, e1 - e0)
-        return torch.from_numpy(out.reshape(t.shape))
+            out[e0:e1] = dequantize(raw[e0 // bs * bb: e1 // bs * bb], t.type, e1 - e0, device=device)
+        return out.reshape(t.shape)
 
     def has(self, name: str) -> bool:
         return name in self.tensors
 
 
 # ---------------------------------------------------------------------------------------------------- dequantisers
-def _f16(b: np.ndarray) -> np.ndarray:
-    return np.ascontiguousarray(b).view(np.float16).astype(np.float32)
+# torch ops over all blocks of a slice, on the tensor's device: the GPU dequantises a 128k x 4096 Q4_K embedding in
+# milliseconds, the CPU (multi-threaded) in about a second.  ``b`` is a uint8 [blocks, bytes per block] tensor.
+def _f16(b: torch.Tensor) -> torch.Tensor:
+    return b.contiguous().view(torch.float16).float()
 
 
-def _nibbles(qs: np.ndarray) -> Tuple[np.ndarray, np.ndarray]:
-    return (qs & 0x0F).astype(np.int16), (qs >> 4).astype(np.int16)
+def _nibbles(qs: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+    return (qs & 0x0F).to(torch.int16), (qs >> 4).to(torch.int16)
 
 
-def _k_scale_min(sc: np.ndarray) -> Tuple[np.ndarray, np.ndarray]:
-    """The 8 six-bit (scale, min) pairs of a K-quant super-block's 12 packed bytes -> two [n, 8] arrays."""
-    sc = sc.astype(np.uint16)
-    d = np.empty(sc.shape[:-1] + (8,), np.uint16)
-    m = np.empty_like(d)
-    d[..., :4] = sc[..., 0:4] & 63
-    m[..., :4] = sc[..., 4:8] & 63
-    d[..., 4:] = (sc[..., 8:12] & 0x0F) | ((sc[..., 0:4] >> 6) << 4)
-    m[..., 4:] = (sc[..., 8:12] >> 4) | ((sc[..., 4:8] >> 6) << 4)
-    return d.astype(np.float32), m.astype(np.float32)
+def _k_scale_min(sc: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+    """The 8 six-bit (scale, min) pairs of a K-quant super-block's 12 packed bytes -> two [n, 8] tensors."""
+    sc = sc.to(torch.int16)
+    d = torch.cat([sc[:, 0:4] & 63, (sc[:, 8:12] & 0x0F) | ((sc[:, 0:4] >> 6) << 4)], 1)
+    m = torch.cat([sc[:, 4:8] & 63, (sc[:, 8:12] >> 4) | ((sc[:, 4:8] >> 6) << 4)], 1)
+    return d.float(), m.float()
 
 
-def dequantize(raw: np.ndarray, ttype: int, n: int) -> np.ndarray:
-    """fp32 values of ``n`` elements stored as ggml type ``ttype`` in the bytes ``raw``."""
+def dequantize(raw, ttype: int, n: int, device=None) -> torch.Tensor:
+    """fp32 values (a torch tensor on ``device``, default the bytes' device) of ``n`` elements stored as ggml type
+    ``ttype`` in the bytes ``raw`` (numpy or torch uint8)."""
     name, bs, bb = GGML_TYPES.get(ttype, (f"type{ttype}", 0, 0))
-    raw = np.asarray(raw, dtype=np.uint8)
+    if isinstance(raw, np.ndarray):
+        raw = torch.from_numpy(np.array(raw, dtype=np.uint8))  # a copy: file maps are read-only
+    if device is not None:
+        raw = raw.to(device)
     if name == "F32":
-        return raw[: 4 * n].view(np.float32).copy()
+        return raw[: 4 * n].contiguous().view(torch.float32).clone()
     if name == "F16":
         return _f16(raw[: 2 * n])
     if name == "BF16":
-        return (raw[: 2 * n].view(np.uint16).astype(np.uint32) << 16).view(np.float32)
+        return raw[: 2 * n].contiguous().view(torch.bfloat16).float()
     if name not in _DEQUANT:
         raise NotImplementedError(f"GGUF tensor type {name} is not supported")
     if n % bs:
@@ -183,100 +186,99 @@ def dequantize(raw: np.ndarray, ttype: int, n: int) -> np.ndarray:
 
 
 def _q8_0(b):
-    return _f16(b[:, :2]) * b[:, 2:].view(np.int8).astype(np.float32)
+    return _f16(b[:, :2]) * b[:, 2:].view(torch.int8).float()
 
 
 def _q4_0(b):
     lo, hi = _nibbles(b[:, 2:])
-    return _f16(b[:, :2]) * (np.concatenate([lo, hi], 1) - 8).astype(np.float32)
+    return _f16(b[:, :2]) * (torch.cat([lo, hi], 1) - 8).float()
 
 
 def _q4_1(b):
     lo, hi = _nibbles(b[:, 4:])
-    return _f16(b[:, :2]) * np.concatenate([lo, hi], 1).astype(np.float32) + _f16(b[:, 2:4])
+    return _f16(b[:, :2]) * torch.cat([lo, hi], 1).float() + _f16(b[:, 2:4])
 
 
-def _q5_hi(qh: np.ndarray) -> Tuple[np.ndarray, np.ndarray]:
-    bits = np.ascontiguousarray(qh).view("<u4").astype(np.uint32)  # [n, 1]
-    j = np.arange(16, dtype=np.uint32)
-    return (((bits >> j) & 1) << 4).astype(np.int16), (((bits >> (j + 16)) & 1) << 4).astype(np.int16)
+def _q5_hi(qh: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+    bits = qh.contiguous().view(torch.int32).to(torch.int64)  # [n, 1]
+    j = torch.arange(16, device=qh.device, dtype=torch.int64)
+    return (((bits >> j) & 1) << 4).to(torch.int16), (((bits >> (j + 16)) & 1) << 4).to(torch.int16)
 
 
 def _q5_0(b):
     h0, h1 = _q5_hi(b[:, 2:6])
     lo, hi = _nibbles(b[:, 6:])
-    return _f16(b[:, :2]) * (np.concatenate([lo | h0, hi | h1], 1) - 16).astype(np.float32)
+    return _f16(b[:, :2]) * (torch.cat([lo | h0, hi | h1], 1) - 16).float()
 
 
 def _q5_1(b):
     h0, h1 = _q5_hi(b[:, 4:8])
     lo, hi = _nibbles(b[:, 8:])
-    return _f16(b[:, :2]) * np.concatenate([lo | h0, hi | h1], 1).astype(np.float32) + _f16(b[:, 2:4])
+    return _f16(b[:, :2]) * torch.cat([lo | h0, hi | h1], 1).float() + _f16(b[:, 2:4])
 
 
 def _q4_k(b):
     d, dmin = _f16(b[:, 0:2]), _f16(b[:, 2:4])
     sc, mn = _k_scale_min(b[:, 4:16])
-    qs = b[:, 16:144].reshape(-1, 4, 32)             # 4 groups of 64 values: 32 bytes each
-    lo, hi = _nibbles(qs)                              # [n, 4, 32]: sub-blocks 2g (low) and 2g + 1 (high)
-    q = np.stack([lo, hi], 2).reshape(-1, 8, 32).astype(np.float32)
+    lo, hi = _nibbles(b[:, 16:144].reshape(-1, 4, 32))  # 4 groups of 64 values: sub-blocks 2g (low), 2g + 1 (high)
+    q = torch.stack([lo, hi], 2).reshape(-1, 8, 32).float()
     return (d[:, :, None] * sc[:, :, None] * q - dmin[:, :, None] * mn[:, :, None]).reshape(-1, 256)
 
 
 def _q5_k(b):
     d, dmin = _f16(b[:, 0:2]), _f16(b[:, 2:4])
     sc, mn = _k_scale_min(b[:, 4:16])
-    qh = b[:, 16:48].astype(np.int16)                  # [n, 32]: bit 2g / 2g + 1 of byte l -> sub-block 2g / 2g + 1
+    qh = b[:, 16:48].to(torch.int16)[:, None, :]  # bit 2g / 2g + 1 of byte l: sub-block 2g / 2g + 1
     lo, hi = _nibbles(b[:, 48:176].reshape(-1, 4, 32))
-    g = np.arange(4)[None, :, None]
-    hb_lo = ((qh[:, None, :] >> (2 * g)) & 1) << 4
-    hb_hi = ((qh[:, None, :] >> (2 * g + 1)) & 1) << 4
-    q = np.stack([lo + hb_lo, hi + hb_hi], 2).reshape(-1, 8, 32).astype(np.float32)
+    g = torch.arange(4, device=b.device, dtype=torch.int16)[None, :, None]
+    q = torch.stack([lo + (((qh >> (2 * g)) & 1) << 4), hi + (((qh >> (2 * g + 1)) & 1) << 4)], 2)
+    q = q.reshape(-1, 8, 32).float()
     return (d[:, :, None] * sc[:, :, None] * q - dmin[:, :, None] * mn[:, :, None]).reshape(-1, 256)
 
 
+def _l16(device) -> torch.Tensor:
+    return torch.arange(32, device=device) // 16  # lane l of a 32-value group -> its 16-value sub-block
+
+
 def _q6_k(b):
-    ql = b[:, 0:128].reshape(-1, 2, 64).astype(np.int16)   # two halves of 128 values
-    qh = b[:, 128:192].reshape(-1, 2, 32).astype(np.int16)
-    sc = b[:, 192:208].view(np.int8).astype(np.float32).reshape(-1, 2, 8)
-    d = _f16(b[:, 208:210])                                  # [n, 1]
+    ql = b[:, 0:128].reshape(-1, 2, 64).to(torch.int16)  # two halves of 128 values
+    qh = b[:, 128:192].reshape(-1, 2, 32).to(torch.int16)
+    sc = b[:, 192:208].view(torch.int8).float().reshape(-1, 2, 4, 2)
+    d = _f16(b[:, 208:210])
     q1 = (ql[:, :, :32] & 0xF) | ((qh & 3) << 4)
     q2 = (ql[:, :, 32:] & 0xF) | (((qh >> 2) & 3) << 4)
     q3 = (ql[:, :, :32] >> 4) | (((qh >> 4) & 3) << 4)
     q4 = (ql[:, :, 32:] >> 4) | (((qh >> 6) & 3) << 4)
-    q = (np.stack([q1, q2, q3, q4], 2) - 32).astype(np.float32)  # [n, half, 4, 32]
-    # scale index: half h, quarter k, lane l -> sc[h, 2k + l // 16]
-    s = sc.reshape(-1, 2, 4, 2)[:, :, :, np.arange(32) // 16]    # [n, 2, 4, 32]
-    return (d[:, :, None, None] * s * q).reshape(-1, 256)
+    q = (torch.stack([q1, q2, q3, q4], 2) - 32).float()  # [n, half, quarter k, 32]: scale sc[half, 2k + l // 16]
+    return (d[:, :, None, None] * sc[:, :, :, _l16(b.device)] * q).reshape(-1, 256)
 
 
 def _q2_k(b):
-    sc = b[:, 0:16].astype(np.int16)                   # 16 sub-blocks of 16: low nibble scale, high nibble min
-    qs = b[:, 16:80].reshape(-1, 2, 32).astype(np.int16)  # two halves of 128 values
+    sc = b[:, 0:16].to(torch.int16).reshape(-1, 2, 4, 2)  # 16 sub-blocks of 16: low nibble scale, high nibble min
+    qs = b[:, 16:80].reshape(-1, 2, 32).to(torch.int16)   # two halves of 128 values
     d, dmin = _f16(b[:, 80:82]), _f16(b[:, 82:84])
-    shift = (2 * np.arange(4, dtype=np.int16))[None, None, :, None]
-    q = ((qs[:, :, None, :] >> shift) & 3).astype(np.float32)  # [n, half, j, 32]: value 128 h + 32 j + l
-    s = sc.reshape(-1, 2, 4, 2)[:, :, :, np.arange(32) // 16]  # scale index 8 h + 2 j + l // 16
-    return (d[:, :, None, None] * (s & 0xF) * q - dmin[:, :, None, None] * (s >> 4)).reshape(-1, 256)
+    shift = (2 * torch.arange(4, device=b.device, dtype=torch.int16))[None, None, :, None]
+    q = ((qs[:, :, None, :] >> shift) & 3).float()       # [n, half, j, 32]: value 128 h + 32 j + l
+    s = sc[:, :, :, _l16(b.device)]                       # scale index 8 h + 2 j + l // 16
+    return (d[:, :, None, None] * (s & 0xF).float() * q - dmin[:, :, None, None] * (s >> 4).float()).reshape(-1, 256)
 
 
 def _q3_k(b):
-    hm = b[:, 0:32].astype(np.int16)                   # high bit of each value: bit 4 h + j of byte l (+16)
-    qs = b[:, 32:96].reshape(-1, 2, 32).astype(np.int16)
-    raw = np.ascontiguousarray(b[:, 96:108]).view("<u4").astype(np.uint32)  # [n, 3]: the packed 6-bit scales
+    hm = b[:, 0:32].to(torch.int16)                       # high bit of value (h, j, l): bit 4 h + j of byte l
+    qs = b[:, 32:96].reshape(-1, 2, 32).to(torch.int16)
+    raw = b[:, 96:108].contiguous().view(torch.int32).to(torch.int64) & 0xFFFFFFFF  # the packed 6-bit scales
     d = _f16(b[:, 108:110])
-    k1, k2 = np.uint32(0x03030303), np.uint32(0x0F0F0F0F)
+    k1, k2 = 0x03030303, 0x0F0F0F0F
     a0, a1, t = raw[:, 0], raw[:, 1], raw[:, 2]
-    aux = np.stack([(a0 & k2) | (((t >> 0) & k1) << 4), (a1 & k2) | (((t >> 2) & k1) << 4),
-                    ((a0 >> 4) & k2) | (((t >> 4) & k1) << 4), ((a1 >> 4) & k2) | (((t >> 6) & k1) << 4)], 1)
-    scales = aux.astype("<u4").view(np.int8).reshape(-1, 16).astype(np.float32) - 32.0  # 16 six-bit scales
-    shift = (2 * np.arange(4, dtype=np.int16))[None, None, :, None]
-    lo = (qs[:, :, None, :] >> shift) & 3                   # [n, half, j, 32]
-    bit = (4 * np.arange(2, dtype=np.int16))[None, :, None, None] + np.arange(4, dtype=np.int16)[None, None, :, None]
+    aux = torch.stack([(a0 & k2) | (((t >> 0) & k1) << 4), (a1 & k2) | (((t >> 2) & k1) << 4),
+                       ((a0 >> 4) & k2) | (((t >> 4) & k1) << 4), ((a1 >> 4) & k2) | (((t >> 6) & k1) << 4)], 1)
+    scales = aux.to(torch.int32).contiguous().view(torch.int8).float().reshape(-1, 2, 4, 2) - 32.0
+    ar = torch.arange(4, device=b.device, dtype=torch.int16)
+    lo = (qs[:, :, None, :] >> (2 * ar)[None, None, :, None]) & 3  # [n, half, j, 32]
+    bit = (4 * torch.arange(2, device=b.device, dtype=torch.int16))[None, :, None, None] + ar[None, None, :, None]
     hi = (hm[:, None, None, :] >> bit) & 1
-    q = (lo - np.where(hi == 1, 0, 4)).astype(np.float32)
-    s = scales.reshape(-1, 2, 4, 2)[:, :, :, np.arange(32) // 16]
-    return (d[:, :, None, None] * s * q).reshape(-1, 256)
+    q = (lo - torch.where(hi == 1, 0, 4)).float()
+    return (d[:, :, None, None] * scales[:, :, :, _l16(b.device)] * q).reshape(-1, 256)
 
 
 _DEQUANT = {"Q8_0": _q8_0, "Q4_0": _q4_0, "Q4_1": _q4_1, "Q5_0": _q5_0, "Q5_1": _q5_1, "Q2_K": _q2_k, "Q3_K": _q3_k,
@@ -422,11 +424,11 @@ def load_gguf_weights(g: GGUFFile, cfg: ModelConfig, device="cpu", dtype=torch.b
     arch = g.metadata["general.architecture"]
 
     def w(name: str) -> torch.Tensor:
-        return g.tensor(name).to(device=device, dtype=dtype)
+        return g.tensor(name, device=device, dtype=dtype)
 
     def norm(name: str) -> torch.Tensor:
-        t = g.tensor(name)
-        return (t - 1.0 if arch == "gemma" else t).to(device=device, dtype=dtype)  # GGUF Gemma stores 1 + w
+        t = g.tensor(name, device=device)
+        return (t - 1.0 if arch == "gemma" else t).to(dtype)  # GGUF Gemma stores 1 + w
 
     f = cfg.ffn
     layers = []
@@ -436,10 +438,10 @@ def load_gguf_weights(g: GGUFFile, cfg: ModelConfig, device="cpu", dtype=torch.b
             wqkv = w(p + "attn_qkv.weight")
             bqkv = w(p + "attn_qkv.bias") if g.has(p + "attn_qkv.bias") else None
         else:
-            q, kk = g.tensor(p + "attn_q.weight"), g.tensor(p + "attn_k.weight")
+            q, kk = w(p + "attn_q.weight"), w(p + "attn_k.weight")
             if arch == "llama":
                 q, kk = unpermute_qk(q, cfg.n_heads), unpermute_qk(kk, cfg.n_kv_heads)
-            wqkv = torch.cat([q, kk, g.tensor(p + "attn_v.weight")], 0).to(device=device, dtype=dtype)
+            wqkv = torch.cat([q, kk, w(p + "attn_v.weight")], 0)
             bqkv = (torch.cat([w(p + f"attn_{x}.bias") for x in "qkv"], 0) if g.has(p + "attn_q.bias") else None)
         if g.has(p + "ffn_gate.weight"):
             w_gate, w_up = w(p + "ffn_gate.weight"), w(p + "ffn_up.weight")

@@ -152,15 +152,15 @@ def _random_blocks(name, n, seed=0):
 def test_block_decoders_match_the_scalar_reference(name):
     raw = _random_blocks(name, 6)
     bs = GGML_TYPES[TYPE_ID[name]][1]
-    got = dequantize(raw.reshape(-1), TYPE_ID[name], 6 * bs).reshape(6, bs)
+    got = dequantize(raw.reshape(-1), TYPE_ID[name], 6 * bs).numpy().reshape(6, bs)
     for i in range(6):
         np.testing.assert_allclose(got[i], ref_block(name, raw[i]), rtol=1e-6, atol=1e-6, err_msg=name)
 
 
 def test_q8_0_and_q4_0_round_trip():
     x = np.random.default_rng(1).normal(0, 1, 32 * 64).astype(np.float32)
-    y8 = dequantize(quantize_q8_0(x), TYPE_ID["Q8_0"], x.size)
-    y4 = dequantize(quantize_q4_0(x), TYPE_ID["Q4_0"], x.size)
+    y8 = dequantize(quantize_q8_0(x), TYPE_ID["Q8_0"], x.size).numpy()
+    y4 = dequantize(quantize_q4_0(x), TYPE_ID["Q4_0"], x.size).numpy()
     amax = np.abs(x.reshape(-1, 32)).max(1, keepdims=True)
     assert np.all(np.abs(y8 - x).reshape(-1, 32) <= amax / 127 * 0.5 + 1e-3 * amax)
     # Q4_0's 16 levels run -8 d .. 7 d around the signed maximum: half a step inside, one step at the far end
@@ -186,8 +186,7 @@ def test_container_round_trip(tmp_path):
     assert torch.equal(g.tensor("f32"), at)
     assert torch.equal(g.tensor("f16"), at.half().float())
     assert torch.equal(g.tensor("bf16"), at.bfloat16().float())
-    assert torch.equal(g.tensor("q8"), torch.from_numpy(dequantize(quantize_q8_0(a), TYPE_ID["Q8_0"], a.size)
-                                                        .reshape(a.shape)))
+    assert torch.equal(g.tensor("q8"), dequantize(quantize_q8_0(a), TYPE_ID["Q8_0"], a.size).reshape(a.shape))
     assert float((g.tensor("q4") - at).abs().max()) < 0.6
     with pytest.raises(NotImplementedError):  # an IQ type
         dequantize(np.zeros(64, np.uint8), 16, 256)
