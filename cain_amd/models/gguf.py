@@ -11,8 +11,9 @@ format (one e8m0 scale per 32 weights, where Q4_K has a 6-bit scale and min per 
 * Container: GGUF v2 / v3, little-endian, every metadata value type, ``general.alignment``.  Tensors are read
   through ``numpy.memmap`` (nothing executes from the file).
 * Tensor types: F32, F16, BF16, Q8_0, Q4_0, Q4_1, Q5_0, Q5_1, Q2_K, Q3_K, Q4_K, Q5_K, Q6_K (Ollama's q4_0 /
-  q4_K_M defaults and its q2_K / q3_K_* / q5_* / q6_K / q8_0 tags).  Others (IQ*, Q8_K, ...) are refused.  Each dequantiser follows the ggml block layout; it is
-  vectorised with numpy over all blocks of a tensor.
+  q4_K_M defaults and its q2_K / q3_K_* / q5_* / q6_K / q8_0 tags).  Others (IQ*, Q8_K, ...) are refused.  Each
+  decoder follows the ggml block layout in torch ops over all blocks of a tensor slice, on the load device: the
+  quantised bytes go to the GPU and are decoded there.
 * Architectures: ``llama`` (Llama 3.1 and Mistral: llama.cpp converts both as ``llama``, with q / k rows permuted
   to interleaved RoPE pairs, undone here -- the same inverse transformers applies, ``tests/test_gguf.py``),
   ``qwen2``, ``gemma`` (norm gains stored as 1 + w: w is restored) and ``phi3`` (fused ``attn_qkv``; ``ffn_up``
