@@ -202,9 +202,19 @@ class EngineBackend(Backend):
         cfg = get_config(model)
         ckpt = checkpoint_for(model)
         info = cfg.as_dict() | ({"checkpoint": ckpt} if ckpt else {"weights": "random-init"})
-        return {"details": {"family": cfg.name.split(":")[0], "parameter_size": f"{cfg.n_params() / 1e9:.1f}B",
-                            "quantization_level": QUANT_LEVEL[self.weight_dtype], "format": "cain-packed"},
-                "model_info": info}
+        out = {"details": {"family": cfg.name.split(":")[0], "parameter_size": f"{cfg.n_params() / 1e9:.1f}B",
+                           "quantization_level": QUANT_LEVEL[self.weight_dtype], "format": "cain-packed"},
+               "model_info": info}
+        if ckpt:  # as Ollama's show: the prompt template and the stop tokens (a checkpoint's)
+            from ..models.hf import load_tokenizer
+
+            tok = load_tokenizer(ckpt, cfg)
+            if tok is not None:
+                out["template"] = tok.chat_template or ""
+                stops = [i for i in (cfg.eos_id, *cfg.stop_ids) if i >= 0]
+                out["parameters"] = "\n".join(f"stop {json.dumps(tok.tok.id_to_token(i))}" for i in stops
+                                               if tok.tok.id_to_token(i) is not None)
+        return out
 
     def run(self, model: str, jobs: List[Job]) -> None:
         eng = self.engine(model)

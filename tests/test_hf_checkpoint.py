@@ -223,6 +223,7 @@ def test_server_serves_a_checkpoint(tmp_path, monkeypatch):
         conn.close()
         assert info["model_info"]["checkpoint"] == str(tmp_path / "g")
         assert info["model_info"]["head_dim"] == 256
+        assert info["template"] == "" and 'stop "</s>"' in info["parameters"]  # eos 2 = </s>
         r = c.generate("gemma-real:2b", "w3 w4 w5", options={"temperature": 0, "num_predict": 5})
     ids = be.engine("gemma-real:2b").encode("w3 w4 w5")
     with torch.no_grad():
