@@ -356,3 +356,42 @@ def test_gguf_sentencepiece_vocabulary(arch, tmp_path):
         assert tok.decode(ids) == "the word energy"
     # phi3: transformers' Phi-3 converter lays Phi-3's own added tokens (ids 32000+) and normaliser over the vocabulary;
     # on this 275-piece toy vocabulary it drops the word boundaries, so only loading and encoding are checked here
+
+
+@pytest.mark.parametrize("arch, their", [("llama", "llama"), ("qwen2", "qwen2"), ("phi3", "phi3"), ("gemma", "gemma2")])
+def test_metadata_keys_match_transformers_gguf_mapping(arch, their):
+    """The GGUF metadata keys config_from_gguf reads are the ones transformers' GGUF loader maps onto the same
+    config fields (transformers.integrations.ggml.GGUF_CONFIG_MAPPING; gemma 1 files use gemma 2's key names)."""
+    from transformers.integrations.ggml import GGUF_CONFIG_MAPPING
+
+    ours = {"block_count": "num_hidden_layers", "context_length": "max_position_embeddings",
+            "embedding_length": "hidden_size", "feed_forward_length": "intermediate_size",
+            "attention.head_count": "num_attention_heads", "attention.head_count_kv": "num_key_value_heads",
+            "rope.freq_base": "rope_theta", "attention.layer_norm_rms_epsilon": "rms_norm_eps"}
+    m = GGUF_CONFIG_MAPPING[their]
+    for key, field in ours.items():
+        assert m.get(key) == field, (arch, key, m.get(key))
+    # and the exporter writes exactly those keys under the architecture's prefix
+    cfg = get_config_for_test(arch)
+    md = GGUFMeta(cfg, arch)
+    for key in ours:
+        assert f"{arch}.{key}" in md
+
+
+def get_config_for_test(arch):
+    from cain_amd.models import TINY
+
+    return TINY[{"llama": "tiny-llama3.1:8b", "qwen2": "tiny-qwen2:1.5b", "phi3": "tiny-phi3:3.8b",
+                 "gemma": "tiny-gemma:2b"}[arch]]
+
+
+def GGUFMeta(cfg, arch):  # noqa: N802 - the metadata export_gguf writes, read back
+    import tempfile
+    from pathlib import Path
+
+    from cain_amd.models import random_weights
+
+    with tempfile.TemporaryDirectory() as td:
+        p = Path(td) / "m.gguf"
+        export_gguf(random_weights(cfg, dtype=torch.float32), p, arch, tensor_type="F16")
+        return GGUFFile(p).metadata
