@@ -258,8 +258,10 @@ def test_q8_0_gguf_is_close_and_engine_loads_it(tmp_path, monkeypatch):
     assert rel < 0.03, rel
 
 
-def test_gguf_tokenizer_through_transformers_converter(tmp_path):
-    """A byte-level BPE vocabulary stored the GGUF way (tokens, merges) comes back as a working tokenizer."""
+@pytest.mark.parametrize("arch", ["qwen2", "llama"])
+def test_gguf_tokenizer_through_transformers_converter(arch, tmp_path):
+    """A byte-level BPE vocabulary stored the GGUF way (tokens, merges; Qwen2's and Llama 3's kind) comes back as a
+    working tokenizer."""
     from tokenizers import Tokenizer, decoders, models, pre_tokenizers, trainers
 
     tok = Tokenizer(models.BPE())
@@ -273,11 +275,11 @@ def test_gguf_tokenizer_through_transformers_converter(tmp_path):
     vocab = spec["model"]["vocab"]
     tokens = [t for t, _ in sorted(vocab.items(), key=lambda kv: kv[1])]
     merges = [m if isinstance(m, str) else " ".join(m) for m in spec["model"]["merges"]]
-    model = make_checkpoint("qwen2", tmp_path / "hf")
+    model = make_checkpoint("qwen2" if arch == "qwen2" else "llama", tmp_path / "hf")
     _, mw, _ = load_pretrained(tmp_path / "hf")
     fields = {"tokenizer.ggml.model": "gpt2", "tokenizer.ggml.tokens": tokens, "tokenizer.ggml.merges": merges,
               "tokenizer.ggml.token_type": [1] * len(tokens)}
-    export_gguf(mw, tmp_path / "t.gguf", "qwen2", tokenizer_fields=fields)
+    export_gguf(mw, tmp_path / "t.gguf", arch, tokenizer_fields=fields)
     _, _, gt = load_gguf(tmp_path / "t.gguf")
     s = "please give me information about remote energy"
     ids = gt.encode(s, add_bos=False)
