@@ -107,12 +107,38 @@ def cmd_generate(args: List[str]) -> None:
     server.generate_main(args)
 
 
+def cmd_convert(args: List[str]) -> None:
+    """``convert <checkpoint dir | .gguf> <out.gguf> [--type F16]``: a checkpoint as a GGUF file with llama.cpp's
+    conventions (models/gguf.py export_gguf), e.g. to run the same weights under llama.cpp / Ollama."""
+    import torch
+
+    from ..models.gguf import ARCHS, export_gguf
+    from ..models.hf import load_pretrained
+
+    ap = argparse.ArgumentParser(prog="python -m cain_amd convert")
+    ap.add_argument("src", help="a Hugging Face checkpoint directory or a GGUF file")
+    ap.add_argument("dst", help="the GGUF file to write")
+    ap.add_argument("--type", default="F16", choices=["F32", "F16", "BF16", "Q8_0", "Q4_0"])
+    ap.add_argument("--arch", default=None, choices=list(ARCHS),
+                    help="GGUF architecture (default: from the checkpoint; Mistral is written as llama)")
+    ns = ap.parse_args(args)
+    cfg, mw, _ = load_pretrained(ns.src, dtype=torch.float32)
+    arch = ns.arch
+    if arch is None:
+        arch = ("gemma" if cfg.norm_add_one else "qwen2" if cfg.qkv_bias else
+                "phi3" if cfg.head_dim == 96 else "llama")
+        print(f"architecture: {arch} (pass --arch to override)")
+    export_gguf(mw, ns.dst, arch, tensor_type=ns.type)
+    print(f"wrote {ns.dst}: {cfg.n_layers} layers, d {cfg.d_model}, {ns.type}")
+
+
 COMMANDS = {
     "config-create": ("[path_to_user_specified_dir]", cmd_config_create),
     "prepare": ("", cmd_prepare),
     "analyze": ("<run_table.csv> [--out DIR]", cmd_analyze),
     "serve": ("[--host H] [--port P] [--models m1,m2] [--device N]", cmd_serve),
-    "generate": ("--model M --prompt P [--num-predict N]", cmd_generate),
+    "generate": ("--model M --prompt P [--num-predict N] [--checkpoint PATH]", cmd_generate),
+    "convert": ("<checkpoint dir | .gguf> <out.gguf> [--type F16|Q8_0|Q4_0|...]", cmd_convert),
     "help": ("", cmd_help),
 }
 

@@ -397,3 +397,23 @@ def GGUFMeta(cfg, arch):  # noqa: N802 - the metadata export_gguf writes, read b
         p = Path(td) / "m.gguf"
         export_gguf(random_weights(cfg, dtype=torch.float32), p, arch, tensor_type="F16")
         return GGUFFile(p).metadata
+
+
+def test_convert_cli_round_trip(tmp_path):
+    """python -m cain_amd convert <hf dir> <out.gguf>: the written file loads back to the checkpoint's logits."""
+    import subprocess
+    import sys
+    from pathlib import Path
+
+    root = Path(__file__).resolve().parent.parent
+    model = make_checkpoint("llama", tmp_path / "hf", scale=4.0)
+    r = subprocess.run([sys.executable, "-m", "cain_amd", "convert", str(tmp_path / "hf"), str(tmp_path / "o.gguf"),
+                        "--type", "F32"], capture_output=True, text=True, cwd=str(root), timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "architecture: llama" in r.stdout
+    _, mg, _ = load_gguf(tmp_path / "o.gguf", dtype=torch.float32)
+    tokens = torch.randint(3, 1024, (1, 8), generator=torch.Generator().manual_seed(2))
+    pos = torch.arange(8)[None]
+    theirs = hf_logits(model, tokens, pos)
+    ours = ReferenceModel(mg).forward(tokens, positions=pos)
+    assert float((ours - theirs).abs().max() / theirs.abs().max()) < 2e-5
