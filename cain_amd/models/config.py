@@ -53,6 +53,8 @@ class ModelConfig:
     # further stop ids beside eos_id (at most 3 reach the sampler): a checkpoint's other end ids and its chat
     # template's turn-end tokens (hf.py / gguf.py), as Ollama stops on its templates' stop strings
     stop_ids: Tuple[int, ...] = ()
+    # the architecture family of a loaded checkpoint (llama, mistral, qwen2, gemma, phi3; "" for the built-in tags)
+    family: str = ""
 
     @property
     def group(self) -> int:

@@ -415,7 +415,7 @@ def config_from_gguf(g: GGUFFile, name: Optional[str] = None) -> ModelConfig:
         rope_theta=float(k("rope.freq_base", 10000.0)), norm_eps=float(k("attention.layer_norm_rms_epsilon", 1e-5)),
         norm_add_one=gemma, embed_scale=gemma, max_context=ctx,
         bos_id=int(md.get("tokenizer.ggml.bos_token_id", 1)), eos_id=int(md.get("tokenizer.ggml.eos_token_id", 2)),
-        rope_freq_factors=factors)
+        rope_freq_factors=factors, family=arch)
     from .hf import with_stop_ids
 
     return with_stop_ids(cfg, gguf_stop_ids(g))

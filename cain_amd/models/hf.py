@@ -148,7 +148,7 @@ def config_from_hf(hf: Union[Dict, PathLike], name: Optional[str] = None,
         vocab=int(hf["vocab_size"]), act=act, tie_embeddings=tie, qkv_bias=qkv_bias, rope_theta=theta,
         rope_scaling=scaling, norm_eps=float(hf.get("rms_norm_eps", 1e-6)), norm_add_one=fam == "gemma",
         embed_scale=fam == "gemma", max_context=max_ctx, bos_id=_first(hf.get("bos_token_id"), 1),
-        eos_id=_last(hf.get("eos_token_id"), 2), stop_ids=_other_ends(hf.get("eos_token_id")))
+        eos_id=_last(hf.get("eos_token_id"), 2), stop_ids=_other_ends(hf.get("eos_token_id")), family=fam)
 
 
 def _other_ends(v) -> Tuple[int, ...]:

@@ -125,8 +125,9 @@ def cmd_convert(args: List[str]) -> None:
     cfg, mw, _ = load_pretrained(ns.src, dtype=torch.float32)
     arch = ns.arch
     if arch is None:
-        arch = ("gemma" if cfg.norm_add_one else "qwen2" if cfg.qkv_bias else
-                "phi3" if cfg.head_dim == 96 else "llama")
+        arch = {"mistral": "llama"}.get(cfg.family, cfg.family)
+        if arch not in ARCHS:
+            raise SystemExit(f"cannot tell the GGUF architecture of {ns.src}: pass --arch")
         print(f"architecture: {arch} (pass --arch to override)")
     export_gguf(mw, ns.dst, arch, tensor_type=ns.type)
     print(f"wrote {ns.dst}: {cfg.n_layers} layers, d {cfg.d_model}, {ns.type}")

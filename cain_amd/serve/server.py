@@ -202,7 +202,8 @@ class EngineBackend(Backend):
         cfg = get_config(model)
         ckpt = checkpoint_for(model)
         info = cfg.as_dict() | ({"checkpoint": ckpt} if ckpt else {"weights": "random-init"})
-        out = {"details": {"family": cfg.name.split(":")[0], "parameter_size": f"{cfg.n_params() / 1e9:.1f}B",
+        out = {"details": {"family": cfg.family or cfg.name.split(":")[0],
+                           "parameter_size": f"{cfg.n_params() / 1e9:.1f}B",
                            "quantization_level": QUANT_LEVEL[self.weight_dtype], "format": "cain-packed"},
                "model_info": info}
         if ckpt:  # as Ollama's show: the prompt template and the stop tokens (a checkpoint's)
