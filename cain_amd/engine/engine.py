@@ -29,7 +29,7 @@ import ctypes
 import math
 import os
 import time
-from dataclasses import dataclass, field
+from dataclasses import dataclass
 from typing import Dict, List, Optional, Sequence, Union
 
 import numpy as np
@@ -37,7 +37,7 @@ import torch
 
 from ..models.config import ModelConfig, get_config, rope_inv_freq
 from ..models.hf import checkpoint_for, load_hf_weights, load_pretrained, load_tokenizer
-from ..models.tokenizer import SyntheticTokenizer, get_tokenizer
+from ..models.tokenizer import get_tokenizer
 from ..models.weights import WEIGHT_DTYPES, ModelWeights, pack_for_engine, random_weights, roundtrip_weights
 
 #: Ollama's default sampling options (SURVEY §2.4 "Sampling" row)
