@@ -85,10 +85,19 @@ struct W4Split {
   float* part;     // [tiles * ks][64 lanes][4] fp32 partial blocks
   unsigned* ctr;   // [tiles] tickets, zero at rest
 };
-constexpr long long W4_CTR_BYTES = 16 * 1024;  // the workspace's ticket region (4,096 tiles), partials after it
+// The engine's GEMM workspace is shared by every weight format: [0, 64 KiB) holds the bf16 batched path's tickets and
+// [64, 80 KiB) the wide path's counters, both zero at rest (gemm.hip GEMM_SLAB_OFFSET).  The W4 tickets (4,096 tiles)
+// live in [0, 16 KiB) -- they too are zero at rest -- and the partials, which are not, start at 80 KiB as the other
+// formats' slabs do (wgemm8.hip W8_SLAB_OFFSET), so a mixed-format forward never reads a partial as a ticket.
+constexpr long long W4_CTR_BYTES = 16 * 1024;
+constexpr long long W4_PART_OFFSET = 80 * 1024;
 
-// 4 waves per SIMD (<= 128 VGPRs): the grid below assumes 16 resident waves per CU
-template <int WAVES, int U, int EPI, bool NORM>
+// 4 waves per SIMD (<= 128 VGPRs): the grid below assumes 16 resident waves per CU.
+// SPLIT is a template parameter, not a runtime branch: with the split path compiled into every instance (round 5),
+// hipcc lost the loop's counted waits -- 15-20 vmcnt(0) per kernel instead of 0-5, the steady-state ring drained at
+// every item -- and MXFP4 batch-1 decode fell 5-13 % on all seven models (tests/test_isa_guard.py now
+// checks the built code object).  Unsplit launches run the SPLIT = false instance, which compiles as before.
+template <int WAVES, int U, int EPI, bool NORM, bool SPLIT>
 __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(4, 4))) void w4_stream_kernel(
     const GemmArgs a, const uint8_t* __restrict__ wsc, int npairs, const W4Split sp) {
   constexpr int XLB = w4_xl_bytes<WAVES>();
@@ -98,7 +107,7 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(4, 4
   __shared__ float row_ss[16];  // NORM: the sum of squares of each activation row
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
-  const int KS = sp.ks;
+  const int KS = SPLIT ? sp.ks : 1;
   const int KQT = a.K >> 7;                   // 128-wide k quads per tile
   const int KQ = KQT / KS;                    // k quads per pair (the host keeps KQT % KS == 0)
   const int qmax = (KQ + WAVES - 1) / WAVES;  // items per pair (every wave walks the same sequence length)
@@ -144,10 +153,6 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(4, 4
   for (int u = 0; u < U; ++u) load_next(ring[u]);
 
   int cp_t = blockIdx.x;
-  // FOLD: the fused QKV epilogue at 8 waves sums each unit once into LDS before the epilogue (below); summing the
-  // own and the partner unit per lane straight from the 8 partial slabs spilled that kernel (28 B per lane at the
-  // 128-register budget of 4 waves per SIMD; 84-102 registers folded)
-  constexpr bool FOLD = EPI == EPI_QKV_ROPE && WAVES == 8;
   EpiIn pre{};
   if (wave == 0 && my_tiles > 0) pre = epi_load_at<EPI>(a, cp_t / KS, lane & 15, lane);
 #pragma unroll
@@ -202,7 +207,7 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(4, 4
     if (wave == 0) {
       const int tile = cp_t / KS;
       if (cp_n > 0) pre = epi_load_at<EPI>(a, tile, lane & 15, lane);  // later tiles (none for fp32 / act epis)
-      if (KS > 1) {
+      if constexpr (SPLIT) {
         // split-K: publish this pair's partial, take the tile's ticket; the last arriver finishes the tile
         f32x4 v = red[buf][0][lane];
 #pragma unroll
@@ -239,15 +244,7 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(4, 4
         if constexpr (NORM) v *= rms_inv(row_ss[min(l & 15, a.M - 1)], a.K, a.eps);
         return v;
       };
-      if constexpr (FOLD) {
-        // pair epilogue at 8 waves: each lane sums its own unit once and writes it back, the epilogue reads its
-        // units (own and partner row) from there -- summing both units per lane held 2 x 8 partials in flight
-        // and spilled.  One wave: its LDS operations complete in order, so the reads see the writes.
-        red[buf][0][lane] = unit_sum(lane);
-        epi_store<EPI>(a, tile, lane & 15, lane, pre, [&](int off) { return red[buf][0][lane + off]; });
-      } else {
-        epi_store<EPI>(a, tile, lane & 15, lane, pre, [&](int off) { return unit_sum(lane + off); });
-      }
+      epi_store<EPI>(a, tile, lane & 15, lane, pre, [&](int off) { return unit_sum(lane + off); });
     }
     buf ^= 1;
   };
@@ -400,8 +397,24 @@ static hipError_t w4_launch_var(int var, const GemmArgs& a, const uint8_t* wsc, 
                                 const W4Split& sp, hipStream_t st) {
   const dim3 g(grid), b8(512), b4(256);
   switch (var) {
-    case W4S_8_4: hipLaunchKernelGGL((w4_stream_kernel<8, 4, EPI, NORM>), g, b8, 0, st, a, wsc, npairs, sp); break;
-    case W4S_4_4: hipLaunchKernelGGL((w4_stream_kernel<4, 4, EPI, NORM>), g, b4, 0, st, a, wsc, npairs, sp); break;
+    case W4S_8_4:
+      // the fused QKV epilogue runs on 4 waves only (at 8 its partner-unit sums spill; w4_variant never picks it)
+      if constexpr (EPI == EPI_QKV_ROPE)
+        hipLaunchKernelGGL((w4_stream_kernel<4, 4, EPI, NORM, false>), g, b4, 0, st, a, wsc, npairs, sp);
+      else if (sp.ks > 1)
+        hipLaunchKernelGGL((w4_stream_kernel<8, 4, EPI, NORM, true>), g, b8, 0, st, a, wsc, npairs, sp);
+      else
+        hipLaunchKernelGGL((w4_stream_kernel<8, 4, EPI, NORM, false>), g, b8, 0, st, a, wsc, npairs, sp);
+      break;
+    case W4S_4_4:
+      if constexpr (EPI != EPI_QKV_ROPE) {
+        if (sp.ks > 1) {
+          hipLaunchKernelGGL((w4_stream_kernel<4, 4, EPI, NORM, true>), g, b4, 0, st, a, wsc, npairs, sp);
+          break;
+        }
+      }
+        hipLaunchKernelGGL((w4_stream_kernel<4, 4, EPI, NORM, false>), g, b4, 0, st, a, wsc, npairs, sp);
+      break;
     case W4T_8_2_1: hipLaunchKernelGGL((w4_tile_kernel<8, 2, 1, EPI, NORM>), g, b8, 0, st, a, wsc); break;
     case W4T_4_4_1: hipLaunchKernelGGL((w4_tile_kernel<4, 4, 1, EPI, NORM>), g, b4, 0, st, a, wsc); break;
     case W4T_8_2_2: hipLaunchKernelGGL((w4_tile_kernel<8, 2, 2, EPI, NORM>), g, b8, 0, st, a, wsc); break;
@@ -453,7 +466,7 @@ static int w4_variant(int N, int K, int M, int epi, int n_cu) {
   (void)N, (void)n_cu;
   const int kq = K / 128;
   if (g_w4_var >= 0) {
-    const int v = g_w4_var;
+    const int v = g_w4_var == W4S_8_4 && epi == EPI_QKV_ROPE ? W4S_4_4 : g_w4_var;  // no 8-wave QKV kernel
     if (!w4_is_stream(v) || w4_stream_fits(W4_WAVES[v], K, M)) return v;  // a stream shape needs its LDS copy
   }
   // 4 waves as well when K is short: below 3 quads per wave of the 8-wave shape its waves idle on the padding
@@ -467,7 +480,7 @@ static int w4_variant(int N, int K, int M, int epi, int n_cu) {
 
 CAIN_API int cain_gemm_w4_variant(int N, int K, int M, int epi) { return w4_variant(N, K, M, epi & EPI_MASK, w4_n_cu()); }
 
-static long long w4_split_bytes(int N, int ks) { return W4_CTR_BYTES + (long long)(N / 16) * ks * 64 * 16; }
+static long long w4_split_bytes(int N, int ks) { return W4_PART_OFFSET + (long long)(N / 16) * ks * 64 * 16; }
 
 // k ranges per tile of a stream-kernel GEMM: the most (up to 4) that keep tiles x ks <= CUs (one pair per CU: the
 // ticket's last arriver adds a memory round trip, so pairs beyond the CU count buy nothing), every range >= 32 k
@@ -478,8 +491,10 @@ static long long w4_split_bytes(int N, int ks) { return W4_CTR_BYTES + (long lon
 // ticket's round trip; with this rule (gemma:2b's down alone) 1,084 -> 1,127 tok/s, qwen2:1.5b unchanged.  A budget
 // of 2 x CUs (gemma:7b / qwen2:7b down, 192 / 224 tiles, in two) measured slower: 559 -> 548, 628 -> 615.  Ranges
 // down to 32 quads (qwen2:1.5b's down alone, 35): 985 / 978 -> 991 / 993 tok/s; its O (6 quads) stays unsplit.
-static int w4_split(int var, int N, int K, int n_cu, long long ws_bytes) {
-  if (!w4_is_stream(var) || g_w4_split == 1) return 1;
+static int w4_split(int var, int N, int K, int epi, int n_cu, long long ws_bytes) {
+  // the fused QKV epilogue has no split instance (its outputs are never narrow enough to pay: 128+ tiles of <= 16
+  // quads on the study's models)
+  if (!w4_is_stream(var) || g_w4_split == 1 || epi == EPI_QKV_ROPE) return 1;
   const int tiles = N / 16, kq = K / 128, waves = W4_WAVES[var];
   auto ok = [&](int k) {
     return k > 1 && kq % k == 0 && kq / k >= waves && tiles <= 4096 && w4_split_bytes(N, k) <= ws_bytes;
@@ -493,7 +508,7 @@ static int w4_split(int var, int N, int K, int n_cu, long long ws_bytes) {
 
 CAIN_API int cain_gemm_w4_split(int N, int K, int M, int epi, long long ws_bytes) {
   const int n_cu = w4_n_cu();
-  return w4_split(w4_variant(N, K, M, epi & EPI_MASK, n_cu), N, K, n_cu, ws_bytes);
+  return w4_split(w4_variant(N, K, M, epi & EPI_MASK, n_cu), N, K, epi & EPI_MASK, n_cu, ws_bytes);
 }
 
 // Workspace a W4 GEMM of this shape may use (split-K tickets + partials; 0: none)
@@ -543,10 +558,10 @@ CAIN_API int cain_gemm_w4_ex(const void* Wp, const void* wsc, const void* X, int
   int np = npairs;
   if (w4_is_stream(var)) {  // persistent: at most the resident workgroups (2 of 8 waves / 4 of 4 waves per CU)
     a.msplit = 1;
-    sp.ks = ws ? w4_split(var, N, K, n_cu, ws_bytes) : 1;
+    sp.ks = ws ? w4_split(var, N, K, epi, n_cu, ws_bytes) : 1;
     if (sp.ks > 1) {
       sp.ctr = static_cast<unsigned*>(ws);
-      sp.part = reinterpret_cast<float*>(static_cast<char*>(ws) + W4_CTR_BYTES);
+      sp.part = reinterpret_cast<float*>(static_cast<char*>(ws) + W4_PART_OFFSET);
       np = npairs * sp.ks;
     }
     grid = std::min(np, n_cu * (g_w4_wgs_per_cu ? g_w4_wgs_per_cu : (waves == 8 ? 2 : 4)));
