@@ -29,7 +29,9 @@ transformers' GGUF processors and, end to end, against transformers' model class
 """
 from __future__ import annotations
 
+import json
 import os
+import re
 import struct
 from dataclasses import dataclass
 from pathlib import Path
@@ -483,7 +485,14 @@ def load_gguf_tokenizer(g: GGUFFile, cfg: Optional[ModelConfig] = None):
         return None
     from .tokenizer import HFTokenizer
 
-    tok = HFTokenizer.from_tokenizer(conv(fields).converted(), cfg.bos_id if cfg else None)
+    bos = md.get("tokenizer.ggml.bos_token_id")
+    tok = HFTokenizer.from_tokenizer(conv(fields).converted(), int(bos) if isinstance(bos, int) else
+                                     (cfg.bos_id if cfg else None))
+    # BOS as llama.cpp adds it: tokenizer.ggml.add_bos_token, else its per-vocabulary default (SentencePiece "llama"
+    # vocabularies -- Llama 2, Mistral, Gemma, Phi-3 -- add one; byte-level BPE "gpt2" ones -- Qwen2 -- do not;
+    # Llama-3 files carry the key set to true).  The converters attach no post-processor, so encode() prepends it.
+    add_bos = md.get("tokenizer.ggml.add_bos_token")
+    tok.add_bos_token = bool(add_bos) if add_bos is not None else md.get("tokenizer.ggml.model") == "llama"
     tok.chat_template = md.get("tokenizer.chat_template") or None
     toks = md["tokenizer.ggml.tokens"]
     for key, field in (("bos_token", "bos_token_id"), ("eos_token", "eos_token_id")):
@@ -512,8 +521,67 @@ def gguf_stop_ids(g: GGUFFile) -> List[int]:
     return ids + [index[t] for t in TURN_END_TOKENS if t in index]
 
 
+def gguf_tokenizer_fields(tokenizer_json: Dict[str, Any], bos_id: Optional[int] = None, eos_id: Optional[int] = None,
+                          chat_template: Optional[str] = None) -> Optional[Dict[str, Any]]:
+    """``tokenizer.ggml.*`` metadata for a Hugging Face ``tokenizer.json`` (the inverse of what load_gguf_tokenizer
+    reads, in llama.cpp's layout), or None when the vocabulary has no GGUF form:
+
+    * byte-level BPE (Llama 3, Qwen2): model "gpt2", tokens by id, merges, control types for added special tokens;
+    * SentencePiece-style BPE with byte fallback (Llama 2, Mistral, Gemma, Phi-3): model "llama", tokens by id,
+      scores = minus the rank of the merge producing the piece (0 for the base pieces; llama.cpp's SPM tokenizer
+      merges by score), byte pieces typed 6 (byte), special tokens 3 (control).
+    """
+    model = tokenizer_json.get("model") or {}
+    if model.get("type") != "BPE":
+        return None
+    vocab: Dict[str, int] = dict(model.get("vocab") or {})
+    special = set()
+    for t in tokenizer_json.get("added_tokens") or []:
+        vocab[t["content"]] = int(t["id"])
+        if t.get("special"):
+            special.add(t["content"])
+    n = max(vocab.values()) + 1 if vocab else 0
+    tokens = [f"[PAD{i}]" for i in range(n)]
+    for t, i in vocab.items():
+        tokens[i] = t
+    merges = [m if isinstance(m, str) else " ".join(m) for m in model.get("merges") or []]
+
+    def has_byte_level(node) -> bool:
+        if not isinstance(node, dict):
+            return False
+        if node.get("type") == "ByteLevel":
+            return True
+        return any(has_byte_level(x) for x in node.get("pretokenizers") or node.get("decoders") or [])
+
+    types = [3 if t in special else 1 for t in tokens]
+    out: Dict[str, Any] = {"tokenizer.ggml.tokens": tokens, "tokenizer.ggml.token_type": types}
+    if has_byte_level(tokenizer_json.get("pre_tokenizer")):
+        out.update({"tokenizer.ggml.model": "gpt2", "tokenizer.ggml.merges": merges})
+    elif model.get("byte_fallback"):
+        scores = [0.0] * n
+        for rank, m in enumerate(merges):
+            i = vocab.get(m.replace(" ", ""))
+            if i is not None and scores[i] == 0.0:
+                scores[i] = -float(rank + 1)
+        for i, t in enumerate(tokens):
+            if re.fullmatch(r"<0x[0-9A-F]{2}>", t):
+                types[i] = 6
+        out.update({"tokenizer.ggml.model": "llama", "tokenizer.ggml.scores": scores})
+    else:
+        return None
+    if bos_id is not None:
+        out["tokenizer.ggml.bos_token_id"] = int(bos_id)
+        # the checkpoint's own BOS rule: its post-processor template names the BOS token
+        out["tokenizer.ggml.add_bos_token"] = tokens[bos_id] in json.dumps(tokenizer_json.get("post_processor") or {})
+    if eos_id is not None:
+        out["tokenizer.ggml.eos_token_id"] = int(eos_id)
+    if chat_template:
+        out["tokenizer.chat_template"] = chat_template
+    return out
+
+
 def export_gguf(mw: ModelWeights, path: Union[str, os.PathLike], arch: str, tensor_type: str = "F16",
-                tokenizer_fields: Optional[Dict[str, Any]] = None) -> None:
+                tokenizer_fields: Optional[Dict[str, Any]] = None, context_length: Optional[int] = None) -> None:
     """Write ``mw`` as a GGUF file of ``arch`` with llama.cpp's conventions (the inverse of ``load_gguf``): q / k
     rows permuted for ``llama``, Gemma gains as 1 + w, Phi-3's fused qkv / gate-up, Llama-3 scaling as a
     ``rope_freqs`` tensor.  2-D weights in ``tensor_type`` (F32 / F16 / BF16 / Q8_0 / Q4_0), norms in F32."""
@@ -524,7 +592,7 @@ def export_gguf(mw: ModelWeights, path: Union[str, os.PathLike], arch: str, tens
         raise ValueError(f"arch must be one of {ARCHS}")
     md: Dict[str, Any] = {
         "general.architecture": arch, "general.name": cfg.name,
-        f"{arch}.block_count": cfg.n_layers, f"{arch}.context_length": cfg.max_context,
+        f"{arch}.block_count": cfg.n_layers, f"{arch}.context_length": int(context_length or cfg.max_context),
         f"{arch}.embedding_length": cfg.d_model, f"{arch}.feed_forward_length": cfg.ffn,
         f"{arch}.attention.head_count": cfg.n_heads, f"{arch}.attention.head_count_kv": cfg.n_kv_heads,
         f"{arch}.attention.key_length": cfg.head_dim, f"{arch}.attention.value_length": cfg.head_dim,

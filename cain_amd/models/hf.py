@@ -157,7 +157,10 @@ def _other_ends(v) -> Tuple[int, ...]:
 
 
 # turn-end tokens of the families' chat templates, on which Ollama's templates stop
-TURN_END_TOKENS = ("<|eot_id|>", "<|eom_id|>", "<|end|>", "<end_of_turn>", "<|im_end|>", "<|endoftext|>", "</s>")
+# in priority order (with_stop_ids keeps 3 beside eos_id): Llama 3.x's eot / eom / end_of_text first, as llama.cpp's
+# end-of-generation set has them
+TURN_END_TOKENS = ("<|eot_id|>", "<|eom_id|>", "<|end_of_text|>", "<|end|>", "<end_of_turn>", "<|im_end|>",
+                   "<|endoftext|>", "</s>")
 
 
 def with_stop_ids(cfg: ModelConfig, extra_ids) -> ModelConfig:

@@ -90,6 +90,9 @@ class HFTokenizer:
     # special-token strings it refers to; None: prompts are used as given
     chat_template: Optional[str] = None
     special_tokens: Dict[str, str] = {}
+    # prepend bos_id on encode(add_bos=True) when the tokenizer's own post-processor does not: GGUF vocabularies
+    # (transformers' GGUF converters attach no BOS template) with tokenizer.ggml.add_bos_token, as llama.cpp does
+    add_bos_token: bool = False
 
     def __init__(self, path: str, bos_id: Optional[int] = None):
         from tokenizers import Tokenizer
@@ -132,7 +135,10 @@ class HFTokenizer:
                                                           **self.special_tokens)
 
     def encode(self, text: str, add_bos: bool = True) -> List[int]:
-        return self.tok.encode(text, add_special_tokens=add_bos).ids
+        ids = self.tok.encode(text, add_special_tokens=add_bos).ids
+        if add_bos and self.add_bos_token and self.bos_id is not None and (not ids or ids[0] != self.bos_id):
+            ids = [int(self.bos_id)] + ids
+        return ids
 
     def piece(self, tid: int) -> str:
         return self.tok.decode([int(tid)], skip_special_tokens=True)
@@ -146,24 +152,39 @@ class HFTokenizer:
 
 
 class StreamDecoder:
-    """Incremental detokenisation of a streamed response: the pieces ``push`` returns concatenate to
-    ``decode(all ids)``, as Ollama's stream concatenates to its response.  Each push decodes the whole sequence so
-    far and returns the new suffix; a character whose bytes are split over tokens (a trailing U+FFFD) is held back
-    until its last byte arrives.  Single-token decodes (``piece``) break such characters and drop SentencePiece's
-    word-boundary spaces."""
+    """Incremental detokenisation of a streamed response: the pieces ``push`` returns, followed by ``flush()`` when
+    the row finishes, concatenate to ``decode(all ids)``, as Ollama's stream concatenates to its response.
+
+    Each push decodes only a short window -- from the previous chunk's start (prefix offset) to the end -- and emits
+    what that window adds beyond the previous chunk (the prefix / read offsets of TGI's and vLLM's detokenisers):
+    decoding the whole sequence per push was quadratic on the scheduler thread for long streamed batches (ADVICE
+    r5).  Starting the window one chunk back keeps tokenizers whose decode depends on the left context (SentencePiece
+    word-boundary spaces, a stripped leading space) consistent.  A character whose bytes are split over tokens (a
+    trailing U+FFFD) is held back until its last byte arrives; ``flush`` emits whatever is still held (a length
+    cutoff inside a character)."""
 
     def __init__(self, tok):
         self.tok = tok
         self.ids: List[int] = []
-        self.sent = 0
+        self.prefix = 0  # start of the decode window
+        self.read = 0    # end of the text already emitted
+
+    def _delta(self):
+        done = self.tok.decode(self.ids[self.prefix:self.read]) if self.read > self.prefix else ""
+        return done, self.tok.decode(self.ids[self.prefix:])
 
     def push(self, ids) -> str:
         self.ids.extend(int(t) for t in ids)
-        text = self.tok.decode(self.ids)
-        if text.endswith("\ufffd"):
+        done, text = self._delta()
+        if text.endswith("\ufffd") or len(text) <= len(done):
             return ""
-        out, self.sent = text[self.sent:], len(text)
-        return out
+        self.prefix, self.read = self.read, len(self.ids)
+        return text[len(done):]
+
+    def flush(self) -> str:
+        done, text = self._delta()
+        self.prefix = self.read = len(self.ids)
+        return text[len(done):]
 
 
 def get_tokenizer(cfg, path: Optional[str] = None):

@@ -109,11 +109,17 @@ def cmd_generate(args: List[str]) -> None:
 
 def cmd_convert(args: List[str]) -> None:
     """``convert <checkpoint dir | .gguf> <out.gguf> [--type F16]``: a checkpoint as a GGUF file with llama.cpp's
-    conventions (models/gguf.py export_gguf), e.g. to run the same weights under llama.cpp / Ollama."""
+    conventions (models/gguf.py export_gguf), e.g. to run the same weights under llama.cpp / Ollama.  A Hugging Face
+    directory's byte-level or SentencePiece-style BPE ``tokenizer.json`` and chat template go into the file's
+    ``tokenizer.ggml.*`` metadata (gguf_tokenizer_fields) and its context length is the checkpoint's
+    ``max_position_embeddings``; a vocabulary with no GGUF form (e.g. word-level) is left out, and the file then loads
+    only where a tokenizer is supplied separately (this package's engine with token ids)."""
+    import json
+
     import torch
 
-    from ..models.gguf import ARCHS, export_gguf
-    from ..models.hf import load_pretrained
+    from ..models.gguf import ARCHS, GGUFFile, export_gguf, gguf_tokenizer_fields, is_gguf
+    from ..models.hf import _chat_template, load_pretrained
 
     ap = argparse.ArgumentParser(prog="python -m cain_amd convert")
     ap.add_argument("src", help="a Hugging Face checkpoint directory or a GGUF file")
@@ -129,8 +135,23 @@ def cmd_convert(args: List[str]) -> None:
         if arch not in ARCHS:
             raise SystemExit(f"cannot tell the GGUF architecture of {ns.src}: pass --arch")
         print(f"architecture: {arch} (pass --arch to override)")
-    export_gguf(mw, ns.dst, arch, tensor_type=ns.type)
-    print(f"wrote {ns.dst}: {cfg.n_layers} layers, d {cfg.d_model}, {ns.type}")
+    src = Path(ns.src)
+    fields, ctx = None, None
+    if is_gguf(src):
+        md = GGUFFile(src).metadata  # a GGUF source keeps its own vocabulary and context length
+        fields = {k: v for k, v in md.items() if k.startswith("tokenizer.")}
+        ctx = md.get(f"{md.get('general.architecture')}.context_length")
+    else:
+        conf = json.loads((src / "config.json").read_text())
+        ctx = conf.get("max_position_embeddings")
+        if (src / "tokenizer.json").exists():
+            fields = gguf_tokenizer_fields(json.loads((src / "tokenizer.json").read_text()), cfg.bos_id, cfg.eos_id,
+                                           _chat_template(src)[0])
+            if fields is None:
+                print("tokenizer.json is not a BPE vocabulary GGUF can hold: written without tokenizer metadata")
+    export_gguf(mw, ns.dst, arch, tensor_type=ns.type, tokenizer_fields=fields, context_length=ctx)
+    print(f"wrote {ns.dst}: {cfg.n_layers} layers, d {cfg.d_model}, {ns.type}"
+          f"{', tokenizer ' + fields['tokenizer.ggml.model'] if fields else ''}")
 
 
 COMMANDS = {

@@ -241,7 +241,11 @@ class EngineBackend(Backend):
         else:
             res = gen()
         ttft = getattr(eng, "last_ttft_ns", 0)
-        for j, r in zip(jobs, res):
+        for j, d, r in zip(jobs, decs, res):
+            if j.stream is not None:
+                tail = d.flush()  # text held back at a length cutoff inside a character
+                if tail:
+                    j.stream(tail)
             j.result = r
             j.ttft_ns = ttft
 
@@ -322,6 +326,10 @@ class EngineBackend(Backend):
         for r in done_rows:
             st, j = live[r], live[r]["job"]
             toks = cb.tokens(r)
+            if j.stream is not None:
+                tail = st["dec"].flush()
+                if tail:
+                    j.stream(tail)
             reason = "stop" if _stopped(toks, cb.options[r]) else "length"
             j.result = GenResult(model, list(cb.prompt_tokens[r]), toks, tok.decode(toks), reason,
                                  load_duration_ns=0, prompt_eval_duration_ns=int(st["t_pre"] - st["t0"]),

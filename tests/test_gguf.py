@@ -285,6 +285,13 @@ def test_gguf_tokenizer_through_transformers_converter(arch, tmp_path):
     ids = gt.encode(s, add_bos=False)
     assert ids == tok.encode(s).ids
     assert gt.decode(ids) == s
+    # byte-level BPE files add no BOS unless tokenizer.ggml.add_bos_token says so (llama.cpp's rule; Llama-3 files
+    # set it, Qwen2 files do not)
+    assert gt.encode(s, add_bos=True) == ids
+    fields.update({"tokenizer.ggml.bos_token_id": 0, "tokenizer.ggml.add_bos_token": True})
+    export_gguf(mw, tmp_path / "b.gguf", arch, tokenizer_fields=fields)
+    _, _, gb = load_gguf(tmp_path / "b.gguf")
+    assert gb.encode(s, add_bos=True) == [0] + ids and gb.encode(s, add_bos=False) == ids
     del model
 
 
@@ -354,6 +361,16 @@ def test_gguf_sentencepiece_vocabulary(arch, tmp_path):
     _, _, tok = load_gguf(tmp_path / "t.gguf")
     ids = tok.encode("the word energy", add_bos=False)
     assert ids and max(ids) < len(toks)
+    # SentencePiece vocabularies get llama.cpp's default BOS (no add_bos_token key in the file): the converters attach
+    # no post-processor, so the tokenizer prepends it itself (raw prompts reached Gemma without BOS)
+    fields["tokenizer.ggml.bos_token_id"] = 1
+    export_gguf(mw, tmp_path / "b.gguf", arch, tokenizer_fields=fields)
+    _, _, tb = load_gguf(tmp_path / "b.gguf")
+    with_bos = tb.encode("the word energy", add_bos=True)
+    assert with_bos[0] == 1 and with_bos[1:] == ids and with_bos.count(1) == 1
+    fields["tokenizer.ggml.add_bos_token"] = False
+    export_gguf(mw, tmp_path / "n.gguf", arch, tokenizer_fields=fields)
+    assert load_gguf(tmp_path / "n.gguf")[2].encode("the word energy", add_bos=True) == ids
     if arch != "phi3":
         assert tok.decode(ids) == "the word energy"
     # phi3: transformers' Phi-3 converter lays Phi-3's own added tokens (ids 32000+) and normaliser over the vocabulary;
@@ -417,3 +434,42 @@ def test_convert_cli_round_trip(tmp_path):
     theirs = hf_logits(model, tokens, pos)
     ours = ReferenceModel(mg).forward(tokens, positions=pos)
     assert float((ours - theirs).abs().max() / theirs.abs().max()) < 2e-5
+
+
+def test_convert_cli_writes_the_tokenizer_and_context(tmp_path):
+    """convert carries a byte-level BPE tokenizer.json (tokens, merges, BOS rule, chat template) into the
+    GGUF's tokenizer.ggml.* metadata and writes the checkpoint's max_position_embeddings, so the file is complete for
+    llama.cpp-style loaders; it loads back to the same encodings here."""
+    import json
+    import subprocess
+    import sys
+    from pathlib import Path
+
+    from tokenizers import Tokenizer, decoders, models, pre_tokenizers, processors, trainers
+
+    from cain_amd.models.gguf import GGUFFile
+
+    root = Path(__file__).resolve().parent.parent
+    make_checkpoint("llama", tmp_path / "hf")
+    conf = json.loads((tmp_path / "hf" / "config.json").read_text())
+    tok = Tokenizer(models.BPE())
+    tok.pre_tokenizer = pre_tokenizers.ByteLevel(add_prefix_space=False)
+    tok.decoder = decoders.ByteLevel()
+    text = ["In 100 words, please give me information about India", "energy of remote and on device inference"] * 20
+    tok.train_from_iterator(text, trainers.BpeTrainer(vocab_size=300, special_tokens=["<s>", "</s>"],
+                                                      initial_alphabet=pre_tokenizers.ByteLevel.alphabet()))
+    tok.post_processor = processors.TemplateProcessing(single="<s> $A", special_tokens=[("<s>", 0)])
+    tok.save(str(tmp_path / "hf" / "tokenizer.json"))
+    conf.update(bos_token_id=0, eos_token_id=1, max_position_embeddings=4096)
+    (tmp_path / "hf" / "config.json").write_text(json.dumps(conf))
+    r = subprocess.run([sys.executable, "-m", "cain_amd", "convert", str(tmp_path / "hf"), str(tmp_path / "o.gguf"),
+                        "--type", "F16"], capture_output=True, text=True, cwd=str(root), timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "tokenizer gpt2" in r.stdout
+    md = GGUFFile(tmp_path / "o.gguf").metadata
+    assert md["llama.context_length"] == 4096
+    assert md["tokenizer.ggml.add_bos_token"] is True and md["tokenizer.ggml.bos_token_id"] == 0
+    _, _, gt = load_gguf(tmp_path / "o.gguf")
+    s = "please give me information about remote energy"
+    assert gt.encode(s, add_bos=True) == tok.encode(s).ids
+    assert gt.encode(s, add_bos=False) == tok.encode(s, add_special_tokens=False).ids

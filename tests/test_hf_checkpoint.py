@@ -321,7 +321,20 @@ def test_stream_decoder_holds_split_characters():
     syn = SyntheticTokenizer(1024)
     sd = StreamDecoder(syn)
     gen = [17, 18, 19, 20, 21, 22]
-    assert "".join(sd.push(gen[i:i + 2]) for i in range(0, 6, 2)) == syn.decode(gen)
+    assert "".join(sd.push(gen[i:i + 2]) for i in range(0, 6, 2)) + sd.flush() == syn.decode(gen)
+    # a length cutoff inside a character: the held-back bytes come out at flush, and the stream equals the response
+    cut = ids[:ids.index(t.encode("世", add_bos=False)[0]) + 2]
+    d2 = StreamDecoder(t)
+    pieces = [d2.push([i]) for i in cut]
+    assert "".join(pieces) + d2.flush() == t.decode(cut)
+    # each push decodes a window from the previous chunk's start, not the whole sequence
+    seen = []
+    orig = t.decode
+    t.decode = lambda x: seen.append(len(x)) or orig(x)
+    d3 = StreamDecoder(t)
+    out = "".join(d3.push([i]) for i in ids) + d3.flush()
+    t.decode = orig
+    assert out == text and max(seen) <= 8 < len(ids)
 
 
 def test_streamed_response_concatenates_to_the_final_text(tmp_path, monkeypatch):
