@@ -212,8 +212,8 @@ def set_wide_gemm_plan(n: int, k: int, bm: int, ks: int, variant: int = -1) -> N
 
 
 def set_wide_gemm_variant(v: int) -> None:
-    """Global wide-GEMM ring variant (csrc/wgemm.hip; per-shape plans override it): 0 default, 4 fp32 slabs, 5 the
-    256-column kernel (csrc/wgemm256.hip; 256-row tiles with N % 256 == 0, else the default)."""
+    """Global wide-GEMM ring variant (csrc/wgemm.hip; per-shape plans override it): 0 default, 4 fp32 slabs;
+    7 / 8 / 9 the timestamped / DMA-only / MFMA-only diagnostic builds of tools/wgemm_trace.py / wgemm_bench.py."""
     load().cain_wgemm_set_variant(int(v))
 
 

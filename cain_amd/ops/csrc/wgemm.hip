@@ -51,9 +51,6 @@
 
 using namespace wg;
 
-hipError_t wg256_main(int epi, bool norm, const GemmArgs& a, const WgArgs& w, int nblk, int abl,
-                      hipStream_t st);  // wgemm256.hip
-
 constexpr int WG_CTR_BYTES = 16 * 1024;  // the workspace region before the slabs (gemm.hip WG_COUNTER_BYTES)
 
 // DX / DW: prefetch distance (stages in flight) of the X and the W ring; the rings have DX + 1 and DW + 1 slots.
@@ -492,7 +489,7 @@ namespace {
 struct WgPlan {
   int bm, nblk, ks, kst;
   size_t part_floats, ss_floats, sc_floats;
-  int variant = 0;  // ring variant (wg_launch_v); 5: the 256-column kernel of wgemm256.hip
+  int variant = 0;  // ring variant (wg_launch_v)
   int bnt = WG_NT;  // 16-column tiles per column block
 };
 
@@ -520,31 +517,8 @@ const WgShape* wg_shape(int N, int K, int bm) {
 }
 
 int g_wgemm_variant = 0;
-// ring variants of the 256-column kernel (wgemm256.hip): 5 the kernel, 6 / 7 its DMA-only / MFMA-only diagnostic
-// builds, 10 the kernel with 4 loading waves, 11 the loader-wave kernel (wg256l_kernel)
-inline bool is_v256(int v) { return v == 5 || v == 6 || v == 7 || v == 10 || v == 11; }
-
-// 256 x 256 tiles (wgemm256.hip): column blocks of 16 tiles, 32-deep W stages (an even number per split: X stages
-// are 64 deep); ~256 workgroups (one per CU: the ring is 160 KiB), at least 8 stages per split, so a split outlasts
-// its 5-stage W prefetch
-WgPlan wg_plan256(int N, int K, int ks_override) {
-  WgPlan p{};
-  p.bm = 256, p.variant = 5, p.bnt = 16;
-  p.nblk = N / 256;
-  const int stages = K / 32;
-  const int target = g_wg_target > 0 ? g_wg_target : 256, ksmax = g_wg_ksmax > 0 ? g_wg_ksmax : 16;
-  int ks = ks_override > 0 ? ks_override : std::max(1, std::min(ksmax, target / p.nblk));
-  ks = std::min(ks, std::max(1, stages / 8));
-  p.kst = (stages + ks - 1) / ks;
-  p.kst += p.kst & 1;  // whole 64-deep X stages per split
-  p.ks = (stages + p.kst - 1) / p.kst;
-  if (p.ks > 1) {
-    p.part_floats = (size_t)p.ks * (N / 16) * (p.bm / 16) * 256;
-    p.ss_floats = (size_t)p.nblk * p.ks * p.bm;
-    p.sc_floats = (size_t)p.ks * (N / 16) * (p.bm / 16) * 16;
-  }
-  return p;
-}
+// (round 5's 256-column kernel, variants 5-7 / 10 / 11, measured slower on every headline shape -- 24.1k against
+// 28.4k tok/s, profiles/r5/README.md -- and left the shipped library in round 6: tools/attic/wgemm256.hip)
 
 WgPlan wg_plan(int N, int K, int M) {
   const int target = g_wg_target > 0 ? g_wg_target : 256, ksmax = g_wg_ksmax > 0 ? g_wg_ksmax : 8;
@@ -552,13 +526,7 @@ WgPlan wg_plan(int N, int K, int M) {
   p.bm = M > 128 ? 256 : 128;
   {
     const WgShape* o = wg_shape(N, K, p.bm);
-    const int variant = o && o->variant >= 0 ? o->variant : g_wgemm_variant;
-    if (is_v256(variant) && p.bm == 256 && N % 256 == 0 && K % 64 == 0) {
-      WgPlan q = wg_plan256(N, K, o ? o->ks : 0);
-      q.variant = variant;
-      return q;
-    }
-    p.variant = is_v256(variant) ? 0 : variant;  // the 256-column kernel's shape rule failed: the default ring
+    p.variant = o && o->variant >= 0 ? o->variant : g_wgemm_variant;
   }
   p.nblk = ((N >> 4) + WG_NT - 1) / WG_NT;
   const int stages = K / WG_BK;
@@ -602,9 +570,7 @@ hipError_t wg_launch(const GemmArgs& a, const WgArgs& w, const WgPlan& p, hipStr
 // variants: 0 = default (fp16 split-K slabs: in the graph-replayed headline 26.33 / 26.17k -> 27.34 / 27.17k tok/s
 // against fp32 slabs, same box, interleaved, profiles/r3/README.md); 4 = fp32 slabs (tests, A/B); diagnostics of
 // tools/wgemm_trace.py / wgemm_bench.py: 7 = default + timestamps, 8 = DMA only, 9 = fragment reads + MFMAs only
-// (results garbage); 5 = the 256-column kernel (wgemm256.hip; 256-row tiles, N % 256 == 0, else variant 0), 6 / 7 its
-// DMA-only / MFMA-only diagnostic builds, 10 its 4-loading-wave form.  Set
-// with cain_wgemm_set_variant / cain_wgemm_set_shape.
+// (results garbage).  Set with cain_wgemm_set_variant / cain_wgemm_set_shape.
 
 template <int BM, int EPI, bool NORM>
 hipError_t wg_launch_v(const GemmArgs& a, const WgArgs& w, const WgPlan& p, hipStream_t st) {
@@ -636,20 +602,6 @@ hipError_t wg_launch_e(int epi, const GemmArgs& a, const WgArgs& w, const WgPlan
     case EPI_QKV_ROPE: return wg_launch_v<BM, EPI_QKV_ROPE, NORM>(a, w, p, st);
     default: return hipErrorInvalidValue;
   }
-}
-
-template <int BM, bool NORM>
-hipError_t wg_reduce_e(int epi, const GemmArgs& a, const WgArgs& w, int n_units, hipStream_t st) {
-  switch (epi) {
-    case EPI_BF16: wg_reduce_launch<BM, EPI_BF16, NORM, true>(a, w, n_units, st); break;
-    case EPI_RESID: wg_reduce_launch<BM, EPI_RESID, NORM, true>(a, w, n_units, st); break;
-    case EPI_F32: wg_reduce_launch<BM, EPI_F32, NORM, true>(a, w, n_units, st); break;
-    case EPI_SILU: wg_reduce_launch<BM, EPI_SILU, NORM, true>(a, w, n_units, st); break;
-    case EPI_GELU: wg_reduce_launch<BM, EPI_GELU, NORM, true>(a, w, n_units, st); break;
-    case EPI_QKV_ROPE: wg_reduce_launch<BM, EPI_QKV_ROPE, NORM, true>(a, w, n_units, st); break;
-    default: return hipErrorInvalidValue;
-  }
-  return hipGetLastError();
 }
 
 }  // namespace
@@ -721,14 +673,6 @@ int wgemm_dispatch(const GemmArgs& a, int epi, bool norm, void* ws, long long ws
   w.part_ss = w.part + p.part_floats;
   w.part_ex = reinterpret_cast<uint8_t*>(w.part_ss + p.ss_floats);
   hipError_t e;
-  if (is_v256(p.variant)) {
-    e = wg256_main(epi, norm, a, w, p.nblk, p.variant == 10 ? 3 : p.variant == 11 ? 4 : p.variant - 5, st);
-    if (e == hipSuccess && p.ks > 1) {
-      const int n_units = (a.N / 16) * (p.bm / 16);
-      e = norm ? wg_reduce_e<256, true>(epi, a, w, n_units, st) : wg_reduce_e<256, false>(epi, a, w, n_units, st);
-    }
-    return int(e);
-  }
   if (p.bm == 256) e = norm ? wg_launch_e<256, true>(epi, a, w, p, st) : wg_launch_e<256, false>(epi, a, w, p, st);
   else e = norm ? wg_launch_e<128, true>(epi, a, w, p, st) : wg_launch_e<128, false>(epi, a, w, p, st);
   return int(e);
