@@ -97,7 +97,7 @@ def main() -> int:
     ap.add_argument("--context", type=int, default=1536)
     ap.add_argument("--steps-per-graph", type=int, default=16)
     ap.add_argument("--no-energy", action="store_true")
-    ap.add_argument("--weights", choices=("bf16", "fp8", "fp4"), default="bf16",
+    ap.add_argument("--weights", choices=("bf16", "fp8", "fp4", "q4_0", "q4_k"), default="bf16",
                     help="GEMM weight storage: bf16 (headline), fp8 e4m3 per-row scaled (W8A8 above 16 rows, W8A16 "
                          "below) or MXFP4 (W4A16 with bf16 activations at <= 16 rows, W4A8 with per-row e4m3 "
                          "activations above: --w4a8-min-rows)")
@@ -114,6 +114,9 @@ def main() -> int:
     ap.add_argument("--single-fp4-models", default="phi3:3.8b,qwen2:7b,gemma:7b,mistral:7b",
                     help="models measured at batch 1 on MXFP4 weights only (the reference's 4-bit class), "
                          "comma-separated: with --single-models and the bench model, the 7 study models")
+    ap.add_argument("--single-q4", default="q4_k",
+                    help="GGUF 4-bit block formats (q4_0, q4_k; comma-separated, empty: none) also measured at batch "
+                         "1 on all 7 models: Ollama's default builds run natively (csrc/gemm_q4.hip)")
     ap.add_argument("--checkpoint", default=None,
                     help="a Hugging Face checkpoint directory or GGUF file for --model (default: random-init weights of "
                          "the model's architecture; models/hf.py, models/gguf.py)")
@@ -259,6 +262,8 @@ def main() -> int:
                       for dt in ("bf16", "fp4")]
             cases += [(m, "fp4") for m in filter(None, ns.single_fp4_models.split(","))
                       if m != ns.model and (m, "fp4") not in cases]
+            q4s = [q for q in filter(None, ns.single_q4.split(",")) if q in ("q4_0", "q4_k")]
+            cases += [(m, q) for q in q4s for m in dict.fromkeys(c[0] for c in cases)]
         sync()
         time.sleep(max(0.0, ns.settle))  # the board returns toward idle after the batched steps
     for model, dtype in cases:
@@ -308,6 +313,8 @@ def main() -> int:
             "scaling": "weak",
             "vs_baseline": round(value / base_tps, 2) if base_tps else None,
             "dtype": ("bf16" if ns.weights == "bf16" else
+                      f"bf16 activations, GGUF {ns.weights.upper()} weights (the blocks' exact values, W4A16)"
+                      if ns.weights in ("q4_0", "q4_k") else
                       (f"MXFP4 (e2m1 + e8m0 block-32) weights; GEMM activations per-row e4m3 above "
                        f"{max(16, ns.w4a8_min_rows)} rows (W4A8: this {ns.batch}-row run), bf16 at or below (W4A16)"
                        if getattr(eng, "w4a8", False) and ns.batch > max(16, ns.w4a8_min_rows) else
@@ -336,9 +343,11 @@ def main() -> int:
             "single_stream_fp8_J_per_token": ss_get(ns.model, "fp8", 1),
             "single_stream_fp4_tok_per_s": ss_get(ns.model, "fp4", 0),
             "single_stream_fp4_J_per_token": ss_get(ns.model, "fp4", 1),
+            "single_stream_q4_k_tok_per_s": ss_get(ns.model, "q4_k", 0),
+            "single_stream_q4_k_J_per_token": ss_get(ns.model, "q4_k", 1),
             "single_stream_by_model": {
                 m: {dt: {"tok_per_s": ss_get(m, dt, 0), "J_per_token": ss_get(m, dt, 1)}
-                    for dt in ("bf16", "fp8", "fp4") if (m, dt) in ss}
+                    for dt in ("bf16", "fp8", "fp4", "q4_0", "q4_k") if (m, dt) in ss}
                 | {"baseline": dict(zip(("tok_per_s", "J_per_token"), BASELINE.get((m, ns.words), (None, None))))}
                 for m in dict.fromkeys(c[0] for c in cases)},
             "baseline": {"tok_per_s": base_tps, "J_per_token": base_jpt, "hardware": "MacBook Pro M2 (est.)"},

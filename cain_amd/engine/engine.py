@@ -113,7 +113,7 @@ def _stopped(toks: List[int], o: Dict) -> bool:
 
 # ============================================================== ctypes structs
 LAYER_FIELDS = ("wqkv", "bqkv", "wo", "wgu", "wdown", "sqkv", "so", "sgu", "sdown", "wqkv8", "wo8", "wgu8", "wdown8")
-WFMT = {"bf16": 0, "fp8": 1, "fp4": 2}  # runtime.hip WFMT_*
+WFMT = {"bf16": 0, "fp8": 1, "fp4": 2, "q4_0": 3, "q4_k": 4}  # runtime.hip WFMT_*
 
 
 class _CainLayer(ctypes.Structure):
@@ -130,7 +130,7 @@ class _CainPlanDesc(ctypes.Structure):
                                                  "part_o", "part_ml", "counters", "gemm_ws")]
                 + [("gemm_ws_bytes", ctypes.c_longlong), ("wfmt", ctypes.c_int), ("lm_head_scale", ctypes.c_void_p)]
                 + [("kv8", ctypes.c_int), ("lm_head8", ctypes.c_void_p), ("x8", ctypes.c_void_p),
-                   ("xs", ctypes.c_void_p), ("x8_ld", ctypes.c_int)])
+                   ("xs", ctypes.c_void_p), ("x8_ld", ctypes.c_int), ("q4_gain", ctypes.c_int)])
 
 
 class _CainRows(ctypes.Structure):
@@ -187,6 +187,9 @@ class DecodeEngine:
         the reference's 4-bit precision class: W4A16 few-row kernels (gemm_w4.hip) up to 16 rows per forward, W4A8
         above (wgemm8.hip FP4: the same bytes on the block-scaled fp4 x fp8 MFMA, activations per row to e4m3) up to
         256; every GEMM K (d_model, q_dim, ffn) must be a multiple of 128 (>= 512 for W4A8).
+        ``weight_dtype="q4_0" / "q4_k"``: llama.cpp's GGUF 4-bit blocks (Ollama's default builds) run natively
+        (gemm_q4.hip: the block values as stored, scales applied per block; 16-row launches) up to 64 rows per
+        forward; every GEMM K must be a multiple of 256.
         ``kv_dtype="fp8"``: the KV cache holds e4m3 elements (half the attention bytes per decode step and half
         the cache memory; csrc/attention.hip KV8).
         ``cu_limit``: run every kernel on a stream whose hardware queue may use only that many CUs (a multiple of
@@ -197,6 +200,9 @@ class DecodeEngine:
             raise ValueError(f"weight_dtype must be one of {WEIGHT_DTYPES}, got {weight_dtype!r}")
         if weight_dtype == "fp4" and any(k % 128 for k in (self.cfg.d_model, self.cfg.q_dim, self.cfg.ffn)):
             raise ValueError(f"weight_dtype='fp4' needs d_model, q_dim and ffn to be multiples of 128 ({self.cfg.name})")
+        if weight_dtype in ("q4_0", "q4_k") and any(k % 256 for k in (self.cfg.d_model, self.cfg.q_dim, self.cfg.ffn)):
+            raise ValueError(f"weight_dtype={weight_dtype!r} needs d_model, q_dim and ffn to be multiples of 256 "
+                             f"({self.cfg.name})")
         if kv_dtype not in ("bf16", "fp8"):
             raise ValueError(f"kv_dtype must be 'bf16' or 'fp8', got {kv_dtype!r}")
         self.weight_dtype = weight_dtype
@@ -211,7 +217,7 @@ class DecodeEngine:
         self.w4a8 = (weight_dtype == "fp4"
                      and all(k % 128 == 0 and k >= 512 for k in (self.cfg.d_model, self.cfg.q_dim, self.cfg.ffn)))
         row_cap = W8_MAX_ROWS if (weight_dtype == "fp4" and not self.w4a8) or (weight_dtype == "fp8" and not self.w8a8) \
-            else MAX_ROWS
+            or weight_dtype in ("q4_0", "q4_k") else MAX_ROWS
         self.device = torch.device(device)
         if backend is None:
             backend = "hip" if self.device.type == "cuda" else "torch"

@@ -310,16 +310,28 @@ def mxfp4_roundtrip_weights(mw: ModelWeights) -> ModelWeights:
     return _roundtrip(mw, lambda w: dequantize_mxfp4(*quantize_mxfp4(w)).to(w.dtype))
 
 
+def q4_roundtrip_weights(mw: ModelWeights, weight_dtype: str) -> ModelWeights:
+    """The torch oracle of a ``weight_dtype="q4_0" / "q4_k"`` engine: the ggml blocks of W diag(g), dequantised by
+    gguf.py's decoders (``_roundtrip``; models/q4.py)."""
+    from .q4 import Q4_FORMATS, q4_roundtrip
+
+    fmt = Q4_FORMATS[weight_dtype]
+    return _roundtrip(mw, lambda w: q4_roundtrip(w, fmt))
+
+
 def roundtrip_weights(mw: ModelWeights, weight_dtype: str) -> ModelWeights:
     """The weights a ``weight_dtype`` engine multiplies by, for the torch oracle."""
     if weight_dtype == "fp8":
         return fp8_roundtrip_weights(mw)
     if weight_dtype == "fp4":
         return mxfp4_roundtrip_weights(mw)
+    if weight_dtype in ("q4_0", "q4_k"):
+        return q4_roundtrip_weights(mw, weight_dtype)
     return mw
 
 
-WEIGHT_DTYPES = ("bf16", "fp8", "fp4")
+# q4_0 / q4_k: llama.cpp's GGUF block formats (models/q4.py, ops/csrc/gemm_q4.hip), Ollama's default builds
+WEIGHT_DTYPES = ("bf16", "fp8", "fp4", "q4_0", "q4_k")
 
 
 def pack_for_engine(mw: ModelWeights, free_natural: bool = False, weight_dtype: str = "bf16",
@@ -331,16 +343,21 @@ def pack_for_engine(mw: ModelWeights, free_natural: bool = False, weight_dtype: 
     fold; each matrix entry becomes the fp8 packing and its scales are stored under ``s<name>``.  With
     ``w8a8`` the same e4m3 bytes are also stored in the W8A8 wide kernel's packing under ``<name>8``.
     ``weight_dtype="fp4"``: MXFP4 (``quantize_mxfp4``), the ``pack_mxfp4`` bytes under ``<name>`` and the e8m0
-    scale bytes under ``s<name>``."""
+    scale bytes under ``s<name>``.  ``weight_dtype="q4_0" / "q4_k"``: ggml blocks of the gain-folded weights
+    (models/q4.py), the ``pack_q4`` codes under ``<name>`` and its scale buffer under ``s<name>``."""
     if weight_dtype not in WEIGHT_DTYPES:
         raise ValueError(f"weight_dtype must be one of {WEIGHT_DTYPES}, got {weight_dtype!r}")
     cfg = mw.cfg
     fp8 = weight_dtype == "fp8"
     fp4 = weight_dtype == "fp4"
+    q4 = weight_dtype in ("q4_0", "q4_k")
     perm = qkv_row_permutation(cfg).to(mw.device)
 
     def put(dst: Dict[str, object], name: str, w: torch.Tensor) -> None:
-        if fp4:
+        if q4:
+            from .q4 import Q4_FORMATS, quant_pack_q4
+            dst[name], dst["s" + name[1:]] = quant_pack_q4(w, Q4_FORMATS[weight_dtype])
+        elif fp4:
             dst[name], dst["s" + name[1:]] = pack_mxfp4(*quantize_mxfp4(w))
         elif fp8:
             q, sc = quantize_fp8_rows(w)
@@ -368,7 +385,7 @@ def pack_for_engine(mw: ModelWeights, free_natural: bool = False, weight_dtype: 
     put(packed, "wlm_head", lm)
     del lm
     packed["lm_head"] = packed.pop("wlm_head")
-    if fp8 or fp4:
+    if fp8 or fp4 or q4:
         packed["lm_head_scale"] = packed.pop("slm_head")
         if w8a8:
             packed["lm_head8"] = packed.pop("wlm_head8")

@@ -36,6 +36,10 @@ CAIN_API int cain_gemm_w4_ex(const void* Wp, const void* wsc, const void* X, int
                              int ldy, const float* bias, int norm, float eps, const int* slot, const int* pos,
                              const float* cos_t, const float* sin_t, void* kc, void* vtc, int H, int Hkv, int hd,
                              int T_max, void* ws, long long ws_bytes, int epi_flags, hipStream_t st);
+CAIN_API int cain_gemm_q4(int fmt, const void* Wq, const void* sc, const void* dd, const float* gain, const void* X,
+                          int ldx, int K, int N, int M, void* Y, int ldy, const float* bias, int norm, float eps,
+                          const int* slot, const int* pos, const float* cos_t, const float* sin_t, void* kc,
+                          void* vtc, int H, int Hkv, int hd, int T_max, int epi_flags, hipStream_t st);
 CAIN_API int cain_gemm_w8a8(const void* Wp8, const float* wscale, const void* X8, int ld8, const float* xs, int K,
                             int N, int M, void* Y, int ldy, const float* bias, const int* slot, const int* pos,
                             const float* cos_t, const float* sin_t, void* kc, void* vtc, int H, int Hkv, int hd,
@@ -73,7 +77,7 @@ CAIN_API int cain_sample_ex(float* logits, int ldl, int V, int* tok, int* pos, i
 extern "C" {
 
 // weight storage of a plan (CainPlanDesc::wfmt)
-enum { WFMT_BF16 = 0, WFMT_FP8 = 1, WFMT_FP4 = 2 };
+enum { WFMT_BF16 = 0, WFMT_FP8 = 1, WFMT_FP4 = 2, WFMT_Q4_0 = 3, WFMT_Q4_K = 4 };
 
 // RMSNorm gains are folded into the weight columns of the GEMM each norm feeds (attn_norm -> wqkv,
 // mlp_norm -> wgu, final_norm -> lm_head; models/weights.py fold_gain), so a norm is just a flag here.
@@ -131,6 +135,8 @@ struct CainPlanDesc {
   void* x8;
   float* xs;
   int x8_ld;
+  // WFMT_Q4_*: 1 when each norm-fed weight's scale buffer ends with its fp32 RMSNorm gain (weights not gain-folded)
+  int q4_gain;
 };
 
 struct CainRows {
@@ -185,6 +191,7 @@ static int g_w4a8_min_rows = 16;
 // rows a forward of this plan may have: 64 for the few-row-only weight formats
 int max_rows(const CainPlanDesc& d) {
   if ((d.wfmt == WFMT_FP4 || d.wfmt == WFMT_FP8) && !d.x8) return d.Mpad < 64 ? d.Mpad : 64;
+  if (d.wfmt == WFMT_Q4_0 || d.wfmt == WFMT_Q4_K) return d.Mpad < 64 ? d.Mpad : 64;  // 16-row launches (gemm_q4.hip)
   return d.Mpad < CAIN_MAX_ROWS ? d.Mpad : CAIN_MAX_ROWS;
 }
 
@@ -205,6 +212,16 @@ int forward(const Plan& p, int M, const CainRows& r, int want_logits, int want_s
       CK(cain_quant_rows(X, ldx, K, M, d.x8, d.x8_ld, d.xs, norm, d.eps, st));
       return cain_gemm_w4a8(W, ws, d.x8, d.x8_ld, d.xs, K, N, M, Y, ldy, bias, r.slot, r.pos, d.cos_t, d.sin_t, kcm,
                             vcm, d.H, d.Hkv, d.hd, d.T_max, d.gemm_ws, d.gemm_ws_bytes, epi, st);
+    }
+    if (d.wfmt == WFMT_Q4_0 || d.wfmt == WFMT_Q4_K) {
+      // GGUF Q4_0 / Q4_K (gemm_q4.hip): ws = [block scales: N K / 16 bytes][Q4_K: (d, dmin): N K / 64 bytes]
+      // [the fp32 norm gain over K, when the plan keeps gains unfolded (a GGUF file's exact values)]
+      const char* sc = static_cast<const char*>(ws);
+      const char* dd = sc + (size_t)N * K / 16;
+      const float* gain = d.q4_gain && norm ? reinterpret_cast<const float*>(dd + (d.wfmt == WFMT_Q4_K ? (size_t)N * K / 64 : 0))
+                                            : nullptr;
+      return cain_gemm_q4(d.wfmt == WFMT_Q4_K, W, sc, dd, gain, X, ldx, K, N, M, Y, ldy, bias, norm, d.eps, r.slot,
+                          r.pos, d.cos_t, d.sin_t, kcm, vcm, d.H, d.Hkv, d.hd, d.T_max, epi, st);
     }
     if (d.wfmt == WFMT_FP4)
       return cain_gemm_w4_ex(W, ws, X, ldx, K, N, M, Y, ldy, bias, norm, d.eps, r.slot, r.pos, d.cos_t, d.sin_t, kcm,
