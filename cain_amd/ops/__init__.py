@@ -17,6 +17,7 @@ op                     source                      replaces (Ollama/llama.cpp)
 ``gemm_w8``            csrc/gemm_w8.hip            the same GEMMs on fp8 (e4m3) weights, <= 64 rows
 ``gemm_w8a8``          csrc/wgemm8.hip             fp8 weights x per-row fp8 activations, 16 < M <= 256
 ``gemm_w4``            csrc/gemm_w4.hip            the same GEMMs on MXFP4 (e2m1 + e8m0) weights, <= 64 rows
+``gemm_q4``            csrc/gemm_q4.hip            the same GEMMs on GGUF Q4_0 / Q4_K blocks (exact values), any M
 ``rmsnorm``            csrc/norm.hip               RMSNorm (standalone; the engine fuses it)
 ``embed``              csrc/norm.hip               embedding gather (+Gemma scale)
 ``attention``          csrc/attention.hip          decode / prefill attention (split-K, in-kernel combine)
@@ -92,6 +93,12 @@ def load() -> ctypes.CDLL:
         lib.cain_gemm_w4_set_split_cap.argtypes = [ci]
         lib.cain_gemm_w4_set_split_min_quads.argtypes = [ci]
         lib.cain_gemm_w4_set_variant.argtypes = [ci]
+        lib.cain_wgemm_set_inline.argtypes = [ci]
+        lib.cain_gemm_q4.argtypes = ([ci, vp, vp, vp, vp, vp, ci, ci, ci, ci, vp, ci, vp, ci, cf, vp, vp, vp, vp, vp,
+                                      vp] + [ci] * 5 + [vp])
+        lib.cain_gemm_q4_rows.argtypes = [ci, ci]
+        lib.cain_wgemm_inline.argtypes = [ci, ci, ci]
+        lib.cain_wgemm_get_inline.argtypes = []
         lib.cain_gemm_w4_variant.argtypes = [ci, ci, ci, ci]
         lib.cain_gemm_w4_set_occupancy.argtypes = [ci]
         lib.cain_gemm_w8a8.argtypes = ([vp, vp, vp, ci, vp, ci, ci, ci, vp, ci, vp, vp, vp, vp, vp, vp, vp]
@@ -137,6 +144,8 @@ def load() -> ctypes.CDLL:
         lib.cain_stream_create_cu_limited.restype = vp
         lib.cain_stream_create_cu_limited.argtypes = [ci]
         lib.cain_stream_destroy.argtypes = [vp]
+        if os.environ.get("CAIN_WGEMM_INLINE") and hasattr(real, "cain_wgemm_set_inline"):  # A/B runs
+            real.cain_wgemm_set_inline(int(os.environ["CAIN_WGEMM_INLINE"]))
         _lib = real
         return real
 
@@ -215,6 +224,21 @@ def set_wide_gemm_variant(v: int) -> None:
     """Global wide-GEMM ring variant (csrc/wgemm.hip; per-shape plans override it): 0 default, 4 fp32 slabs;
     7 / 8 / 9 the timestamped / DMA-only / MFMA-only diagnostic builds of tools/wgemm_trace.py / wgemm_bench.py."""
     load().cain_wgemm_set_variant(int(v))
+
+
+def set_wide_gemm_inline(mode: int) -> None:
+    """Split-K combine of the wide GEMM (csrc/wgemm.hip wg_inline_combine): 1 inside the GEMM launch (default),
+    0 a separate wgemm_reduce_kernel launch, 2 inside the launch with partners that never wait (tests)."""
+    load().cain_wgemm_set_inline(int(mode))
+
+
+def wide_gemm_inline_mode() -> int:
+    return int(load().cain_wgemm_get_inline())
+
+
+def wide_gemm_inline(n: int, k: int, m: int) -> bool:
+    """Whether the next wide-GEMM launch of this shape combines its split-K slabs in-launch."""
+    return bool(load().cain_wgemm_inline(int(n), int(k), int(m)))
 
 
 def clear_wide_gemm_plans() -> None:
@@ -356,6 +380,41 @@ def gemm_w4(wq: torch.Tensor, wsc: torch.Tensor, x: torch.Tensor, n: int, epi: i
 
 
 _W4_WS: dict = {}
+
+
+def gemm_q4(fmt: int, wq: torch.Tensor, sbuf: torch.Tensor, x: torch.Tensor, n: int, epi: int = EPI_BF16,
+            bias=None, out: Optional[torch.Tensor] = None, norm: bool = False, eps: float = 1e-6, rope=None,
+            gain: bool = False) -> torch.Tensor:
+    """GGUF Q4_0 (``fmt`` 0) / Q4_K (1) weight GEMM (``csrc/gemm_q4.hip``; any M, 16-row launches): y = epi(B(x) @
+    W^T) with W the blocks' exact values and (``wq``, ``sbuf``) = ``models.q4.pack_q4(...)``; ``gain``: the scale
+    buffer ends with the fp32 RMSNorm gain, applied to the activations (``norm`` must be set).  Same epilogues,
+    RMSNorm fusion and ``rope`` arguments as ``gemm_w8``."""
+    lib = load()
+    _gpu(wq, sbuf, x)
+    M, K = x.shape
+    assert x.dtype == torch.bfloat16 and x.stride(1) == 1 and M >= 1
+    assert wq.dtype == torch.uint8 and wq.shape[0] * 16 == n and wq.shape[1] * 128 == K, (tuple(wq.shape), K, n)
+    sc_bytes, dd_bytes = n * K // 16, (n * K // 64 if fmt == 1 else 0)
+    assert sbuf.dtype == torch.uint8 and sbuf.numel() == sc_bytes + dd_bytes + (4 * K if gain else 0)
+    n_out = n // 2 if epi in (EPI_SILU, EPI_GELU) else n
+    if epi == EPI_RESID:
+        assert out is not None and out.shape == (M, n_out), "EPI_RESID updates `out` (the residual) in place"
+    if out is None:
+        out = torch.empty(M, n_out, device=x.device, dtype=torch.float32 if epi == EPI_F32 else torch.bfloat16)
+    r = rope or {}
+    if epi == EPI_QKV_ROPE:
+        assert rope is not None, "EPI_QKV_ROPE needs the rope/cache arguments"
+    T_max = r["kc"].shape[-2] if rope else 0
+    if rope and is_fp8_cache(r["kc"]):
+        epi |= EPI_KV_FP8
+    base = sbuf.data_ptr()
+    rc = lib.cain_gemm_q4(int(fmt), _p(wq), base, base + sc_bytes, (base + sc_bytes + dd_bytes) if gain else None,
+                          _p(x), x.stride(0), K, n, M, _p(out), out.stride(0), _p(bias), int(bool(norm)), eps,
+                          _p(r.get("slot")), _p(r.get("pos")), _p(r.get("cos_t")), _p(r.get("sin_t")),
+                          _p(r.get("kc")), _p(r.get("vtc")), r.get("H", 0), r.get("Hkv", 0), r.get("hd", 0), T_max,
+                          epi, _stream())
+    _check(rc, "gemm_q4")
+    return out
 
 
 def _w4_ws(device, nbytes: int) -> torch.Tensor:

@@ -76,7 +76,16 @@ constexpr int WG_CTR_BYTES = 16 * 1024;  // the workspace region before the slab
 // fp32); tests/test_wgemm_gpu.py compares them with fp32 slabs on such rows.  (Round 3's loader alternatives -- loader-wave sums of squares, W-only / X-only
 // loader roles, rotated k start, non-temporal X, stage-ordered prologue -- and the in-launch split-K combine all
 // measured within box-to-box noise or slower, profiles/r3/README.md, and were removed.)
-template <int BM, int DX, int DW, int EPI, bool NORM, int NDMA, int ABL = 0, bool H16 = false>
+template <int BM, int EPI, bool NORM, bool H16, bool COH>
+__device__ __forceinline__ void wg_reduce_unit(const GemmArgs& a, const WgArgs& w, int unit, int n_units, int lane,
+                                               int ks);
+
+template <int BM, int EPI, bool NORM, bool H16>
+__device__ void wg_inline_combine(const GemmArgs& a, const WgArgs& w, int blk, int kc, int n_units, int nthr,
+                                  unsigned* flags);
+
+// INL: the split-K combine inside this launch (wg_inline_combine below) instead of wgemm_reduce_kernel
+template <int BM, int DX, int DW, int EPI, bool NORM, int NDMA, int ABL = 0, bool H16 = false, bool INL = false>
 __global__ __launch_bounds__(64 * (8 + NDMA), (8 + NDMA) / 4) void wgemm_kernel(const GemmArgs a, const WgArgs w) {
   using G = WgGeo<BM>;
   constexpr bool MSQ = NORM;                        // MFMA X X^T sums of squares
@@ -329,20 +338,42 @@ __global__ __launch_bounds__(64 * (8 + NDMA), (8 + NDMA) / 4) void wgemm_kernel(
               const int ex = max(__builtin_amdgcn_frexp_expf(mx) - 14, 0);  // mx < 2^(ex + 14)
 #pragma unroll
               for (int i = 0; i < 4; ++i) sv[i] = __builtin_amdgcn_ldexpf(v[i], -ex);
-              w.part_ex[e] = (uint8_t)ex;
+              if constexpr (INL) __hip_atomic_store(w.part_ex + e, (uint8_t)ex, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              else w.part_ex[e] = (uint8_t)ex;
             }
             f16x4 h;  // (the clamp only bites on non-finite partials)
 #pragma unroll
             for (int i = 0; i < 4; ++i) h[i] = (_Float16)fminf(fmaxf(sv[i], -65504.f), 65504.f);
-            reinterpret_cast<f16x4*>(w.part)[e] = h;
+            if constexpr (INL)  // write-through: read by the partners' combine in this launch
+              __hip_atomic_store(reinterpret_cast<uint64_t*>(w.part) + e, __builtin_bit_cast(uint64_t, h),
+                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            else
+              reinterpret_cast<f16x4*>(w.part)[e] = h;
+          } else if constexpr (INL) {
+            const f32x4 v = acc[tn][mb];
+            uint64_t* d = reinterpret_cast<uint64_t*>(reinterpret_cast<f32x4*>(w.part) + e);
+            __hip_atomic_store(d, __builtin_bit_cast(uint64_t, f32x2{v[0], v[1]}), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(d + 1, __builtin_bit_cast(uint64_t, f32x2{v[2], v[3]}), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
           } else {
             reinterpret_cast<f32x4*>(w.part)[e] = acc[tn][mb];
           }
         }
     }
     if constexpr (NORM) {
-      for (int r = threadIdx.x; r < BM; r += NTHR)
-        w.part_ss[((size_t)blk * w.ks + kc) * BM + r] = s_ss[r] + s_ss[BM + r];
+      for (int r = threadIdx.x; r < BM; r += NTHR) {
+        float* d = w.part_ss + ((size_t)blk * w.ks + kc) * BM + r;
+        if constexpr (INL) __hip_atomic_store(d, s_ss[r] + s_ss[BM + r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else *d = s_ss[r] + s_ss[BM + r];
+      }
+    }
+    if constexpr (INL) {
+      // two words of the (drained) ring past the row sums: the kernel's LDS is all dynamic, sized to 160 KiB, so
+      // a static __shared__ here would not fit
+      wg_inline_combine<BM, EPI, NORM, H16>(a, w, blk, kc, nblk * WG_NT * G::RB, NTHR,
+                                            reinterpret_cast<unsigned*>(smem + 2 * BM * sizeof(float)));
+      return;
     }
     if constexpr (ABL == 3) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -405,62 +436,88 @@ __global__ __launch_bounds__(64 * (8 + NDMA), (8 + NDMA) / 4) void wgemm_kernel(
 // (two for QKV: position, then the tables).
 template <int BM, int EPI, bool NORM, int KS, bool H16 = false>
 __global__ __launch_bounds__(256) void wgemm_reduce_kernel(const GemmArgs a, const WgArgs w, int n_units) {
-  constexpr int RB = BM / 16;
   const int lane = threadIdx.x & 63;
   // this workgroup's 4 units on the XCD that wrote their column block's slabs (wg_block_of; w.bnt tiles per block)
-  const int unit = wg_reduce_block(blockIdx.x, w.bnt * RB / 4, w.xcd_blk) * 4 + (threadIdx.x >> 6);
+  const int unit = wg_reduce_block(blockIdx.x, w.bnt * (BM / 16) / 4, w.xcd_blk) * 4 + (threadIdx.x >> 6);
   if (unit >= n_units) return;
+  wg_reduce_unit<BM, EPI, NORM, H16, false>(a, w, unit, n_units, lane, KS ? KS : w.ks);
+}
+
+// One unit's combine: the ks slab pieces (+ row sums / exponents), the epilogue.  COH: the slabs were published
+// write-through by partners still running in this launch -- read them with agent-scope loads (past this CU's L1),
+// as the W4 split-K and the attention merge do.  Up to WG_INL_KS pieces are loaded before the first add.
+constexpr int WG_INL_KS = 8;
+template <int BM, int EPI, bool NORM, bool H16, bool COH>
+__device__ __forceinline__ void wg_reduce_unit(const GemmArgs& a, const WgArgs& w, int unit, int n_units, int lane,
+                                               int ks) {
+  constexpr int RB = BM / 16;
   const int gt = unit / RB, rb = unit - gt * RB;
   const int ntiles = a.N >> 4;
   const int m = rb * 16 + (lane & 15);
   const bool live = gt < ntiles;
   const EpiIn e = live ? epi_load_at<EPI>(a, gt, m, lane) : EpiIn{};
-  const int ks = KS ? KS : w.ks;
   using slab_t = std::conditional_t<H16, f16x4, f32x4>;
   const slab_t* src = reinterpret_cast<const slab_t*>(w.part) + (size_t)unit * 64 + lane;
-  auto widen = [](const slab_t& x) -> f32x4 {
-    if constexpr (H16) return f32x4{(float)x[0], (float)x[1], (float)x[2], (float)x[3]};
-    else return x;
+  auto ld_slab = [&](int k) -> f32x4 {
+    const slab_t* q = src + (size_t)k * n_units * 64;
+    if constexpr (COH && H16) {
+      const f16x4 h = __builtin_bit_cast(f16x4, __hip_atomic_load(reinterpret_cast<const uint64_t*>(q),
+                                                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+      return f32x4{(float)h[0], (float)h[1], (float)h[2], (float)h[3]};
+    } else if constexpr (COH) {
+      const uint64_t* d = reinterpret_cast<const uint64_t*>(q);
+      const f32x2 lo = __builtin_bit_cast(f32x2, __hip_atomic_load(d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+      const f32x2 hi = __builtin_bit_cast(f32x2, __hip_atomic_load(d + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+      return f32x4{lo[0], lo[1], hi[0], hi[1]};
+    } else if constexpr (H16) {
+      const f16x4 h = *q;
+      return f32x4{(float)h[0], (float)h[1], (float)h[2], (float)h[3]};
+    } else {
+      return *q;
+    }
+  };
+  const uint8_t* exsrc = w.part_ex + (size_t)unit * 64 + lane;  // H16 without NORM: the lane's exponent per split
+  auto ld_ex = [&](int k) -> int {
+    const uint8_t* q = exsrc + (size_t)k * n_units * 64;
+    if constexpr (COH) return __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else return *q;
+  };
+  const float* ssrc = w.part_ss + (size_t)(gt / w.bnt) * ks * BM + m;
+  auto ld_ss = [&](int k) -> float {
+    if constexpr (COH) return __hip_atomic_load(ssrc + k * BM, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else return ssrc[k * BM];
   };
   auto unscale = [](f32x4 x, int ex) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) x[i] = __builtin_amdgcn_ldexpf(x[i], ex);
     return x;
   };
-  const uint8_t* exsrc = w.part_ex + (size_t)unit * 64 + lane;  // H16 without NORM: the lane's exponent per split
-  const float* ssrc = w.part_ss + (size_t)(gt / w.bnt) * ks * BM + m;
   f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
   float ss = 0.f;
-  if constexpr (KS > 0) {
-    slab_t p[KS];
-    float q[KS];
-    int ex[KS];
+  f32x4 p[WG_INL_KS];
+  float q[WG_INL_KS];
+  int ex[WG_INL_KS];
+  // every piece's loads before the first add (up to WG_INL_KS; more pieces in a second pass).  No branch around a
+  // load: past the last piece a lane re-loads the last one (a cache hit) and adds it times 0 -- a conditional load
+  // made hipcc wait for each one (vmcnt(0) per piece: one memory round trip per piece)
+  for (int k0 = 0; k0 < ks; k0 += WG_INL_KS) {
 #pragma unroll
-    for (int k = 0; k < KS; ++k) p[k] = src[(size_t)k * n_units * 64];
+    for (int k = 0; k < WG_INL_KS; ++k) p[k] = ld_slab(min(k0 + k, ks - 1));
     if constexpr (H16 && !NORM) {
 #pragma unroll
-      for (int k = 0; k < KS; ++k) ex[k] = exsrc[(size_t)k * n_units * 64];
+      for (int k = 0; k < WG_INL_KS; ++k) ex[k] = ld_ex(min(k0 + k, ks - 1));
     }
     if constexpr (NORM) {
 #pragma unroll
-      for (int k = 0; k < KS; ++k) q[k] = ssrc[k * BM];
+      for (int k = 0; k < WG_INL_KS; ++k) q[k] = ld_ss(min(k0 + k, ks - 1));
     }
 #pragma unroll
-    for (int k = 0; k < KS; ++k) {
-      if constexpr (H16 && NORM) v += widen(p[k]) * __builtin_sqrtf(q[k] + 1e-30f);
-      else if constexpr (H16) v += unscale(widen(p[k]), ex[k]);
-      else v += widen(p[k]);
-      if constexpr (NORM) ss += q[k];
-    }
-  } else {
-    for (int k = 0; k < ks; ++k) {
-      const f32x4 pk = widen(src[(size_t)k * n_units * 64]);
-      if constexpr (H16 && NORM) v += pk * __builtin_sqrtf(ssrc[k * BM] + 1e-30f);
-      else if constexpr (H16) v += unscale(pk, exsrc[(size_t)k * n_units * 64]);
-      else v += pk;
-    }
-    if constexpr (NORM) {
-      for (int k = 0; k < ks; ++k) ss += ssrc[k * BM];
+    for (int k = 0; k < WG_INL_KS; ++k) {
+      const float on = k0 + k < ks ? 1.f : 0.f;
+      if constexpr (H16 && NORM) v += p[k] * (__builtin_sqrtf(q[k] + 1e-30f) * on);
+      else if constexpr (H16) v += unscale(p[k], ex[k]) * on;
+      else v += p[k] * on;
+      if constexpr (NORM) ss += q[k] * on;
     }
   }
   if constexpr (NORM) v *= rms_inv(ss, a.K, a.eps);
@@ -469,6 +526,73 @@ __global__ __launch_bounds__(256) void wgemm_reduce_kernel(const GemmArgs a, con
   for (int i = 0; i < 4; ++i) pv[i] = __shfl_xor(v[i], 32, 64);
   if (!live) return;
   epi_store<EPI>(a, gt, m, lane, e, [&](int off) { return off ? pv : v; });
+}
+
+// In-launch split-K combine (the three wgemm_reduce_kernel launches per layer were 0.62 ms of the
+// 8.98 ms headline step).  The ks partners of a column block are one workgroup per CU, all resident together (the
+// host takes this path only when the grid fits the CU budget), so after publishing its slab write-through each
+// partner arrives on the block's ticket and WAITS for the others -- bounded: past WG_INL_SPIN the wait gives up --
+// then claims its own 1/ks of the block's units (one bit of the block's claim word) and combines them.  The LAST
+// arriver never waits: it combines its own piece, then claims every piece still unclaimed (a partner that gave up
+// waiting, or has not claimed yet) and combines those too, so the block completes whatever the residency; the
+// claim bit decides who combines a piece, exactly once.  The workgroup that leaves the block last resets its three
+// words (arrivals, claims, exits) for the next launch.  Counters: w.counters[3 * blk + {0, 1, 2}], zero at rest.
+constexpr long long WG_INL_SPIN = 20000;  // s_memrealtime ticks (100 MHz): 200 us
+template <int BM, int EPI, bool NORM, bool H16>
+__device__ void wg_inline_combine(const GemmArgs& a, const WgArgs& w, int blk, int kc, int n_units, int nthr,
+                                  unsigned* flags) {
+  unsigned& s_go = flags[0];
+  unsigned& s_claim = flags[1];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nwaves = nthr >> 6;
+  unsigned* ctr = w.counters + 3 * blk;
+  const int ks = w.ks;
+  const unsigned all = ks >= 32 ? 0xffffffffu : (1u << ks) - 1u;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's slab stores are done
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned t = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned go = t + 1 == unsigned(ks) ? 2u : 0u;  // 2: last arriver
+    if (!go) {
+      const long long t0 = __builtin_amdgcn_s_memrealtime();
+      while (true) {
+        if (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= unsigned(ks)) {
+          go = 1u;
+          break;
+        }
+        if (__builtin_amdgcn_s_memrealtime() - t0 > w.spin) break;
+        __builtin_amdgcn_s_sleep(2);
+      }
+    }
+    s_go = go;
+    s_claim = go ? (__hip_atomic_fetch_or(ctr + 1, 1u << kc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> kc) & 1u
+                 : 1u;  // 1: not mine to combine
+  }
+  __syncthreads();
+  const int upb = WG_NT * (BM / 16);  // units per column block
+  const int u0 = blk * upb;
+  auto combine = [&](int piece) {  // units [piece * upb / ks, (piece + 1) * upb / ks) of the block
+    const int b = piece * upb / ks, e = (piece + 1) * upb / ks;
+    for (int u = b + wave; u < e; u += nwaves) wg_reduce_unit<BM, EPI, NORM, H16, true>(a, w, u0 + u, n_units, lane, ks);
+  };
+  if (!s_claim) combine(kc);
+  if (s_go == 2u) {
+    __syncthreads();
+    if (threadIdx.x == 0)
+      s_claim = __hip_atomic_fetch_or(ctr + 1, all, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const unsigned left = ~s_claim & all;
+    for (int pc = 0; pc < ks; ++pc)
+      if ((left >> pc) & 1u) combine(pc);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if (__hip_atomic_fetch_add(ctr + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1 == unsigned(ks)) {
+      // every partner is past its last use of the block's words: ready for the next launch (launch-ordered)
+      __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(ctr + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(ctr + 2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
 }
 
 template <int BM, int EPI, bool NORM, bool H16 = false>
@@ -549,15 +673,33 @@ WgPlan wg_plan(int N, int K, int M) {
   return p;
 }
 
+// In-launch split-K combine (wg_inline_combine): cain_wgemm_set_inline(1) (CAIN_WGEMM_INLINE=1); 0 (default) the separate
+// wgemm_reduce_kernel launch (A/B, tests).  Taken only where every partner can be resident at once -- one
+// workgroup per CU (the ring's LDS), so grid <= the CU budget -- and the block's words fit the counter region.
+int g_wg_inline = 0;
+inline bool wg_use_inline(const WgPlan& p) {
+  return g_wg_inline && p.ks > 1 && p.ks <= 32 && p.nblk * p.ks <= cain_cu_budget() &&
+         3 * p.nblk * (int)sizeof(unsigned) <= WG_CTR_BYTES;
+}
+
 template <int BM, int DX, int DW, int EPI, bool NORM, int NDMA, int ABL = 0, bool H16 = true>
 hipError_t wg_launch(const GemmArgs& a, const WgArgs& w, const WgPlan& p, hipStream_t st) {
   using G = WgGeo<BM>;
   constexpr int lds = (DW + 1) * G::W_BYTES + (DX + 1) * G::X_BYTES;
   static_assert(lds <= 160 * 1024, "LDS");
-  static bool attr = [] {
-    return hipFuncSetAttribute(reinterpret_cast<const void*>(&wgemm_kernel<BM, DX, DW, EPI, NORM, NDMA, ABL, H16>),
-                               hipFuncAttributeMaxDynamicSharedMemorySize, lds) == hipSuccess;
-  }();
+  auto set_lds = [](const void* k) {
+    return hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, lds) == hipSuccess;
+  };
+  if constexpr (ABL == 0) {
+    if (wg_use_inline(p)) {
+      static bool attr_inl = set_lds(reinterpret_cast<const void*>(&wgemm_kernel<BM, DX, DW, EPI, NORM, NDMA, 0, H16, true>));
+      if (!attr_inl) return hipErrorInvalidConfiguration;
+      hipLaunchKernelGGL((wgemm_kernel<BM, DX, DW, EPI, NORM, NDMA, 0, H16, true>), dim3(p.nblk * p.ks),
+                         dim3(64 * (8 + NDMA)), lds, st, a, w);
+      return hipGetLastError();
+    }
+  }
+  static bool attr = set_lds(reinterpret_cast<const void*>(&wgemm_kernel<BM, DX, DW, EPI, NORM, NDMA, ABL, H16>));
   if (!attr) return hipErrorInvalidConfiguration;
   hipLaunchKernelGGL((wgemm_kernel<BM, DX, DW, EPI, NORM, NDMA, ABL, H16>), dim3(p.nblk * p.ks), dim3(64 * (8 + NDMA)),
                      lds, st, a, w);
@@ -612,6 +754,11 @@ CAIN_API int cain_wgemm_min_m() { return g_wgemm_min_m; }
 // A/B switches for tests and tuning tools (take effect for launches and graph captures after the call).
 CAIN_API void cain_wgemm_set_min_m(int m) { g_wgemm_min_m = m; }
 CAIN_API void cain_wgemm_set_variant(int v) { g_wgemm_variant = v; }
+// 0: separate reduce launch; 1: in-launch combine (default); 2: in-launch combine whose partners never wait, so the
+// last arriver combines every piece (the give-up path, for tests)
+CAIN_API void cain_wgemm_set_inline(int mode) { g_wg_inline = mode < 0 ? 0 : mode > 2 ? 2 : mode; }
+CAIN_API int cain_wgemm_get_inline() { return g_wg_inline; }
+
 CAIN_API void cain_wgemm_set_split(int target, int ksmax) { g_wg_target = target, g_wg_ksmax = ksmax; }
 // Per-shape plan: split count (<= 0: the default rule) and ring variant (< 0: the global one) for GEMMs of N
 // columns over K with the bm-row tile (128 or 256).  Returns 0, or -1 when the table is full.
@@ -644,6 +791,10 @@ CAIN_API int cain_wgemm_eligible(int N, int K, int M) {
   return mm > 0 && M > mm && M <= 256 && K % WG_BK == 0 && N % 16 == 0 && K >= 4 * WG_BK;
 }
 
+CAIN_API int cain_wgemm_inline(int N, int K, int M) {  // 1: this shape's next launch combines in-launch
+  return cain_wgemm_eligible(N, K, M) && wg_use_inline(wg_plan(N, K, M));
+}
+
 CAIN_API long long cain_wgemm_ws_bytes(int N, int K, int M) {
   if (!cain_wgemm_eligible(N, K, M)) return 0;
   const WgPlan p = wg_plan(N, K, M);
@@ -666,9 +817,10 @@ int wgemm_dispatch(const GemmArgs& a, int epi, bool norm, void* ws, long long ws
   // fetched per XCD); 25.8k -> 26.3k tok/s.
   w.xcd_blk = p.ks > 1 && p.nblk % 8 == 0;
   w.bnt = p.bnt;
-  // [counter region: 2 per column block, zero at rest][slabs][sums]
+  // [counter region: 3 words per column block for the in-launch combine, zero at rest][slabs][sums]
   w.counters = static_cast<unsigned*>(ws);
   w.stamps = g_wg_stamps;
+  w.spin = g_wg_inline == 2 ? 0 : WG_INL_SPIN;
   w.part = reinterpret_cast<float*>(static_cast<char*>(ws) + WG_CTR_BYTES);
   w.part_ss = w.part + p.part_floats;
   w.part_ex = reinterpret_cast<uint8_t*>(w.part_ss + p.ss_floats);

@@ -80,7 +80,8 @@ struct WgArgs {
   uint8_t* part_ex; // [ks][n_units][64 lanes] power-of-two exponent of each non-NORM fp16 slab lane (value = half * 2^ex)
   int xcd_blk;      // 1: a column block's split partners and its reducers share one XCD (wgemm.hip)
   int bnt;          // 16-column tiles per column block of the main kernel (wgemm.hip: WG_NT = 8, wgemm256.hip: 16)
-  unsigned* counters;  // workspace head (WG_CTR_BYTES, zero at rest; unused by the kernels)
+  unsigned* counters;  // workspace head (WG_CTR_BYTES, zero at rest): the in-launch combine's words (wgemm.hip)
   unsigned long long* stamps;  // diagnostic build only (wgemm.hip ABL 3): [grid][2 waves][8] timestamps
+  long long spin;   // in-launch combine: how long a partner waits for the others (s_memrealtime ticks; 0: never)
 };
 

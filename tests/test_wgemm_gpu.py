@@ -161,3 +161,60 @@ def test_fp16_slabs_scale_outlier_rows(norm, scale):
     for rows in (slice(0, None, 7), slice(1, None, 7)):  # outlier rows and ordinary rows, each against fp32
         assert rel_err(y16[rows], y32[rows]) < 2e-3, (rows, rel_err(y16[rows], y32[rows]))
         assert rel_err(y16[rows], ref[rows]) < 3e-3
+
+
+@pytest.mark.parametrize("N,K,norm,epi,variant", [(4096, 4096, False, "resid", 0), (6144, 4096, True, "f32", 0),
+                                                  (4096, 14336, False, "f32", 0), (4096, 4096, True, "f32", 4),
+                                                  (2048, 8192, True, "f32", 0)])
+def test_inline_combine_matches_the_reduce_launch(N, K, norm, epi, variant):
+    """the split-K combine inside the GEMM launch (wg_inline_combine) gives the same outputs as
+    the separate wgemm_reduce_kernel launch -- also on the give-up path, where no partner waits and the last arriver
+    combines every piece -- and leaves the block counters at zero for the next launch."""
+    torch.manual_seed(N ^ K)
+    M = 256
+    W = (torch.randn(N, K, device=DEV) * 0.02).bfloat16()
+    x = (2 * torch.randn(M, K, device=DEV)).bfloat16()
+    x[7] *= 300.0  # an outlier row (fp16 slab scaling)
+    wp = pack_mfma_a(W)
+    r0 = torch.randn(M, N, device=DEV).bfloat16()
+    outs = {}
+    mode0 = ops.wide_gemm_inline_mode()
+    try:
+        ops.set_wide_gemm_variant(variant)
+        for mode in (0, 1, 2, 1):
+            ops.set_wide_gemm_inline(mode)
+            assert ops.wide_gemm_inline(N, K, M) == (mode > 0 and ops.wide_gemm_plan(N, K, M)[0] > 1)
+            if epi == "resid":
+                r = r0.clone()
+                ops.skinny_gemm(wp, x, N, ops.EPI_RESID, out=r, norm=norm)
+                outs.setdefault(mode, []).append(r)
+            else:
+                outs.setdefault(mode, []).append(ops.skinny_gemm(wp, x, N, ops.EPI_F32, norm=norm, eps=1e-6))
+            torch.cuda.synchronize()
+            ws = ops._ws_cache[DEV]
+            assert int(ws[16384:16384 + 4096].count_nonzero()) == 0  # the wide path's counter words, reset
+    finally:
+        ops.set_wide_gemm_inline(mode0)
+        ops.set_wide_gemm_variant(0)
+    assert ops.wide_gemm_plan(N, K, M)[0] > 1  # a split plan: the combine ran
+    ref = _normed(x, norm) @ W.float().t() + (r0.float() if epi == "resid" else 0)
+    assert rel_err(outs[0][0], ref) < (1e-2 if epi == "resid" else 2e-3)
+    for mode in (1, 2):
+        for y in outs[mode]:
+            assert bool((y == outs[0][0]).all()), mode  # same pieces summed in the same order
+
+
+def test_inline_combine_falls_back_when_the_grid_exceeds_the_cus():
+    """A split plan whose grid is larger than the CU count cannot have every partner resident: it runs the separate
+    reduce launch (the plan override asks for 16 splits of 32 column blocks = 512 workgroups)."""
+    N, K, M = 4096, 4096, 256
+    mode0 = ops.wide_gemm_inline_mode()
+    try:
+        ops.set_wide_gemm_inline(1)
+        ops.set_wide_gemm_plan(N, K, 256, 16, 0)
+        assert not ops.wide_gemm_inline(N, K, M)
+        ops.set_wide_gemm_plan(N, K, 256, 4, 0)
+        assert ops.wide_gemm_inline(N, K, M)
+    finally:
+        ops.clear_wide_gemm_plans()
+        ops.set_wide_gemm_inline(mode0)
