@@ -64,6 +64,14 @@ __device__ __forceinline__ bf16x8 q4_frag(uint32_t w) {
 
 __device__ __forceinline__ float q4_h2f(uint32_t h) { return float(__builtin_bit_cast(_Float16, (uint16_t)h)); }
 
+// sum over the 4 lanes of a quad (4j .. 4j + 3) by two DPP quad permutations (xor 1, xor 2): no LDS round trip (the
+// ds_bpermute of __shfl_xor cost ~6 % of qwen2:1.5b's batch-1 rate in the staging); every lane gets the same value
+__device__ __forceinline__ float q4_quad_sum(float v) {
+  v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, false));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, false));
+  return v;
+}
+
 __device__ __forceinline__ void q4_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 template <int WAVES>
@@ -78,7 +86,9 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(4, 4
   constexpr int XLB = q4_xl_bytes<WAVES>();
   constexpr int XCH = XLB / (WAVES * 64 * 16);  // 16-byte activation chunks staged per thread (upper bound)
   __shared__ __attribute__((aligned(16))) char q4_xs[XLB];
-  __shared__ __attribute__((aligned(16))) f32x4 red[2][WAVES][64];
+  // per wave, its 16 x 16 partial in [activation row m][weight row n] order (the epilogues' lane order, read back
+  // as one 16-byte vector per lane)
+  __shared__ __attribute__((aligned(16))) float red[2][WAVES][256];
   __shared__ float row_ss[16];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
@@ -131,13 +141,24 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(4, 4
   int cp_t = blockIdx.x;
   EpiIn pre{};
   if (wave == 0 && my_tiles > 0) pre = epi_load_at<EPI>(a, cp_t, lane & 15, lane);
+  const bool gained = q4.gain != nullptr;
 #pragma unroll
   for (int i = 0; i < XCH; ++i) {
     const int c = (int)threadIdx.x + i * WAVES * 64;
     if (c < nch) *reinterpret_cast<bf16x8*>(q4_xs + (size_t)c * 16) = xst[i];
+    if (!gained) {
+      // the block sums straight from the staged registers: a 32-element block is 4 consecutive chunks, i.e. the 4
+      // lanes of a quad (cpr = K / 8 is a multiple of 4), summed in a fixed order
+      float sum = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) sum += bf2f(xst[i][j]);
+      sum = q4_quad_sum(sum);
+      if (c < nch && (c & 3) == 0) xsum[c >> 2] = sum;  // chunk c / 4 = row * NB + block
+    }
   }
   q4_barrier();
-  // sums of squares of the RAW rows (fixed order: wave w owns rows w, w + WAVES, ...)
+  // sums of squares of the RAW rows (fixed order: wave w owns rows w, w + WAVES, ...); the first tile end's barrier
+  // orders them before the epilogue reads them, unless the gain pass below rewrites the rows first
   if constexpr (NORM) {
     for (int r = wave; r < a.M; r += WAVES) {
       const char* xr = q4_xs + (size_t)r * cpr * 16;
@@ -151,34 +172,33 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(4, 4
       for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
       if (lane == 0) row_ss[r] = v;
     }
-    q4_barrier();
   }
-  // x' = bf16(x * gain) in place, and the 32-element block sums of x' (the values the MFMAs multiply): one thread
-  // per (row, block)
-  for (int rb = threadIdx.x; rb < a.M * NB; rb += WAVES * 64) {
-    const int r = rb / NB, b = rb - r * NB;
-    bf16x8* xp = reinterpret_cast<bf16x8*>(q4_xs + ((size_t)r * a.K + b * 32) * 2);
-    float sum = 0.f;
+  if (gained) {
+    // a separate gain (weights not gain-folded: a GGUF file's values): x' = bf16(x * gain) in place, then the block
+    // sums of x' (the values the MFMAs multiply), one thread per (row, block)
+    if constexpr (NORM) q4_barrier();  // the raw rows' sums of squares are taken
+    for (int rb = threadIdx.x; rb < a.M * NB; rb += WAVES * 64) {
+      const int r = rb / NB, b = rb - r * NB;
+      bf16x8* xp = reinterpret_cast<bf16x8*>(q4_xs + ((size_t)r * a.K + b * 32) * 2);
+      float sum = 0.f;
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      bf16x8 x8 = xp[c];
-      if (q4.gain) {
+      for (int c = 0; c < 4; ++c) {
+        bf16x8 x8 = xp[c];
         const f32x4 g0 = *reinterpret_cast<const f32x4*>(q4.gain + b * 32 + c * 8);
         const f32x4 g1 = *reinterpret_cast<const f32x4*>(q4.gain + b * 32 + c * 8 + 4);
 #pragma unroll
         for (int j = 0; j < 4; ++j) x8[j] = (__bf16)(bf2f(x8[j]) * g0[j]), x8[4 + j] = (__bf16)(bf2f(x8[4 + j]) * g1[j]);
         xp[c] = x8;
-      }
 #pragma unroll
-      for (int j = 0; j < 8; ++j) sum += bf2f(x8[j]);
+        for (int j = 0; j < 8; ++j) sum += bf2f(x8[j]);
+      }
+      xsum[rb] = sum;
     }
-    xsum[rb] = sum;
+    q4_barrier();
   }
-  q4_barrier();
 
   // A operand: this lane's activation row m = lane & 15 (rows >= M multiply zeros), k group g
   const int g = lane >> 4;
-  const bool xrow = (lane & 15) < a.M;
   const int xm = min(lane & 15, a.M - 1);
   const __bf16* xl_row = reinterpret_cast<const __bf16*>(q4_xs) + (size_t)xm * a.K + g * 8;
   const float* xs_row = xsum + (size_t)xm * NB + g;
@@ -187,58 +207,58 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(4, 4
   f32x4 corr = f32x4{0.f, 0.f, 0.f, 0.f};  // sum_b (128 s_nb + o_nb) X_b
   int cp_e = 0, buf = 0;
 
-  auto step = [&](const Quad& q, int p) {
-    float sc[4], c2 = 0.f;
+  // one item: the 4 MFMAs (one per 32-block, zero accumulator) issue back to back, THEN their per-block scale-and-add
+  // (sched_barrier): interleaved, every FMA waited out its MFMA's latency (s_nop 2-7 each, profiles/r6).  `on` = 0
+  // zeroes a padding item's contribution (past its wave's quads, or past the end), so no branch wraps the MFMAs.
+  auto step = [&](const Quad& q, int p_raw, float on) {
+    const int p = min(p_raw, KQ - 1);
+    // this lane's weight row: the 4 block scales of the quad, and (for the correction MFMA) block 4p + g's
+    // coefficient -- the 16-bit entry picked by selects, not a lane-divergent branch
+    float sc[4], c2;
+    const uint32_t wg = (g & 2) ? q.s[1] : q.s[0];
+    const uint32_t vg = (g & 1) ? (wg >> 16) : (wg & 0xffffu);
     if constexpr (FMT == Q4F_0) {
 #pragma unroll
-      for (int s = 0; s < 4; ++s) sc[s] = q4_h2f(q.s[s >> 1] >> (16 * (s & 1)));
-      c2 = 136.f * (g == 0 ? sc[0] : g == 1 ? sc[1] : g == 2 ? sc[2] : sc[3]);  // 128 d + 8 d
+      for (int s = 0; s < 4; ++s) sc[s] = on * q4_h2f(q.s[s >> 1] >> (16 * (s & 1)));
+      c2 = (136.f * on) * q4_h2f(vg);  // 128 d + 8 d
     } else {
-      const float d = q4_h2f(q.d), dmin = q4_h2f(q.d >> 16);
-      float mn[4];
+      const float d = on * q4_h2f(q.d), dmin = on * q4_h2f(q.d >> 16);
 #pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        const uint32_t v = q.s[s >> 1] >> (16 * (s & 1));
-        sc[s] = d * float(v & 0xffu), mn[s] = dmin * float((v >> 8) & 0xffu);
-      }
-      c2 = g == 0 ? 128.f * sc[0] + mn[0] : g == 1 ? 128.f * sc[1] + mn[1] : g == 2 ? 128.f * sc[2] + mn[2]
-                                                                               : 128.f * sc[3] + mn[3];
+      for (int s = 0; s < 4; ++s) sc[s] = d * float((q.s[s >> 1] >> (16 * (s & 1))) & 0xffu);
+      c2 = 128.f * d * float(vg & 0xffu) + dmin * float(vg >> 8);
     }
+    f32x4 t[4];
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-      const bf16x8 wf = q4_frag(q.w[s]);
-      bf16x8 xv = {};
-      if (xrow) xv = *reinterpret_cast<const bf16x8*>(xl_row + p * 128 + s * 32);
-      const f32x4 t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xv, wf, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-      acc += t * sc[s];
+      // rows >= M read the last row (their outputs are never stored; a row of D depends on that row of A only)
+      const bf16x8 xv = *reinterpret_cast<const bf16x8*>(xl_row + p * 128 + s * 32);
+      t[s] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xv, q4_frag(q.w[s]), f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
     }
     // correction: A = the block sums (activation row m, block 4p + g), B = this lane's coefficient (weight row n,
     // block 4p + g); rows >= M hold the last row's sums, whose outputs the epilogue never stores
     corr = __builtin_amdgcn_mfma_f32_16x16x4f32(xs_row[p * 4], c2, corr, 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) acc += t[s] * sc[s];
   };
 
   // tile end: this wave's partial D'[m = 4g + i][n = lane & 15] into LDS; wave 0 sums the waves and reads the
   // TRANSPOSE (the epilogues take lane L = (act row L & 15, weight rows 4 (L >> 4) + i))
   auto tile_end = [&]() {
-    red[buf][wave][lane] = acc - corr;
+    const f32x4 v = acc - corr;  // D'[m = 4g + i][n = lane & 15]
+#pragma unroll
+    for (int i = 0; i < 4; ++i) red[buf][wave][(4 * g + i) * 16 + (lane & 15)] = v[i];
     acc = f32x4{0.f, 0.f, 0.f, 0.f};
     corr = f32x4{0.f, 0.f, 0.f, 0.f};
     q4_barrier();
     if (wave == 0) {
       const int tile = cp_t;
       if (cp_t != (int)blockIdx.x) pre = epi_load_at<EPI>(a, tile, lane & 15, lane);
-      const float* rf = reinterpret_cast<const float*>(&red[buf][0][0]);
-      auto unit_sum = [&](int L) -> f32x4 {
-        const int m = L & 15, gL = L >> 4;
-        f32x4 v;
+      auto unit_sum = [&](int L) -> f32x4 {  // lane L: activation row L & 15, weight rows 4 (L >> 4) + i
+        const int m = L & 15, off = m * 16 + 4 * (L >> 4);
+        f32x4 v = *reinterpret_cast<const f32x4*>(&red[buf][0][off]);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int src = 16 * (m >> 2) + 4 * gL + i;  // lane holding D'[m][n = 4 gL + i], element m & 3
-          float s = 0.f;
-#pragma unroll
-          for (int w = 0; w < WAVES; ++w) s += rf[((size_t)w * 64 + src) * 4 + (m & 3)];
-          v[i] = s;
-        }
+        for (int w = 1; w < WAVES; ++w) v += *reinterpret_cast<const f32x4*>(&red[buf][w][off]);
         if constexpr (NORM) v *= rms_inv(row_ss[min(m, a.M - 1)], a.K, a.eps);
         return v;
       };
@@ -253,7 +273,7 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(4, 4
       const int p = wave + cp_e * WAVES;
       const bool live = i0 + u < n_items;
       load_next(ring[(u + U) % (U + 1)]);
-      if (live && p < KQ) step(ring[u], p);
+      step(ring[u], p, (live && p < KQ) ? 1.f : 0.f);
       if (live && cp_e == qmax - 1) tile_end();
       if (++cp_e == qmax) cp_e = 0, cp_t += G;
     }
@@ -263,8 +283,9 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(4, 4
 // ================================================================ launch
 template <bool NORM, int EPI, int FMT>
 static hipError_t q4_launch_w(int waves, const GemmArgs& a, const Q4Args& q, int grid, int npairs, hipStream_t st) {
-  if (waves == 8)
-    hipLaunchKernelGGL((q4_stream_kernel<8, 4, EPI, NORM, FMT>), dim3(grid), dim3(512), 0, st, a, q, npairs);
+  if (EPI != EPI_QKV_ROPE && waves == 8)  // (the fused QKV epilogue has no 8-wave instance: it spills there)
+    hipLaunchKernelGGL((q4_stream_kernel<8, 4, EPI == EPI_QKV_ROPE ? EPI_BF16 : EPI, NORM, FMT>), dim3(grid),
+                       dim3(512), 0, st, a, q, npairs);
   else
     hipLaunchKernelGGL((q4_stream_kernel<4, 4, EPI, NORM, FMT>), dim3(grid), dim3(256), 0, st, a, q, npairs);
   return hipGetLastError();

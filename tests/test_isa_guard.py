@@ -63,3 +63,22 @@ def test_no_split_or_eight_wave_qkv_instance(stream_kernels):
     for name in stream_kernels:
         waves, u, epi, norm, split = _params(name)
         assert not (epi == 5 and (split or waves == 8)), name
+
+
+# gemm_q4.hip's stream kernels: the same loop, plus the activation-staging loop's gain loads (4 waits)
+Q4_LIMIT = {0: 9, 1: 9, 2: 5, 3: 5, 4: 5, 5: 21}
+
+
+def test_q4_stream_kernels_keep_counted_waits():
+    from cain_amd import build
+
+    lib = build.build_kernels()
+    found = {}
+    for co in isa_guard.code_objects(lib):
+        found.update(isa_guard.kernel_loop_waits(isa_guard.disassemble(co), "q4_stream_kernel"))
+    assert len(found) >= 20
+    for name, (n_loop, waits) in found.items():
+        m = re.search(r"q4_stream_kernelILi(\d+)ELi(\d+)ELi(\d+)ELb(\d)ELi(\d)E", name)
+        waves, u, epi, norm, fmt = (int(x) for x in m.groups())
+        assert n_loop > 0 and waits <= Q4_LIMIT[epi], f"{name}: {waits} vmcnt(0) in its loops"
+        assert not (epi == 5 and waves == 8), name

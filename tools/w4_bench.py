@@ -87,7 +87,7 @@ def main() -> int:
         out = torch.zeros(M, n_out, device=dev, dtype=torch.float32 if epi == ops.EPI_F32 else torch.bfloat16)
         rp = rope if epi == ops.EPI_QKV_ROPE else None
         for dt, cp in [(dt, cp) for dt in ns.dtypes.split(",") for cp in ns.copies.split(",")]:
-            bpp = {"fp4": 0.5 + 1 / 32, "fp8": 1.0, "bf16": 2.0}[dt]
+            bpp = {"fp4": 0.5 + 1 / 32, "fp8": 1.0, "bf16": 2.0, "q4_0": 0.5 + 1 / 16, "q4_k": 0.5 + 1 / 16 + 1 / 64}[dt]
             wbytes = int(N * K * bpp)
             ncopy = int(cp) if int(cp) > 0 else max(2, min(16, (768 << 20) // max(1, wbytes) + 1))
             if dt == "fp4":
@@ -108,6 +108,27 @@ def main() -> int:
                                               copies=ncopy, us=round(us, 2), TBps=round(wbytes / us / 1e6, 2))), flush=True)
                 ops.set_w4_variant(-1)
                 ops.set_w4_occupancy(0)
+            elif dt in ("q4_0", "q4_k"):
+                fmt = 1 if dt == "q4_k" else 0
+                nsb = N * K // 16 + (N * K // 64 if fmt else 0)
+                # random codes, scales 0x3c00 (fp16 1.0) / (sc, m) = (1, 0) and (d, dmin) = (1, 0): finite values
+                def rnd_sb():
+                    sb = torch.zeros(nsb, device=dev, dtype=torch.uint8)
+                    if fmt == 0:
+                        sb.view(torch.int16)[:] = 0x2c00
+                    else:
+                        sb[: N * K // 16].view(torch.int16)[:] = 1
+                        sb[N * K // 16:].view(torch.int32)[:] = 0x2c00
+                    return sb
+                ws = [(torch.randint(0, 256, (N // 16, K // 128, 64, 16), device=dev, dtype=torch.uint8), rnd_sb())
+                      for _ in range(ncopy)]
+
+                def fn(i, ws=ws):
+                    wq, sb = ws[i % len(ws)]
+                    ops.gemm_q4(fmt, wq, sb, xk, N, epi, out=out, norm=norm, rope=rp)
+                us = graph_time(fn)
+                print(json.dumps(dict(role=role, dtype=dt, N=N, K=K, M=M, us=round(us, 2),
+                                      TBps=round(wbytes / us / 1e6, 2))), flush=True)
             elif dt == "fp8":
                 ws = [(torch.randint(0, 120, (N // 16, K // 64, 64, 16), device=dev, dtype=torch.uint8),
                        torch.full((N,), 0.01, device=dev)) for _ in range(ncopy)]
