@@ -165,6 +165,23 @@ def attention_splits(M: int, Hkv: int, T_max: int) -> int:
     return int(max(1, min(64, ns)))
 
 
+def _load_ckpt(ckpt, cfg: ModelConfig, device, weight_dtype: str) -> ModelWeights:
+    w = load_hf_weights(ckpt, cfg, device=device)
+    _attach_native(w, ckpt, cfg, weight_dtype, device)
+    return w
+
+
+def _attach_native(weights: ModelWeights, path, cfg: ModelConfig, weight_dtype: str, device) -> None:
+    """A GGUF checkpoint run on a GGUF block format (weight_dtype q4_0 / q4_k): keep its blocks as stored
+    (models/q4.py gguf_q4_native) for pack_for_engine, instead of re-quantising the decoded values."""
+    from ..models.gguf import GGUFFile, is_gguf
+
+    if weight_dtype in ("q4_0", "q4_k") and path and is_gguf(path):
+        from ..models.q4 import Q4_FORMATS, gguf_q4_native
+
+        weights.native = gguf_q4_native(GGUFFile(path), cfg, Q4_FORMATS[weight_dtype], device=device)
+
+
 class DecodeEngine:
     @classmethod
     def from_pretrained(cls, path: str, device: Union[str, torch.device] = "cuda", name: Optional[str] = None,
@@ -173,6 +190,7 @@ class DecodeEngine:
         ``models/hf.py``): the same kernels and options as a tag's engine (``weight_dtype="fp4"`` quantises the
         checkpoint's bf16 weights to MXFP4 at load, as the packing of random weights does)."""
         cfg, weights, tok = load_pretrained(path, name=name, device=torch.device(device))
+        _attach_native(weights, path, cfg, kw.get("weight_dtype", "bf16"), torch.device(device))
         return cls(cfg, device=device, weights=weights, tokenizer=tok, **kw)
 
     def __init__(self, model: Union[str, ModelConfig], device: Union[str, torch.device] = "cuda",
@@ -238,7 +256,7 @@ class DecodeEngine:
         self.keep_natural = keep_natural
         t0 = time.perf_counter_ns()
         if weights is None:
-            weights = (load_hf_weights(ckpt, self.cfg, device=self.device) if ckpt
+            weights = (_load_ckpt(ckpt, self.cfg, self.device, weight_dtype) if ckpt
                        else random_weights(self.cfg, device=self.device, seed=seed))
         self.weights = weights
         if backend == "hip":
@@ -335,6 +353,7 @@ class DecodeEngine:
         self.gemm_ws = torch.zeros(max(ws, 16) // 4 + 1, device=dev, dtype=torch.int32)
         d.gemm_ws, d.gemm_ws_bytes = _ptr(self.gemm_ws), ws
         d.wfmt, d.lm_head_scale = WFMT[self.weight_dtype], _ptr(packed.get("lm_head_scale"))
+        d.q4_gain = int(bool(packed.get("q4_gain")))  # GGUF blocks as stored: gains applied to the activations
         self._desc = d
         self._plans: Dict[int, int] = {}
         self._graphs: Dict[tuple, int] = {}

@@ -311,7 +311,14 @@ def quantize_q4_0(x: np.ndarray) -> np.ndarray:
     return np.concatenate([d.astype(np.float16).view(np.uint8), qs], 1).reshape(-1)
 
 
-_QUANT = {"Q8_0": quantize_q8_0, "Q4_0": quantize_q4_0}
+def quantize_q4_k(x: np.ndarray) -> np.ndarray:
+    """Q4_K blocks (models/q4.py's min/max fit) of ``x`` (length a multiple of 256)."""
+    from .q4 import quantize_q4_k as q4k
+
+    return q4k(torch.from_numpy(np.asarray(x, np.float32).reshape(-1, 256))).numpy().reshape(-1)
+
+
+_QUANT = {"Q8_0": quantize_q8_0, "Q4_0": quantize_q4_0, "Q4_K": quantize_q4_k}
 
 
 # ---------------------------------------------------------------------------------------------------- writer

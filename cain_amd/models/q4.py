@@ -142,3 +142,58 @@ def q4_roundtrip(w: torch.Tensor, fmt: int) -> torch.Tensor:
     """The values a Q4 engine multiplies by: dequant(quant(w)), in w's dtype (the torch oracle)."""
     n, k = w.shape
     return dequantize_q4(quantize_q4(w, fmt), fmt, n, k).to(w.dtype)
+
+
+def gguf_q4_native(g, cfg, fmt: int, device="cpu") -> Dict[str, object]:
+    """A GGUF file's GEMM weights as ggml blocks of ``fmt`` (uint8 [N, K / elems, bytes]) in the engine's natural
+    row order -- the same row operations as ``gguf.load_gguf_weights`` (Llama q / k un-permuted, q / k / v
+    concatenated, Phi-3's fused gate/up split), applied to whole rows of blocks, so no value changes.  Tensors the
+    file stores in another type (a Q4_K_M file's Q6_K tensors, an F16 output head) are quantised to ``fmt`` from
+    their decoded values and listed under ``requantized``.  Result: {"fmt", "layers": [{wqkv, wo, w_gate, w_up,
+    w_down}], "lm_head", "requantized"}, attached to ``ModelWeights.native`` for ``pack_for_engine``."""
+    import numpy as np
+
+    from .gguf import unpermute_qk
+
+    arch = g.metadata["general.architecture"]
+    bb, be = _BLOCK_BYTES[fmt], _BLOCK_ELEMS[fmt]
+    requant = []
+
+    def blocks(name: str) -> torch.Tensor:
+        t = g.tensors[name]
+        n, k = t.shape
+        if t.type == GGML_TYPE[fmt]:
+            return torch.from_numpy(np.array(g.raw(name))).to(device).reshape(n, k // be, bb)
+        requant.append(f"{name} ({t.type_name})")
+        return quantize_q4(g.tensor(name, device=device, dtype=torch.float32), fmt)
+
+    f = cfg.ffn
+    layers = []
+    for i in range(cfg.n_layers):
+        p = f"blk.{i}."
+        if g.has(p + "attn_qkv.weight"):
+            qkv = blocks(p + "attn_qkv.weight")
+        else:
+            q, kk = blocks(p + "attn_q.weight"), blocks(p + "attn_k.weight")
+            if arch == "llama":
+                q, kk = unpermute_qk(q, cfg.n_heads), unpermute_qk(kk, cfg.n_kv_heads)
+            qkv = torch.cat([q, kk, blocks(p + "attn_v.weight")], 0)
+        if g.has(p + "ffn_gate.weight"):
+            gate, up = blocks(p + "ffn_gate.weight"), blocks(p + "ffn_up.weight")
+        else:  # phi3: ffn_up = [gate; up]
+            gu = blocks(p + "ffn_up.weight")
+            gate, up = gu[:f].contiguous(), gu[f:].contiguous()
+        layers.append({"wqkv": qkv.contiguous(), "wo": blocks(p + "attn_output.weight"), "w_gate": gate,
+                       "w_up": up, "w_down": blocks(p + "ffn_down.weight")})
+    lm = blocks("output.weight") if g.has("output.weight") else blocks("token_embd.weight")
+    return {"fmt": fmt, "layers": layers, "lm_head": lm, "requantized": requant}
+
+
+def pack_native(blocks: torch.Tensor, fmt: int, gain: Optional[torch.Tensor] = None,
+                rows: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Pack ggml blocks [N, K / elems, bytes] (rows reordered by ``rows`` first) for the kernel, the RMSNorm gain
+    appended unfolded (a file's values stay exact)."""
+    n = blocks.shape[0]
+    k = blocks.shape[1] * _BLOCK_ELEMS[fmt]
+    b = blocks if rows is None else blocks[rows]
+    return pack_q4(q4_fields(b.contiguous(), fmt, n, k), fmt, gain)

@@ -227,6 +227,9 @@ class ModelWeights:
     lm_head: torch.Tensor               # [V, d] (aliases embed when tied)
     layers: List[LayerWeights]
     packed: Dict[str, object] = field(default_factory=dict)
+    # weights kept in a file's quantised form (models/q4.py gguf_q4_native: GGUF Q4_0 / Q4_K blocks), packed as
+    # stored by pack_for_engine when the engine's weight_dtype is that format
+    native: Dict[str, object] = field(default_factory=dict)
 
     @property
     def device(self) -> torch.device:
@@ -316,6 +319,8 @@ def q4_roundtrip_weights(mw: ModelWeights, weight_dtype: str) -> ModelWeights:
     from .q4 import Q4_FORMATS, q4_roundtrip
 
     fmt = Q4_FORMATS[weight_dtype]
+    if mw.native.get("fmt") == fmt:
+        return mw  # a GGUF file's blocks run as stored: the loaded (decoded) weights are the values, gains separate
     return _roundtrip(mw, lambda w: q4_roundtrip(w, fmt))
 
 
@@ -352,6 +357,33 @@ def pack_for_engine(mw: ModelWeights, free_natural: bool = False, weight_dtype: 
     fp4 = weight_dtype == "fp4"
     q4 = weight_dtype in ("q4_0", "q4_k")
     perm = qkv_row_permutation(cfg).to(mw.device)
+
+    native = None
+    if q4:
+        from .q4 import Q4_FORMATS, pack_native
+        if mw.native.get("fmt") == Q4_FORMATS[weight_dtype]:
+            native = mw.native
+    if native is not None:
+        # a GGUF file's blocks as stored: row operations only (QKV RoPE order, gate/up interleave), the norm gains
+        # appended to the scale buffers of the GEMMs they feed instead of folded in (runtime.hip q4_gain)
+        fmt = native["fmt"]
+        layers = []
+        for lw, nl in zip(mw.layers, native["layers"]):
+            ga = effective_gain(cfg, lw.attn_norm).float()
+            gm = effective_gain(cfg, lw.mlp_norm).float()
+            lp: Dict[str, object] = {"bqkv": None if lw.bqkv is None else lw.bqkv.float()[perm].contiguous()}
+            lp["wqkv"], lp["sqkv"] = pack_native(nl["wqkv"], fmt, ga, rows=perm)
+            lp["wo"], lp["so"] = pack_native(nl["wo"], fmt)
+            g_, u_ = nl["w_gate"], nl["w_up"]
+            gu = interleave_tiles(g_.reshape(g_.shape[0], -1), u_.reshape(u_.shape[0], -1), tile=8)
+            lp["wgu"], lp["sgu"] = pack_native(gu.reshape(-1, *g_.shape[1:]), fmt, gm)
+            lp["wdown"], lp["sdown"] = pack_native(nl["w_down"], fmt)
+            layers.append(lp)
+        packed = {"layers": layers, "weight_dtype": weight_dtype, "q4_gain": True}
+        packed["lm_head"], packed["lm_head_scale"] = pack_native(native["lm_head"], fmt,
+                                                                 effective_gain(cfg, mw.final_norm).float())
+        mw.packed = packed
+        return packed
 
     def put(dst: Dict[str, object], name: str, w: torch.Tensor) -> None:
         if q4:

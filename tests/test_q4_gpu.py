@@ -173,3 +173,38 @@ def test_q4_engine_generate_graph_equals_eager():
     b = eng.generate(prompts, 10, opts, use_graph=False)
     assert [r.tokens for r in a] == [r.tokens for r in b]
     eng.close()
+
+
+@pytest.mark.parametrize("family,arch", [("llama", "llama"), ("gemma", "gemma")])
+@pytest.mark.parametrize("ttype,wd", [("Q4_K", "q4_k"), ("Q4_0", "q4_0")])
+def test_gguf_file_runs_its_blocks_as_stored(family, arch, ttype, wd, tmp_path):
+    """A GGUF file of Q4_K / Q4_0 weights on weight_dtype q4_k / q4_0: the engine packs the file's blocks as stored
+    (norm gains applied to the activations, not folded into the values) and its logits match the fp32 oracle of the
+    file's decoded weights (transformers-free: gguf.py's decoders)."""
+    import sys
+    from pathlib import Path
+
+    sys.path.insert(0, str(Path(__file__).parent))
+    from hf_fixtures import make_checkpoint
+
+    from cain_amd.models.gguf import export_gguf, load_gguf
+    from cain_amd.models.hf import load_pretrained
+
+    make_checkpoint(family, tmp_path / "hf", scale=4.0)
+    _, mw, _ = load_pretrained(tmp_path / "hf", dtype=torch.float32)
+    for lw in mw.layers:  # non-unit gains: the separate-gain path must apply them
+        lw.attn_norm = lw.attn_norm + 0.3 * torch.rand_like(lw.attn_norm)
+        lw.mlp_norm = lw.mlp_norm + 0.3 * torch.rand_like(lw.mlp_norm)
+    export_gguf(mw, tmp_path / "m.gguf", arch, tensor_type=ttype)
+    eng = DecodeEngine.from_pretrained(str(tmp_path / "m.gguf"), device="cuda", max_batch=2, max_context=256,
+                                       weight_dtype=wd)
+    assert eng._packed.get("q4_gain") and eng.weights.native["requantized"] == []
+    _, mg, _ = load_gguf(tmp_path / "m.gguf", dtype=torch.float32)
+    ref = ReferenceModel(mg)
+    ids = [[1, 5, 9, 33, 100, 7, 64], [1, 200, 3]]
+    got = eng.last_logits(ids)
+    for i, p in enumerate(ids):
+        want = ref.forward(torch.tensor([p]))[0, -1]
+        cos = torch.nn.functional.cosine_similarity(got[i].float().cpu(), want.float(), dim=0)
+        assert cos > 0.999, (family, wd, i, float(cos))
+    eng.close()

@@ -118,3 +118,31 @@ def test_engine_rejects_q4_on_widths_not_a_multiple_of_256():
 
     with pytest.raises(ValueError, match="multiples of 256"):
         DecodeEngine("tiny-qwen2:1.5b", device="cpu", max_batch=1, max_context=64, weight_dtype="q4_k")
+
+
+@pytest.mark.parametrize("family,arch", [("llama", "llama"), ("gemma", "gemma")])
+@pytest.mark.parametrize("ttype,fmt", [("Q4_K", 1), ("Q4_0", 0)])
+def test_gguf_blocks_are_kept_as_stored(family, arch, ttype, fmt, tmp_path):
+    """a GGUF file whose weights are Q4_K / Q4_0 runs its blocks as stored -- gguf_q4_native's
+    blocks decode to exactly the values load_gguf_weights decodes (after the same row operations: Llama q / k
+    un-permuted, q / k / v concatenated), so nothing is re-quantised."""
+    from hf_fixtures import make_checkpoint
+
+    from cain_amd.models.gguf import GGUFFile, export_gguf, load_gguf
+    from cain_amd.models.hf import load_pretrained
+    from cain_amd.models.q4 import gguf_q4_native
+
+    make_checkpoint(family, tmp_path / "hf", scale=4.0)
+    _, mw, _ = load_pretrained(tmp_path / "hf", dtype=torch.float32)
+    export_gguf(mw, tmp_path / "m.gguf", arch, tensor_type=ttype)
+    cfg, mg, _ = load_gguf(tmp_path / "m.gguf", dtype=torch.float32)
+    nat = gguf_q4_native(GGUFFile(tmp_path / "m.gguf"), cfg, fmt)
+    assert nat["requantized"] == []
+
+    def dq(b):
+        return dequantize_q4(b, fmt, b.shape[0], b.shape[1] * (256 if fmt else 32))
+
+    for lw, nl in zip(mg.layers, nat["layers"]):
+        for name in ("wqkv", "wo", "w_gate", "w_up", "w_down"):
+            assert torch.equal(dq(nl[name]), getattr(lw, name)), name
+    assert torch.equal(dq(nat["lm_head"]), mg.lm_head)

@@ -191,7 +191,7 @@ def test_inline_combine_matches_the_reduce_launch(N, K, norm, epi, variant):
             else:
                 outs.setdefault(mode, []).append(ops.skinny_gemm(wp, x, N, ops.EPI_F32, norm=norm, eps=1e-6))
             torch.cuda.synchronize()
-            ws = ops._ws_cache[DEV]
+            ws = ops._ws_cache[x.device]
             assert int(ws[16384:16384 + 4096].count_nonzero()) == 0  # the wide path's counter words, reset
     finally:
         ops.set_wide_gemm_inline(mode0)
