@@ -148,6 +148,26 @@ def h1_rows(subsets) -> List[dict]:
 
 
 IDLE_SUB = "idle_subtracted_J"
+IDLE_NORM = "idle_normalised_J"
+
+
+def add_idle_normalised(df) -> Optional[float]:
+    """Per-session idle normalisation: each study session ran on a fresh box whose idle floor
+    differs by ~40 W, and at short lengths the client board's idle x window is most of the gross energy, so box
+    identity inflates the spread.  ``idle_normalised_J`` = gross + (idle_ref - the row's ``idle_power_W``) x its
+    ``energy_window_s``: every run charged at ONE idle floor, idle_ref = the mean session idle power of the pooled
+    table (returned).  Gross (the reference's quantity) and idle-subtracted stay as they are."""
+    import pandas as pd
+
+    if not {"idle_power_W", "energy_window_s", ENERGY} <= set(df.columns):
+        return None
+    idle = pd.to_numeric(df["idle_power_W"], errors="coerce")
+    win = pd.to_numeric(df["energy_window_s"], errors="coerce")
+    if not idle.notna().any():
+        return None
+    ref = float(idle.dropna().mean())
+    df[IDLE_NORM] = df[ENERGY] + (ref - idle) * win
+    return ref
 
 
 def energy_view_rows(subsets) -> List[dict]:
@@ -160,7 +180,7 @@ def energy_view_rows(subsets) -> List[dict]:
         a, b = subsets.get(f"{ON_DEVICE}_{label}"), subsets.get(f"{REMOTE}_{label}")
         if a is None or b is None:
             continue
-        for view, col in (("gross", ENERGY), ("idle_subtracted", IDLE_SUB)):
+        for view, col in (("gross", ENERGY), ("idle_normalised", IDLE_NORM), ("idle_subtracted", IDLE_SUB)):
             if col not in a.columns or col not in b.columns:
                 continue
             x = pd.to_numeric(a[col], errors="coerce").dropna()
@@ -171,6 +191,7 @@ def energy_view_rows(subsets) -> List[dict]:
             mx, my = float(x.mean()), float(y.mean())
             rows.append({"length": label, "words": L, "view": view, "n_on_device": int(len(x)),
                          "n_remote": int(len(y)), "mean_on_device": mx, "mean_remote": my,
+                         "sd_on_device": float(x.std()), "sd_remote": float(y.std()),
                          "ratio": mx / my if my > 0 else float("nan"), "W": w.statistic, "p": w.p_value,
                          "cliffs_delta": c.estimate, "magnitude": c.magnitude})
     return rows
@@ -282,6 +303,8 @@ def h1_markdown(rows) -> str:
 
 
 def _h2_cell(c, latex: bool) -> str:
+    if not np.isfinite(c["rho"]):
+        return "n/a (constant)"  # e.g. the remote arm's client GPU %, 0 by construction
     coef = f"{c['rho']:.3f}"
     p = "<0.001" if c["p"] < 0.001 else f"{c['p']:.3f}"
     s = f"{coef} ({p}{c['stars']})"
@@ -317,12 +340,13 @@ def h2_markdown(rows) -> str:
 
 
 def energy_views_markdown(rows) -> str:
-    lines = ["| Length | View | On-device J (mean) | Remote J (mean) | On-device / remote | W | p | Cliff's delta |",
-             "|---|---|---|---|---|---|---|---|"]
+    lines = ["| Length | View | On-device J (mean / SD) | Remote J (mean / SD) | On-device / remote | W | p | "
+             "Cliff's delta |", "|---|---|---|---|---|---|---|---|"]
     for r in rows:
         ratio = f"{r['ratio']:.2f}x" if r["ratio"] == r["ratio"] else "n/a"
-        lines.append(f"| {_title(r['length'])} ({r['words']}) | {r['view']} | {r['mean_on_device']:.2f} | "
-                     f"{r['mean_remote']:.2f} | {ratio} | {r['W']:.0f} | {_p_fmt(r['p'])} | "
+        lines.append(f"| {_title(r['length'])} ({r['words']}) | {r['view']} | {r['mean_on_device']:.2f} / "
+                     f"{r.get('sd_on_device', float('nan')):.2f} | {r['mean_remote']:.2f} / "
+                     f"{r.get('sd_remote', float('nan')):.2f} | {ratio} | {r['W']:.0f} | {_p_fmt(r['p'])} | "
                      f"{r['cliffs_delta']:.3f} ({r['magnitude']}) |")
     return "\n".join(lines) + "\n"
 
@@ -460,11 +484,13 @@ def analyze(path, out: Optional[Path] = None, plots: bool = False, fmt: str = "b
     out = Path(out) if out else paths[0].parent / "analysis"
     out.mkdir(parents=True, exist_ok=True)
     df = load_run_table(paths, rederive=rederive)
+    idle_ref = add_idle_normalised(df)
     subsets = make_subsets(df)
     res = {"source": ", ".join(str(p) for p in paths), "n_rows": int(len(df)), "subset_sizes": {k: int(len(v)) for k, v in subsets.items()},
            "summary": summary_rows(subsets), "shapiro": shapiro_rows(subsets), "h1": h1_rows(subsets),
            "h2": h2_rows(subsets), "per_model": per_model_rows(df) if "model" in df.columns else [],
-           "energy_views": energy_view_rows(subsets), "rederived_remote_board": bool(rederive)}
+           "energy_views": energy_view_rows(subsets), "rederived_remote_board": bool(rederive),
+           "idle_ref_W": idle_ref}
     texts = {}
     if fmt in ("latex", "both"):
         texts.update({"summary.tex": summary_latex(res["summary"]), "h1.tex": h1_latex(res["h1"]),

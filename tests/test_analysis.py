@@ -167,13 +167,32 @@ def test_energy_views_and_remote_board_rederivation(tmp_path):
     fixed = analyze(p, tmp_path / "fixed", quiet=True, rederive=True)
     v_raw = {(r["length"], r["view"]): r for r in raw["energy_views"]}
     v_fix = {(r["length"], r["view"]): r for r in fixed["energy_views"]}
-    assert set(v_fix) == {(L, v) for L in ("short", "medium", "long") for v in ("gross", "idle_subtracted")}
+    assert set(v_fix) == {(L, v) for L in ("short", "medium", "long")
+                          for v in ("gross", "idle_normalised", "idle_subtracted")}
+    # one idle floor across the table: the idle-normalised view is the gross one
+    assert v_fix[("long", "idle_normalised")]["ratio"] == pytest.approx(v_fix[("long", "gross")]["ratio"])
     # as written: remote gross is the client's CPU only -> a 1000x ratio; rederived: board idle included -> 1000/261
     assert v_raw[("long", "gross")]["ratio"] == pytest.approx(1000.0, rel=1e-3)
     assert v_fix[("long", "gross")]["ratio"] == pytest.approx(1000.0 / 261.0, rel=1e-3)
     # the idle-subtracted view does not change: the board's part is idle - idle = 0
     assert v_fix[("long", "idle_subtracted")]["ratio"] == pytest.approx(v_raw[("long", "idle_subtracted")]["ratio"])
     assert (tmp_path / "fixed" / "energy_views.md").read_text().count("idle_subtracted") == 3
+
+
+def test_idle_normalised_view_removes_box_idle_spread():
+    """sessions on boxes with different idle floors; the idle-normalised energy charges every run
+    at the table's mean idle power, so two runs with the same request energy on a 240 W and a 300 W box agree."""
+    import pandas as pd
+
+    from cain_amd.analysis.report import IDLE_NORM, add_idle_normalised
+
+    df = pd.DataFrame(dict(energy_usage_J=[240 * 2 + 100, 300 * 2 + 100], idle_power_W=[240.0, 300.0],
+                           energy_window_s=[2.0, 2.0]))
+    ref = add_idle_normalised(df)
+    assert ref == pytest.approx(270.0)
+    assert df[IDLE_NORM].tolist() == pytest.approx([640.0, 640.0])
+    # a table without idle columns has no such view
+    assert add_idle_normalised(pd.DataFrame(dict(energy_usage_J=[1.0]))) is None
 
 
 def test_replicate_run_tables_pool(tmp_path):
