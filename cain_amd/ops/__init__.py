@@ -123,6 +123,10 @@ def load() -> ctypes.CDLL:
         lib.cain_attention_set_ring.argtypes = [ci]
         lib.cain_sample.argtypes = [vp, ci, ci, vp, vp, vp, ci, vp, vp, vp, vp, vp, ci, ci, vp, vp]
         lib.cain_sample_cm.argtypes = [vp, ci, ci, vp, vp, vp, vp, ci, vp, vp, vp, vp, vp, ci, ci, vp, vp]
+        lib.cain_sample_lean.argtypes = [vp, ci, ci, vp, vp, vp, vp, ci, vp, vp, vp, vp, vp, ci, ci, vp, vp]
+        lib.cain_gemm_set_cmax.argtypes = [vp]
+        lib.cain_gemm_set_cmax.restype = None
+        lib.cain_gemm_cmax_take.argtypes = []
         lib.cain_sample_set_cm.argtypes = [ci]
         lib.cain_gemm_set_skinny_split.argtypes = [ci]
         lib.cain_sample_ex.argtypes = [vp, ci, ci, vp, vp, vp, ci, vp, vp, vp, vp, vp, ci, ci, vp, vp,
@@ -317,7 +321,8 @@ def qkv_rope(wp, x, n, q_out, kc, vtc, slot, pos, cos_t, sin_t, H, Hkv, hd, bias
 
 
 def gemm_w8(wq: torch.Tensor, scale: torch.Tensor, x: torch.Tensor, n: int, epi: int = EPI_BF16, bias=None,
-            out: Optional[torch.Tensor] = None, norm: bool = False, eps: float = 1e-6, rope=None) -> torch.Tensor:
+            out: Optional[torch.Tensor] = None, norm: bool = False, eps: float = 1e-6, rope=None,
+            cmax: Optional[torch.Tensor] = None) -> torch.Tensor:
     """fp8-weight GEMM (``csrc/gemm_w8.hip``, M <= 64): y = epi(B(x) @ (q * scale)^T) with q packed by
     ``models.weights.pack_mfma_a_fp8`` and ``scale`` the per-row fp32 scales.  Same epilogues and RMSNorm
     fusion as ``skinny_gemm``; ``rope`` = dict(kc, vtc, slot, pos, cos_t, sin_t, H, Hkv, hd) for
@@ -339,16 +344,19 @@ def gemm_w8(wq: torch.Tensor, scale: torch.Tensor, x: torch.Tensor, n: int, epi:
     T_max = r["kc"].shape[-2] if rope else 0
     if rope and is_fp8_cache(r["kc"]):
         epi |= EPI_KV_FP8
+    _cmax_set(lib, cmax, epi)
     rc = lib.cain_gemm_w8(_p(wq), _p(scale), _p(x), x.stride(0), K, n, M, _p(out), out.stride(0), _p(bias),
                           int(bool(norm)), eps, _p(r.get("slot")), _p(r.get("pos")), _p(r.get("cos_t")),
                           _p(r.get("sin_t")), _p(r.get("kc")), _p(r.get("vtc")), r.get("H", 0), r.get("Hkv", 0),
                           r.get("hd", 0), T_max, epi, _stream())
     _check(rc, "gemm_w8")
+    _cmax_check(lib, cmax)
     return out
 
 
 def gemm_w4(wq: torch.Tensor, wsc: torch.Tensor, x: torch.Tensor, n: int, epi: int = EPI_BF16, bias=None,
-            out: Optional[torch.Tensor] = None, norm: bool = False, eps: float = 1e-6, rope=None) -> torch.Tensor:
+            out: Optional[torch.Tensor] = None, norm: bool = False, eps: float = 1e-6, rope=None,
+            cmax: Optional[torch.Tensor] = None) -> torch.Tensor:
     """MXFP4-weight GEMM (``csrc/gemm_w4.hip``, M <= 64): y = epi(B(x) @ dequant(codes, scales)^T) with
     (``wq``, ``wsc``) = ``models.weights.pack_mxfp4(...)``.  Same epilogues, RMSNorm fusion and ``rope`` arguments
     as ``gemm_w8``."""
@@ -371,20 +379,35 @@ def gemm_w4(wq: torch.Tensor, wsc: torch.Tensor, x: torch.Tensor, n: int, epi: i
         epi |= EPI_KV_FP8
     nb = int(lib.cain_gemm_w4_ws_bytes(n, K, M))
     ws = _w4_ws(x.device, nb)
+    _cmax_set(lib, cmax, epi)
     rc = lib.cain_gemm_w4_ex(_p(wq), _p(wsc), _p(x), x.stride(0), K, n, M, _p(out), out.stride(0), _p(bias),
                              int(bool(norm)), eps, _p(r.get("slot")), _p(r.get("pos")), _p(r.get("cos_t")),
                              _p(r.get("sin_t")), _p(r.get("kc")), _p(r.get("vtc")), r.get("H", 0), r.get("Hkv", 0),
                              r.get("hd", 0), T_max, _p(ws), nb, epi, _stream())
     _check(rc, "gemm_w4")
+    _cmax_check(lib, cmax)
     return out
 
 
 _W4_WS: dict = {}
 
 
+def _cmax_set(lib, cmax, epi: int) -> None:
+    """``cmax`` ([M][N / 16] fp32): the few-row fp32-logits GEMM also writes each row's 16-column chunk maxima (the
+    chunk-maximum samplers' input, gemm_epi.h epi_cmax)."""
+    if cmax is not None:
+        assert epi == EPI_F32 and cmax.dtype == torch.float32 and cmax.is_contiguous()
+        lib.cain_gemm_set_cmax(_p(cmax))
+
+
+def _cmax_check(lib, cmax) -> None:
+    if cmax is not None and int(lib.cain_gemm_cmax_take()) != 1:
+        raise RuntimeError("this GEMM shape does not write chunk maxima (few-row stream kernels only)")
+
+
 def gemm_q4(fmt: int, wq: torch.Tensor, sbuf: torch.Tensor, x: torch.Tensor, n: int, epi: int = EPI_BF16,
             bias=None, out: Optional[torch.Tensor] = None, norm: bool = False, eps: float = 1e-6, rope=None,
-            gain: bool = False) -> torch.Tensor:
+            gain: bool = False, cmax: Optional[torch.Tensor] = None) -> torch.Tensor:
     """GGUF Q4_0 (``fmt`` 0) / Q4_K (1) weight GEMM (``csrc/gemm_q4.hip``; any M, 16-row launches): y = epi(B(x) @
     W^T) with W the blocks' exact values and (``wq``, ``sbuf``) = ``models.q4.pack_q4(...)``; ``gain``: the scale
     buffer ends with the fp32 RMSNorm gain, applied to the activations (``norm`` must be set).  Same epilogues,
@@ -408,12 +431,14 @@ def gemm_q4(fmt: int, wq: torch.Tensor, sbuf: torch.Tensor, x: torch.Tensor, n: 
     if rope and is_fp8_cache(r["kc"]):
         epi |= EPI_KV_FP8
     base = sbuf.data_ptr()
+    _cmax_set(lib, cmax, epi)
     rc = lib.cain_gemm_q4(int(fmt), _p(wq), base, base + sc_bytes, (base + sc_bytes + dd_bytes) if gain else None,
                           _p(x), x.stride(0), K, n, M, _p(out), out.stride(0), _p(bias), int(bool(norm)), eps,
                           _p(r.get("slot")), _p(r.get("pos")), _p(r.get("cos_t")), _p(r.get("sin_t")),
                           _p(r.get("kc")), _p(r.get("vtc")), r.get("H", 0), r.get("Hkv", 0), r.get("hd", 0), T_max,
                           epi, _stream())
     _check(rc, "gemm_q4")
+    _cmax_check(lib, cmax)
     return out
 
 
@@ -651,7 +676,8 @@ def attention(q, kc, vtc, slot, pos, H, Hkv, hd, nsplit, scale, out=None, part_o
 def set_sample_cm(mode: int) -> None:
     """Chunk-maximum sampler (the LM head writes 16-column chunk maxima, the sampler reads only the chunks above a
     provable threshold; same tokens).  mode 0 off, 1 every decode forward, 2 forwards of more than 64 rows (the
-    default: 42 vs 62 us at 256 rows; at batch 1 the two-stage kernel is faster).  A/B switch for tests and
+    default: 42 vs 62 us at 256 rows; at batch 1 the two-stage kernel is faster), 3 the lean chunk-maximum kernel
+    (sample.hip sample_lean_kernel) on every forward whose LM head wrote the maxima.  A/B switch for tests and
     profiles, read at every forward / graph capture."""
     load().cain_sample_set_cm(int(mode))
 
@@ -719,13 +745,19 @@ def sample_params_tensor(rows, device) -> torch.Tensor:
 
 
 def sample(logits, tok, pos, gen, n_gen, max_new, done, hist, slot, params, T_max, split: bool = False,
-           cmax=None) -> None:
+           cmax=None, lean: bool = False) -> None:
     """On-device sampling + decode-state update (csrc/sample.hip).  ``split``: the two-stage kernel (vocabulary
     slices on 16 workgroups per row, last-arriver merge) that decode forwards of <= 64 rows use; ``cmax`` ([M][V/16]
     fp32 maxima of the logits' 16-column chunks, as the few-row LM head writes them): the chunk-maximum kernel that
-    single-stream decode uses; otherwise the one-workgroup-per-row kernel."""
+    single-stream decode uses (``lean``: the lean chunk-maximum kernel); otherwise the one-workgroup-per-row
+    kernel."""
     lib = load()
     M, V = logits.shape[0], logits.shape[1]
+    if cmax is not None and lean:
+        _check(lib.cain_sample_lean(_p(logits), logits.stride(0), V, _p(cmax), _p(tok), _p(pos), _p(gen),
+                                    gen.stride(0), _p(n_gen), _p(max_new), _p(done), _p(hist), _p(slot), T_max, M,
+                                    _p(params), _stream()), "sample_lean")
+        return
     if cmax is not None:
         _check(lib.cain_sample_cm(_p(logits), logits.stride(0), V, _p(cmax), _p(tok), _p(pos), _p(gen), gen.stride(0),
                                   _p(n_gen), _p(max_new), _p(done), _p(hist), _p(slot), T_max, M, _p(params),

@@ -1036,6 +1036,14 @@ CAIN_API int cain_gemm_cmax_take() {
   g_next_cmax = nullptr, g_cmax_used = 0;
   return u;
 }
+// The weight-format kernels' side (gemm_w8 / gemm_w4 / gemm_q4 at few rows): the pending buffer for an fp32-logits
+// GEMM of N columns, now marked written (null: none pending or N not whole chunks).
+CAIN_API float* cain_gemm_cmax_claim(int N) {
+  if (!g_next_cmax || N % 16) return nullptr;
+  float* p = g_next_cmax;
+  g_next_cmax = nullptr, g_cmax_used = 1;
+  return p;
+}
 
 // Entry used by the runtime and the bindings.  norm != 0 selects the fused RMSNorm (gain pre-folded into Wp).
 CAIN_API int cain_skinny_gemm_ex(const void* Wp, const void* X, int ldx, int K, int N, int M, void* Y, int ldy,

@@ -200,3 +200,13 @@ __device__ __forceinline__ void epi_store(const GemmArgs& a, int gt, int m, int 
   }
 }
 
+// The LM head's per-row maximum of the 16-column chunk gt (the chunk-maximum samplers' first stage, sample.hip):
+// lanes c, c + 16, c + 32, c + 48 hold row c's 16 values v.  Called by whole waves (two xor shuffles); no-op without
+// a cmax buffer (uniform).
+__device__ __forceinline__ void epi_cmax(const GemmArgs& a, int gt, int m, int lane, const f32x4& v) {
+  if (!a.cmax) return;
+  float mx = fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3]));
+  mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+  mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+  if ((lane >> 4) == 0 && m < a.M) a.cmax[(size_t)m * a.ld_cm + gt] = mx;
+}

@@ -262,7 +262,13 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(4, 4
         if constexpr (NORM) v *= rms_inv(row_ss[min(m, a.M - 1)], a.K, a.eps);
         return v;
       };
-      epi_store<EPI>(a, tile, lane & 15, lane, pre, [&](int off) { return unit_sum(lane + off); });
+      if constexpr (EPI == EPI_F32) {  // the LM head: logits + chunk maxima
+        const f32x4 v = unit_sum(lane);
+        epi_store<EPI>(a, tile, lane & 15, lane, pre, [&](int) { return v; });
+        epi_cmax(a, tile, lane & 15, lane, v);
+      } else {
+        epi_store<EPI>(a, tile, lane & 15, lane, pre, [&](int off) { return unit_sum(lane + off); });
+      }
     }
     buf ^= 1;
   };
@@ -322,6 +328,8 @@ static int q4_rows(int K, int epi) {  // rows per launch at this K and epilogue 
 }
 CAIN_API int cain_gemm_q4_rows(int K, int epi) { return q4_rows(K, epi & EPI_MASK); }
 
+CAIN_API float* cain_gemm_cmax_claim(int N);  // gemm.hip
+
 // Same GEMM arguments as cain_gemm_w4 (gemm_w4.hip) plus the format (0 Q4_0, 1 Q4_K), its scale arrays and the
 // RMSNorm gain to apply to the activations (null: none).  M > 16 (a prefill chunk) runs as 16-row launches.
 CAIN_API int cain_gemm_q4(int fmt, const void* Wq, const void* sc, const void* dd, const float* gain, const void* X,
@@ -334,6 +342,7 @@ CAIN_API int cain_gemm_q4(int fmt, const void* Wq, const void* sc, const void* d
   const int rows = q4_rows(K, epi);
   if (rows == 0) return -1;
   const int n_cu = cain_cu_budget();
+  float* cm = epi == EPI_F32 ? cain_gemm_cmax_claim(N) : nullptr;  // the LM head: the sampler's chunk maxima too
   for (int m0 = 0; m0 < M; m0 += rows) {
     const int mc = std::min(rows, M - m0);
     const int waves = q4_waves(K, mc, epi);  // > 0: mc <= rows
@@ -348,6 +357,7 @@ CAIN_API int cain_gemm_q4(int fmt, const void* Wq, const void* sc, const void* d
     a.kc = reinterpret_cast<__bf16*>(kc), a.vtc = reinterpret_cast<__bf16*>(vtc);
     a.H = H, a.Hkv = Hkv, a.hd = hd, a.T_max = T_max, a.kv8 = (epi_flags & EPI_KV_FP8) ? 1 : 0;
     a.msplit = 1;
+    if (cm) a.cmax = cm + (size_t)m0 * (N / 16), a.ld_cm = N / 16;
     const Q4Args q{static_cast<const uint8_t*>(sc), static_cast<const uint32_t*>(dd), gain};
     const int npairs = N / 16;
     const int grid = std::min(npairs, n_cu * (waves == 8 ? 2 : 4));

@@ -233,6 +233,7 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(4, 4
           if (lane == 0) sp.ctr[tile] = 0u;  // ready for the next launch (launch-ordered)
           red[buf][0][lane] = sum;  // one wave: its LDS operations complete in order
           epi_store<EPI>(a, tile, lane & 15, lane, pre, [&](int off) { return red[buf][0][lane + off]; });
+          if constexpr (EPI == EPI_F32) epi_cmax(a, tile, lane & 15, lane, sum);
         }
         buf ^= 1;
         return;
@@ -244,7 +245,13 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(4, 4
         if constexpr (NORM) v *= rms_inv(row_ss[min(l & 15, a.M - 1)], a.K, a.eps);
         return v;
       };
-      epi_store<EPI>(a, tile, lane & 15, lane, pre, [&](int off) { return unit_sum(lane + off); });
+      if constexpr (EPI == EPI_F32) {  // the LM head: logits + chunk maxima
+        const f32x4 v = unit_sum(lane);
+        epi_store<EPI>(a, tile, lane & 15, lane, pre, [&](int) { return v; });
+        epi_cmax(a, tile, lane & 15, lane, v);
+      } else {
+        epi_store<EPI>(a, tile, lane & 15, lane, pre, [&](int off) { return unit_sum(lane + off); });
+      }
     }
     buf ^= 1;
   };
@@ -521,6 +528,7 @@ CAIN_API int cain_gemm_w4_ex(const void* Wp, const void* wsc, const void* X, int
                              int ldy, const float* bias, int norm, float eps, const int* slot, const int* pos,
                              const float* cos_t, const float* sin_t, void* kc, void* vtc, int H, int Hkv, int hd,
                              int T_max, void* ws, long long ws_bytes, int epi_flags, hipStream_t st);
+CAIN_API float* cain_gemm_cmax_claim(int N);  // gemm.hip
 
 // Same arguments as cain_gemm_w8 (gemm_w8.hip); Wp is the MXFP4 packing, wsc its e8m0 scale bytes.  No workspace:
 // never split (cain_gemm_w4_ex is the engine's entry).
@@ -551,6 +559,8 @@ CAIN_API int cain_gemm_w4_ex(const void* Wp, const void* wsc, const void* X, int
   const int n_cu = w4_n_cu();
   const int var = w4_variant(N, K, M, epi, n_cu);
   const int nb = W4_NB[var], waves = W4_WAVES[var];
+  if (epi == EPI_F32 && w4_is_stream(var))  // the few-row LM head also writes the sampler's chunk maxima
+    if (float* cm = cain_gemm_cmax_claim(N)) a.cmax = cm, a.ld_cm = N / 16;
   a.msplit = (M + 16 * nb - 1) / (16 * nb);
   const int npairs = N / 16 * a.msplit;
   int grid = npairs;

@@ -222,8 +222,14 @@ __global__ __launch_bounds__(WAVES * 64) void skinny_w8_kernel(const GemmArgs a,
       }
       return v;
     };
-    epi_store<EPI>(a, t0 + t, mo + 16 * b + (lane & 15), lane, pre[t][b],
-                   [&](int off) { return unit_sum(lane + off); });
+    if constexpr (EPI == EPI_F32) {  // the LM head: logits + chunk maxima
+      const f32x4 v = unit_sum(lane);
+      epi_store<EPI>(a, t0 + t, mo + 16 * b + (lane & 15), lane, pre[t][b], [&](int) { return v; });
+      epi_cmax(a, t0 + t, mo + 16 * b + (lane & 15), lane, v);
+    } else {
+      epi_store<EPI>(a, t0 + t, mo + 16 * b + (lane & 15), lane, pre[t][b],
+                     [&](int off) { return unit_sum(lane + off); });
+    }
   }
 }
 
@@ -273,6 +279,8 @@ static hipError_t w8_launch_e(int epi, int var, const GemmArgs& a, const float* 
 #undef CAIN_W8_VAR
 }
 
+CAIN_API float* cain_gemm_cmax_claim(int N);  // gemm.hip
+
 // Same arguments as cain_gemm (gemm.hip) plus the per-row weight scales; Wp is the fp8 packing.
 CAIN_API int cain_gemm_w8(const void* Wp, const float* wscale, const void* X, int ldx, int K, int N, int M, void* Y,
                           int ldy, const float* bias, int norm, float eps, const int* slot, const int* pos,
@@ -289,6 +297,8 @@ CAIN_API int cain_gemm_w8(const void* Wp, const float* wscale, const void* X, in
   a.slot = slot, a.pos = pos, a.cos_t = cos_t, a.sin_t = sin_t;
   a.kc = reinterpret_cast<__bf16*>(kc), a.vtc = reinterpret_cast<__bf16*>(vtc);
   a.H = H, a.Hkv = Hkv, a.hd = hd, a.T_max = T_max, a.kv8 = (epi_flags & EPI_KV_FP8) ? 1 : 0;
+  if (epi == EPI_F32)  // the few-row LM head also writes the sampler's chunk maxima
+    if (float* cm = cain_gemm_cmax_claim(N)) a.cmax = cm, a.ld_cm = N / 16;
   // (round 2-3's A/B overrides of waves / pairs in flight / tiles / row blocks are fixed at the measured rule)
   constexpr int f_w = 0, f_u = 0, f_nt = 0, f_nb = 0;
   const int nb = f_nb ? (f_nb >= 2 ? 2 : 1) : (M > 16 ? 2 : 1);

@@ -68,6 +68,9 @@ CAIN_API int cain_sample_cm_enabled();
 CAIN_API int cain_sample_cm(float* logits, int ldl, int V, const float* cmax, int* tok, int* pos, int* gen, int ldg,
                             int* n_gen, const int* max_new, int* done, int* hist, const int* slot, int T_max, int M,
                             const void* params, hipStream_t st);
+CAIN_API int cain_sample_lean(float* logits, int ldl, int V, const float* cmax, int* tok, int* pos, int* gen, int ldg,
+                              int* n_gen, const int* max_new, int* done, int* hist, const int* slot, int T_max, int M,
+                              const void* params, hipStream_t st);
 CAIN_API void cain_gemm_set_cmax(float* cmax);
 CAIN_API int cain_gemm_cmax_take();
 CAIN_API int cain_sample_ex(float* logits, int ldl, int V, int* tok, int* pos, int* gen, int ldg, int* n_gen,
@@ -254,9 +257,10 @@ int forward(const Plan& p, int M, const CainRows& r, int want_logits, int want_s
             /*EPI_RESID*/ 1));
   }
   if (want_logits) {
-    // the LM head also writes the chunk maxima the chunk-max sampler starts from (skinny or wide bf16 kernel)
+    // the LM head also writes the chunk maxima the chunk-max samplers start from (the bf16 skinny / wide kernels and
+    // the few-row fp8 / MXFP4 / Q4 kernels; a kernel that does not leaves cain_gemm_cmax_take() at 0)
     const int cm_mode = cain_sample_cm_enabled();
-    if (p.cmax && (cm_mode == 1 || (cm_mode == 2 && M > 64))) cain_gemm_set_cmax(p.cmax);
+    if (p.cmax && (cm_mode == 1 || cm_mode == 3 || (cm_mode == 2 && M > 64))) cain_gemm_set_cmax(p.cmax);
     CK(gemm(d.lm_head, d.lm_head8, d.lm_head_scale, d.x, d.d, d.d, d.V, d.logits, d.V, nullptr, 1, nullptr, nullptr,
             /*EPI_F32*/ 2));
   }
@@ -264,9 +268,12 @@ int forward(const Plan& p, int M, const CainRows& r, int want_logits, int want_s
   if (want_sample) {
     // the chunk-max sampler refuses (< 0) vocabularies beyond its chunk capacity: the two-stage / one-workgroup
     // kernels take those
-    const int e = cm ? cain_sample_cm(d.logits, d.V, d.V, p.cmax, r.tok, r.pos, r.gen, r.ldg, r.n_gen, r.max_new,
-                                      r.done, r.hist, r.slot, d.T_max, M, r.sample_params, st)
-                     : -1;
+    const int cm_mode = cain_sample_cm_enabled();
+    const int e = !cm ? -1
+                  : cm_mode == 3 ? cain_sample_lean(d.logits, d.V, d.V, p.cmax, r.tok, r.pos, r.gen, r.ldg, r.n_gen,
+                                                    r.max_new, r.done, r.hist, r.slot, d.T_max, M, r.sample_params, st)
+                                 : cain_sample_cm(d.logits, d.V, d.V, p.cmax, r.tok, r.pos, r.gen, r.ldg, r.n_gen,
+                                                  r.max_new, r.done, r.hist, r.slot, d.T_max, M, r.sample_params, st);
     if (e > 0) CK(e);
     if (e < 0)
       CK(cain_sample_ex(d.logits, d.V, d.V, r.tok, r.pos, r.gen, r.ldg, r.n_gen, r.max_new, r.done, r.hist, r.slot,
@@ -294,8 +301,8 @@ CAIN_API void* cain_plan_create(const CainPlanDesc* desc) {
       p->sample_ws = nullptr;  // the one-workgroup sampler needs no workspace
     }
   }
-  // LM-head chunk maxima ([Mpad][V / 16]): bf16 weights only (the kernels that write them)
-  if (desc->wfmt == WFMT_BF16 && desc->V % 64 == 0 && desc->Mpad > 0) {
+  // LM-head chunk maxima ([Mpad][V / 16])
+  if (desc->V % 64 == 0 && desc->Mpad > 0) {
     if (hipMalloc(&p->cmax, (size_t)desc->Mpad * (desc->V / 16) * sizeof(float)) != hipSuccess) p->cmax = nullptr;
   }
   return p;

@@ -924,3 +924,318 @@ CAIN_API int cain_sample_cm(float* logits, int ldl, int V, const float* cmax, in
 }
 
 CAIN_API int cain_sample_params_size() { return int(sizeof(SampleParams)); }
+
+// =====================================================================================================
+// Lean chunk-maximum sampler (the few-row sampler at <= 12 us).  Same inputs as sample_cm_kernel
+// -- the logits and the LM head's chunk maxima (gemm_epi.h epi_cmax, written by every few-row LM-head kernel: bf16,
+// fp8, MXFP4 and GGUF Q4) -- and the same candidates in the same order, so the same token for the same seed.  The
+// round-3 trace of the two-stage kernel (profiles/r3/sampler_trace_final.log) put its 29 us in a chain of
+// workgroup-wide phases, the slowest the exact K-th largest of 256 thread maxima (7 us: a 21-stage bitonic sort of
+// shuffles, then 96 LDS reads per thread).  Here every phase is at most a few LDS reads per thread:
+//   1. chunk maxima -> registers (16-byte loads, issued first) and LDS; the repeat penalty: each chunk holding
+//      recent ids has ONE owner (the first history slot in it), which applies the penalty to every distinct recent
+//      id of its chunk (a 16-bit mask from one scan of the history), writes the chunk back and corrects the chunk's
+//      maximum in LDS -- so the maxima are exact after the penalty and the threshold needs K, not K + R;
+//   2. tau_c = a LOWER BOUND of the K-th largest chunk maximum: G >= 2K groups (64 / 128 / 256) take the maximum of
+//      256 / G thread maxima, and the K-th largest group maximum has K distinct chunks >= it (ln_kth_bound: one
+//      16-byte-read rank pass over G values, no sort);
+//   3. chunks >= tau_c (typically 1-2 K) gathered by one LDS atomic per thread that has any (most have none), their
+//      16 logits staged in LDS with one 16-byte load per thread;
+//   4. the same bound over the staged logits, the elements above it gathered, ranked (value desc, index asc) and
+//      drawn (draw_topk_wave), the decode state advanced.
+// A threshold that lets more than LN_CAP chunks or MAXC elements through is tightened to the exact K-th (value,
+// index) pair of those gathered (ln_tighten) and the gather repeated: exact in every case, ties included.
+// =====================================================================================================
+constexpr int LN_NJ = 64;                      // chunk maxima per thread
+constexpr int LN_C_MAX = LN_NJ * SS_THREADS;   // chunks per row: V <= 262,144
+constexpr int LN_CAP = 256;                    // chunks staged per row (16 logits each)
+static_assert(LN_CAP == SS_THREADS, "one staged chunk id per thread");
+
+// Lower bound of the K-th largest (1 <= K <= 256) of the row elements behind the 256 per-thread values tv (each an
+// element of the row, or -inf): the K-th largest of G group maxima (group g: threads g, g + G, ...) in (value desc,
+// group asc) order.  Every thread calls it; ends with a barrier.
+__device__ float ln_kth_bound(float tv, int K, float* s_a, float* s_b, float* s_tau) {
+  const int tid = threadIdx.x;
+  const int G = K <= 32 ? 64 : (K <= 64 ? 128 : 256);
+  s_a[tid] = tv;
+  __syncthreads();
+  if (tid < G) {
+    float g = tv;
+    for (int q = tid + G; q < SS_THREADS; q += G) g = fmaxf(g, s_a[q]);
+    s_b[tid] = g;
+  }
+  __syncthreads();
+  if (tid < G) {
+    const float g = s_b[tid];
+    const f32x4* b4 = reinterpret_cast<const f32x4*>(s_b);
+    int r = 0;
+#pragma unroll 8
+    for (int b = 0; b < G / 4; ++b) {
+      const f32x4 v = b4[b];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) r += (v[j] > g) || (v[j] == g && 4 * b + j < tid);
+    }
+    if (r == K - 1) *s_tau = g;  // ranks are a permutation of [0, G): exactly one writer
+  }
+  __syncthreads();
+  return *s_tau;
+}
+
+// Append this thread's kept items (bit k of keep) as (val(k), id(k)): one LDS atomic per thread that has any, then
+// a loop over its set bits.  The list is in arrival order (rank_candidates orders it); entries past MAXC are dropped,
+// *s_nc counts them all.  The caller zeroes *s_nc before a barrier; ends with a barrier.
+template <class Val, class Id>
+__device__ void ln_gather(uint64_t keep, Val val, Id id, float* cval, int* cidx, int* s_nc) {
+  const int cnt = __popcll(keep);
+  int base = cnt ? atomicAdd(s_nc, cnt) : 0;
+  while (keep) {
+    const int k = __builtin_ctzll(keep);
+    keep &= keep - 1;
+    if (base < MAXC) {
+      cval[base] = val(k);
+      cidx[base] = id(k);
+    }
+    ++base;
+  }
+  __syncthreads();
+}
+
+// The exact K-th (value desc, id asc) of the n <= MAXC stored entries -> (*s_tv, *s_ti): a threshold pair every
+// top-K item passes (the stored entries are a subset of the items above the previous threshold).  Ends with a barrier.
+__device__ void ln_tighten(const float* cval, const int* cidx, int n, int K, float* s_tv, int* s_ti) {
+  for (int a = threadIdx.x; a < n; a += SS_THREADS) {
+    const float va = cval[a];
+    const int ia = cidx[a];
+    int r = 0;
+    for (int b = 0; b < n; ++b) r += (cval[b] > va) || (cval[b] == va && cidx[b] < ia);
+    if (r == K - 1) *s_tv = va, *s_ti = ia;
+  }
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(SS_THREADS) void sample_lean_kernel(
+    float* __restrict__ logits, int ldl, int V, const float* __restrict__ cmax, int* __restrict__ tok,
+    int* __restrict__ pos, int* __restrict__ gen, int ldg, int* __restrict__ n_gen, const int* __restrict__ max_new,
+    int* __restrict__ done, int* __restrict__ hist, const int* __restrict__ slot, int T_max,
+    const SampleParams* __restrict__ params, unsigned long long* __restrict__ trace) {
+  const int m = blockIdx.x;
+  if (slot[m] < 0 || done[m]) return;
+  const int tid = threadIdx.x, lane = tid & 63;
+  auto stamp = [&](int i) {
+    if (trace && tid == 0) trace[(size_t)m * 8 + i] = __builtin_amdgcn_s_memrealtime();
+  };
+  stamp(0);
+  const SampleParams P = params[m];
+  float* lg = logits + (size_t)m * ldl;
+  const int C = V >> 4, C4 = C >> 2;
+  extern __shared__ __attribute__((aligned(16))) float ln_smem[];
+  float* s_cm = ln_smem;                           // [C] chunk maxima (exact after the penalty)
+  f32x4* s_lv4 = reinterpret_cast<f32x4*>(ln_smem + ((C + 3) & ~3));  // [LN_CAP * 4] staged logits, 4 per entry
+  __shared__ int s_hist[HIST];
+  __shared__ float s_a[SS_THREADS], s_b[SS_THREADS];
+  __shared__ float sv[SS_KMAX];
+  __shared__ int si[SS_KMAX];
+  __shared__ __attribute__((aligned(16))) float cval[MAXC + 4];
+  __shared__ __attribute__((aligned(16))) int cidx[MAXC + 4];
+  __shared__ int s_ch[LN_CAP];
+  __shared__ float s_tau, s_tv;
+  __shared__ int s_ti, s_nc, s_choice;
+
+  // ---- 1. chunk maxima (thread t: chunks 4 (t + 256 j) .. + 3; unconditional clamped loads, masked) and, in flight
+  // with them, the history ids and each history id's chunk
+  const f32x4* cm4 = reinterpret_cast<const f32x4*>(cmax + (size_t)m * C);
+  f32x4 cq[LN_NJ / 4];
+#pragma unroll
+  for (int j = 0; j < LN_NJ / 4; ++j) cq[j] = cm4[min(tid + j * SS_THREADS, C4 - 1)];
+  const int ng = n_gen[m];
+  const int nrep = (P.repeat_penalty != 1.0f && P.repeat_last_n > 0) ? min(min(P.repeat_last_n, HIST), ng) : 0;
+  int hid = -1;
+  if (tid < nrep) hid = hist[(size_t)m * HIST + ((ng - 1 - tid) & (HIST - 1))];
+  if (hid >= V) hid = -1;
+  f32x4 hc[4];
+  if (nrep > 0) {
+    const f32x4* src = reinterpret_cast<const f32x4*>(lg + (size_t)(hid >= 0 ? hid >> 4 : 0) * 16);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) hc[q] = src[q];
+  }
+  if (tid < HIST) s_hist[tid] = hid;
+  float cv[LN_NJ];
+#pragma unroll
+  for (int j = 0; j < LN_NJ / 4; ++j)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) cv[4 * j + i] = tid + j * SS_THREADS < C4 ? cq[j][i] : -INFINITY;
+  if (nrep > 0) {  // (uniform) the chunk maxima go through LDS, where the penalised chunks are corrected
+    f32x4* s_cm4 = reinterpret_cast<f32x4*>(s_cm);
+#pragma unroll
+    for (int j = 0; j < LN_NJ / 4; ++j)
+      if (tid + j * SS_THREADS < C4) s_cm4[tid + j * SS_THREADS] = cq[j];
+    __syncthreads();
+    if (hid >= 0) {
+      // one scan of the history: owner = no earlier slot in the same chunk; mask = the distinct recent ids in it
+      const int ch = hid >> 4;
+      bool owner = true;
+      uint32_t mask = 0;
+      const i32x4* h4 = reinterpret_cast<const i32x4*>(s_hist);
+#pragma unroll
+      for (int b = 0; b < HIST / 4; ++b) {
+        const i32x4 h = h4[b];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const bool same = h[j] >= 0 && (h[j] >> 4) == ch;
+          owner &= !(same && 4 * b + j < tid);
+          mask |= same ? 1u << (h[j] & 15) : 0u;
+        }
+      }
+      if (owner) {
+        float mx = -INFINITY;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const float v = hc[q][i];
+            const float pv = v > 0.f ? v / P.repeat_penalty : v * P.repeat_penalty;
+            hc[q][i] = (mask >> (4 * q + i)) & 1u ? pv : v;
+            mx = fmaxf(mx, hc[q][i]);
+          }
+          reinterpret_cast<f32x4*>(lg + (size_t)ch * 16)[q] = hc[q];
+        }
+        s_cm[ch] = mx;
+      }
+    }
+    __syncthreads();
+    const f32x4* s_cm4r = reinterpret_cast<const f32x4*>(s_cm);
+#pragma unroll
+    for (int j = 0; j < LN_NJ / 4; ++j) {
+      const f32x4 v = s_cm4r[min(tid + j * SS_THREADS, C4 - 1)];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) cv[4 * j + i] = tid + j * SS_THREADS < C4 ? v[i] : -INFINITY;
+    }
+  } else {
+    f32x4* s_cm4 = reinterpret_cast<f32x4*>(s_cm);
+#pragma unroll
+    for (int j = 0; j < LN_NJ / 4; ++j)
+      if (tid + j * SS_THREADS < C4) s_cm4[tid + j * SS_THREADS] = cq[j];
+  }
+  stamp(1);
+
+  int K = P.top_k;
+  if (K <= 0 || K > SS_KMAX) K = SS_KMAX;
+  if (K > V) K = V;
+  if (P.temperature <= 0.f) K = 1;
+
+  // ---- 2. tau_c, then the chunks above it
+  float bv = -INFINITY;
+#pragma unroll
+  for (int k = 0; k < LN_NJ; ++k) bv = fmaxf(bv, cv[k]);
+  auto cid = [&](int k) { return 4 * (tid + (k >> 2) * SS_THREADS) + (k & 3); };
+  float tv = ln_kth_bound(bv, K, s_a, s_b, &s_tau);
+  int ti = 0x7fffffff;
+  stamp(2);
+  int n_ch = 0;
+#pragma unroll 1
+  for (int attempt = 0; attempt < 4; ++attempt) {
+    if (tid == 0) s_nc = 0;
+    __syncthreads();
+    uint64_t keep = 0;
+#pragma unroll
+    for (int k = 0; k < LN_NJ; ++k) {
+      const bool in = cv[k] > tv || (cv[k] == tv && cid(k) <= ti);
+      keep |= (uint64_t)(in && cv[k] > -INFINITY) << k;
+    }
+    ln_gather(keep, [&](int k) { return s_cm[cid(k)]; }, cid, cval, cidx, &s_nc);
+    n_ch = s_nc;
+    if (n_ch <= LN_CAP) break;
+    ln_tighten(cval, cidx, min(n_ch, MAXC), K, &s_tv, &s_ti);
+    tv = s_tv, ti = s_ti;
+  }
+  n_ch = min(n_ch, LN_CAP);
+  s_ch[tid] = tid < n_ch ? cidx[tid] : 0;  // (SS_THREADS == LN_CAP) entries past n_ch: chunk 0, loaded and masked
+  __syncthreads();
+  stamp(3);
+
+  // ---- 3. the gathered chunks' logits: quad q = tid + 256 u of chunk entry q >> 2 (one 16-byte load each)
+  const int nq = n_ch * 4;
+  float ev[16];
+  int eid[16];
+  f32x4 lq[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int q = min(tid + u * SS_THREADS, max(nq - 1, 0));
+    lq[u] = reinterpret_cast<const f32x4*>(lg + (size_t)s_ch[q >> 2] * 16)[q & 3];
+  }
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int q = tid + u * SS_THREADS;
+    const bool in = q < nq;
+    if (in) s_lv4[q] = lq[u];
+    const int base = in ? s_ch[q >> 2] * 16 + (q & 3) * 4 : 0x7ffff000;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      ev[4 * u + i] = in ? lq[u][i] : -INFINITY;
+      eid[4 * u + i] = base + i;
+    }
+  }
+  stamp(4);
+
+  // ---- 4. the bound over the staged logits, the elements above it, ranked and drawn
+  float bv2 = -INFINITY;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) bv2 = fmaxf(bv2, ev[k]);
+  tv = ln_kth_bound(bv2, K, s_a, s_b, &s_tau);
+  ti = 0x7fffffff;
+  const float* s_lv = reinterpret_cast<const float*>(s_lv4);
+  int nc = 0;
+#pragma unroll 1
+  for (int attempt = 0; attempt < 4; ++attempt) {
+    if (tid == 0) s_nc = 0;
+    __syncthreads();
+    uint64_t keep = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const bool in = ev[k] > tv || (ev[k] == tv && eid[k] <= ti);
+      keep |= (uint64_t)(in && ev[k] > -INFINITY) << k;
+    }
+    ln_gather(
+        keep, [&](int k) { return s_lv[(tid + (k >> 2) * SS_THREADS) * 4 + (k & 3)]; },
+        [&](int k) {
+          const int q = tid + (k >> 2) * SS_THREADS;
+          return s_ch[q >> 2] * 16 + (q & 3) * 4 + (k & 3);
+        },
+        cval, cidx, &s_nc);
+    nc = s_nc;
+    if (nc <= MAXC) break;
+    ln_tighten(cval, cidx, MAXC, K, &s_tv, &s_ti);
+    tv = s_tv, ti = s_ti;
+  }
+  nc = min(nc, MAXC);
+  stamp(5);
+  const int nk = rank_candidates(cval, cidx, nc, K, sv, si, SS_THREADS);
+  stamp(6);
+  if (tid < 64) {
+    const int pick = nk == 0 ? 0 : (P.temperature <= 0.f ? si[0] : draw_topk_wave(sv, si, nk, P, ng));
+    if (lane == 0) s_choice = pick;
+  }
+  __syncthreads();
+  if (tid == 0) advance_row(m, s_choice, ng, P, tok, pos, gen, ldg, n_gen, max_new, done, hist, T_max);
+  stamp(7);
+}
+
+static size_t ln_lds_bytes(int V) { return ((size_t)((V >> 4) + 3) / 4 * 4 + LN_CAP * 16) * sizeof(float); }
+
+// The lean chunk-maximum sampler (V % 64 == 0, V / 16 <= LN_C_MAX); cmax as the LM head wrote it.  < 0: refused.
+// The trace (cain_sample_set_trace) takes [M][8] timestamps: start, maxima exact, tau_c, chunks gathered, logits
+// staged, elements gathered, ranked, end.
+CAIN_API int cain_sample_lean(float* logits, int ldl, int V, const float* cmax, int* tok, int* pos, int* gen, int ldg,
+                              int* n_gen, const int* max_new, int* done, int* hist, const int* slot, int T_max, int M,
+                              const void* params, hipStream_t st) {
+  if (!cmax || V % 64 || V / 16 > LN_C_MAX) return -1;
+  const size_t lds = ln_lds_bytes(V);
+  static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&sample_lean_kernel),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize,
+                                               int(ln_lds_bytes(LN_C_MAX * 16))) == hipSuccess;
+  if (!attr) return -1;
+  hipLaunchKernelGGL(sample_lean_kernel, dim3(M), dim3(SS_THREADS), lds, st, logits, ldl, V, cmax, tok, pos, gen, ldg,
+                     n_gen, max_new, done, hist, slot, T_max, reinterpret_cast<const SampleParams*>(params),
+                     g_sample_trace);
+  return int(hipGetLastError());
+}

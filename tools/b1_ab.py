@@ -31,7 +31,13 @@ def main() -> int:
     ap.add_argument("--trials", type=int, default=3)
     ap.add_argument("--label", default=os.environ.get("CAIN_KERNELS_LIB", "default"))
     ap.add_argument("--out", default=None, help="append the JSON lines to this file too")
+    ap.add_argument("--sample-cm", type=int, default=None,
+                    help="sampler A/B: cain_amd.ops.set_sample_cm mode (3 = the lean chunk-maximum kernel)")
     a = ap.parse_args()
+    if a.sample_cm is not None:
+        from cain_amd import ops
+
+        ops.set_sample_cm(a.sample_cm)
     n_tok = tokens_for_words(a.words)
     opts = dict(eos_id=-1)
     for model in filter(None, a.models.split(",")):
@@ -48,7 +54,7 @@ def main() -> int:
                                  [dict(opts, seed=8 + t)])[0]
                 torch.cuda.synchronize()
                 rates.append(r.eval_count / (time.perf_counter() - t0))
-            rec = {"label": a.label, "model": model, "dtype": dtype, "tok_per_s": round(statistics.median(rates), 1),
+            rec = {"label": a.label, "sample_cm": a.sample_cm, "model": model, "dtype": dtype, "tok_per_s": round(statistics.median(rates), 1),
                    "trials": [round(x, 1) for x in rates], "tokens": n_tok}
             print(json.dumps(rec), flush=True)
             if a.out:
