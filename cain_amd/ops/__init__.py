@@ -150,6 +150,8 @@ def load() -> ctypes.CDLL:
         lib.cain_stream_destroy.argtypes = [vp]
         if os.environ.get("CAIN_WGEMM_INLINE") and hasattr(real, "cain_wgemm_set_inline"):  # A/B runs
             real.cain_wgemm_set_inline(int(os.environ["CAIN_WGEMM_INLINE"]))
+        if os.environ.get("CAIN_SAMPLE_CM"):  # A/B runs (set_sample_cm)
+            real.cain_sample_set_cm(int(os.environ["CAIN_SAMPLE_CM"]))
         _lib = real
         return real
 
@@ -675,10 +677,11 @@ def attention(q, kc, vtc, slot, pos, H, Hkv, hd, nsplit, scale, out=None, part_o
 
 def set_sample_cm(mode: int) -> None:
     """Chunk-maximum sampler (the LM head writes 16-column chunk maxima, the sampler reads only the chunks above a
-    provable threshold; same tokens).  mode 0 off, 1 every decode forward, 2 forwards of more than 64 rows (the
-    default: 42 vs 62 us at 256 rows; at batch 1 the two-stage kernel is faster), 3 the lean chunk-maximum kernel
-    (sample.hip sample_lean_kernel) on every forward whose LM head wrote the maxima.  A/B switch for tests and
-    profiles, read at every forward / graph capture."""
+    provable threshold; same tokens).  mode 0 off, 1 the round-3 chunk-maximum kernel on every decode forward, 2
+    that kernel on forwards of more than 64 rows (42 vs 62 us at 256 rows; the two-stage kernel below), 3 the lean
+    chunk-maximum kernel (sample.hip sample_lean_kernel) on every forward whose LM head wrote the maxima (the
+    default: 10.3 vs 30.0 us in-graph at batch 1, profiles/r6/sampler/).  A/B switch for tests and profiles, read at
+    every forward / graph capture (env CAIN_SAMPLE_CM at load)."""
     load().cain_sample_set_cm(int(mode))
 
 

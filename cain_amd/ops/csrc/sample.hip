@@ -54,15 +54,25 @@ constexpr int MAXC = 1024;  // candidate cap after top-k (ties included)
 // only, not by the batch row: a request that continuous batching moves to another row (ContinuousBatch.retire)
 // keeps its stream, so an Ollama `seed` reproduces the same tokens however the batch is packed (rows without a
 // seed get a unique one on the host, engine._row_options).
+// Inclusive wave64 prefix sum on DPP row operations (row_shr 1 / 2 / 4 / 8 inside each 16-lane row, then
+// row_bcast 15 / 31 carry the row totals): six VALU operations instead of six LDS round trips of __shfl_up.
+template <int CTRL, int ROWS>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, ROWS, 0xf, false));
+}
 __device__ __forceinline__ float wave_incl_scan(float v) {
-  const int lane = threadIdx.x & 63;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const float t = __shfl_up(v, o, 64);
-    if (lane >= o) v += t;
-  }
+  v += dpp_f<0x111, 0xf>(v);
+  v += dpp_f<0x112, 0xf>(v);
+  v += dpp_f<0x114, 0xf>(v);
+  v += dpp_f<0x118, 0xf>(v);
+  v += dpp_f<0x142, 0xa>(v);  // row_bcast:15 -> rows 1, 3
+  v += dpp_f<0x143, 0xc>(v);  // row_bcast:31 -> rows 2, 3
   return v;
 }
+__device__ __forceinline__ float lane63(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 63));
+}
+__device__ __forceinline__ float wave_total(float v) { return lane63(wave_incl_scan(v)); }
 
 __device__ int draw_topk_wave(const float* sv, const int* si, int n, const SampleParams& P, int ng) {
   const int lane = threadIdx.x & 63;
@@ -70,7 +80,7 @@ __device__ int draw_topk_wave(const float* sv, const int* si, int n, const Sampl
   const float mx = sv[0] * invT;
   float z = 0.f;
   for (int i = lane; i < n; i += 64) z += __expf(sv[i] * invT - mx);
-  z = wave_sum(z);
+  z = wave_total(z);
   // top-p: smallest prefix with cumulative probability >= top_p
   int cut = n;
   if (P.top_p > 0.f && P.top_p < 1.f) {
@@ -81,12 +91,12 @@ __device__ int draw_topk_wave(const float* sv, const int* si, int n, const Sampl
       const float c = carry + wave_incl_scan(pi);
       const unsigned long long hit = __ballot(i < n && c >= P.top_p);
       if (hit) { cut = c0 + __ffsll((long long)hit); break; }
-      carry = __shfl(c, 63, 64);
+      carry = lane63(c);
     }
   }
   float zc = 0.f;
   for (int i = lane; i < cut; i += 64) zc += __expf(sv[i] * invT - mx);
-  zc = wave_sum(zc);
+  zc = wave_total(zc);
   const uint64_t r = mix64(P.seed ^ mix64(uint64_t(ng) * 0x632BE59BD9B4E019ull + 0x9E3779B97F4A7C15ull));
   const float u = float(r >> 40) * (1.0f / 16777216.0f) * zc;
   int pick = si[cut - 1];
@@ -97,7 +107,7 @@ __device__ int draw_topk_wave(const float* sv, const int* si, int n, const Sampl
     const float c = carry + wave_incl_scan(ei);
     const unsigned long long hit = __ballot(i < cut && u < c);
     if (hit) { pick = si[c0 + __ffsll((long long)hit) - 1]; break; }
-    carry = __shfl(c, 63, 64);
+    carry = lane63(c);
   }
   return pick;
 }
@@ -906,11 +916,12 @@ __global__ __launch_bounds__(SS_THREADS) void sample_cm_kernel(
 }
 
 // The chunk-maximum sampler (V % 64 == 0, V / 16 <= 64 * 256); cmax as the LM head wrote it (cain_gemm_set_cmax).
-// cain_sample_set_cm: 0 off, 1 every forward whose LM head wrote the maxima, 2 only forwards of
-// more than 64 rows (the default).  It draws the same tokens; at one row its one-workgroup chain of phases (37.4 us
-// on qwen2:1.5b, profiles/r3/README.md) is longer than the two-stage kernel's 16-way split (29 us); at 256 rows it
-// takes 42 us against the one-workgroup-per-row kernel's 62 us (+0.2-0.3 % in-graph on the headline).
-static int g_sample_cm = 2;
+// cain_sample_set_cm: 0 off, 1 this kernel on every forward whose LM head wrote the maxima, 2 this kernel only on
+// forwards of more than 64 rows, 3 the lean kernel below on every forward whose LM head wrote them (the default).
+// They draw the same tokens; at one row this kernel's one-workgroup chain of phases (37.4 us on qwen2:1.5b,
+// profiles/r3/README.md) is longer than the two-stage kernel's 16-way split (29 us); at 256 rows it takes 42 us
+// against the one-workgroup-per-row kernel's 62 us (+0.2-0.3 % in-graph on the headline).
+static int g_sample_cm = 3;  // the lean kernel wherever the LM head wrote the maxima (cain_sample_lean, below)
 CAIN_API int cain_sample_cm_enabled() { return g_sample_cm; }
 // A/B switch for tests and tools (takes effect at the next forward / graph capture).
 CAIN_API void cain_sample_set_cm(int on) { g_sample_cm = on; }
@@ -925,71 +936,113 @@ CAIN_API int cain_sample_cm(float* logits, int ldl, int V, const float* cmax, in
 
 CAIN_API int cain_sample_params_size() { return int(sizeof(SampleParams)); }
 
+
 // =====================================================================================================
 // Lean chunk-maximum sampler (the few-row sampler at <= 12 us).  Same inputs as sample_cm_kernel
 // -- the logits and the LM head's chunk maxima (gemm_epi.h epi_cmax, written by every few-row LM-head kernel: bf16,
-// fp8, MXFP4 and GGUF Q4) -- and the same candidates in the same order, so the same token for the same seed.  The
-// round-3 trace of the two-stage kernel (profiles/r3/sampler_trace_final.log) put its 29 us in a chain of
-// workgroup-wide phases, the slowest the exact K-th largest of 256 thread maxima (7 us: a 21-stage bitonic sort of
-// shuffles, then 96 LDS reads per thread).  Here every phase is at most a few LDS reads per thread:
-//   1. chunk maxima -> registers (16-byte loads, issued first) and LDS; the repeat penalty: each chunk holding
-//      recent ids has ONE owner (the first history slot in it), which applies the penalty to every distinct recent
-//      id of its chunk (a 16-bit mask from one scan of the history), writes the chunk back and corrects the chunk's
-//      maximum in LDS -- so the maxima are exact after the penalty and the threshold needs K, not K + R;
-//   2. tau_c = a LOWER BOUND of the K-th largest chunk maximum: G >= 2K groups (64 / 128 / 256) take the maximum of
-//      256 / G thread maxima, and the K-th largest group maximum has K distinct chunks >= it (ln_kth_bound: one
-//      16-byte-read rank pass over G values, no sort);
-//   3. chunks >= tau_c (typically 1-2 K) gathered by one LDS atomic per thread that has any (most have none), their
-//      16 logits staged in LDS with one 16-byte load per thread;
-//   4. the same bound over the staged logits, the elements above it gathered, ranked (value desc, index asc) and
-//      drawn (draw_topk_wave), the decode state advanced.
+// fp8, MXFP4 and GGUF Q4) -- and the same candidates in the same order, so the same token for the same seed.
+//
+// The two-stage kernel's 29 us (profiles/r3/sampler_trace_final.log) and a first 256-thread version of this one
+// (31 us; profiles/r6/sampler/) were chains of workgroup-wide phases whose cost is what each wave issues on the
+// critical path: a wave64 VALU instruction takes 4 cycles, a shuffle is an LDS round trip (ds_bpermute), a rank
+// pass over 128 values by one wave ~3 us.  Here 1,024 threads each hold at most 16 chunk maxima, reductions and
+// scans are DPP row operations, and every rank count is split over up to 16 threads of a DPP row:
+//   1. every independent load first (chunk maxima, the 64 history slots, row state, options).  The repeat penalty
+//      (llama.cpp semantics: each distinct recent id once) marks the recent ids in an LDS bitmap of ids and one of
+//      chunks (one atomicOr each: the first setter of an id is its distinct occurrence);
+//   2. tau_c = a LOWER BOUND of the K-th largest post-penalty logit: the chunks holding no recent id have exact
+//      maxima, so with the other chunks masked to -inf, G = 64 / 128 / 256 groups (G >= 2K up to K = 128) of
+//      consecutive threads take their maximum (DPP row_shr), and the K-th largest group maximum (ln_bound: each
+//      group's rank counted by 16 / R threads) has K distinct unpenalised logits >= it;
+//   3. every chunk whose (pre-penalty) maximum is >= tau_c -- the penalty only lowers an unpenalised logit's chunk
+//      mates, never the logit, so every unpenalised top-K logit lies in one -- gathered by one LDS atomic per thread
+//      that has any (ln_gather), and their 16 logits loaded, 16-byte quads, two per thread;
+//   4. the unpenalised logits >= tau_c of those chunks plus the distinct recent ids' penalised logits >= tau_c
+//      (loaded by the history lanes in step 1, off the critical path) gathered, ranked (value desc, index asc; ln_rank)
+//      and drawn (draw_topk_wave), the decode state advanced.
 // A threshold that lets more than LN_CAP chunks or MAXC elements through is tightened to the exact K-th (value,
-// index) pair of those gathered (ln_tighten) and the gather repeated: exact in every case, ties included.
+// index) pair of the gathered set (ln_tighten) and the gather repeated: exact in every case, ties included.  The
+// logits are not modified (the penalty lives in registers).
 // =====================================================================================================
-constexpr int LN_NJ = 64;                      // chunk maxima per thread
-constexpr int LN_C_MAX = LN_NJ * SS_THREADS;   // chunks per row: V <= 262,144
-constexpr int LN_CAP = 256;                    // chunks staged per row (16 logits each)
-static_assert(LN_CAP == SS_THREADS, "one staged chunk id per thread");
+constexpr int LN_THREADS = 1024;
+constexpr int LN_NJ = 16;                     // chunk maxima per thread
+constexpr int LN_C_MAX = LN_NJ * LN_THREADS;  // chunks per row: V <= 262,144
+// chunks whose logits are loaded (4 quads each: two quads per thread): K <= 256 chunks without recent ids plus the
+// <= 64 chunks with some
+constexpr int LN_CAP = 512;
+constexpr int LN_QT = LN_CAP * 4 / LN_THREADS;  // quads per thread
+static_assert(LN_CAP >= SS_KMAX + HIST && LN_CAP <= MAXC, "staging capacity");
 
-// Lower bound of the K-th largest (1 <= K <= 256) of the row elements behind the 256 per-thread values tv (each an
-// element of the row, or -inf): the K-th largest of G group maxima (group g: threads g, g + G, ...) in (value desc,
-// group asc) order.  Every thread calls it; ends with a barrier.
-__device__ float ln_kth_bound(float tv, int K, float* s_a, float* s_b, float* s_tau) {
-  const int tid = threadIdx.x;
-  const int G = K <= 32 ? 64 : (K <= 64 ? 128 : 256);
-  s_a[tid] = tv;
+// Running max / sum over groups of GS consecutive lanes of each 16-lane DPP row (row_shr, lanes past the row start
+// read the identity): the lane with (lane % GS) == GS - 1 ends with its group's total.
+template <int CTRL>
+__device__ __forceinline__ int dpp_i(int old, int v) {
+  return __builtin_amdgcn_update_dpp(old, v, CTRL, 0xf, 0xf, false);
+}
+template <int GS>
+__device__ __forceinline__ float group_max(float x) {
+  const int ninf = __builtin_bit_cast(int, -INFINITY);
+  if constexpr (GS >= 2) x = fmaxf(x, __builtin_bit_cast(float, dpp_i<0x111>(ninf, __builtin_bit_cast(int, x))));
+  if constexpr (GS >= 4) x = fmaxf(x, __builtin_bit_cast(float, dpp_i<0x112>(ninf, __builtin_bit_cast(int, x))));
+  if constexpr (GS >= 8) x = fmaxf(x, __builtin_bit_cast(float, dpp_i<0x114>(ninf, __builtin_bit_cast(int, x))));
+  if constexpr (GS >= 16) x = fmaxf(x, __builtin_bit_cast(float, dpp_i<0x118>(ninf, __builtin_bit_cast(int, x))));
+  return x;
+}
+template <int GS>
+__device__ __forceinline__ int group_sum(int x) {
+  if constexpr (GS >= 2) x += dpp_i<0x111>(0, x);
+  if constexpr (GS >= 4) x += dpp_i<0x112>(0, x);
+  if constexpr (GS >= 8) x += dpp_i<0x114>(0, x);
+  if constexpr (GS >= 16) x += dpp_i<0x118>(0, x);
+  return x;
+}
+
+// Lower bound of the K-th largest (1 <= K <= 64 R) row element behind the per-thread values tv (each an element of the
+// row, or -inf): 64 R groups of GS = 16 / R consecutive threads take their maximum; group a's rank among the group
+// maxima (value desc, group asc) is counted by the GS threads of group a over R^2 16-byte reads each and summed in
+// the row; the group of rank K - 1 writes its maximum.  K distinct row elements are >= it.  Every thread calls it
+// (R uniform); ends with a barrier.
+template <int R>
+__device__ float ln_bound_r(float tv, int K, float* s_g, float* s_tau) {
+  constexpr int GS = 16 / R;
+  const int tid = threadIdx.x, lane = tid & 63;
+  tv = group_max<GS>(tv);
+  const int a = tid / GS, p = tid % GS;
+  if (p == GS - 1) s_g[a] = tv;
   __syncthreads();
-  if (tid < G) {
-    float g = tv;
-    for (int q = tid + G; q < SS_THREADS; q += G) g = fmaxf(g, s_a[q]);
-    s_b[tid] = g;
-  }
-  __syncthreads();
-  if (tid < G) {
-    const float g = s_b[tid];
-    const f32x4* b4 = reinterpret_cast<const f32x4*>(s_b);
-    int r = 0;
-#pragma unroll 8
-    for (int b = 0; b < G / 4; ++b) {
-      const f32x4 v = b4[b];
+  const float ga = s_g[a];  // (only lane GS - 1 of the group held the whole maximum)
+  const f32x4* g4 = reinterpret_cast<const f32x4*>(s_g);
+  int r = 0;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) r += (v[j] > g) || (v[j] == g && 4 * b + j < tid);
-    }
-    if (r == K - 1) *s_tau = g;  // ranks are a permutation of [0, G): exactly one writer
+  for (int i = 0; i < R * R; ++i) {
+    const int q = p + GS * i;
+    const f32x4 v = g4[q];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) r += (v[j] > ga) || (v[j] == ga && 4 * q + j < a);
   }
+  r = group_sum<GS>(r);  // complete in lane GS - 1
+  if (p == GS - 1 && r == K - 1) *s_tau = ga;  // ranks are a permutation of [0, G): one writer
+  (void)lane;
   __syncthreads();
   return *s_tau;
 }
 
+// R for a bound of the K-th largest: G = 64 R >= 2 K up to K = 128 (uniform across the workgroup)
+__device__ __forceinline__ float ln_bound(float tv, int K, float* s_g, float* s_tau) {
+  if (K <= 32) return ln_bound_r<1>(tv, K, s_g, s_tau);
+  if (K <= 64) return ln_bound_r<2>(tv, K, s_g, s_tau);
+  return ln_bound_r<4>(tv, K, s_g, s_tau);
+}
+
 // Append this thread's kept items (bit k of keep) as (val(k), id(k)): one LDS atomic per thread that has any, then
-// a loop over its set bits.  The list is in arrival order (rank_candidates orders it); entries past MAXC are dropped,
-// *s_nc counts them all.  The caller zeroes *s_nc before a barrier; ends with a barrier.
+// a loop over its set bits.  The list is in arrival order (ln_rank orders it); entries past MAXC are dropped, *s_nc
+// counts them all.  The caller zeroes *s_nc before a barrier; ends with a barrier.
 template <class Val, class Id>
-__device__ void ln_gather(uint64_t keep, Val val, Id id, float* cval, int* cidx, int* s_nc) {
-  const int cnt = __popcll(keep);
+__device__ void ln_gather(uint32_t keep, Val val, Id id, float* cval, int* cidx, int* s_nc) {
+  const int cnt = __popc(keep);
   int base = cnt ? atomicAdd(s_nc, cnt) : 0;
   while (keep) {
-    const int k = __builtin_ctzll(keep);
+    const int k = __builtin_ctz(keep);
     keep &= keep - 1;
     if (base < MAXC) {
       cval[base] = val(k);
@@ -1000,10 +1053,29 @@ __device__ void ln_gather(uint64_t keep, Val val, Id id, float* cval, int* cidx,
   __syncthreads();
 }
 
+// ln_gather for items held in a register array: the loop over the set bits is unrolled over the array (a dynamic
+// register index would go through scratch memory).
+template <int NE, class Id>
+__device__ void ln_gather_regs(uint32_t keep, const float (&v)[NE], Id id, float* cval, int* cidx, int* s_nc) {
+  const int cnt = __popc(keep);
+  int base = cnt ? atomicAdd(s_nc, cnt) : 0;
+#pragma unroll
+  for (int k = 0; k < NE; ++k) {
+    if ((keep >> k) & 1u) {
+      if (base < MAXC) {
+        cval[base] = v[k];
+        cidx[base] = id(k);
+      }
+      ++base;
+    }
+  }
+  __syncthreads();
+}
+
 // The exact K-th (value desc, id asc) of the n <= MAXC stored entries -> (*s_tv, *s_ti): a threshold pair every
 // top-K item passes (the stored entries are a subset of the items above the previous threshold).  Ends with a barrier.
 __device__ void ln_tighten(const float* cval, const int* cidx, int n, int K, float* s_tv, int* s_ti) {
-  for (int a = threadIdx.x; a < n; a += SS_THREADS) {
+  for (int a = threadIdx.x; a < n; a += LN_THREADS) {
     const float va = cval[a];
     const int ia = cidx[a];
     int r = 0;
@@ -1013,108 +1085,129 @@ __device__ void ln_tighten(const float* cval, const int* cidx, int n, int K, flo
   __syncthreads();
 }
 
-__global__ __launch_bounds__(SS_THREADS) void sample_lean_kernel(
-    float* __restrict__ logits, int ldl, int V, const float* __restrict__ cmax, int* __restrict__ tok,
+// Rank the n <= MAXC candidates (value desc, index asc) and write the first K in order to sv / si, TPC threads of a
+// DPP row per candidate (each counts every TPC-th 16-byte group, the row sums).  Returns min(n, K); ends with a barrier.
+template <int TPC>
+__device__ void ln_rank_t(const float* cval, const int* cidx, int n, int K, float* sv, int* si) {
+  const int tid = threadIdx.x, n4 = (n + 3) >> 2;
+  const f32x4* cv4 = reinterpret_cast<const f32x4*>(cval);
+  const i32x4* ci4 = reinterpret_cast<const i32x4*>(cidx);
+  for (int a0 = 0; a0 < n; a0 += LN_THREADS / TPC) {
+    const int a = a0 + tid / TPC, p = tid % TPC;
+    const int ac = min(a, n - 1);
+    const float va = cval[ac];
+    const int ia = cidx[ac];
+    int r = 0;
+    for (int q = p; q < n4; q += TPC) {
+      const f32x4 v = cv4[q];
+      const i32x4 ix = ci4[q];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) r += (v[j] > va) || (v[j] == va && ix[j] < ia);
+    }
+    r = group_sum<TPC>(r);
+    if (a < n && p == TPC - 1 && r < K) {
+      sv[r] = va;
+      si[r] = ia;
+    }
+  }
+  __syncthreads();
+}
+
+__device__ int ln_rank(float* cval, int* cidx, int n, int K, float* sv, int* si) {
+  const int n4 = (n + 3) >> 2;
+  if ((int)threadIdx.x < n4 * 4 - n) {  // pad to whole 16-byte groups with entries that rank last
+    cval[n + threadIdx.x] = -INFINITY;
+    cidx[n + threadIdx.x] = 0x7fffffff;
+  }
+  __syncthreads();
+  if (n <= 64) ln_rank_t<16>(cval, cidx, n, K, sv, si);
+  else if (n <= 128) ln_rank_t<8>(cval, cidx, n, K, sv, si);
+  else if (n <= 256) ln_rank_t<4>(cval, cidx, n, K, sv, si);
+  else if (n <= 512) ln_rank_t<2>(cval, cidx, n, K, sv, si);
+  else ln_rank_t<1>(cval, cidx, n, K, sv, si);
+  return min(n, K);
+}
+
+typedef uint32_t ln_u32x4 __attribute__((ext_vector_type(4)));
+
+__global__ __launch_bounds__(LN_THREADS) void sample_lean_kernel(
+    const float* __restrict__ logits, int ldl, int V, const float* __restrict__ cmax, int* __restrict__ tok,
     int* __restrict__ pos, int* __restrict__ gen, int ldg, int* __restrict__ n_gen, const int* __restrict__ max_new,
     int* __restrict__ done, int* __restrict__ hist, const int* __restrict__ slot, int T_max,
     const SampleParams* __restrict__ params, unsigned long long* __restrict__ trace) {
-  const int m = blockIdx.x;
-  if (slot[m] < 0 || done[m]) return;
-  const int tid = threadIdx.x, lane = tid & 63;
+  const int m = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
   auto stamp = [&](int i) {
     if (trace && tid == 0) trace[(size_t)m * 8 + i] = __builtin_amdgcn_s_memrealtime();
   };
   stamp(0);
-  const SampleParams P = params[m];
-  float* lg = logits + (size_t)m * ldl;
+  // ---- 1. every load that depends on no other first: the chunk maxima (thread t: chunks 4 (t + 1024 j) .. + 3;
+  // unconditional clamped loads, masked after), the 64 history slots (wave 0), the row's state and options
   const int C = V >> 4, C4 = C >> 2;
+  const f32x4* cm4 = reinterpret_cast<const f32x4*>(cmax + (size_t)m * C);
+  f32x4 cq[LN_NJ / 4];
+#pragma unroll
+  for (int j = 0; j < LN_NJ / 4; ++j) cq[j] = cm4[min(tid + j * LN_THREADS, C4 - 1)];
+  const int hslot = tid < HIST ? hist[(size_t)m * HIST + tid] : -1;
+  const int sl = slot[m], dn = done[m], ng = n_gen[m];
+  const SampleParams P = params[m];
+  if (sl < 0 || dn) return;
+  const float* lg = logits + (size_t)m * ldl;
   extern __shared__ __attribute__((aligned(16))) float ln_smem[];
-  float* s_cm = ln_smem;                           // [C] chunk maxima (exact after the penalty)
-  f32x4* s_lv4 = reinterpret_cast<f32x4*>(ln_smem + ((C + 3) & ~3));  // [LN_CAP * 4] staged logits, 4 per entry
-  __shared__ int s_hist[HIST];
-  __shared__ float s_a[SS_THREADS], s_b[SS_THREADS];
+  float* s_cm = ln_smem;                                           // [C] chunk maxima (the tightening's values)
+  uint32_t* s_bm = reinterpret_cast<uint32_t*>(ln_smem + C4 * 4);  // [V / 32] recent ids, then [C / 32] their chunks
+  const int bm_words = (((V + 127) >> 7) << 2);
+  uint32_t* s_cbm = s_bm + bm_words;
+  __shared__ float s_g[256];
   __shared__ float sv[SS_KMAX];
   __shared__ int si[SS_KMAX];
   __shared__ __attribute__((aligned(16))) float cval[MAXC + 4];
   __shared__ __attribute__((aligned(16))) int cidx[MAXC + 4];
-  __shared__ int s_ch[LN_CAP];
   __shared__ float s_tau, s_tv;
   __shared__ int s_ti, s_nc, s_choice;
 
-  // ---- 1. chunk maxima (thread t: chunks 4 (t + 256 j) .. + 3; unconditional clamped loads, masked) and, in flight
-  // with them, the history ids and each history id's chunk
-  const f32x4* cm4 = reinterpret_cast<const f32x4*>(cmax + (size_t)m * C);
-  f32x4 cq[LN_NJ / 4];
-#pragma unroll
-  for (int j = 0; j < LN_NJ / 4; ++j) cq[j] = cm4[min(tid + j * SS_THREADS, C4 - 1)];
-  const int ng = n_gen[m];
   const int nrep = (P.repeat_penalty != 1.0f && P.repeat_last_n > 0) ? min(min(P.repeat_last_n, HIST), ng) : 0;
-  int hid = -1;
-  if (tid < nrep) hid = hist[(size_t)m * HIST + ((ng - 1 - tid) & (HIST - 1))];
-  if (hid >= V) hid = -1;
-  f32x4 hc[4];
-  if (nrep > 0) {
-    const f32x4* src = reinterpret_cast<const f32x4*>(lg + (size_t)(hid >= 0 ? hid >> 4 : 0) * 16);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) hc[q] = src[q];
-  }
-  if (tid < HIST) s_hist[tid] = hid;
-  float cv[LN_NJ];
+  f32x4* s_cm4 = reinterpret_cast<f32x4*>(s_cm);
 #pragma unroll
   for (int j = 0; j < LN_NJ / 4; ++j)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) cv[4 * j + i] = tid + j * SS_THREADS < C4 ? cq[j][i] : -INFINITY;
-  if (nrep > 0) {  // (uniform) the chunk maxima go through LDS, where the penalised chunks are corrected
-    f32x4* s_cm4 = reinterpret_cast<f32x4*>(s_cm);
-#pragma unroll
-    for (int j = 0; j < LN_NJ / 4; ++j)
-      if (tid + j * SS_THREADS < C4) s_cm4[tid + j * SS_THREADS] = cq[j];
+    if (tid + j * LN_THREADS < C4) s_cm4[tid + j * LN_THREADS] = cq[j];
+  // history slot s holds a recent id iff it is one of the last nrep written: (ng - 1 - s) mod 64 < nrep
+  int hid = (tid < HIST && ((ng - 1 - tid) & (HIST - 1)) < nrep) ? hslot : -1;
+  if (hid >= V) hid = -1;
+  float hv = 0.f;  // the recent id's logit (history lanes; needed in step 4 only)
+  bool hfirst = false;
+  float cv[LN_NJ];  // this thread's chunk maxima; the bound sees the penalised chunks' as -inf
+  float bv = -INFINITY;
+  if (nrep > 0) {  // (uniform)
+    if (tid < HIST) hv = lg[hid >= 0 ? hid : 0];
+    ln_u32x4* bm4 = reinterpret_cast<ln_u32x4*>(s_bm);
+    const int nz4 = (bm_words + ((C + 127) >> 7 << 2)) >> 2;
+    for (int w = tid; w < nz4; w += LN_THREADS) bm4[w] = ln_u32x4{0u, 0u, 0u, 0u};
     __syncthreads();
     if (hid >= 0) {
-      // one scan of the history: owner = no earlier slot in the same chunk; mask = the distinct recent ids in it
+      const uint32_t bit = 1u << (hid & 31);
+      hfirst = !(atomicOr(&s_bm[hid >> 5], bit) & bit);
       const int ch = hid >> 4;
-      bool owner = true;
-      uint32_t mask = 0;
-      const i32x4* h4 = reinterpret_cast<const i32x4*>(s_hist);
-#pragma unroll
-      for (int b = 0; b < HIST / 4; ++b) {
-        const i32x4 h = h4[b];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const bool same = h[j] >= 0 && (h[j] >> 4) == ch;
-          owner &= !(same && 4 * b + j < tid);
-          mask |= same ? 1u << (h[j] & 15) : 0u;
-        }
-      }
-      if (owner) {
-        float mx = -INFINITY;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const float v = hc[q][i];
-            const float pv = v > 0.f ? v / P.repeat_penalty : v * P.repeat_penalty;
-            hc[q][i] = (mask >> (4 * q + i)) & 1u ? pv : v;
-            mx = fmaxf(mx, hc[q][i]);
-          }
-          reinterpret_cast<f32x4*>(lg + (size_t)ch * 16)[q] = hc[q];
-        }
-        s_cm[ch] = mx;
-      }
+      atomicOr(&s_cbm[ch >> 5], 1u << (ch & 31));
     }
     __syncthreads();
-    const f32x4* s_cm4r = reinterpret_cast<const f32x4*>(s_cm);
 #pragma unroll
     for (int j = 0; j < LN_NJ / 4; ++j) {
-      const f32x4 v = s_cm4r[min(tid + j * SS_THREADS, C4 - 1)];
+      const int c0 = 4 * (tid + j * LN_THREADS);  // 4 consecutive chunks: 4 bits of one word
+      const uint32_t pb = c0 < C ? (s_cbm[c0 >> 5] >> (c0 & 31)) & 0xfu : 0u;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) cv[4 * j + i] = tid + j * SS_THREADS < C4 ? v[i] : -INFINITY;
+      for (int i = 0; i < 4; ++i) {
+        cv[4 * j + i] = tid + j * LN_THREADS < C4 ? cq[j][i] : -INFINITY;
+        bv = fmaxf(bv, (pb >> i) & 1u ? -INFINITY : cv[4 * j + i]);
+      }
     }
   } else {
-    f32x4* s_cm4 = reinterpret_cast<f32x4*>(s_cm);
 #pragma unroll
     for (int j = 0; j < LN_NJ / 4; ++j)
-      if (tid + j * SS_THREADS < C4) s_cm4[tid + j * SS_THREADS] = cq[j];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        cv[4 * j + i] = tid + j * LN_THREADS < C4 ? cq[j][i] : -INFINITY;
+        bv = fmaxf(bv, cv[4 * j + i]);
+      }
   }
   stamp(1);
 
@@ -1123,85 +1216,78 @@ __global__ __launch_bounds__(SS_THREADS) void sample_lean_kernel(
   if (K > V) K = V;
   if (P.temperature <= 0.f) K = 1;
 
-  // ---- 2. tau_c, then the chunks above it
-  float bv = -INFINITY;
-#pragma unroll
-  for (int k = 0; k < LN_NJ; ++k) bv = fmaxf(bv, cv[k]);
-  auto cid = [&](int k) { return 4 * (tid + (k >> 2) * SS_THREADS) + (k & 3); };
-  float tv = ln_kth_bound(bv, K, s_a, s_b, &s_tau);
+  // ---- 2. tau_c
+  float tv = ln_bound(bv, K, s_g, &s_tau);
   int ti = 0x7fffffff;
   stamp(2);
+
+  // ---- 3. the chunks whose maximum is >= tau_c
+  auto cid = [&](int k) { return 4 * (tid + (k >> 2) * LN_THREADS) + (k & 3); };
+  // (a tightening ranks the gathered chunks without recent ids: their maxima are post-penalty logits)
+  auto cval_of = [&](int k) {
+    const int c = cid(k);
+    return nrep > 0 && ((s_cbm[c >> 5] >> (c & 31)) & 1u) ? -INFINITY : s_cm[c];
+  };
   int n_ch = 0;
 #pragma unroll 1
   for (int attempt = 0; attempt < 4; ++attempt) {
-    if (tid == 0) s_nc = 0;
+    if (tid == 0) s_nc = 0, s_tv = tv, s_ti = ti;  // (kept if a tightening finds no K-th)
     __syncthreads();
-    uint64_t keep = 0;
+    uint32_t keep = 0;
 #pragma unroll
     for (int k = 0; k < LN_NJ; ++k) {
       const bool in = cv[k] > tv || (cv[k] == tv && cid(k) <= ti);
-      keep |= (uint64_t)(in && cv[k] > -INFINITY) << k;
+      keep |= uint32_t(in && cv[k] > -INFINITY) << k;
     }
-    ln_gather(keep, [&](int k) { return s_cm[cid(k)]; }, cid, cval, cidx, &s_nc);
+    ln_gather(keep, cval_of, cid, cval, cidx, &s_nc);
     n_ch = s_nc;
     if (n_ch <= LN_CAP) break;
     ln_tighten(cval, cidx, min(n_ch, MAXC), K, &s_tv, &s_ti);
     tv = s_tv, ti = s_ti;
   }
   n_ch = min(n_ch, LN_CAP);
-  s_ch[tid] = tid < n_ch ? cidx[tid] : 0;  // (SS_THREADS == LN_CAP) entries past n_ch: chunk 0, loaded and masked
-  __syncthreads();
   stamp(3);
-
-  // ---- 3. the gathered chunks' logits: quad q = tid + 256 u of chunk entry q >> 2 (one 16-byte load each)
+  // their logits: quad tid of chunk entry tid >> 2 (chunk ids read from cidx before the next gather's first
+  // barrier; without any chunk, chunk 0 is loaded and masked); the recent ids among them are masked out (their
+  // penalised values come from the history lanes)
   const int nq = n_ch * 4;
-  float ev[16];
-  int eid[16];
-  f32x4 lq[4];
+  constexpr int NE = 4 * LN_QT + 1;
+  float ev[NE];
+  int eb[LN_QT];
+  f32x4 lq[LN_QT];
 #pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    const int q = min(tid + u * SS_THREADS, max(nq - 1, 0));
-    lq[u] = reinterpret_cast<const f32x4*>(lg + (size_t)s_ch[q >> 2] * 16)[q & 3];
+  for (int u = 0; u < LN_QT; ++u) {  // quad tid + 1024 u of chunk entry (tid + 1024 u) >> 2
+    const int q = tid + u * LN_THREADS;
+    const int ch = nq > 0 ? cidx[min(q, nq - 1) >> 2] : 0;
+    lq[u] = reinterpret_cast<const f32x4*>(lg + (size_t)ch * 16)[q & 3];
+    eb[u] = ch * 16 + (q & 3) * 4;
   }
 #pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    const int q = tid + u * SS_THREADS;
-    const bool in = q < nq;
-    if (in) s_lv4[q] = lq[u];
-    const int base = in ? s_ch[q >> 2] * 16 + (q & 3) * 4 : 0x7ffff000;
+  for (int u = 0; u < LN_QT; ++u) {
+    const bool qin = tid + u * LN_THREADS < nq;
+    const uint32_t pen4 = nrep > 0 ? (s_bm[eb[u] >> 5] >> (eb[u] & 31)) & 0xfu : 0u;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      ev[4 * u + i] = in ? lq[u][i] : -INFINITY;
-      eid[4 * u + i] = base + i;
-    }
+    for (int i = 0; i < 4; ++i) ev[4 * u + i] = qin && !((pen4 >> i) & 1u) ? lq[u][i] : -INFINITY;
   }
+  // the last item: the distinct recent id's penalised logit (history lanes)
+  ev[NE - 1] = hfirst ? (hv > 0.f ? hv / P.repeat_penalty : hv * P.repeat_penalty) : -INFINITY;
+  auto eid = [&](int k) { return k < NE - 1 ? eb[k >> 2] + (k & 3) : hid; };  // (k constant after unrolling)
   stamp(4);
 
-  // ---- 4. the bound over the staged logits, the elements above it, ranked and drawn
-  float bv2 = -INFINITY;
-#pragma unroll
-  for (int k = 0; k < 16; ++k) bv2 = fmaxf(bv2, ev[k]);
-  tv = ln_kth_bound(bv2, K, s_a, s_b, &s_tau);
-  ti = 0x7fffffff;
-  const float* s_lv = reinterpret_cast<const float*>(s_lv4);
+  // ---- 4. the elements >= tau_c (with a tightened chunk pair (tau_c, c_K): value tau_c up to c_K's last id)
+  ti = ti == 0x7fffffff ? ti : ti * 16 + 15;
   int nc = 0;
 #pragma unroll 1
   for (int attempt = 0; attempt < 4; ++attempt) {
-    if (tid == 0) s_nc = 0;
+    if (tid == 0) s_nc = 0, s_tv = tv, s_ti = ti;
     __syncthreads();
-    uint64_t keep = 0;
+    uint32_t keep = 0;
 #pragma unroll
-    for (int k = 0; k < 16; ++k) {
-      const bool in = ev[k] > tv || (ev[k] == tv && eid[k] <= ti);
-      keep |= (uint64_t)(in && ev[k] > -INFINITY) << k;
+    for (int i = 0; i < NE; ++i) {
+      const bool in = ev[i] > tv || (ev[i] == tv && eid(i) <= ti);
+      keep |= uint32_t(in && ev[i] > -INFINITY) << i;
     }
-    ln_gather(
-        keep, [&](int k) { return s_lv[(tid + (k >> 2) * SS_THREADS) * 4 + (k & 3)]; },
-        [&](int k) {
-          const int q = tid + (k >> 2) * SS_THREADS;
-          return s_ch[q >> 2] * 16 + (q & 3) * 4 + (k & 3);
-        },
-        cval, cidx, &s_nc);
+    ln_gather_regs(keep, ev, eid, cval, cidx, &s_nc);
     nc = s_nc;
     if (nc <= MAXC) break;
     ln_tighten(cval, cidx, MAXC, K, &s_tv, &s_ti);
@@ -1209,7 +1295,7 @@ __global__ __launch_bounds__(SS_THREADS) void sample_lean_kernel(
   }
   nc = min(nc, MAXC);
   stamp(5);
-  const int nk = rank_candidates(cval, cidx, nc, K, sv, si, SS_THREADS);
+  const int nk = ln_rank(cval, cidx, nc, K, sv, si);
   stamp(6);
   if (tid < 64) {
     const int pick = nk == 0 ? 0 : (P.temperature <= 0.f ? si[0] : draw_topk_wave(sv, si, nk, P, ng));
@@ -1220,22 +1306,24 @@ __global__ __launch_bounds__(SS_THREADS) void sample_lean_kernel(
   stamp(7);
 }
 
-static size_t ln_lds_bytes(int V) { return ((size_t)((V >> 4) + 3) / 4 * 4 + LN_CAP * 16) * sizeof(float); }
+static size_t ln_lds_bytes(int V) {
+  const size_t C = (size_t)V >> 4;
+  return C * sizeof(float) + (size_t)((V + 127) >> 7) * 16 + (size_t)((C + 127) >> 7) * 16;
+}
 
 // The lean chunk-maximum sampler (V % 64 == 0, V / 16 <= LN_C_MAX); cmax as the LM head wrote it.  < 0: refused.
-// The trace (cain_sample_set_trace) takes [M][8] timestamps: start, maxima exact, tau_c, chunks gathered, logits
-// staged, elements gathered, ranked, end.
+// The trace (cain_sample_set_trace) takes [M][8] timestamps: start, penalty marked, tau_c, chunks gathered, logits
+// loaded, elements gathered, ranked, end.
 CAIN_API int cain_sample_lean(float* logits, int ldl, int V, const float* cmax, int* tok, int* pos, int* gen, int ldg,
                               int* n_gen, const int* max_new, int* done, int* hist, const int* slot, int T_max, int M,
                               const void* params, hipStream_t st) {
   if (!cmax || V % 64 || V / 16 > LN_C_MAX) return -1;
-  const size_t lds = ln_lds_bytes(V);
   static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&sample_lean_kernel),
                                                hipFuncAttributeMaxDynamicSharedMemorySize,
                                                int(ln_lds_bytes(LN_C_MAX * 16))) == hipSuccess;
   if (!attr) return -1;
-  hipLaunchKernelGGL(sample_lean_kernel, dim3(M), dim3(SS_THREADS), lds, st, logits, ldl, V, cmax, tok, pos, gen, ldg,
-                     n_gen, max_new, done, hist, slot, T_max, reinterpret_cast<const SampleParams*>(params),
-                     g_sample_trace);
+  hipLaunchKernelGGL(sample_lean_kernel, dim3(M), dim3(LN_THREADS), ln_lds_bytes(V), st, logits, ldl, V, cmax, tok,
+                     pos, gen, ldg, n_gen, max_new, done, hist, slot, T_max,
+                     reinterpret_cast<const SampleParams*>(params), g_sample_trace);
   return int(hipGetLastError());
 }

@@ -52,10 +52,29 @@ def test_chunk_max_sampler_same_tokens(name):
     opts = [dict(seed=21, eos_id=-1), dict(temperature=0.0, eos_id=-1), dict(repeat_penalty=0.9, seed=5, eos_id=-1)]
     out = []
     saved = ops.sample_cm_mode()
-    for cm in (1, 0):
+    for cm in (3, 1, 0):  # the lean chunk-maximum kernel, the round-3 one, the two-stage kernel
         ops.set_sample_cm(cm)
         eng = DecodeEngine(name, device="cuda", max_batch=4, max_context=256, seed=7, steps_per_graph=4)
         out.append([r.tokens for r in eng.generate(PROMPTS, 24, opts)])
+        eng.close()
+    ops.set_sample_cm(saved)
+    assert out[0] == out[2] and out[1] == out[2]
+
+
+@pytest.mark.parametrize("dtype", ["fp8", "fp4", "q4_0", "q4_k"])
+def test_lean_sampler_on_every_lm_head_format(dtype):
+    """Single-stream decode on every few-row weight format: the fp8 / MXFP4 / Q4 LM heads write the chunk maxima,
+    and the lean chunk-maximum sampler generates exactly the tokens of the two-stage sampler (which reads the full
+    logits)."""
+    from cain_amd import ops
+    opts = [dict(seed=21, eos_id=-1)]
+    out = []
+    saved = ops.sample_cm_mode()
+    for cm in (3, 0):
+        ops.set_sample_cm(cm)
+        eng = DecodeEngine("tiny-llama3.1:8b", device="cuda", max_batch=1, max_context=256, seed=7,
+                           steps_per_graph=4, weight_dtype=dtype)
+        out.append([r.tokens for r in eng.generate(PROMPTS[:1], 32, opts)])
         eng.close()
     ops.set_sample_cm(saved)
     assert out[0] == out[1]
@@ -69,13 +88,13 @@ def test_chunk_max_sampler_wide_batch_same_tokens():
     opts = [dict(seed=100 + i, eos_id=-1) if i % 3 else dict(temperature=0.0, eos_id=-1) for i in range(80)]
     out = []
     saved = ops.sample_cm_mode()
-    for cm in (1, 0):
+    for cm in (3, 1, 0):
         ops.set_sample_cm(cm)
         eng = DecodeEngine("tiny-llama3.1:8b", device="cuda", max_batch=80, max_context=256, seed=7, steps_per_graph=4)
         out.append([r.tokens for r in eng.generate(prompts, 12, opts)])
         eng.close()
     ops.set_sample_cm(saved)
-    assert out[0] == out[1]
+    assert out[0] == out[2] and out[1] == out[2]
 
 
 def test_greedy_first_token_matches_oracle():
