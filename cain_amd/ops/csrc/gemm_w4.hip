@@ -480,7 +480,9 @@ static int w4_variant(int N, int K, int M, int epi, int n_cu) {
   // items (qwen2:1.5b, K = 1536: gate/up 7.4 vs 8.6 us, O 3.9 vs 4.1; profiles/r4/ab/w4_short_k.jsonl)
   const bool w4 = (epi == EPI_QKV_ROPE || kq < 24) && w4_stream_fits(4, K, M);
   if (w4) return W4S_4_4;
-  if (w4_stream_fits(8, K, M)) return W4S_8_4;
+  // (not the fused QKV epilogue: it has no 8-wave instance, and the 4-wave one stages only 28 KiB of activations --
+  // rows x K beyond that take the tile kernel)
+  if (epi != EPI_QKV_ROPE && w4_stream_fits(8, K, M)) return W4S_8_4;
   if (M > 16) return kq >= 32 ? W4T_8_2_2 : W4T_4_2_2;
   return kq >= 32 ? W4T_8_2_1 : W4T_4_4_1;
 }

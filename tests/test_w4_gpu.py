@@ -255,6 +255,41 @@ def test_w4_qkv_rope_kv_append(H, Hkv, hd, M, kv8, var, occ):
     ops.set_w4_occupancy(0)
 
 
+@pytest.mark.parametrize("M,K", [(10, 1536), (16, 1536), (12, 2048), (6, 4096), (1, 1536)])
+def test_w4_qkv_rope_rule_between_the_staging_sizes(M, K):
+    """Rows x K between the 4-wave stream kernel's 28 KiB activation copy and the 8-wave one's 48 KiB (qwen2:1.5b's
+    prefill chunks of 10-16 rows, llama3.1:8b's continuous batches of 4-6): the fused QKV epilogue has no 8-wave
+    instance, so the rule takes the tile kernel (a round-6 regression ran these on the 4-wave kernel with a partial
+    activation copy)."""
+    torch.manual_seed(90 + M)
+    H, Hkv, hd, T_max, S = 12, 2, 128, 64, 32
+    qkv_dim = (H + 2 * Hkv) * hd
+    W = (torch.randn(qkv_dim, K, device=DEV) * 0.03).bfloat16()
+    bias = torch.randn(qkv_dim, device=DEV)
+    x = torch.randn(M, K, device=DEV).bfloat16()
+    per = rope_pair_order(hd).to(DEV)
+    perm = torch.cat([h * hd + per for h in range(H + Hkv)] + [torch.arange((H + Hkv) * hd, qkv_dim, device=DEV)])
+    c, s = quantize_mxfp4(W)
+    wq, ws = pack_mxfp4(c[perm].contiguous(), s[perm].contiguous())
+    inv = 1.0 / (10000.0 ** (torch.arange(0, hd, 2, dtype=torch.float64) / hd))
+    ang = torch.arange(T_max, dtype=torch.float64)[:, None] * inv[None]
+    cos_t, sin_t = ang.cos().float().to(DEV), ang.sin().float().to(DEV)
+    kc = torch.zeros(S, Hkv, T_max, hd, device=DEV).bfloat16()
+    vt = torch.zeros(S, Hkv, hd, T_max, device=DEV).bfloat16()
+    q = torch.zeros(M, H * hd, device=DEV).bfloat16()
+    slot = torch.randperm(S, device=DEV)[:M].int()
+    pos = torch.randint(0, T_max, (M,), device=DEV).int()
+    ops.gemm_w4(wq, ws, x, qkv_dim, ops.EPI_QKV_ROPE, bias=bias[perm], out=q,
+                rope=dict(kc=kc, vtc=vt, slot=slot, pos=pos, cos_t=cos_t, sin_t=sin_t, H=H, Hkv=Hkv, hd=hd))
+    ref = (x.float() @ dequantize_mxfp4(c, s).t() + bias).bfloat16().float()
+    kn, vn = ops.unpack_kcache(kc), ops.unpack_vcache(vt)
+    for m in range(M):
+        p, sl = int(pos[m]), int(slot[m])
+        assert rel_err(q[m].view(H, hd), _rot(ref[m, : H * hd].view(H, hd), cos_t[p], sin_t[p])) < 1e-2, m
+        assert rel_err(kn[sl, :, p], _rot(ref[m, H * hd:(H + Hkv) * hd].view(Hkv, hd), cos_t[p], sin_t[p])) < 1e-2
+        assert rel_err(vn[sl, :, p], ref[m, (H + Hkv) * hd:].view(Hkv, hd)) < 1e-2
+
+
 FP4_TINY = sorted(n for n, c in TINY.items() if not (c.d_model % 128 or c.q_dim % 128 or c.ffn % 128))
 
 
