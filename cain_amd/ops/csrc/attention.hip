@@ -260,6 +260,39 @@ __global__ __launch_bounds__(AW * 64, OCC) void attn_decode_kernel(
     s_ticket = __hip_atomic_fetch_add(counters + mk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
   if (s_ticket != unsigned(nsplit - 1)) return;
+  if (nsplit <= 8 && nout <= 2 * AW * 64) {
+    // up to 8 splits and 2 outputs per thread (the few-row decode of every study model but gemma:2b's 8 x 256 query
+    // dims): each thread loads its outputs' partials and every split's (m, l) at once -- one round trip of sc1 loads,
+    // no LDS pass, instead of the (m, l) pass, a barrier and then the partials.  Measured one box, interleaved
+    // (profiles/r6/attn_combine/): batch-1 MXFP4 llama3.1:8b +0.9 %, qwen2:1.5b +1.2 %; an LDS variant for 4 outputs
+    // per thread lost on llama / qwen and gemma:2b kept the pass below.
+    if (threadIdx.x == 0) counters[mk] = 0u;  // ready for the next launch (launch-ordered)
+    for (int e = threadIdx.x; e < nout; e += AW * 64) {
+      const int gg = e / HD, d = e - (e / HD) * HD;
+      float mj[8], lj[8], oj[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {  // clamped: every load unconditional, the split index masked after
+        const int jj = min(j, nsplit - 1);
+        const int li = gg * nsplit + jj;
+        mj[j] = __hip_atomic_load(pml + li * 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        lj[j] = __hip_atomic_load(pml + li * 2 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        oj[j] = __hip_atomic_load(part_o + (pbase + (size_t)gg * nsplit + jj) * HD + d, __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_AGENT);
+      }
+      float Mx = -INFINITY;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) Mx = j < nsplit ? fmaxf(Mx, mj[j]) : Mx;
+      float num = 0.f, den = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float f = (j < nsplit && mj[j] != -INFINITY) ? exp2f(mj[j] - Mx) : 0.f;
+        num += f * oj[j];
+        den += f * lj[j];
+      }
+      out[(size_t)m * ldo + (kh * G + gg) * HD + d] = f2bf(den > 0.f ? num * fast_rcp(den) : 0.f);
+    }
+    return;
+  }
   // split weights into LDS once (sc1 loads: never served from this CU's stale L1)
   __shared__ float s_w[16 * 64];   // [gg][j] merge weight 2^(m_j - M) / den
   const int nw = G * nsplit;      // <= 16 * 64

@@ -219,7 +219,7 @@ def test_attention_split_combine(H, Hkv, hd, lengths):
     pos = torch.tensor([L - 1 for L in lengths], device=DEV, dtype=torch.int32)
     counters = torch.zeros(M * Hkv, device=DEV, dtype=torch.int32)
     kp, vp = ops.pack_kcache(kc), ops.pack_vcache(vt.transpose(-1, -2))  # the kernel's cache layouts
-    for nsplit in (1, 3, 16, 64, 16):  # repeated nsplit: the in-kernel counters must reset
+    for nsplit in (1, 3, 8, 16, 64, 2, 16):  # repeated nsplit: the in-kernel counters must reset
         out = ops.attention(q, kp, vp, slot, pos, H, Hkv, hd, nsplit, 1.0 / math.sqrt(hd), counters=counters)
         for m, L in enumerate(lengths):
             ref = _attn_ref(q[m].view(H, hd), kc[m].float(), vt[m].float().transpose(-1, -2), L, H // Hkv)
