@@ -223,7 +223,39 @@ __global__ __launch_bounds__(AW * 64, OCC) void attn_decode_kernel(
   // reducer's L2 never holds another group's line that is still being written
   const int mls = ((G * nsplit * 2 + 31) / 32) * 32;
   float* pml = part_ml + (size_t)mk * mls;
-  for (int e = threadIdx.x; e < nout; e += AW * 64) {
+  // 3 to 8 outputs per thread (gemma:2b's 8 query heads x 256 dims on 4 waves): publish and merge 4 consecutive dims
+  // per thread with 16-byte write-through stores and sc1 loads, and request every split's partials and (m, l) in one
+  // round trip -- the per-element path below issued 8 x 8 dependent-free but 4-byte loads per thread
+  // (compiled for head_dim 256 only: the hd <= 128 bodies keep their code unchanged)
+  const bool vec = HD >= 256 && nsplit > 1 && nsplit <= 8 && nout > 2 * AW * 64 && nout <= 8 * AW * 64;
+  if (vec) {
+    const __amdgpu_buffer_rsrc_t po_r = slab_rsrc(part_o);
+    for (int qd = threadIdx.x; qd < nout / 4; qd += AW * 64) {
+      const int e0 = qd * 4, gg = e0 / HD, d0 = e0 - (e0 / HD) * HD;
+      float Mx = -INFINITY;
+#pragma unroll
+      for (int w = 0; w < AW; ++w) Mx = fmaxf(Mx, s_m[w][gg]);
+      float lsum = 0.f;
+      f32x4 osum = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int w = 0; w < AW; ++w) {
+        const float mw = s_m[w][gg];
+        if (mw == -INFINITY) continue;
+        const float f = exp2f(mw - Mx);
+        lsum += f * s_l[w][gg];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) osum[i] += f * s_o[w][d0 + i][gg];
+      }
+      const size_t pi = pbase + (size_t)gg * nsplit + sp;
+      st_wt(po_r, (int)((pi * HD + d0) * 4), osum);
+      if (d0 == 0) {
+        const int li = gg * nsplit + sp;
+        __hip_atomic_store(pml + li * 2 + 0, Mx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(pml + li * 2 + 1, lsum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  }
+  for (int e = threadIdx.x; e < (vec ? 0 : nout); e += AW * 64) {
     const int gg = e / HD, d = e - (e / HD) * HD;
     float Mx = -INFINITY;
 #pragma unroll
@@ -260,6 +292,42 @@ __global__ __launch_bounds__(AW * 64, OCC) void attn_decode_kernel(
     s_ticket = __hip_atomic_fetch_add(counters + mk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
   if (s_ticket != unsigned(nsplit - 1)) return;
+  if (vec) {
+    if (threadIdx.x == 0) counters[mk] = 0u;  // ready for the next launch (launch-ordered)
+    const __amdgpu_buffer_rsrc_t po_r = slab_rsrc(part_o);
+    for (int qd = threadIdx.x; qd < nout / 4; qd += AW * 64) {
+      const int e0 = qd * 4, gg = e0 / HD, d0 = e0 - (e0 / HD) * HD;
+      float mj[8], lj[8];
+      f32x4 oj[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {  // clamped: every load unconditional, the split index masked after
+        const int jj = min(j, nsplit - 1);
+        const int li = gg * nsplit + jj;
+        const f32x2 ml = __builtin_bit_cast(
+            f32x2, __hip_atomic_load(reinterpret_cast<const uint64_t*>(pml + li * 2), __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_AGENT));
+        mj[j] = ml[0], lj[j] = ml[1];
+        oj[j] = ld_wt(po_r, (int)(((pbase + (size_t)gg * nsplit + jj) * HD + d0) * 4));
+      }
+      float Mx = -INFINITY;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) Mx = j < nsplit ? fmaxf(Mx, mj[j]) : Mx;
+      float den = 0.f;
+      f32x4 num = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float f = (j < nsplit && mj[j] != -INFINITY) ? exp2f(mj[j] - Mx) : 0.f;
+        den += f * lj[j];
+        num += f * oj[j];
+      }
+      const float r = den > 0.f ? fast_rcp(den) : 0.f;
+      bf16x4 o4;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) o4[i] = f2bf(num[i] * r);
+      *reinterpret_cast<bf16x4*>(out + (size_t)m * ldo + (kh * G + gg) * HD + d0) = o4;
+    }
+    return;
+  }
   if (nsplit <= 8 && nout <= 2 * AW * 64) {
     // up to 8 splits and 2 outputs per thread (the few-row decode of every study model but gemma:2b's 8 x 256 query
     // dims): each thread loads its outputs' partials and every split's (m, l) at once -- one round trip of sc1 loads,
