@@ -159,7 +159,14 @@ def attention_splits(M: int, Hkv: int, T_max: int) -> int:
         # 10.9 -> 7.7 us per call at 8 splits (4: 9.1, 16: 8.5), qwen2:1.5b 11.2 -> 8.2, gemma:2b 18.9 -> 13.2,
         # phi3 (32 pairs, 2 splits) 9.7 -> 9.2, llama at 2 rows (4 splits) 11.2 -> 9.4 -- the in-kernel combine's
         # round trips cost less than one workgroup per pair walking the whole context.
-        few = min(8, T_max // 128, 64 // (M * Hkv))
+        # Round 6, with the one-round-trip split combine (profiles/r6/attn_combine/splits_ab.jsonl, one box,
+        # interleaved): a single (row, kv head) pair -- gemma:2b's MQA at batch 1 -- takes 16 splits of >= 3 blocks
+        # (1,235 -> 1,256 tok/s); qwen2:1.5b (2 pairs) lost 0.6 % at 12 or 16 and llama3.1:8b (8 pairs) gained 0.5 %
+        # at 12, so the others keep 8.  CAIN_ATTN_FEW_SPLITS / CAIN_ATTN_MIN_BLOCKS override both for A/B runs.
+        one = M * Hkv == 1
+        cap = int(os.environ.get("CAIN_ATTN_FEW_SPLITS", "0") or 0) or (16 if one else 8)
+        min_blocks = int(os.environ.get("CAIN_ATTN_MIN_BLOCKS", "0") or 0) or (3 if one else 4)
+        few = min(cap, T_max // (32 * min_blocks), 64 // (M * Hkv))
         return int(max(1, min(64, max(few, math.ceil((T_max // 32) / 64)))))
     ns = max(1, min(T_max // 128, math.ceil(256 / (M * Hkv))))
     return int(max(1, min(64, ns)))

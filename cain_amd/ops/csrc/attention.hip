@@ -227,7 +227,7 @@ __global__ __launch_bounds__(AW * 64, OCC) void attn_decode_kernel(
   // per thread with 16-byte write-through stores and sc1 loads, and request every split's partials and (m, l) in one
   // round trip -- the per-element path below issued 8 x 8 dependent-free but 4-byte loads per thread
   // (compiled for head_dim 256 only: the hd <= 128 bodies keep their code unchanged)
-  const bool vec = HD >= 256 && nsplit > 1 && nsplit <= 8 && nout > 2 * AW * 64 && nout <= 8 * AW * 64;
+  const bool vec = HD >= 256 && nsplit > 1 && nsplit <= 16 && nout > 2 * AW * 64 && nout <= 8 * AW * 64;
   if (vec) {
     const __amdgpu_buffer_rsrc_t po_r = slab_rsrc(part_o);
     for (int qd = threadIdx.x; qd < nout / 4; qd += AW * 64) {
@@ -295,70 +295,84 @@ __global__ __launch_bounds__(AW * 64, OCC) void attn_decode_kernel(
   if (vec) {
     if (threadIdx.x == 0) counters[mk] = 0u;  // ready for the next launch (launch-ordered)
     const __amdgpu_buffer_rsrc_t po_r = slab_rsrc(part_o);
-    for (int qd = threadIdx.x; qd < nout / 4; qd += AW * 64) {
-      const int e0 = qd * 4, gg = e0 / HD, d0 = e0 - (e0 / HD) * HD;
-      float mj[8], lj[8];
-      f32x4 oj[8];
+    auto merge = [&](auto ns_c) {  // NS >= nsplit loads per output, clamped (every load unconditional, masked after)
+      constexpr int NS = decltype(ns_c)::value;
+      for (int qd = threadIdx.x; qd < nout / 4; qd += AW * 64) {
+        const int e0 = qd * 4, gg = e0 / HD, d0 = e0 - (e0 / HD) * HD;
+        float mj[NS], lj[NS];
+        f32x4 oj[NS];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {  // clamped: every load unconditional, the split index masked after
-        const int jj = min(j, nsplit - 1);
-        const int li = gg * nsplit + jj;
-        const f32x2 ml = __builtin_bit_cast(
-            f32x2, __hip_atomic_load(reinterpret_cast<const uint64_t*>(pml + li * 2), __ATOMIC_RELAXED,
-                                     __HIP_MEMORY_SCOPE_AGENT));
-        mj[j] = ml[0], lj[j] = ml[1];
-        oj[j] = ld_wt(po_r, (int)(((pbase + (size_t)gg * nsplit + jj) * HD + d0) * 4));
+        for (int j = 0; j < NS; ++j) {
+          const int jj = min(j, nsplit - 1);
+          const int li = gg * nsplit + jj;
+          const f32x2 ml = __builtin_bit_cast(
+              f32x2, __hip_atomic_load(reinterpret_cast<const uint64_t*>(pml + li * 2), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT));
+          mj[j] = ml[0], lj[j] = ml[1];
+          oj[j] = ld_wt(po_r, (int)(((pbase + (size_t)gg * nsplit + jj) * HD + d0) * 4));
+        }
+        float Mx = -INFINITY;
+#pragma unroll
+        for (int j = 0; j < NS; ++j) Mx = j < nsplit ? fmaxf(Mx, mj[j]) : Mx;
+        float den = 0.f;
+        f32x4 num = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int j = 0; j < NS; ++j) {
+          const float f = (j < nsplit && mj[j] != -INFINITY) ? exp2f(mj[j] - Mx) : 0.f;
+          den += f * lj[j];
+          num += f * oj[j];
+        }
+        const float r = den > 0.f ? fast_rcp(den) : 0.f;
+        bf16x4 o4;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) o4[i] = f2bf(num[i] * r);
+        *reinterpret_cast<bf16x4*>(out + (size_t)m * ldo + (kh * G + gg) * HD + d0) = o4;
       }
-      float Mx = -INFINITY;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) Mx = j < nsplit ? fmaxf(Mx, mj[j]) : Mx;
-      float den = 0.f;
-      f32x4 num = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float f = (j < nsplit && mj[j] != -INFINITY) ? exp2f(mj[j] - Mx) : 0.f;
-        den += f * lj[j];
-        num += f * oj[j];
-      }
-      const float r = den > 0.f ? fast_rcp(den) : 0.f;
-      bf16x4 o4;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) o4[i] = f2bf(num[i] * r);
-      *reinterpret_cast<bf16x4*>(out + (size_t)m * ldo + (kh * G + gg) * HD + d0) = o4;
-    }
+    };
+    if (nsplit <= 8)
+      merge(std::integral_constant<int, 8>{});
+    else
+      merge(std::integral_constant<int, 16>{});
     return;
   }
-  if (nsplit <= 8 && nout <= 2 * AW * 64) {
-    // up to 8 splits and 2 outputs per thread (the few-row decode of every study model but gemma:2b's 8 x 256 query
+  if (nsplit <= 16 && nout <= 2 * AW * 64) {
+    // up to 16 splits and 2 outputs per thread (the few-row decode of every study model but gemma:2b's 8 x 256 query
     // dims): each thread loads its outputs' partials and every split's (m, l) at once -- one round trip of sc1 loads,
     // no LDS pass, instead of the (m, l) pass, a barrier and then the partials.  Measured one box, interleaved
     // (profiles/r6/attn_combine/): batch-1 MXFP4 llama3.1:8b +0.9 %, qwen2:1.5b +1.2 %; an LDS variant for 4 outputs
-    // per thread lost on llama / qwen and gemma:2b kept the pass below.
+    // per thread lost on llama / qwen and gemma:2b takes the 16-byte path above.
     if (threadIdx.x == 0) counters[mk] = 0u;  // ready for the next launch (launch-ordered)
-    for (int e = threadIdx.x; e < nout; e += AW * 64) {
-      const int gg = e / HD, d = e - (e / HD) * HD;
-      float mj[8], lj[8], oj[8];
+    auto merge = [&](auto ns_c) {  // NS >= nsplit loads per output, clamped (every load unconditional, masked after)
+      constexpr int NS = decltype(ns_c)::value;
+      for (int e = threadIdx.x; e < nout; e += AW * 64) {
+        const int gg = e / HD, d = e - (e / HD) * HD;
+        float mj[NS], lj[NS], oj[NS];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {  // clamped: every load unconditional, the split index masked after
-        const int jj = min(j, nsplit - 1);
-        const int li = gg * nsplit + jj;
-        mj[j] = __hip_atomic_load(pml + li * 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        lj[j] = __hip_atomic_load(pml + li * 2 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        oj[j] = __hip_atomic_load(part_o + (pbase + (size_t)gg * nsplit + jj) * HD + d, __ATOMIC_RELAXED,
-                                  __HIP_MEMORY_SCOPE_AGENT);
+        for (int j = 0; j < NS; ++j) {
+          const int jj = min(j, nsplit - 1);
+          const int li = gg * nsplit + jj;
+          mj[j] = __hip_atomic_load(pml + li * 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          lj[j] = __hip_atomic_load(pml + li * 2 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          oj[j] = __hip_atomic_load(part_o + (pbase + (size_t)gg * nsplit + jj) * HD + d, __ATOMIC_RELAXED,
+                                    __HIP_MEMORY_SCOPE_AGENT);
+        }
+        float Mx = -INFINITY;
+#pragma unroll
+        for (int j = 0; j < NS; ++j) Mx = j < nsplit ? fmaxf(Mx, mj[j]) : Mx;
+        float num = 0.f, den = 0.f;
+#pragma unroll
+        for (int j = 0; j < NS; ++j) {
+          const float f = (j < nsplit && mj[j] != -INFINITY) ? exp2f(mj[j] - Mx) : 0.f;
+          num += f * oj[j];
+          den += f * lj[j];
+        }
+        out[(size_t)m * ldo + (kh * G + gg) * HD + d] = f2bf(den > 0.f ? num * fast_rcp(den) : 0.f);
       }
-      float Mx = -INFINITY;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) Mx = j < nsplit ? fmaxf(Mx, mj[j]) : Mx;
-      float num = 0.f, den = 0.f;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float f = (j < nsplit && mj[j] != -INFINITY) ? exp2f(mj[j] - Mx) : 0.f;
-        num += f * oj[j];
-        den += f * lj[j];
-      }
-      out[(size_t)m * ldo + (kh * G + gg) * HD + d] = f2bf(den > 0.f ? num * fast_rcp(den) : 0.f);
-    }
+    };
+    if (nsplit <= 8)
+      merge(std::integral_constant<int, 8>{});
+    else
+      merge(std::integral_constant<int, 16>{});
     return;
   }
   // split weights into LDS once (sc1 loads: never served from this CU's stale L1)

@@ -103,3 +103,21 @@ def test_reference_model_kv_cache_matches_full_forward(name):
                      m.forward(t[:, 9:], cache=cache)], 1)
     assert torch.allclose(inc, full, atol=1e-4)
     assert len(cache) == cfg.n_layers and cache[0][0].shape[1] == 12
+
+
+def test_attention_split_rule(monkeypatch):
+    """engine.attention_splits: few (row, kv head) pairs split over positions (<= 8, >= 4 blocks of 32 per split at
+    full context); a single pair (gemma:2b's MQA at batch 1) takes up to 16 splits of >= 3 blocks; many pairs fill
+    ~256 workgroups; the A/B overrides apply."""
+    from cain_amd.engine.engine import attention_splits
+
+    monkeypatch.delenv("CAIN_ATTN_FEW_SPLITS", raising=False)
+    monkeypatch.delenv("CAIN_ATTN_MIN_BLOCKS", raising=False)
+    assert attention_splits(1, 1, 1536) == 16   # gemma:2b, one row
+    assert attention_splits(1, 2, 1536) == 8    # qwen2:1.5b
+    assert attention_splits(1, 8, 1536) == 8    # llama3.1:8b
+    assert attention_splits(1, 32, 1536) == 2   # phi3:3.8b (MHA: 32 pairs)
+    assert attention_splits(1, 1, 512) == 5     # short context: >= 3 blocks per split
+    assert attention_splits(256, 8, 1536) == 1  # the headline's 2,048 pairs
+    monkeypatch.setenv("CAIN_ATTN_FEW_SPLITS", "4")
+    assert attention_splits(1, 1, 1536) == 4 and attention_splits(1, 8, 1536) == 4
