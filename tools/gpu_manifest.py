@@ -226,6 +226,33 @@ SETS = {
         prof("headline_r5", "--steps 1 --warmup 1 --no-single --no-energy"),
         ("smoke", 300, f"{PY} -c 'import __graft_entry__ as g; g.smoke(); print(\"smoke ok\")'"),
     ],
+    # ---- round 6 (its one-off call scripts are folded in here; the reverted experiments' patches and data are under
+    # profiles/r6/<name>/)
+    # the lean chunk-maximum sampler: its tests, the per-phase trace, batch-1 A/B against the round-3 kernel
+    # (profiles/r6/sampler/)
+    "r6_lean": [("lean_tests", 300, f"{TEST} tests/test_sample_lean_gpu.py"),
+                ("lean_trace", 200, f"{PY} -u tools/sample_lean_trace.py")] + [
+        (f"b1_cm{mode}_{i}", 300, f"{PY} -u tools/b1_ab.py --models llama3.1:8b,qwen2:1.5b --dtype fp4 --trials 3 "
+         f"--sample-cm {mode} --label cm{mode} --out gpurun_out/r6_lean/b1.jsonl")
+        for i in range(2) for mode in (1, 3)],
+    # batch-1 kernel statistics on MXFP4 (profiles/r6/prof/, profiles/r6/sampler/)
+    "r6_b1_prof": [(f"prof_b1_{m.replace(':', '_')}", 300,
+                    f"rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r6_b1_prof/{m.replace(':', '_')} "
+                    f"-o b1 -- {PY} tools/b1_ab.py --models {m} --dtype fp4 --trials 1 --label prof && find "
+                    f"gpurun_out/r6_b1_prof -name '*kernel_trace.csv' -delete")
+                   for m in ("llama3.1:8b", "qwen2:1.5b", "gemma:2b")],
+    # PMC counters of the batch-1 gate/up GEMM, MXFP4 against GGUF Q4_0 (profiles/r6/q4/pmc_gateup_fp4_vs_q4_0.json):
+    # 8 SQ counters in one pass, no trace domain beside the kernel trace
+    "r6_pmc_q4": [(f"pmc_{dt}", 120,
+                   f"rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES "
+                   f"SQ_WAIT_INST_ANY SQ_BUSY_CYCLES --kernel-trace --stats -d gpurun_out/r6_pmc_q4/{dt} -o pmc -- "
+                   f"{PY} tools/w4_bench.py --roles gateup --dtypes {dt} --variants rule") for dt in ("fp4", "q4_0")],
+    # batch-1 rates of the seven models on MXFP4 and Q4_K, one box (profiles/r6/b1_fp4_7models_final.jsonl)
+    "r6_b1_seven": [(f"b1_{dt}", 900, f"{PY} -u tools/b1_ab.py --dtype {dt} --trials 3 --label {dt} "
+                     f"--out gpurun_out/r6_b1_seven/b1.jsonl") for dt in ("fp4", "q4_k")],
+    # the final tree: the GPU suite and the smoke test (profiles/r6/tests/)
+    "r6_final": [("gpu_suite", 900, f"{PY} -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread"),
+                 ("smoke", 200, f"{PY} -u -c 'import __graft_entry__ as g; g.smoke()'")],
 }
 
 
