@@ -22,7 +22,7 @@ def test_compare_flags_only_regressions_beyond_tolerance():
 
 
 def test_committed_table_covers_the_study_models():
-    path = ROOT / "profiles" / "baselines" / "b1_shapes_mi355x.json"
+    path = ROOT / "baselines" / "b1_shapes_mi355x.json"
     doc = json.loads(path.read_text())
     shapes = doc["shapes"]
     for m in shape_baseline.MODELS:

@@ -250,10 +250,10 @@ SETS = {
     # batch-1 rates of the seven models on MXFP4 and Q4_K, one box (profiles/r6/b1_fp4_7models_final.jsonl)
     "r6_b1_seven": [(f"b1_{dt}", 900, f"{PY} -u tools/b1_ab.py --dtype {dt} --trials 3 --label {dt} "
                      f"--out gpurun_out/r6_b1_seven/b1.jsonl") for dt in ("fp4", "q4_k")],
-    # the same-box per-shape regression table (tools/shape_baseline.py; profiles/baselines/): record it, and check a
+    # the same-box per-shape regression table (tools/shape_baseline.py; baselines/): record it, and check a
     # build against it before any batch-1 A/B is believed
     "r6_shapes": [("record", 900, f"{PY} -u tools/shape_baseline.py record --out gpurun_out/r6_shapes/b1_shapes_mi355x.json")],
-    "shapes_check": [("check", 900, f"{PY} -u tools/shape_baseline.py check profiles/baselines/b1_shapes_mi355x.json")],
+    "shapes_check": [("check", 900, f"{PY} -u tools/shape_baseline.py check baselines/b1_shapes_mi355x.json")],
     # the final tree: the GPU suite and the smoke test (profiles/r6/tests/)
     "r6_final": [("gpu_suite", 900, f"{PY} -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread"),
                  ("smoke", 200, f"{PY} -u -c 'import __graft_entry__ as g; g.smoke()'")],

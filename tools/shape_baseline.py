@@ -3,8 +3,8 @@
 (VERDICT r5 weak 5 / item 1 -- round 5's 5-13 % MXFP4 loss went unnoticed because every A/B compared two new
 builds with each other and nothing with a fixed reference).
 
-  record:  python3 tools/shape_baseline.py record --out profiles/baselines/b1_shapes_mi355x.json
-  check:   python3 tools/shape_baseline.py check profiles/baselines/b1_shapes_mi355x.json [--tol 0.08]
+  record:  python3 tools/shape_baseline.py record --out baselines/b1_shapes_mi355x.json
+  check:   python3 tools/shape_baseline.py check baselines/b1_shapes_mi355x.json [--tol 0.08]
 
 Both run tools/w4_bench.py (in-graph µs per call, weights rotated past the Infinity Cache: the decode step's cost) on
 the seven study models' QKV / O / gate-up / down / LM-head shapes at one row, MXFP4 (the shape rule's kernel) and
