@@ -9,7 +9,8 @@ builds with each other and nothing with a fixed reference).
 Both run tools/w4_bench.py (in-graph µs per call, weights rotated past the Infinity Cache: the decode step's cost) on
 the seven study models' QKV / O / gate-up / down / LM-head shapes at one row, MXFP4 (the shape rule's kernel) and
 GGUF Q4_K.  `check` prints one JSON line per shape with its ratio to the table and exits 1 when any shape is slower
-than the table by more than --tol (box-to-box spread is ~1-3 %, so the default 8 % flags a real loss, not noise).
+than the table by more than --tol (a second box measured 0.94-1.06 of the table per shape, mean 0.998, so the
+default 8 % flags a real loss, not noise: baselines/checks/).
 """
 from __future__ import annotations
 
