@@ -33,7 +33,14 @@ def main() -> int:
     ap.add_argument("--out", default=None, help="append the JSON lines to this file too")
     ap.add_argument("--sample-cm", type=int, default=None,
                     help="sampler A/B: cain_amd.ops.set_sample_cm mode (3 = the lean chunk-maximum kernel)")
+    ap.add_argument("--w4-split", type=int, default=None,
+                    help="A/B: force k ranges per tile of the MXFP4 stream GEMMs wherever the shape allows "
+                         "(cain_amd.ops.set_w4_split; 0 = the rule)")
     a = ap.parse_args()
+    if a.w4_split is not None:
+        from cain_amd import ops
+
+        ops.set_w4_split(a.w4_split)
     if a.sample_cm is not None:
         from cain_amd import ops
 
@@ -54,7 +61,7 @@ def main() -> int:
                                  [dict(opts, seed=8 + t)])[0]
                 torch.cuda.synchronize()
                 rates.append(r.eval_count / (time.perf_counter() - t0))
-            rec = {"label": a.label, "sample_cm": a.sample_cm, "model": model, "dtype": dtype, "tok_per_s": round(statistics.median(rates), 1),
+            rec = {"label": a.label, "sample_cm": a.sample_cm, "w4_split": a.w4_split, "model": model, "dtype": dtype, "tok_per_s": round(statistics.median(rates), 1),
                    "trials": [round(x, 1) for x in rates], "tokens": n_tok}
             print(json.dumps(rec), flush=True)
             if a.out:
